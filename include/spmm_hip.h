@@ -1,0 +1,221 @@
+/*
+ * spmm_hip.h — C ABI of the MI355X-native SpMM engine (libspmm_hip.so).
+ *
+ * This is the drop-in boundary for the two hot paths of
+ * xuyifangreeneyes/spmm-denseblock:
+ *
+ *   Path A  CSR x dense   replaces gespmm_csrmm<T>          (gespmm_csrmm.h:422-426)
+ *                          and the legacy cusparseScsrmm / cusparseScsrmm2 call
+ *                          sites (run_csrmm.cu:133-142, test_csrmm.cu:126-129)
+ *   Path B  BSR x dense   replaces rocsparse_bsrmm_template<T> (rocsparse_bsrmm.h:102-256)
+ *                          and cusparseSbsrmm (run_bsrmm.cu:160-165), plus the
+ *                          per-block cublasSgemm variant (block_cublas.cu:123-136)
+ *   Prep    csr2bsr / bsr2csr / nnzb on the HOST (north_star: conversion stays
+ *           CPU-side preprocessing), replacing cusparseXcsr2bsrNnz +
+ *           cusparseScsr2bsr (run_bsrmm.cu:116-142) and cusparseSbsr2csr
+ *           (bsr2csr.cu:186-188).
+ *
+ * Conventions
+ *   - Plain C: pointers, sizes, enums. No HIP or torch types in signatures;
+ *     a stream is passed as an opaque `void*` (a hipStream_t, 0 = default).
+ *   - The caller owns every device buffer (the reference cudaMallocs in its
+ *     drivers). Kernels never allocate; a handle may keep a small internal
+ *     workspace (merge-path carries, layout staging) that it grows lazily.
+ *   - Numeric values of spmm_status_t / spmm_direction_t / spmm_operation_t
+ *     mirror cusparseStatus_t / cusparseDirection_t / cusparseOperation_t so a
+ *     caller's HANDLE_CUSPARSE_ERROR-style checks keep working.
+ *   - All index arrays are int32, as in the reference. fp32 values unless the
+ *     function name says otherwise.
+ */
+#ifndef SPMM_HIP_H
+#define SPMM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPMM_HIP_VERSION 100 /* 1.0.0 */
+
+typedef enum {
+  SPMM_STATUS_SUCCESS = 0,
+  SPMM_STATUS_NOT_INITIALIZED = 1,
+  SPMM_STATUS_ALLOC_FAILED = 2,
+  SPMM_STATUS_INVALID_VALUE = 3,
+  SPMM_STATUS_ARCH_MISMATCH = 4,
+  SPMM_STATUS_MAPPING_ERROR = 5,
+  SPMM_STATUS_EXECUTION_FAILED = 6,
+  SPMM_STATUS_INTERNAL_ERROR = 7,
+  SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED = 8,
+  SPMM_STATUS_ZERO_PIVOT = 9,
+  SPMM_STATUS_NOT_SUPPORTED = 10
+} spmm_status_t;
+
+typedef enum { SPMM_DIRECTION_ROW = 0, SPMM_DIRECTION_COLUMN = 1 } spmm_direction_t;
+
+typedef enum {
+  SPMM_OPERATION_NON_TRANSPOSE = 0,
+  SPMM_OPERATION_TRANSPOSE = 1,
+  SPMM_OPERATION_CONJUGATE_TRANSPOSE = 2
+} spmm_operation_t;
+
+/* Storage order of a dense matrix (explicit in the *_ex entry points). */
+typedef enum { SPMM_ORDER_ROW = 0, SPMM_ORDER_COL = 1 } spmm_order_t;
+
+typedef enum { SPMM_INDEX_BASE_ZERO = 0, SPMM_INDEX_BASE_ONE = 1 } spmm_index_base_t;
+
+typedef enum { SPMM_MATRIX_TYPE_GENERAL = 0 } spmm_matrix_type_t;
+
+typedef struct spmm_context* spmm_handle_t;    /* ~ cusparseHandle_t  */
+typedef struct spmm_mat_descr* spmm_mat_descr_t; /* ~ cusparseMatDescr_t */
+
+/* ------------------------------------------------------------------------ */
+/* Handle / descriptor lifecycle (cusparseCreate, cusparseSetStream, ...)     */
+/* ------------------------------------------------------------------------ */
+int spmm_get_version(void);
+const char* spmm_get_status_string(spmm_status_t status);
+
+spmm_status_t spmm_create(spmm_handle_t* handle);
+spmm_status_t spmm_destroy(spmm_handle_t handle);
+spmm_status_t spmm_set_stream(spmm_handle_t handle, void* stream);
+spmm_status_t spmm_get_stream(spmm_handle_t handle, void** stream);
+
+spmm_status_t spmm_create_mat_descr(spmm_mat_descr_t* descr);
+spmm_status_t spmm_destroy_mat_descr(spmm_mat_descr_t descr);
+spmm_status_t spmm_set_mat_type(spmm_mat_descr_t descr, spmm_matrix_type_t type);
+spmm_status_t spmm_set_mat_index_base(spmm_mat_descr_t descr, spmm_index_base_t base);
+
+/* Per-launch device timing of the dominant kernel (hipEvents recorded on the
+ * handle's stream around each main-kernel launch). Used by bench.py for the
+ * roofline figure; off by default, costs two event records per launch. */
+spmm_status_t spmm_set_kernel_timing(spmm_handle_t handle, int enable);
+/* Synchronises the recorded events, returns up to max_count durations (ms),
+ * oldest first, and clears the record. */
+spmm_status_t spmm_get_kernel_times(spmm_handle_t handle, float* ms, int max_count, int* count);
+
+/* Tuning knob for the CSR merge-path kernel: resident waves per CU the grid
+ * is sized for (0 = default). */
+spmm_status_t spmm_set_csr_waves_per_cu(spmm_handle_t handle, int waves_per_cu);
+
+/* ------------------------------------------------------------------------ */
+/* Path A: CSR x dense                                                         */
+/* ------------------------------------------------------------------------ */
+
+/* Drop-in for gespmm_csrmm<float> (gespmm_csrmm.h:422-426):
+ *   C[A_nrows x B_ncols] = A(csr) * B, B and C row-major (ld = B_ncols),
+ *   C overwritten (no alpha/beta), empty rows give 0. nnz is read from
+ *   A_rowPtr[A_nrows] on the device. Runs on `stream` with a process-wide
+ *   default handle. */
+spmm_status_t spmm_gespmm_csrmm_f32(int A_nrows, int B_ncols, const int* A_rowPtr,
+                                    const int* A_colInd, const float* A_val,
+                                    const float* B, float* C, void* stream);
+
+/* Drop-in for cusparseScsrmm (run_csrmm.cu:135-137):
+ *   C(m x n, col-major, ldc) = alpha*op(A)(m x k) * B(k x n, col-major, ldb) + beta*C.
+ * Only transA = NON_TRANSPOSE is supported (as in the reference call sites). */
+spmm_status_t spmm_scsrmm(spmm_handle_t handle, spmm_operation_t transA, int m, int n, int k,
+                          int nnz, const float* alpha, const spmm_mat_descr_t descrA,
+                          const float* csrValA, const int* csrRowPtrA, const int* csrColIndA,
+                          const float* B, int ldb, const float* beta, float* C, int ldc);
+
+/* Drop-in for cusparseScsrmm2 (run_csrmm.cu:139-142, test_csrmm.cu:126-129):
+ *   transB = NON_TRANSPOSE: B col-major k x n (ldb >= k);
+ *   transB = TRANSPOSE:     B row-major k x n (ldb >= n);  C col-major. */
+spmm_status_t spmm_scsrmm2(spmm_handle_t handle, spmm_operation_t transA,
+                           spmm_operation_t transB, int m, int n, int k, int nnz,
+                           const float* alpha, const spmm_mat_descr_t descrA,
+                           const float* csrValA, const int* csrRowPtrA,
+                           const int* csrColIndA, const float* B, int ldb,
+                           const float* beta, float* C, int ldc);
+
+/* General form with explicit dense storage orders (host-pointer alpha/beta).
+ *   C(m x n) = alpha * A(m x k, csr) * B(k x n) + beta * C
+ * orderB/orderC = SPMM_ORDER_ROW is the fast (native) layout; column-major
+ * operands are staged through the handle workspace. beta == 0 never reads C. */
+spmm_status_t spmm_csrmm_ex_f32(spmm_handle_t handle, int m, int n, int k, int nnz,
+                                float alpha, const int* csrRowPtr, const int* csrColInd,
+                                const float* csrVal, spmm_index_base_t base,
+                                const float* B, int ldb, spmm_order_t orderB, float beta,
+                                float* C, int ldc, spmm_order_t orderC);
+
+/* ------------------------------------------------------------------------ */
+/* Path B: BSR x dense                                                         */
+/* ------------------------------------------------------------------------ */
+
+/* Drop-in for cusparseSbsrmm (run_bsrmm.cu:160-165) and, with alpha/beta
+ * passed by pointer, rocsparse_bsrmm_template<float> (rocsparse_bsrmm.h:102-108):
+ *   C(mb*bs x n, col-major, ldc) = alpha * A(bsr, mb x kb blocks) * op(B) + beta * C
+ *   dir: block storage (ROW: val[b*bs*bs + r*bs + c]; COLUMN: val[b*bs*bs + c*bs + r])
+ *   transB = NON_TRANSPOSE: B col-major (kb*bs x n, ldb >= kb*bs)
+ *   transB = TRANSPOSE:     B row-major (kb*bs x n, ldb >= n)
+ * Status behaviour follows rocsparse_bsrmm.h:109-176 (NOT_INITIALIZED for a
+ * null handle, INVALID_VALUE for null descr / negative sizes / null pointers /
+ * bad ld, MATRIX_TYPE_NOT_SUPPORTED for transA != N or a bad transB, SUCCESS
+ * quick return when mb, n, kb or nnzb is 0). */
+spmm_status_t spmm_sbsrmm(spmm_handle_t handle, spmm_direction_t dir,
+                          spmm_operation_t transA, spmm_operation_t transB, int mb, int n,
+                          int kb, int nnzb, const float* alpha, const spmm_mat_descr_t descrA,
+                          const float* bsrValA, const int* bsrRowPtrA, const int* bsrColIndA,
+                          int blockDim, const float* B, int ldb, const float* beta, float* C,
+                          int ldc);
+
+/* General form with explicit dense storage orders.
+ *   C(mb*bs x n) = alpha * A(bsr) * B(kb*bs x n) + beta * C
+ * bs in {16, 32} runs on fp32 MFMA (v_mfma_f32_{16x16x4,32x32x2}_f32); other
+ * block sizes run a VALU kernel. The per-block cublasSgemm variant of
+ * block_cublas.cu:123-136 is dir = COLUMN, orderB = ROW, orderC = COL, beta = 1. */
+spmm_status_t spmm_bsrmm_ex_f32(spmm_handle_t handle, spmm_direction_t dir, int mb, int kb,
+                                int n, int nnzb, int blockDim, float alpha,
+                                const int* bsrRowPtr, const int* bsrColInd,
+                                const float* bsrVal, const float* B, int ldb,
+                                spmm_order_t orderB, float beta, float* C, int ldc,
+                                spmm_order_t orderC);
+
+/* fp16 A and B (IEEE binary16 bit patterns), fp32 accumulate and fp32 C.
+ * bs = 16 runs on v_mfma_f32_16x16x32_f16 with two blocks per instruction. */
+spmm_status_t spmm_bsrmm_ex_f16(spmm_handle_t handle, spmm_direction_t dir, int mb, int kb,
+                                int n, int nnzb, int blockDim, float alpha,
+                                const int* bsrRowPtr, const int* bsrColInd,
+                                const uint16_t* bsrVal, const uint16_t* B, int ldb,
+                                spmm_order_t orderB, float beta, float* C, int ldc,
+                                spmm_order_t orderC);
+
+/* ------------------------------------------------------------------------ */
+/* Preprocessing on the HOST (all pointers are host pointers)                  */
+/* ------------------------------------------------------------------------ */
+
+/* cusparseXcsr2bsrNnz semantics (run_bsrmm.cu:121-131): fills
+ * bsrRowPtr[mb+1] (mb = ceil(m/blockDim)) and *nnzbTotal. */
+spmm_status_t spmm_xcsr2bsr_nnz(spmm_direction_t dir, int m, int n, const int* csrRowPtr,
+                                const int* csrColInd, int blockDim, int* bsrRowPtr,
+                                int* nnzbTotal);
+
+/* cusparseScsr2bsr semantics (run_bsrmm.cu:136-142): bsrRowPtr must come from
+ * spmm_xcsr2bsr_nnz; bsrColInd[nnzb] sorted per block row; bsrVal[nnzb*bs*bs]
+ * zero-filled, values placed per `dir`. Duplicate (row, col) entries are
+ * summed. */
+spmm_status_t spmm_scsr2bsr(spmm_direction_t dir, int m, int n, const float* csrVal,
+                            const int* csrRowPtr, const int* csrColInd, int blockDim,
+                            const int* bsrRowPtr, float* bsrVal, int* bsrColInd);
+
+/* cusparseSbsr2csr semantics (bsr2csr.cu:177-188): every block expanded,
+ * explicit zeros kept: nnz = nnzb*bs*bs, csrRowPtr[mb*bs+1]. */
+spmm_status_t spmm_sbsr2csr(spmm_direction_t dir, int mb, int nb, const float* bsrVal,
+                            const int* bsrRowPtr, const int* bsrColInd, int blockDim,
+                            float* csrVal, int* csrRowPtr, int* csrColInd);
+
+/* calculateNnzb (utility.cc:47-69) over a CSR pattern: number of nonzero
+ * bs x bs blocks. */
+int64_t spmm_calculate_nnzb(int n, const int* csrRowPtr, const int* csrColInd, int blockDim);
+
+/* nnz-balanced contiguous row partition for multi-GPU sharding:
+ * bounds[0] = 0, bounds[nparts] = m, part p owns rows [bounds[p], bounds[p+1]).
+ * Minimises the max over parts of (nnz + rows) by a prefix search on rowptr. */
+spmm_status_t spmm_csr_partition_rows(int m, const int* csrRowPtr, int nparts, int* bounds);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* SPMM_HIP_H */

@@ -1,0 +1,86 @@
+// ref_harness.cpp — C entry points around the reference's own host functions.
+// Appended (by oracle/Makefile) after the function bodies cut from
+// /root/reference; it sees the reference's `static std::mt19937_64 gen`
+// (load_data.cc:12) because it lives in the same translation unit.
+// TEST INFRASTRUCTURE ONLY (oracle/_ref, git-ignored output).
+#include <cstdint>
+#include <cstring>
+
+namespace ref_harness {
+std::vector<int> g_csr_rp, g_csr_ci, g_bsr_rp, g_bsr_ci;
+std::vector<float> g_bsr_val;
+
+std::vector<std::vector<int>> edges_of(int n, const int* rowptr, const int* colind) {
+  std::vector<std::vector<int>> e(n);
+  for (int i = 0; i < n; ++i)
+    for (int j = rowptr[i]; j < rowptr[i + 1]; ++j) e[i].push_back(colind[j]);
+  return e;
+}
+}  // namespace ref_harness
+
+extern "C" {
+
+void ref_seed(uint64_t s) { gen.seed(s); }
+
+// randomDenseMatrix (load_data.cc:38-40) -> out[n*dim]
+void ref_random_dense(int n, int dim, float lo, float hi, float* out) {
+  float* p = randomDenseMatrix(n, dim, lo, hi);
+  std::memcpy(out, p, sizeof(float) * (size_t)n * dim);
+  free(p);
+}
+
+// randomCSRMatrix (load_data.cc:42-69), dump = false. Returns nnz or -1.
+int64_t ref_random_csr(int m, int n, float p, float lo, float hi, int* rowptr, int* colind,
+                       float* val, int64_t cap) {
+  int *rp = nullptr, *ci = nullptr;
+  float* v = nullptr;
+  const int nnz = randomCSRMatrix(m, n, p, &rp, &ci, &v, lo, hi, false);
+  if (nnz > cap) return -1;
+  std::memcpy(rowptr, rp, sizeof(int) * (size_t)(m + 1));
+  std::memcpy(colind, ci, sizeof(int) * (size_t)nnz);
+  std::memcpy(val, v, sizeof(float) * (size_t)nnz);
+  free(rp); free(ci); free(v);
+  return nnz;
+}
+
+// randomBSRMatrix (load_data.cc:81-113), dump = false.
+int64_t ref_random_bsr(int mb, int nb, int bs, float p, float lo, float hi, int* rowptr,
+                       int* colind, float* val, int64_t cap_blocks) {
+  int *rp = nullptr, *ci = nullptr;
+  float* v = nullptr;
+  const int nnzb = randomBSRMatrix(mb, nb, bs, p, &rp, &ci, &v, lo, hi, false);
+  if (nnzb > cap_blocks) return -1;
+  std::memcpy(rowptr, rp, sizeof(int) * (size_t)(mb + 1));
+  std::memcpy(colind, ci, sizeof(int) * (size_t)nnzb);
+  std::memcpy(val, v, sizeof(float) * (size_t)nnzb * bs * bs);
+  free(rp); free(ci); free(v);
+  return nnzb;
+}
+
+// calculateNnzb (utility.cc:47-69) on a CSR pattern.
+int64_t ref_calculate_nnzb(int n, const int* rowptr, const int* colind, int bs) {
+  return calculateNnzb(ref_harness::edges_of(n, rowptr, colind), bs);
+}
+
+// divide_matrix (divide.cu:52-127): runs it and keeps the five outputs;
+// sizes are returned through `sizes` = {csr_rp, csr_ci, bsr_rp, bsr_ci, bsr_val}.
+void ref_divide_matrix(int n, const int* rowptr, const int* colind, int bs, float density,
+                       int64_t* sizes) {
+  using namespace ref_harness;
+  g_csr_rp.clear(); g_csr_ci.clear(); g_bsr_rp.clear(); g_bsr_ci.clear(); g_bsr_val.clear();
+  divide_matrix(edges_of(n, rowptr, colind), g_csr_rp, g_csr_ci, g_bsr_rp, g_bsr_ci, g_bsr_val,
+                n, bs, density);
+  sizes[0] = g_csr_rp.size(); sizes[1] = g_csr_ci.size(); sizes[2] = g_bsr_rp.size();
+  sizes[3] = g_bsr_ci.size(); sizes[4] = g_bsr_val.size();
+}
+
+void ref_divide_fetch(int* csr_rp, int* csr_ci, int* bsr_rp, int* bsr_ci, float* bsr_val) {
+  using namespace ref_harness;
+  std::copy(g_csr_rp.begin(), g_csr_rp.end(), csr_rp);
+  std::copy(g_csr_ci.begin(), g_csr_ci.end(), csr_ci);
+  std::copy(g_bsr_rp.begin(), g_bsr_rp.end(), bsr_rp);
+  std::copy(g_bsr_ci.begin(), g_bsr_ci.end(), bsr_ci);
+  std::copy(g_bsr_val.begin(), g_bsr_val.end(), bsr_val);
+}
+
+}  // extern "C"

@@ -1,0 +1,197 @@
+// api.cpp — extern "C" SpMM entry points: argument checks (mirroring the
+// reference's status behaviour) and dispatch to the HIP launchers.
+#include <cstdint>
+
+#include "context.hpp"
+
+using namespace spmm;
+
+namespace {
+
+// Workspace carve-up: [carries | staged B | staged C], 256-byte aligned.
+struct WsLayout {
+  size_t carry_off = 0, carry_bytes = 0, b_off = 0, c_off = 0, total = 0;
+};
+
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, float alpha,
+                         const int* rowptr, const int* colind, const float* val, int base,
+                         const float* B, int ldb, spmm_order_t orderB, float beta, float* C,
+                         int ldc, spmm_order_t orderC) {
+  WsLayout L;
+  L.carry_bytes = csrmm_carry_bytes(ctx, m, n, nullptr);
+  L.b_off = align256(L.carry_bytes);
+  const size_t b_bytes = orderB == SPMM_ORDER_COL ? (size_t)k * n * sizeof(float) : 0;
+  L.c_off = align256(L.b_off + b_bytes);
+  const size_t c_bytes = orderC == SPMM_ORDER_COL ? (size_t)m * n * sizeof(float) : 0;
+  L.total = L.c_off + c_bytes;
+  spmm_status_t st = ensure_workspace(ctx, L.total);
+  if (st != SPMM_STATUS_SUCCESS) return st;
+  char* ws = static_cast<char*>(ctx->ws);
+  int nw = 0;
+  csrmm_carry_bytes(ctx, m, n, &nw);
+  const int ntiles_max = (n + 63) / 64;
+  float* carry_val = reinterpret_cast<float*>(ws);
+  int* carry_row = reinterpret_cast<int*>(ws + (size_t)nw * ntiles_max * 64 * sizeof(float));
+
+  const float* Bx = B;
+  int ldbx = ldb;
+  if (orderB == SPMM_ORDER_COL) {
+    // B (k x n col-major) is an (n x k) row-major matrix with ld ldb.
+    float* Bt = reinterpret_cast<float*>(ws + L.b_off);
+    st = launch_transpose(ctx, n, k, B, ldb, Bt, n, 0.f);
+    if (st != SPMM_STATUS_SUCCESS) return st;
+    Bx = Bt;
+    ldbx = n;
+  }
+  if (orderC == SPMM_ORDER_ROW) {
+    return launch_csrmm_rowmajor(ctx, m, n, rowptr, colind, val, base, Bx, ldbx, alpha, beta, C,
+                                 ldc, carry_val, carry_row, nnz_hint);
+  }
+  float* Ct = reinterpret_cast<float*>(ws + L.c_off);
+  st = launch_csrmm_rowmajor(ctx, m, n, rowptr, colind, val, base, Bx, ldbx, alpha, 0.f, Ct, n,
+                             carry_val, carry_row, nnz_hint);
+  if (st != SPMM_STATUS_SUCCESS) return st;
+  // C (m x n col-major, ldc) is an (n x m) row-major matrix with ld ldc.
+  return launch_transpose(ctx, m, n, Ct, n, C, ldc, beta);
+}
+
+}  // namespace
+
+extern "C" {
+
+spmm_status_t spmm_gespmm_csrmm_f32(int A_nrows, int B_ncols, const int* A_rowPtr,
+                                    const int* A_colInd, const float* A_val, const float* B,
+                                    float* C, void* stream) {
+  if (A_nrows < 0 || B_ncols < 0) return SPMM_STATUS_INVALID_VALUE;
+  if (A_nrows == 0 || B_ncols == 0) return SPMM_STATUS_SUCCESS;
+  if (!A_rowPtr || !A_colInd || !A_val || !B || !C) return SPMM_STATUS_INVALID_VALUE;
+  spmm_context* ctx = default_context();
+  if (!ctx) return SPMM_STATUS_NOT_INITIALIZED;
+  ctx->stream = reinterpret_cast<hipStream_t>(stream);
+  // nnz is only known on the device (A_rowPtr[A_nrows]); -1 sizes the grid
+  // from the row count.
+  return csrmm_impl(ctx, A_nrows, B_ncols, A_nrows, -1, 1.f, A_rowPtr, A_colInd, A_val, 0, B,
+                    B_ncols, SPMM_ORDER_ROW, 0.f, C, B_ncols, SPMM_ORDER_ROW);
+}
+
+spmm_status_t spmm_csrmm_ex_f32(spmm_handle_t handle, int m, int n, int k, int nnz, float alpha,
+                                const int* csrRowPtr, const int* csrColInd, const float* csrVal,
+                                spmm_index_base_t base, const float* B, int ldb,
+                                spmm_order_t orderB, float beta, float* C, int ldc,
+                                spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (m < 0 || n < 0 || k < 0 || nnz < 0) return SPMM_STATUS_INVALID_VALUE;
+  if (base != SPMM_INDEX_BASE_ZERO && base != SPMM_INDEX_BASE_ONE)
+    return SPMM_STATUS_INVALID_VALUE;
+  if ((orderB != SPMM_ORDER_ROW && orderB != SPMM_ORDER_COL) ||
+      (orderC != SPMM_ORDER_ROW && orderC != SPMM_ORDER_COL))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  if (!csrRowPtr || !C || (k > 0 && !B) || (nnz > 0 && (!csrColInd || !csrVal)))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (orderB == SPMM_ORDER_ROW ? ldb < n : ldb < (k > 0 ? k : 1)) return SPMM_STATUS_INVALID_VALUE;
+  if (orderC == SPMM_ORDER_ROW ? ldc < n : ldc < m) return SPMM_STATUS_INVALID_VALUE;
+  return csrmm_impl(handle, m, n, k, nnz, alpha, csrRowPtr, csrColInd, csrVal, (int)base, B, ldb,
+                    orderB, beta, C, ldc, orderC);
+}
+
+spmm_status_t spmm_scsrmm2(spmm_handle_t handle, spmm_operation_t transA,
+                           spmm_operation_t transB, int m, int n, int k, int nnz,
+                           const float* alpha, const spmm_mat_descr_t descrA,
+                           const float* csrValA, const int* csrRowPtrA, const int* csrColIndA,
+                           const float* B, int ldb, const float* beta, float* C, int ldc) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (!descrA || !alpha || !beta) return SPMM_STATUS_INVALID_VALUE;
+  if (transA != SPMM_OPERATION_NON_TRANSPOSE) return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  if (transB != SPMM_OPERATION_NON_TRANSPOSE && transB != SPMM_OPERATION_TRANSPOSE)
+    return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  const spmm_order_t ob =
+      transB == SPMM_OPERATION_NON_TRANSPOSE ? SPMM_ORDER_COL : SPMM_ORDER_ROW;
+  return spmm_csrmm_ex_f32(handle, m, n, k, nnz, *alpha, csrRowPtrA, csrColIndA, csrValA,
+                           descrA->base, B, ldb, ob, *beta, C, ldc, SPMM_ORDER_COL);
+}
+
+spmm_status_t spmm_scsrmm(spmm_handle_t handle, spmm_operation_t transA, int m, int n, int k,
+                          int nnz, const float* alpha, const spmm_mat_descr_t descrA,
+                          const float* csrValA, const int* csrRowPtrA, const int* csrColIndA,
+                          const float* B, int ldb, const float* beta, float* C, int ldc) {
+  return spmm_scsrmm2(handle, transA, SPMM_OPERATION_NON_TRANSPOSE, m, n, k, nnz, alpha, descrA,
+                      csrValA, csrRowPtrA, csrColIndA, B, ldb, beta, C, ldc);
+}
+
+static spmm_status_t bsr_checks(int mb, int kb, int n, int nnzb, int bs, const int* rowptr,
+                                const int* colind, const void* val, const void* B, int ldb,
+                                spmm_order_t orderB, const void* C, int ldc,
+                                spmm_order_t orderC, bool* quick) {
+  *quick = false;
+  if (mb < 0 || n < 0 || kb < 0 || nnzb < 0 || bs <= 0) return SPMM_STATUS_INVALID_VALUE;
+  if ((orderB != SPMM_ORDER_ROW && orderB != SPMM_ORDER_COL) ||
+      (orderC != SPMM_ORDER_ROW && orderC != SPMM_ORDER_COL))
+    return SPMM_STATUS_INVALID_VALUE;
+  // Quick return (rocsparse_bsrmm.h:152-154): C is left untouched.
+  if (mb == 0 || n == 0 || kb == 0 || nnzb == 0) {
+    *quick = true;
+    return SPMM_STATUS_SUCCESS;
+  }
+  if (!val || !rowptr || !colind || !B || !C) return SPMM_STATUS_INVALID_VALUE;
+  const long long K = (long long)kb * bs, M = (long long)mb * bs;
+  if (orderB == SPMM_ORDER_COL ? ldb < K : ldb < n) return SPMM_STATUS_INVALID_VALUE;
+  if (orderC == SPMM_ORDER_COL ? ldc < M : ldc < n) return SPMM_STATUS_INVALID_VALUE;
+  return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t spmm_bsrmm_ex_f32(spmm_handle_t handle, spmm_direction_t dir, int mb, int kb, int n,
+                                int nnzb, int blockDim, float alpha, const int* bsrRowPtr,
+                                const int* bsrColInd, const float* bsrVal, const float* B, int ldb,
+                                spmm_order_t orderB, float beta, float* C, int ldc,
+                                spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) return SPMM_STATUS_INVALID_VALUE;
+  bool quick = false;
+  spmm_status_t st = bsr_checks(mb, kb, n, nnzb, blockDim, bsrRowPtr, bsrColInd, bsrVal, B, ldb,
+                                orderB, C, ldc, orderC, &quick);
+  if (st != SPMM_STATUS_SUCCESS || quick) return st;
+  return launch_bsrmm_f32(handle, dir, mb, kb, n, nnzb, blockDim, alpha, bsrRowPtr, bsrColInd,
+                          bsrVal, B, ldb, orderB, beta, C, ldc, orderC);
+}
+
+spmm_status_t spmm_bsrmm_ex_f16(spmm_handle_t handle, spmm_direction_t dir, int mb, int kb, int n,
+                                int nnzb, int blockDim, float alpha, const int* bsrRowPtr,
+                                const int* bsrColInd, const uint16_t* bsrVal, const uint16_t* B,
+                                int ldb, spmm_order_t orderB, float beta, float* C, int ldc,
+                                spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) return SPMM_STATUS_INVALID_VALUE;
+  bool quick = false;
+  spmm_status_t st = bsr_checks(mb, kb, n, nnzb, blockDim, bsrRowPtr, bsrColInd, bsrVal, B, ldb,
+                                orderB, C, ldc, orderC, &quick);
+  if (st != SPMM_STATUS_SUCCESS || quick) return st;
+  return launch_bsrmm_f16(handle, dir, mb, kb, n, nnzb, blockDim, alpha, bsrRowPtr, bsrColInd,
+                          bsrVal, B, ldb, orderB, beta, C, ldc, orderC);
+}
+
+spmm_status_t spmm_sbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_operation_t transA,
+                          spmm_operation_t transB, int mb, int n, int kb, int nnzb,
+                          const float* alpha, const spmm_mat_descr_t descrA,
+                          const float* bsrValA, const int* bsrRowPtrA, const int* bsrColIndA,
+                          int blockDim, const float* B, int ldb, const float* beta, float* C,
+                          int ldc) {
+  // Check order follows rocsparse_bsrmm.h:109-176.
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (!descrA) return SPMM_STATUS_INVALID_VALUE;
+  if (transA != SPMM_OPERATION_NON_TRANSPOSE) return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  if (transB != SPMM_OPERATION_NON_TRANSPOSE && transB != SPMM_OPERATION_TRANSPOSE)
+    return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  if (mb < 0 || n < 0 || kb < 0 || nnzb < 0 || blockDim <= 0) return SPMM_STATUS_INVALID_VALUE;
+  if (mb == 0 || n == 0 || kb == 0 || nnzb == 0) return SPMM_STATUS_SUCCESS;
+  if (!alpha || !beta) return SPMM_STATUS_INVALID_VALUE;
+  if (descrA->base != SPMM_INDEX_BASE_ZERO) return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  const spmm_order_t ob =
+      transB == SPMM_OPERATION_NON_TRANSPOSE ? SPMM_ORDER_COL : SPMM_ORDER_ROW;
+  return spmm_bsrmm_ex_f32(handle, dir, mb, kb, n, nnzb, blockDim, *alpha, bsrRowPtrA, bsrColIndA,
+                           bsrValA, B, ldb, ob, *beta, C, ldc, SPMM_ORDER_COL);
+}
+
+}  // extern "C"

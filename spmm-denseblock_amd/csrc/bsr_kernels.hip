@@ -1,0 +1,404 @@
+// bsr_kernels.hip — Path B: BSR x dense on gfx950 (MI355X).
+//
+// Semantic target is cusparseSbsrmm (run_bsrmm.cu:160-165, bsrmm.cu:141-144):
+//   C = alpha * A_bsr * op(B) + beta * C
+// with DIRECTION_ROW / COLUMN block storage. The reference's own transcription
+// of rocSPARSE (rocsparse_bsrmm_impl.h:315-389) indexes column tiles with
+// blockDim.y instead of blockIdx.y (:326) and writes nothing for bs 16/32 at
+// K <= 256, so it is not used as an oracle. The
+// epilogue follows its rocSPARSE convention (impl.h:381-388): beta == 0 gives
+// C = alpha*sum without reading C, else C = fma(beta, C, alpha*sum).
+//
+// Kernels:
+//  * bs = 32, fp32: every nonzero block is an MFMA A-tile of
+//    v_mfma_f32_32x32x2_f32. A wave owns 32 rows (the block row) x 32 output
+//    columns; a block contributes 16 MFMAs. The k index inside an MFMA pair
+//    is permuted (step s, lane half h -> k = 16h + s) so each lane's A
+//    fragment is 16 contiguous floats of one block row (4 x dwordx4) and,
+//    for column-major B, its B fragment is 16 contiguous floats too.
+//  * bs = 16, fp32: v_mfma_f32_16x16x4_f32, k = 4q + s, 4 column tiles per
+//    wave sharing the A fragment (one dwordx4 per block).
+//  * bs = 16, fp16 A/B: v_mfma_f32_16x16x32_f16 consumes TWO blocks of the
+//    block row per instruction (k 0-15 from block b, 16-31 from block b+1).
+//  * any other bs: a VALU kernel with the same semantics.
+// Fragments of block b+1 are loaded while block b's MFMAs issue.
+#include <hip/hip_runtime.h>
+
+#include "context.hpp"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float epi(float acc, float alpha, float beta, const float* p) {
+  return beta == 0.f ? alpha * acc : __builtin_fmaf(beta, *p, alpha * acc);
+}
+
+// ---------------------------------------------------------------------------
+// bs = 32 fp32 MFMA. Block = 4 waves, each wave a 32-column slice.
+// ---------------------------------------------------------------------------
+template <bool ROWDIR, bool BROW, bool CROW>
+__global__ __launch_bounds__(256) void bsr32_f32_mfma_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int br = blockIdx.x;
+  const int j0 = (blockIdx.y * (blockDim.x >> 6) + wv) * 32;
+  if (j0 >= n) return;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int jcol = j0 + r;
+  const bool jok = jcol < n;
+  const int jld = jok ? jcol : j0;
+
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+
+  float a[16], b[16], an[16], bn[16];
+  auto load_frags = [&](int k, float (&fa)[16], float (&fb)[16]) {
+    const int bc = colind[k];
+    const float* ab = val + (size_t)k * 1024;
+    if constexpr (ROWDIR) {
+      const f32x4* p = reinterpret_cast<const f32x4*>(ab + r * 32 + 16 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 x = p[q];
+        fa[4 * q + 0] = x[0]; fa[4 * q + 1] = x[1]; fa[4 * q + 2] = x[2]; fa[4 * q + 3] = x[3];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) fa[s] = ab[(16 * h + s) * 32 + r];
+    }
+    const size_t krow = (size_t)bc * 32 + 16 * h;
+    if constexpr (BROW) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) fb[s] = B[(krow + s) * ldb + jld];
+    } else {
+      const f32x4* p = reinterpret_cast<const f32x4*>(B + (size_t)jld * ldb + krow);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 x = p[q];
+        fb[4 * q + 0] = x[0]; fb[4 * q + 1] = x[1]; fb[4 * q + 2] = x[2]; fb[4 * q + 3] = x[3];
+      }
+    }
+  };
+
+  if (k0 < k1) load_frags(k0, a, b);
+  for (int k = k0; k < k1; ++k) {
+    if (k + 1 < k1) load_frags(k + 1, an, bn);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) { a[s] = an[s]; b[s] = bn[s]; }
+  }
+
+  if (!jok) return;
+  const size_t row0 = (size_t)br * 32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = row0 + 8 * g + 4 * h + e;
+      float* p = CROW ? C + row * ldc + jcol : C + (size_t)jcol * ldc + row;
+      *p = epi(acc[4 * g + e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 16 fp32 MFMA. Each wave: 16 rows x 64 columns (4 tiles of 16).
+// ---------------------------------------------------------------------------
+template <bool ROWDIR, bool BROW, bool CROW>
+__global__ __launch_bounds__(256) void bsr16_f32_mfma_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  constexpr int NT = 4;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int br = blockIdx.x;
+  const int j0 = (blockIdx.y * (blockDim.x >> 6) + wv) * (16 * NT);
+  if (j0 >= n) return;
+  const int r = lane & 15;
+  const int q = lane >> 4;
+  int jld[NT];
+  bool jok[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int jc = j0 + 16 * t + r;
+    jok[t] = jc < n;
+    jld[t] = jok[t] ? jc : j0;
+  }
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float a[4], b[NT][4], an[4], bn[NT][4];
+  auto load_frags = [&](int k, float (&fa)[4], float (&fb)[NT][4]) {
+    const int bc = colind[k];
+    const float* ab = val + (size_t)k * 256;
+    if constexpr (ROWDIR) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(ab + r * 16 + 4 * q);
+      fa[0] = x[0]; fa[1] = x[1]; fa[2] = x[2]; fa[3] = x[3];
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) fa[s] = ab[(4 * q + s) * 16 + r];
+    }
+    const size_t krow = (size_t)bc * 16 + 4 * q;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if constexpr (BROW) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) fb[t][s] = B[(krow + s) * ldb + jld[t]];
+      } else {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(B + (size_t)jld[t] * ldb + krow);
+        fb[t][0] = x[0]; fb[t][1] = x[1]; fb[t][2] = x[2]; fb[t][3] = x[3];
+      }
+    }
+  };
+
+  if (k0 < k1) load_frags(k0, a, b);
+  for (int k = k0; k < k1; ++k) {
+    if (k + 1 < k1) load_frags(k + 1, an, bn);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[t][s], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      a[s] = an[s];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[t][s] = bn[t][s];
+    }
+  }
+
+  const size_t row0 = (size_t)br * 16 + 4 * q;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (!jok[t]) continue;
+    const int jc = j0 + 16 * t + r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float* p = CROW ? C + (row0 + e) * ldc + jc : C + (size_t)jc * ldc + row0 + e;
+      *p = epi(acc[t][e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 16 fp16 MFMA (v_mfma_f32_16x16x32_f16): two blocks per instruction.
+// Lane quad q: q < 2 -> block b, k = 8q + e; q >= 2 -> block b+1, k = 8(q-2) + e.
+// ---------------------------------------------------------------------------
+template <bool ROWDIR, bool BROW, bool CROW>
+__global__ __launch_bounds__(256) void bsr16_f16_mfma_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
+    float beta, float* __restrict__ C, int ldc) {
+  constexpr int NT = 4;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int br = blockIdx.x;
+  const int j0 = (blockIdx.y * (blockDim.x >> 6) + wv) * (16 * NT);
+  if (j0 >= n) return;
+  const int r = lane & 15;
+  const int q = lane >> 4;
+  const int half = q >> 1;     // which block of the pair
+  const int kq = 8 * (q & 1);  // k offset inside the block
+  int jld[NT];
+  bool jok[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int jc = j0 + 16 * t + r;
+    jok[t] = jc < n;
+    jld[t] = jok[t] ? jc : j0;
+  }
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f16x8 a, b[NT], an, bn[NT];
+  // k: first block of the pair; kk = k + half is this lane's block.
+  auto load_frags = [&](int k, f16x8& fa, f16x8 (&fb)[NT]) {
+    const int kk = k + half;
+    const bool valid = kk < k1;
+    const int kl = valid ? kk : k;  // in-bounds block for the dummy half
+    const int bc = colind[kl];
+    const _Float16* ab = val + (size_t)kl * 256;
+    if constexpr (ROWDIR) {
+      fa = *reinterpret_cast<const f16x8*>(ab + r * 16 + kq);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) fa[e] = ab[(kq + e) * 16 + r];
+    }
+    if (!valid) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) fa[e] = (_Float16)0.f;
+    }
+    const size_t krow = (size_t)bc * 16 + kq;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if constexpr (BROW) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) fb[t][e] = B[(krow + e) * ldb + jld[t]];
+      } else {
+        fb[t] = *reinterpret_cast<const f16x8*>(B + (size_t)jld[t] * ldb + krow);
+      }
+    }
+  };
+
+  if (k0 < k1) load_frags(k0, a, b);
+  for (int k = k0; k < k1; k += 2) {
+    if (k + 2 < k1) load_frags(k + 2, an, bn);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[t], acc[t], 0, 0, 0);
+    a = an;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b[t] = bn[t];
+  }
+
+  const size_t row0 = (size_t)br * 16 + 4 * q;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (!jok[t]) continue;
+    const int jc = j0 + 16 * t + r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float* p = CROW ? C + (row0 + e) * ldc + jc : C + (size_t)jc * ldc + row0 + e;
+      *p = epi(acc[t][e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generic VALU kernel: any bs, any storage. Thread = one output element per
+// row step; block = (64 columns) x (4 row lanes), grid = (mb, ceil(n/64)).
+// Accumulation order: blocks of the block row in order, k = 0..bs-1 inside.
+// ---------------------------------------------------------------------------
+template <typename TV>
+__global__ __launch_bounds__(256) void bsr_generic_kernel(
+    int mb, int n, int bs, bool rowdir, const int* __restrict__ rowptr,
+    const int* __restrict__ colind, const TV* __restrict__ val, const TV* __restrict__ B, int ldb,
+    bool brow, float alpha, float beta, float* __restrict__ C, int ldc, bool crow) {
+  const int jj = threadIdx.x & 63;
+  const int rl = threadIdx.x >> 6;
+  const int br = blockIdx.x;
+  const int j = blockIdx.y * 64 + jj;
+  if (j >= n) return;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  const size_t bs2 = (size_t)bs * bs;
+  for (int rr = rl; rr < bs; rr += 4) {
+    float acc = 0.f;
+    for (int k = k0; k < k1; ++k) {
+      const size_t bc = (size_t)colind[k] * bs;
+      const TV* ab = val + (size_t)k * bs2;
+      for (int c = 0; c < bs; ++c) {
+        const float av = (float)(rowdir ? ab[rr * bs + c] : ab[c * bs + rr]);
+        const float bv = (float)(brow ? B[(bc + c) * ldb + j] : B[(size_t)j * ldb + bc + c]);
+        acc = __builtin_fmaf(av, bv, acc);
+      }
+    }
+    const size_t row = (size_t)br * bs + rr;
+    float* p = crow ? C + row * ldc + j : C + (size_t)j * ldc + row;
+    *p = epi(acc, alpha, beta, p);
+  }
+}
+
+#define SPMM_BSR_DISPATCH(KERNEL, GRID, BLOCK, STREAM, ROWD, BR, CR, ...)                   \
+  do {                                                                                    \
+    if (ROWD) {                                                                           \
+      if (BR) {                                                                           \
+        if (CR) hipLaunchKernelGGL((KERNEL<true, true, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);   \
+        else hipLaunchKernelGGL((KERNEL<true, true, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);     \
+      } else {                                                                            \
+        if (CR) hipLaunchKernelGGL((KERNEL<true, false, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
+        else hipLaunchKernelGGL((KERNEL<true, false, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);    \
+      }                                                                                   \
+    } else {                                                                              \
+      if (BR) {                                                                           \
+        if (CR) hipLaunchKernelGGL((KERNEL<false, true, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
+        else hipLaunchKernelGGL((KERNEL<false, true, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);    \
+      } else {                                                                            \
+        if (CR) hipLaunchKernelGGL((KERNEL<false, false, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__); \
+        else hipLaunchKernelGGL((KERNEL<false, false, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);   \
+      }                                                                                   \
+    }                                                                                     \
+  } while (0)
+
+bool aligned(const void* p, int bytes) { return reinterpret_cast<uintptr_t>(p) % bytes == 0; }
+
+}  // namespace
+
+namespace spmm {
+
+spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, int kb, int n,
+                               int nnzb, int bs, float alpha, const int* rowptr,
+                               const int* colind, const float* val, const float* B, int ldb,
+                               spmm_order_t orderB, float beta, float* C, int ldc,
+                               spmm_order_t orderC) {
+  (void)kb;
+  (void)nnzb;
+  if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  const bool rowd = dir == SPMM_DIRECTION_ROW;
+  const bool brow = orderB == SPMM_ORDER_ROW;
+  const bool crow = orderC == SPMM_ORDER_ROW;
+  const bool vec_ok = aligned(val, 16) && (brow || (aligned(B, 16) && ldb % 4 == 0));
+  const int slot = timing_begin(ctx);
+  if (bs == 32 && vec_ok) {
+    const int waves = n <= 32 ? 1 : (n <= 64 ? 2 : 4);
+    dim3 grid(mb, (n + 32 * waves - 1) / (32 * waves));
+    SPMM_BSR_DISPATCH(bsr32_f32_mfma_kernel, grid, dim3(64 * waves), ctx->stream, rowd, brow, crow,
+                      mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+  } else if (bs == 16 && vec_ok) {
+    const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
+    dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
+    SPMM_BSR_DISPATCH(bsr16_f32_mfma_kernel, grid, dim3(64 * waves), ctx->stream, rowd, brow, crow,
+                      mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+  } else {
+    dim3 grid(mb, (n + 63) / 64);
+    hipLaunchKernelGGL(bsr_generic_kernel<float>, grid, dim3(256), 0, ctx->stream, mb, n, bs,
+                       rowd, rowptr, colind, val, B, ldb, brow, alpha, beta, C, ldc, crow);
+  }
+  timing_end(ctx, slot);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, int kb, int n,
+                               int nnzb, int bs, float alpha, const int* rowptr,
+                               const int* colind, const uint16_t* val16, const uint16_t* B16,
+                               int ldb, spmm_order_t orderB, float beta, float* C, int ldc,
+                               spmm_order_t orderC) {
+  (void)kb;
+  (void)nnzb;
+  if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  const _Float16* val = reinterpret_cast<const _Float16*>(val16);
+  const _Float16* B = reinterpret_cast<const _Float16*>(B16);
+  const bool rowd = dir == SPMM_DIRECTION_ROW;
+  const bool brow = orderB == SPMM_ORDER_ROW;
+  const bool crow = orderC == SPMM_ORDER_ROW;
+  const bool vec_ok = aligned(val, 16) && (brow || (aligned(B, 16) && ldb % 8 == 0));
+  const int slot = timing_begin(ctx);
+  if (bs == 16 && vec_ok) {
+    const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
+    dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
+    SPMM_BSR_DISPATCH(bsr16_f16_mfma_kernel, grid, dim3(64 * waves), ctx->stream, rowd, brow, crow,
+                      mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+  } else {
+    dim3 grid(mb, (n + 63) / 64);
+    hipLaunchKernelGGL(bsr_generic_kernel<_Float16>, grid, dim3(256), 0, ctx->stream, mb, n, bs,
+                       rowd, rowptr, colind, val, B, ldb, brow, alpha, beta, C, ldc, crow);
+  }
+  timing_end(ctx, slot);
+  return from_hip(hipGetLastError());
+}
+
+}  // namespace spmm

@@ -1,0 +1,87 @@
+// context.hpp — internal state behind spmm_handle_t / spmm_mat_descr_t.
+//
+// The reference has no handle of its own: gespmm_csrmm<T> launches on the
+// legacy default stream (gespmm_csrmm.h:401-405) and the cuSPARSE paths use a
+// cusparseHandle_t created in each driver (run_csrmm.cu:104). Here the handle
+// carries the stream, a lazily grown device workspace (merge-path carries and
+// column-major staging), the device's CU count for grid sizing, and an
+// optional ring of hipEvent pairs used to time the dominant kernel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+#include "spmm_hip.h"
+
+struct spmm_mat_descr {
+  spmm_matrix_type_t type = SPMM_MATRIX_TYPE_GENERAL;
+  spmm_index_base_t base = SPMM_INDEX_BASE_ZERO;
+};
+
+struct spmm_context {
+  hipStream_t stream = nullptr;
+  int device = 0;
+  int num_cus = 256;
+  int csr_waves_per_cu = 0;  // 0 = default
+
+  // Device workspace (grown, never shrunk; freed in spmm_destroy).
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+
+  // Kernel timing ring.
+  bool timing = false;
+  std::vector<hipEvent_t> ev_start, ev_stop;
+  size_t ev_used = 0;
+
+  std::mutex mu;  // serialises workspace growth for the shared default handle
+};
+
+namespace spmm {
+
+// Grow the handle workspace to at least `bytes`. Not graph-capture safe on
+// the first (growing) call; steady-state calls never allocate.
+spmm_status_t ensure_workspace(spmm_context* ctx, size_t bytes);
+
+// Record a start/stop event pair around the next main-kernel launch when
+// timing is on. Returns the pair index or -1.
+int timing_begin(spmm_context* ctx);
+void timing_end(spmm_context* ctx, int slot);
+
+// Process-wide default handle for the handle-less gespmm entry point.
+spmm_context* default_context();
+
+inline spmm_status_t from_hip(hipError_t e) {
+  if (e == hipSuccess) return SPMM_STATUS_SUCCESS;
+  if (e == hipErrorOutOfMemory) return SPMM_STATUS_ALLOC_FAILED;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return SPMM_STATUS_ARCH_MISMATCH;
+  return SPMM_STATUS_EXECUTION_FAILED;
+}
+
+// Kernel launchers (csr_kernels.hip / bsr_kernels.hip). Pointers are device
+// pointers; all shape checks have been done by the API layer.
+spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* rowptr,
+                                    const int* colind, const float* val, int base,
+                                    const float* B, int ldb, float alpha, float beta, float* C,
+                                    int ldc, float* carry_val, int* carry_row, int nnz_hint);
+size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n, int* nwaves_out);
+
+spmm_status_t launch_transpose(spmm_context* ctx, int rows, int cols, const float* src,
+                               int ld_src, float* dst, int ld_dst, float beta);
+
+spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, int kb, int n,
+                               int nnzb, int bs, float alpha, const int* rowptr,
+                               const int* colind, const float* val, const float* B, int ldb,
+                               spmm_order_t orderB, float beta, float* C, int ldc,
+                               spmm_order_t orderC);
+
+spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, int kb, int n,
+                               int nnzb, int bs, float alpha, const int* rowptr,
+                               const int* colind, const uint16_t* val, const uint16_t* B,
+                               int ldb, spmm_order_t orderB, float beta, float* C, int ldc,
+                               spmm_order_t orderC);
+
+}  // namespace spmm

@@ -1,0 +1,441 @@
+// csr_kernels.hip — Path A: CSR x dense on gfx950 (MI355X).
+//
+// Replaces the GE-SpMM kernels of the reference (gespmm_csrmm.h:95-166,
+// spmm_test2, dispatched by gespmm_csrmm -> spmmWrapper(2, 8, ...) at
+// gespmm_csrmm.h:422-426) and the legacy cusparseScsrmm/csrmm2 calls.
+//
+// Design:
+//  * Merge-path work split. The reference gives each CSR row to one warp
+//    (gespmm_csrmm.h:105), so a power-law hub row (ogbn-products max degree
+//    ~17k) serialises on one warp while short rows idle lanes. Here the
+//    (rows + nnz) merge path is cut into equal pieces, one per wave64; each
+//    wave finds its start/end coordinates with a 32-ary cooperative search
+//    on rowptr (5 dependent loads for 2.4M rows), walks its nnz range and
+//    emits every row that ends inside it. The one row a wave leaves
+//    unfinished becomes a "carry" that a tiny fix-up kernel adds in wave
+//    order (deterministic, no atomics).
+//  * One nnz per wave-instruction. All 64 lanes gather the same B row: lane l
+//    owns columns [VEC*l, VEC*l+VEC) of a 64*VEC-wide column tile, so a
+//    gather is one coalesced 256/512/1024-byte global_load_dword{,x2,x4}
+//    whose row base is wave-uniform (v_readlane -> SGPR, saddr addressing).
+//    colind/val are read 64 at a time with one coalesced vector load each
+//    and broadcast with v_readlane; no LDS is needed because nothing
+//    gathered is reused inside the wave (a LDS round trip would be pure
+//    overhead, cdna_hip_programming.md App. B "GEMV" row).
+//  * Latency hiding: B rows are software-pipelined in groups of U=8 nnz,
+//    loads for group g+1 issued before group g is consumed, so up to 16 row
+//    gathers are in flight per wave across row boundaries.
+//  * Each output element is a sequential fp32 FMA chain in CSR order, like
+//    the reference's `acc += val * B[...]` (gespmm_csrmm.h:124-129, contracted
+//    to FMA by nvcc): rows that a single wave finishes are bit-identical to
+//    the sequential oracle; rows split across waves differ only by the
+//    association of the carry sum.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "context.hpp"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerWG = 4;
+constexpr int kWG = kWave * kWavesPerWG;
+constexpr int kU = 8;            // nnz per pipeline group
+constexpr int kR = 4;            // colind/val registers per lane per chunk
+constexpr int kChunk = kWave * kR / kU;  // groups per chunk (32)
+constexpr int kMinItemsPerWave = 512;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int VEC> struct Vec;
+template <> struct Vec<1> { typedef float T; };
+template <> struct Vec<2> { typedef f32x2 T; };
+template <> struct Vec<4> { typedef f32x4 T; };
+
+template <int VEC>
+__device__ __forceinline__ typename Vec<VEC>::T vload(const float* p) {
+  return *reinterpret_cast<const typename Vec<VEC>::T*>(p);
+}
+template <int VEC>
+__device__ __forceinline__ void vstore(float* p, typename Vec<VEC>::T v) {
+  *reinterpret_cast<typename Vec<VEC>::T*>(p) = v;
+}
+template <int VEC>
+__device__ __forceinline__ float vget(const typename Vec<VEC>::T& v, int c) {
+  if constexpr (VEC == 1) return v; else return v[c];
+}
+template <int VEC>
+__device__ __forceinline__ void vset(typename Vec<VEC>::T& v, int c, float x) {
+  if constexpr (VEC == 1) v = x; else v[c] = x;
+}
+
+// Waits for a pending load into `x` right here. Used on the (rare) reload
+// paths so that the common path that merges with them after a branch does
+// not inherit a conservative vmcnt(0) for the reloaded register.
+template <typename T>
+__device__ __forceinline__ void settle(T& x) {
+  asm volatile("" : "+v"(x));
+}
+
+__device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float rdlanef(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Merge-path search for two diagonals at once: lanes 0-31 search d0, lanes
+// 32-63 search d1. A[i] = rowptr[i+1]-rp0 (row-end offsets), B[j] = j.
+// Returns (per lane) the number of row ends consumed before the diagonal.
+__device__ __forceinline__ int merge_search2(const int* __restrict__ rowptr, int rp0, int m,
+                                             long long nnz, long long d0, long long d1,
+                                             int lane) {
+  const long long d = lane < 32 ? d0 : d1;
+  int lo = (int)max(0LL, d - nnz);
+  int hi = (int)min(d, (long long)m);
+  const int t = lane & 31;
+  while (true) {
+    const int len = hi - lo;
+    const bool active = len > 0;
+    if (!__any(active)) break;
+    const int p = lo + (int)(((long long)(t + 1) * len) / 33);
+    bool pred = false;
+    if (active) {
+      const long long a = (long long)rowptr[p + 1] - rp0;
+      pred = a <= d - p - 1;
+    }
+    const unsigned long long mask = __ballot(pred);
+    const unsigned half = lane < 32 ? (unsigned)mask : (unsigned)(mask >> 32);
+    const int c = __popc(half);
+    if (active) {
+      const int nlo = (c == 0) ? lo : lo + (int)(((long long)c * len) / 33) + 1;
+      const int nhi = (c == 32) ? hi : lo + (int)(((long long)(c + 1) * len) / 33);
+      lo = nlo;
+      hi = nhi;
+    }
+  }
+  return lo;
+}
+
+template <int VEC>
+__global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
+    int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, int base, const float* __restrict__ B, int ldb, float alpha,
+    float beta, float* __restrict__ C, int ldc, float* __restrict__ carry_val,
+    int* __restrict__ carry_row, int nwaves) {
+  typedef typename Vec<VEC>::T vec;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
+  if (w >= nwaves) return;
+  const int ct = blockIdx.y;
+  const int tile0 = ct * (kWave * VEC);
+  const int col0 = tile0 + lane * VEC;
+  const bool col_ok = col0 < n;
+  const int col_ld = col_ok ? col0 : tile0;  // safe in-bounds column for masked lanes
+
+  const int rp0 = rowptr[0];
+  const long long nnz = (long long)rowptr[m] - rp0;
+  const long long total = (long long)m + nnz;
+  const long long per = (total + nwaves - 1) / nwaves;
+  const long long d0 = min((long long)w * per, total);
+  const long long d1 = min(d0 + per, total);
+
+  const int ires = merge_search2(rowptr, rp0, m, nnz, d0, d1, lane);
+  const int i0 = rdlane(ires, 0);
+  const int i1 = rdlane(ires, 32);
+  const int j0 = (int)(d0 - i0);
+  const int j1 = (int)(d1 - i1);
+  const int aoff = rp0 - base;  // array offset of relative nnz 0
+  const int J = j1 - j0;
+  const int slot = ct * nwaves + w;
+
+  // Row ends: lane l holds raw rowptr[rbase+1+l] for 64 rows, reloaded in
+  // place when exhausted (one pipeline drain per 64 rows). The load is free
+  // of arithmetic (clamped instead of masked, rp0 subtracted on the scalar)
+  // so nothing waits for it before its first v_readlane.
+  auto load_rowends = [&](int rb) -> int { return rowptr[min(rb + 1 + lane, m)]; };
+  int rbase = i0;
+  int rev = load_rowends(rbase);
+  int i = i0;
+  int cur_end = (i < i1) ? rdlane(rev, 0) - rp0 : INT_MAX;
+
+  float acc[VEC];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
+
+  const float* Bb = B - (size_t)base * ldb;  // row 0 of B for 1-based colind
+  float* Ct = C + col0;
+
+  auto emit = [&](int row) {
+    float* cp = Ct + (size_t)row * ldc;
+    vec out;
+    if (beta == 0.f) {
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) vset<VEC>(out, c, alpha * acc[c]);
+    } else {
+      const vec old = vload<VEC>(col_ok ? cp : Ct);
+#pragma unroll
+      for (int c = 0; c < VEC; ++c)
+        vset<VEC>(out, c, __builtin_fmaf(beta, vget<VEC>(old, c), alpha * acc[c]));
+    }
+    if (col_ok) vstore<VEC>(cp, out);
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
+  };
+  auto advance_row = [&]() {
+    ++i;
+    if (i - rbase == kWave) {
+      rbase += kWave;
+      rev = load_rowends(rbase);
+      settle(rev);
+    }
+    cur_end = (i < i1) ? rdlane(rev, i - rbase) - rp0 : INT_MAX;
+  };
+
+  // nnz are processed in groups of kU aligned to absolute array positions:
+  // group g covers array indices [gs + kU*g, gs + kU*(g+1)); indices outside
+  // the wave's range [A0, A1) are loaded (harmlessly) but never consumed.
+  // colind/val of a chunk of kChunk groups (kChunk*kU = 256 nnz) sit in kR
+  // registers per lane, lane l / register r <-> index chunk_base + kR*l + r,
+  // so the register of nnz u of a group is the compile-time u % kR. They are
+  // reloaded in place every kChunk groups (one pipeline drain per 256 nnz).
+  const int A0 = aoff + j0, A1 = aoff + j1;
+  const int gs = A0 & ~(kU - 1);
+  const int G = J > 0 ? (A1 - gs + kU - 1) / kU : 0;
+  if (G > 0) {
+    int colv[kR];
+    float valv[kR];
+    auto load_chunk = [&](int c) {
+      const int cb = gs + c * (kChunk * kU) + kR * lane;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int idx = min(cb + r, A1 - 1);
+        colv[r] = colind[idx];
+        valv[r] = val[idx];
+      }
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        settle(colv[r]);
+        settle(valv[r]);
+      }
+    };
+    float b0[kU][VEC], b1[kU][VEC];
+    float v0[kU], v1[kU];  // values of the groups in flight (wave-uniform)
+
+    auto issue = [&](float (&dst)[kU][VEC], float (&vdst)[kU], int g) {
+      if ((g & (kChunk - 1)) == 0) load_chunk(g / kChunk);
+      const int lb = (g & (kChunk - 1)) * (kU / kR);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int l = lb + u / kR;
+        vdst[u] = rdlanef(valv[u % kR], l);
+        // Wave-uniform row base (SGPRs) + per-lane column offset.
+        const float* rowp = Bb + (size_t)rdlane(colv[u % kR], l) * ldb;
+        const vec x = vload<VEC>(rowp + col_ld);
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) dst[u][c] = vget<VEC>(x, c);
+      }
+    };
+    auto consume = [&](float (&src)[kU][VEC], const float (&vsrc)[kU], int g) {
+      const int ag = gs + g * kU;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int a = ag + u;
+        if (a >= A0 && a < A1) {
+          const int j = a - aoff;
+          while (cur_end <= j) {  // cur_end is INT_MAX once i reaches i1
+            emit(i);
+            advance_row();
+          }
+#pragma unroll
+          for (int c = 0; c < VEC; ++c) acc[c] = __builtin_fmaf(vsrc[u], src[u][c], acc[c]);
+        }
+      }
+    };
+
+    issue(b0, v0, 0);
+    for (int g = 0; g < G; g += 2) {
+      if (g + 1 < G) issue(b1, v1, g + 1);
+      consume(b0, v0, g);
+      if (g + 1 < G) {
+        if (g + 2 < G) issue(b0, v0, g + 2);
+        consume(b1, v1, g + 1);
+      }
+    }
+  }
+  // Rows whose end marker lies at or before j1 but after the last nnz.
+  while (i < i1) {
+    emit(i);
+    advance_row();
+  }
+  // Carry: the partial of row i1 accumulated over [max(j0, start(i1)), j1).
+  bool has_carry = false;
+  if (i1 < m && J > 0) {
+    const int rs1 = rowptr[i1] - rp0;
+    has_carry = j1 > rs1;
+  }
+  if (has_carry) {
+    if (lane == 0) carry_row[slot] = i1;
+    vec out;
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) vset<VEC>(out, c, acc[c]);
+    vstore<VEC>(carry_val + (size_t)slot * (kWave * VEC) + lane * VEC, out);
+  } else if (lane == 0) {
+    carry_row[slot] = -1;
+  }
+}
+
+// Adds the carries of rows split across waves, summed in wave order. One
+// wave per carry slot; only the first slot of a run of equal rows works.
+template <int VEC>
+__global__ __launch_bounds__(kWG) void csr_carry_fixup_kernel(int n, float alpha,
+                                                              float* __restrict__ C, int ldc,
+                                                              const float* __restrict__ carry_val,
+                                                              const int* __restrict__ carry_row,
+                                                              int nwaves) {
+  typedef typename Vec<VEC>::T vec;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
+  if (w >= nwaves) return;
+  const int ct = blockIdx.y;
+  const int base_slot = ct * nwaves;
+  const int r = carry_row[base_slot + w];
+  if (r < 0) return;
+  if (w > 0 && carry_row[base_slot + w - 1] == r) return;
+  const int col0 = ct * (kWave * VEC) + lane * VEC;
+  vec sum = vload<VEC>(carry_val + (size_t)(base_slot + w) * (kWave * VEC) + lane * VEC);
+  for (int w2 = w + 1; w2 < nwaves && carry_row[base_slot + w2] == r; ++w2) {
+    const vec x = vload<VEC>(carry_val + (size_t)(base_slot + w2) * (kWave * VEC) + lane * VEC);
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) vset<VEC>(sum, c, vget<VEC>(sum, c) + vget<VEC>(x, c));
+  }
+  if (col0 < n) {
+    float* cp = C + (size_t)r * ldc + col0;
+    vec cur = vload<VEC>(cp);
+#pragma unroll
+    for (int c = 0; c < VEC; ++c)
+      vset<VEC>(cur, c, __builtin_fmaf(alpha, vget<VEC>(sum, c), vget<VEC>(cur, c)));
+    vstore<VEC>(cp, cur);
+  }
+}
+
+// dst (cols x rows, ld_dst) = transpose(src (rows x cols, ld_src)) [+ beta*dst]
+__global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols,
+                                                        const float* __restrict__ src,
+                                                        int ld_src, float* __restrict__ dst,
+                                                        int ld_dst, float beta) {
+  __shared__ float tile[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int r = r0 + ty + k, c = c0 + tx;
+    if (r < rows && c < cols) tile[ty + k][tx] = src[(size_t)r * ld_src + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int c = c0 + ty + k, r = r0 + tx;
+    if (r < rows && c < cols) {
+      float* p = dst + (size_t)c * ld_dst + r;
+      const float x = tile[tx][ty + k];
+      *p = (beta == 0.f) ? x : __builtin_fmaf(beta, *p, x);
+    }
+  }
+}
+
+int pick_vec(int n, const float* B, int ldb, const float* C, int ldc) {
+  auto aligned = [](const void* p, int bytes) {
+    return (reinterpret_cast<uintptr_t>(p) % bytes) == 0;
+  };
+  if (n > 128 && n % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 && aligned(B, 16) && aligned(C, 16))
+    return 4;
+  if (n > 64 && n % 2 == 0 && ldb % 2 == 0 && ldc % 2 == 0 && aligned(B, 8) && aligned(C, 8))
+    return 2;
+  return 1;
+}
+
+// Waves in the merge-path grid: enough that each gets >= kMinItemsPerWave
+// items, capped at the resident target (waves_per_cu x CUs) so the whole
+// grid runs in one round. nnz < 0 (unknown on the host) sizes from m.
+int csr_nwaves(spmm_context* ctx, int m, long long nnz) {
+  const int wpc = ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu : 16;
+  const long long cap = (long long)ctx->num_cus * wpc;
+  const long long total = nnz >= 0 ? (long long)m + nnz : (long long)m * 32;
+  long long nw = (total + kMinItemsPerWave - 1) / kMinItemsPerWave;
+  if (nw < 1) nw = 1;
+  if (nw > cap) nw = cap;
+  return (int)nw;
+}
+
+}  // namespace
+
+namespace spmm {
+
+size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n, int* nwaves_out) {
+  // The grid does not depend on nnz beyond the cap: size it for the cap.
+  const int wpc = ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu : 16;
+  const int nw = ctx->num_cus * wpc;
+  (void)m;
+  const int ntiles_max = (n + 63) / 64;  // VEC = 1 worst case
+  if (nwaves_out) *nwaves_out = nw;
+  const size_t slots = (size_t)nw * ntiles_max;
+  return slots * 64 * sizeof(float) + slots * sizeof(int) + 256;
+}
+
+spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* rowptr,
+                                    const int* colind, const float* val, int base,
+                                    const float* B, int ldb, float alpha, float beta, float* C,
+                                    int ldc, float* carry_val, int* carry_row, int nnz_hint) {
+  if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  const int vec = pick_vec(n, B, ldb, C, ldc);
+  const int tile = kWave * vec;
+  const int ntiles = (n + tile - 1) / tile;
+  const int nw = csr_nwaves(ctx, m, nnz_hint);
+  dim3 grid((nw + kWavesPerWG - 1) / kWavesPerWG, ntiles);
+  dim3 block(kWG);
+  const int slot = timing_begin(ctx);
+  switch (vec) {
+    case 4:
+      hipLaunchKernelGGL(csr_mergepath_kernel<4>, grid, block, 0, ctx->stream, m, n, rowptr,
+                         colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw);
+      break;
+    case 2:
+      hipLaunchKernelGGL(csr_mergepath_kernel<2>, grid, block, 0, ctx->stream, m, n, rowptr,
+                         colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw);
+      break;
+    default:
+      hipLaunchKernelGGL(csr_mergepath_kernel<1>, grid, block, 0, ctx->stream, m, n, rowptr,
+                         colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw);
+      break;
+  }
+  timing_end(ctx, slot);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return from_hip(e);
+  switch (vec) {
+    case 4:
+      hipLaunchKernelGGL(csr_carry_fixup_kernel<4>, grid, block, 0, ctx->stream, n, alpha, C, ldc,
+                         carry_val, carry_row, nw);
+      break;
+    case 2:
+      hipLaunchKernelGGL(csr_carry_fixup_kernel<2>, grid, block, 0, ctx->stream, n, alpha, C, ldc,
+                         carry_val, carry_row, nw);
+      break;
+    default:
+      hipLaunchKernelGGL(csr_carry_fixup_kernel<1>, grid, block, 0, ctx->stream, n, alpha, C, ldc,
+                         carry_val, carry_row, nw);
+      break;
+  }
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_transpose(spmm_context* ctx, int rows, int cols, const float* src,
+                               int ld_src, float* dst, int ld_dst, float beta) {
+  if (rows == 0 || cols == 0) return SPMM_STATUS_SUCCESS;
+  dim3 grid((cols + 31) / 32, (rows + 31) / 32);
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, ctx->stream, rows, cols, src, ld_src,
+                     dst, ld_dst, beta);
+  return from_hip(hipGetLastError());
+}
+
+}  // namespace spmm

@@ -1,0 +1,187 @@
+// prep.cpp — host-side preprocessing: csr2bsr, bsr2csr, nnzb, row partition.
+//
+// north_star keeps format conversion as CPU-side preprocessing; these replace
+// the GPU cuSPARSE conversions of the reference drivers:
+//   cusparseXcsr2bsrNnz + cusparseScsr2bsr   run_bsrmm.cu:116-142, csr2bsr.cu:176-192
+//   cusparseSbsr2csr                         bsr2csr.cu:177-188
+//   calculateNnzb                            utility.cc:47-69
+// and the CPU block extraction of divide_matrix (divide.cu:52-127) at
+// density -> 0. Index arrays are bit-exact with the oracle (tests/test_prep.py).
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "spmm_hip.h"
+
+namespace {
+
+inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+// Collects the sorted distinct block columns of block row `br`.
+// `mark` has nb entries, all -1 on entry and on exit.
+// Returns false on a column index outside [0, nb*bs).
+bool block_cols(int br, int bs, int m, const int* rowptr, const int* colind, int base,
+                std::vector<int>& mark, std::vector<int>& out) {
+  out.clear();
+  const int r0 = br * bs, r1 = std::min(m, r0 + bs);
+  const int nb = (int)mark.size();
+  for (int r = r0; r < r1; ++r) {
+    for (int j = rowptr[r] - base; j < rowptr[r + 1] - base; ++j) {
+      const int c = colind[j] - base;
+      if (c < 0 || c / bs >= nb) {
+        for (int bc : out) mark[bc] = -1;
+        return false;
+      }
+      const int bc = c / bs;
+      if (mark[bc] < 0) {
+        mark[bc] = 0;
+        out.push_back(bc);
+      }
+    }
+  }
+  for (int bc : out) mark[bc] = -1;
+  std::sort(out.begin(), out.end());
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+spmm_status_t spmm_xcsr2bsr_nnz(spmm_direction_t dir, int m, int n, const int* csrRowPtr,
+                                const int* csrColInd, int blockDim, int* bsrRowPtr,
+                                int* nnzbTotal) {
+  if (dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) return SPMM_STATUS_INVALID_VALUE;
+  if (m < 0 || n < 0 || blockDim <= 0) return SPMM_STATUS_INVALID_VALUE;
+  if (!csrRowPtr || !bsrRowPtr || !nnzbTotal) return SPMM_STATUS_INVALID_VALUE;
+  const int mb = ceil_div(m, blockDim), nb = ceil_div(n, blockDim);
+  if (m > 0 && csrRowPtr[m] - csrRowPtr[0] > 0 && !csrColInd) return SPMM_STATUS_INVALID_VALUE;
+  const int base = m > 0 ? csrRowPtr[0] : 0;
+  std::vector<int> mark(std::max(nb, 1), -1), cols;
+  bsrRowPtr[0] = 0;
+  long long acc = 0;
+  for (int br = 0; br < mb; ++br) {
+    if (!block_cols(br, blockDim, m, csrRowPtr, csrColInd, base, mark, cols))
+      return SPMM_STATUS_INVALID_VALUE;
+    acc += (long long)cols.size();
+    if (acc > INT32_MAX) return SPMM_STATUS_INVALID_VALUE;
+    bsrRowPtr[br + 1] = (int)acc;
+  }
+  *nnzbTotal = (int)acc;
+  return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t spmm_scsr2bsr(spmm_direction_t dir, int m, int n, const float* csrVal,
+                            const int* csrRowPtr, const int* csrColInd, int blockDim,
+                            const int* bsrRowPtr, float* bsrVal, int* bsrColInd) {
+  if (dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) return SPMM_STATUS_INVALID_VALUE;
+  if (m < 0 || n < 0 || blockDim <= 0) return SPMM_STATUS_INVALID_VALUE;
+  if (!csrRowPtr || !bsrRowPtr) return SPMM_STATUS_INVALID_VALUE;
+  const int bs = blockDim;
+  const int mb = ceil_div(m, bs), nb = ceil_div(n, bs);
+  const int nnzb = bsrRowPtr[mb];
+  if (nnzb > 0 && (!bsrVal || !bsrColInd || !csrColInd || !csrVal))
+    return SPMM_STATUS_INVALID_VALUE;
+  const int base = m > 0 ? csrRowPtr[0] : 0;
+  const size_t bs2 = (size_t)bs * bs;
+  std::vector<int> mark(std::max(nb, 1), -1), cols;
+  for (int br = 0; br < mb; ++br) {
+    if (!block_cols(br, bs, m, csrRowPtr, csrColInd, base, mark, cols))
+      return SPMM_STATUS_INVALID_VALUE;
+    const int k0 = bsrRowPtr[br];
+    if (bsrRowPtr[br + 1] - k0 != (int)cols.size()) return SPMM_STATUS_INVALID_VALUE;
+    for (size_t t = 0; t < cols.size(); ++t) {
+      bsrColInd[k0 + t] = cols[t];
+      mark[cols[t]] = k0 + (int)t;
+    }
+    std::memset(bsrVal + (size_t)k0 * bs2, 0, cols.size() * bs2 * sizeof(float));
+    const int r0 = br * bs, r1 = std::min(m, r0 + bs);
+    for (int r = r0; r < r1; ++r) {
+      const int rr = r - r0;
+      for (int j = csrRowPtr[r] - base; j < csrRowPtr[r + 1] - base; ++j) {
+        const int c = csrColInd[j] - base;
+        const int k = mark[c / bs], cc = c % bs;
+        const size_t off = (size_t)k * bs2 + (dir == SPMM_DIRECTION_ROW
+                                                  ? (size_t)rr * bs + cc
+                                                  : (size_t)cc * bs + rr);
+        bsrVal[off] += csrVal[j];
+      }
+    }
+    for (int bc : cols) mark[bc] = -1;
+  }
+  return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t spmm_sbsr2csr(spmm_direction_t dir, int mb, int nb, const float* bsrVal,
+                            const int* bsrRowPtr, const int* bsrColInd, int blockDim,
+                            float* csrVal, int* csrRowPtr, int* csrColInd) {
+  if (dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) return SPMM_STATUS_INVALID_VALUE;
+  if (mb < 0 || nb < 0 || blockDim <= 0) return SPMM_STATUS_INVALID_VALUE;
+  if (!bsrRowPtr || !csrRowPtr) return SPMM_STATUS_INVALID_VALUE;
+  const int bs = blockDim;
+  const size_t bs2 = (size_t)bs * bs;
+  const int base = mb > 0 ? bsrRowPtr[0] : 0;
+  if (mb > 0 && bsrRowPtr[mb] - base > 0 && (!bsrVal || !bsrColInd || !csrVal || !csrColInd))
+    return SPMM_STATUS_INVALID_VALUE;
+  long long pos = 0;
+  csrRowPtr[0] = 0;
+  for (int br = 0; br < mb; ++br) {
+    const int k0 = bsrRowPtr[br] - base, k1 = bsrRowPtr[br + 1] - base;
+    for (int rr = 0; rr < bs; ++rr) {
+      for (int k = k0; k < k1; ++k) {
+        const long long cb = (long long)(bsrColInd[k] - base) * bs;
+        const float* blk = bsrVal + (size_t)k * bs2;
+        for (int c = 0; c < bs; ++c) {
+          csrColInd[pos] = (int)(cb + c);
+          csrVal[pos] = dir == SPMM_DIRECTION_ROW ? blk[(size_t)rr * bs + c]
+                                                  : blk[(size_t)c * bs + rr];
+          ++pos;
+        }
+      }
+      if (pos > INT32_MAX) return SPMM_STATUS_INVALID_VALUE;
+      csrRowPtr[(size_t)br * bs + rr + 1] = (int)pos;
+    }
+  }
+  (void)nb;
+  return SPMM_STATUS_SUCCESS;
+}
+
+int64_t spmm_calculate_nnzb(int n, const int* csrRowPtr, const int* csrColInd, int blockDim) {
+  if (n < 0 || blockDim <= 0 || !csrRowPtr) return -1;
+  const int mb = ceil_div(n, blockDim);
+  const int base = n > 0 ? csrRowPtr[0] : 0;
+  int maxc = 0;
+  for (int j = 0; j < csrRowPtr[n] - base; ++j) maxc = std::max(maxc, csrColInd[j] - base);
+  const int nb = std::max(ceil_div(n, blockDim), maxc / blockDim + 1);
+  std::vector<int> mark(std::max(nb, 1), -1), cols;
+  int64_t total = 0;
+  for (int br = 0; br < mb; ++br) {
+    if (!block_cols(br, blockDim, n, csrRowPtr, csrColInd, base, mark, cols)) return -1;
+    total += (int64_t)cols.size();
+  }
+  return total;
+}
+
+spmm_status_t spmm_csr_partition_rows(int m, const int* csrRowPtr, int nparts, int* bounds) {
+  if (m < 0 || nparts <= 0 || !csrRowPtr || !bounds) return SPMM_STATUS_INVALID_VALUE;
+  // Cost of the prefix [0, i) = nnz before row i + i (one unit per row for
+  // its output write), monotone in i: cut at equal cost quantiles.
+  const long long base = csrRowPtr[0];
+  const long long total = (long long)csrRowPtr[m] - base + m;
+  bounds[0] = 0;
+  for (int p = 1; p < nparts; ++p) {
+    const long long target = (total * p) / nparts;
+    int lo = bounds[p - 1], hi = m;
+    while (lo < hi) {  // first i with cost(i) >= target
+      const int mid = lo + (hi - lo) / 2;
+      const long long cost = (long long)csrRowPtr[mid] - base + mid;
+      if (cost < target) lo = mid + 1; else hi = mid;
+    }
+    bounds[p] = lo;
+  }
+  bounds[nparts] = m;
+  return SPMM_STATUS_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,168 @@
+"""Device SpMM entry points over torch tensors (HIP memory + streams only).
+
+torch is plumbing here: it owns the device buffers and the stream; every
+FLOP runs in the hand-written gfx950 kernels of libspmm_hip.so, called
+through the C ABI. The functions mirror the reference's operator interfaces:
+
+  gespmm_csrmm(...)   gespmm_csrmm<float>(A_nrows, B_ncols, rowPtr, colInd, val, B, C)
+                      (gespmm_csrmm.h:422-426): C = A*B, row-major, overwritten
+  csrmm(...)          cusparseScsrmm / csrmm2 with explicit storage orders
+  bsrmm(...)          cusparseSbsrmm / rocsparse_bsrmm_template<float>
+  bsrmm_f16(...)      fp16 A/B, fp32 accumulate (config 5)
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_float, c_int, c_void_p
+
+import torch
+
+from ._lib import (DIRECTION_ROW, ORDER_COL, ORDER_ROW, SpmmError, check, lib)
+
+
+def _ptr(t: torch.Tensor | None) -> c_void_p:
+    return c_void_p(t.data_ptr() if t is not None and t.numel() else 0)
+
+
+def _need(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must live on a HIP device (there is no CPU path)")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+class Handle:
+    """spmm_handle_t bound to a torch stream (default: the current stream)."""
+
+    def __init__(self, stream: torch.cuda.Stream | None = None):
+        h = c_void_p()
+        check(lib().spmm_create(byref(h)), "spmm_create")
+        self._h = h
+        self.set_stream(stream if stream is not None else torch.cuda.current_stream())
+
+    @property
+    def raw(self) -> c_void_p:
+        return self._h
+
+    def set_stream(self, stream: torch.cuda.Stream) -> None:
+        self.stream = stream
+        check(lib().spmm_set_stream(self._h, c_void_p(stream.cuda_stream)), "spmm_set_stream")
+
+    def set_timing(self, enable: bool) -> None:
+        check(lib().spmm_set_kernel_timing(self._h, int(enable)), "spmm_set_kernel_timing")
+
+    def kernel_times(self, max_count: int = 1 << 16) -> list[float]:
+        """Durations (ms) of every main-kernel launch since the last call,
+        measured with hipEvents on the handle's stream."""
+        buf = (c_float * max_count)()
+        cnt = c_int(0)
+        check(lib().spmm_get_kernel_times(self._h, buf, max_count, byref(cnt)),
+              "spmm_get_kernel_times")
+        return list(buf[: cnt.value])
+
+    def set_csr_waves_per_cu(self, w: int) -> None:
+        check(lib().spmm_set_csr_waves_per_cu(self._h, w), "spmm_set_csr_waves_per_cu")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().spmm_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_handles: dict[int, Handle] = {}
+
+
+def default_handle() -> Handle:
+    dev = torch.cuda.current_device()
+    h = _handles.get(dev)
+    if h is None:
+        h = _handles[dev] = Handle()
+    h.set_stream(torch.cuda.current_stream())
+    return h
+
+
+def gespmm_csrmm(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor,
+                 B: torch.Tensor, C: torch.Tensor | None = None) -> torch.Tensor:
+    """Drop-in for gespmm_csrmm<float> (gespmm_csrmm.h:422-426).
+    rowptr int32[m+1], colind int32[nnz], val f32[nnz], B f32[k, K] row-major;
+    returns C f32[m, K] (overwritten, no alpha/beta)."""
+    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                      (val, torch.float32, "val"), (B, torch.float32, "B")):
+        _need(t, dt, nm)
+    m = rowptr.numel() - 1
+    K = B.shape[1]
+    if C is None:
+        C = torch.empty((m, K), dtype=torch.float32, device=B.device)
+    _need(C, torch.float32, "C")
+    if C.shape != (m, K):
+        raise ValueError(f"C must be {(m, K)}, got {tuple(C.shape)}")
+    check(lib().spmm_gespmm_csrmm_f32(m, K, _ptr(rowptr), _ptr(colind), _ptr(val), _ptr(B),
+                                      _ptr(C), c_void_p(torch.cuda.current_stream().cuda_stream)),
+          "spmm_gespmm_csrmm_f32")
+    return C
+
+
+def csrmm(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torch.Tensor, *,
+          m: int | None = None, n: int, k: int, ldb: int, order_b: int = ORDER_ROW,
+          C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW, alpha: float = 1.0,
+          beta: float = 0.0, base: int = 0, handle: Handle | None = None) -> torch.Tensor:
+    """C(m x n) = alpha * A(m x k, csr) * B(k x n) + beta * C with explicit
+    storage orders and leading dimensions (spmm_csrmm_ex_f32)."""
+    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                      (val, torch.float32, "val"), (B, torch.float32, "B"),
+                      (C, torch.float32, "C")):
+        _need(t, dt, nm)
+    h = handle or default_handle()
+    m = rowptr.numel() - 1 if m is None else m
+    check(lib().spmm_csrmm_ex_f32(h.raw, m, n, k, colind.numel(), alpha, _ptr(rowptr),
+                                  _ptr(colind), _ptr(val), base, _ptr(B), ldb, order_b, beta,
+                                  _ptr(C), ldc, order_c), "spmm_csrmm_ex_f32")
+    return C
+
+
+def bsrmm(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torch.Tensor, *,
+          mb: int, kb: int, n: int, bs: int, ldb: int, order_b: int = ORDER_ROW,
+          C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW, alpha: float = 1.0,
+          beta: float = 0.0, direction: int = DIRECTION_ROW,
+          handle: Handle | None = None) -> torch.Tensor:
+    """C(mb*bs x n) = alpha * A(bsr) * B(kb*bs x n) + beta * C (spmm_bsrmm_ex_f32)."""
+    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                      (val, torch.float32, "val"), (B, torch.float32, "B"),
+                      (C, torch.float32, "C")):
+        _need(t, dt, nm)
+    h = handle or default_handle()
+    check(lib().spmm_bsrmm_ex_f32(h.raw, direction, mb, kb, n, colind.numel(), bs, alpha,
+                                  _ptr(rowptr), _ptr(colind), _ptr(val), _ptr(B), ldb, order_b,
+                                  beta, _ptr(C), ldc, order_c), "spmm_bsrmm_ex_f32")
+    return C
+
+
+def bsrmm_f16(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torch.Tensor, *,
+              mb: int, kb: int, n: int, bs: int, ldb: int, order_b: int = ORDER_ROW,
+              C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW, alpha: float = 1.0,
+              beta: float = 0.0, direction: int = DIRECTION_ROW,
+              handle: Handle | None = None) -> torch.Tensor:
+    """fp16 A and B, fp32 accumulate / C (spmm_bsrmm_ex_f16)."""
+    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                      (val, torch.float16, "val"), (B, torch.float16, "B"),
+                      (C, torch.float32, "C")):
+        _need(t, dt, nm)
+    h = handle or default_handle()
+    check(lib().spmm_bsrmm_ex_f16(h.raw, direction, mb, kb, n, colind.numel(), bs, alpha,
+                                  _ptr(rowptr), _ptr(colind), _ptr(val), _ptr(B), ldb, order_b,
+                                  beta, _ptr(C), ldc, order_c), "spmm_bsrmm_ex_f16")
+    return C
+
+
+__all__ = ["Handle", "default_handle", "gespmm_csrmm", "csrmm", "bsrmm", "bsrmm_f16",
+           "SpmmError", "ORDER_ROW", "ORDER_COL"]

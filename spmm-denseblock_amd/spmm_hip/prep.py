@@ -1,0 +1,167 @@
+"""Host-side preprocessing and data feeders (numpy in, numpy out).
+
+Thin wrappers over the C ABI of libspmm_hip.so:
+  csr2bsr / bsr2csr / calculate_nnzb / partition_rows   (include/spmm_hip.h)
+  rng_seed / random_array / random_csr / random_bsr /
+  load_csr / dump_csr / load_graph / powerlaw_csr / community_csr (include/spmm_host.h)
+All conversion work happens in the library's C++ (north_star: CPU-side
+preprocessing), not in Python.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_int, c_int64, c_void_p
+
+import numpy as np
+
+from ._lib import check, lib
+
+
+def _p(a: np.ndarray) -> c_void_p:
+    return c_void_p(a.ctypes.data) if a is not None and a.size else c_void_p(0)
+
+
+def _i32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _take(ptr: c_void_p, n: int, dtype) -> np.ndarray:
+    """Copy n elements from a malloc'ed C array and free it."""
+    if not ptr.value:
+        raise MemoryError("libspmm_hip returned a null array")
+    if n:
+        buf = (ctypes.c_byte * (n * np.dtype(dtype).itemsize)).from_address(ptr.value)
+        out = np.frombuffer(buf, dtype=dtype).copy()
+    else:
+        out = np.zeros(0, dtype=dtype)
+    lib().spmm_host_free(ptr)
+    return out
+
+
+# --------------------------------------------------------------- conversions
+def csr2bsr(m: int, n: int, rowptr, colind, val, bs: int, direction: int = 0):
+    """cusparseXcsr2bsrNnz + cusparseScsr2bsr semantics (run_bsrmm.cu:116-142).
+    Returns (bsr_rowptr[mb+1], bsr_colind[nnzb], bsr_val[nnzb*bs*bs])."""
+    rowptr, colind, val = _i32(rowptr), _i32(colind), _f32(val)
+    mb = (m + bs - 1) // bs
+    brp = np.zeros(mb + 1, dtype=np.int32)
+    nnzb = c_int(0)
+    check(lib().spmm_xcsr2bsr_nnz(direction, m, n, _p(rowptr), _p(colind), bs, _p(brp),
+                                  byref(nnzb)), "spmm_xcsr2bsr_nnz")
+    bci = np.zeros(nnzb.value, dtype=np.int32)
+    bval = np.zeros(nnzb.value * bs * bs, dtype=np.float32)
+    check(lib().spmm_scsr2bsr(direction, m, n, _p(val), _p(rowptr), _p(colind), bs, _p(brp),
+                              _p(bval), _p(bci)), "spmm_scsr2bsr")
+    return brp, bci, bval
+
+
+def bsr2csr(mb: int, nb: int, rowptr, colind, val, bs: int, direction: int = 0):
+    """cusparseSbsr2csr semantics (bsr2csr.cu:177-188): nnz = nnzb*bs*bs."""
+    rowptr, colind, val = _i32(rowptr), _i32(colind), _f32(val)
+    nnz = int(rowptr[-1] - rowptr[0]) * bs * bs
+    rp = np.zeros(mb * bs + 1, dtype=np.int32)
+    ci = np.zeros(nnz, dtype=np.int32)
+    v = np.zeros(nnz, dtype=np.float32)
+    check(lib().spmm_sbsr2csr(direction, mb, nb, _p(val), _p(rowptr), _p(colind), bs, _p(v),
+                              _p(rp), _p(ci)), "spmm_sbsr2csr")
+    return rp, ci, v
+
+
+def calculate_nnzb(n: int, rowptr, colind, bs: int) -> int:
+    """calculateNnzb (utility.cc:47-69)."""
+    rowptr, colind = _i32(rowptr), _i32(colind)
+    r = lib().spmm_calculate_nnzb(n, _p(rowptr), _p(colind), bs)
+    if r < 0:
+        raise ValueError("spmm_calculate_nnzb: invalid input")
+    return int(r)
+
+
+def partition_rows(rowptr, nparts: int) -> np.ndarray:
+    """nnz-balanced contiguous row split: bounds[nparts+1]."""
+    rowptr = _i32(rowptr)
+    b = np.zeros(nparts + 1, dtype=np.int32)
+    check(lib().spmm_csr_partition_rows(rowptr.size - 1, _p(rowptr), nparts, _p(b)),
+          "spmm_csr_partition_rows")
+    return b
+
+
+# -------------------------------------------------------------- data feeders
+def rng_seed(seed: int = 1234) -> None:
+    lib().spmm_host_rng_seed(seed)
+
+
+def random_array(n: int, lo: float = -1.0, hi: float = 1.0) -> np.ndarray:
+    """randomArray (load_data.cc:29-36) from the shared mt19937_64."""
+    out = np.empty(n, dtype=np.float32)
+    lib().spmm_host_random_array(n, lo, hi, _p(out))
+    return out
+
+
+def random_dense_matrix(n: int, dim: int, lo: float = -1.0, hi: float = 1.0) -> np.ndarray:
+    """randomDenseMatrix (load_data.cc:38-40), returned as (n, dim) row-major."""
+    return random_array(n * dim, lo, hi).reshape(n, dim)
+
+
+def random_csr(m: int, n: int, p: float, lo: float = -1.0, hi: float = 1.0):
+    """randomCSRMatrix (load_data.cc:42-69) -> (rowptr, colind, val)."""
+    rp = np.zeros(m + 1, dtype=np.int32)
+    ci, v = c_void_p(), c_void_p()
+    nnz = lib().spmm_host_random_csr(m, n, p, lo, hi, _p(rp), byref(ci), byref(v))
+    if nnz < 0:
+        raise ValueError("spmm_host_random_csr failed")
+    return rp, _take(ci, nnz, np.int32), _take(v, nnz, np.float32)
+
+
+def random_bsr(mb: int, nb: int, bs: int, p: float, lo: float = -1.0, hi: float = 1.0):
+    """randomBSRMatrix (load_data.cc:81-113) -> (rowptr, colind, val)."""
+    rp = np.zeros(mb + 1, dtype=np.int32)
+    ci, v = c_void_p(), c_void_p()
+    nnzb = lib().spmm_host_random_bsr(mb, nb, bs, p, lo, hi, _p(rp), byref(ci), byref(v))
+    if nnzb < 0:
+        raise ValueError("spmm_host_random_bsr failed")
+    return rp, _take(ci, nnzb, np.int32), _take(v, nnzb * bs * bs, np.float32)
+
+
+def dump_csr(prefix: str, rowptr, colind) -> None:
+    rowptr, colind = _i32(rowptr), _i32(colind)
+    if lib().spmm_host_dump_csr(prefix.encode(), rowptr.size - 1, colind.size, _p(rowptr),
+                                _p(colind)) != 0:
+        raise OSError(f"dump_csr({prefix}) failed")
+
+
+def load_csr(prefix: str):
+    """loadCSRFromFile (load_data.cc:143-165) -> (rowptr, colind)."""
+    rp, ci, n, nnz = c_void_p(), c_void_p(), c_int(0), c_int64(0)
+    if lib().spmm_host_load_csr(prefix.encode(), byref(rp), byref(ci), byref(n), byref(nnz)) != 0:
+        raise OSError(f"load_csr({prefix}) failed")
+    return _take(rp, n.value + 1, np.int32), _take(ci, nnz.value, np.int32)
+
+
+def load_graph(filename: str):
+    """loadGraphFromFile (load_data.cc:167-184) + convertGraphToCSR."""
+    rp, ci, n, nnz = c_void_p(), c_void_p(), c_int(0), c_int64(0)
+    if lib().spmm_host_load_graph(filename.encode(), byref(rp), byref(ci), byref(n),
+                                  byref(nnz)) != 0:
+        raise OSError(f"load_graph({filename}) failed")
+    return _take(rp, n.value + 1, np.int32), _take(ci, nnz.value, np.int32)
+
+
+def powerlaw_csr(n: int, nnz: int, max_deg: int, gamma: float = 2.3, seed: int = 1234):
+    """Chung-Lu power-law stand-in for an OGB graph (include/spmm_host.h)."""
+    rp, ci = c_void_p(), c_void_p()
+    if lib().spmm_host_gen_powerlaw_csr(n, nnz, max_deg, gamma, seed, byref(rp), byref(ci)) != 0:
+        raise ValueError("spmm_host_gen_powerlaw_csr: invalid parameters")
+    return _take(rp, n + 1, np.int32), _take(ci, nnz, np.int32)
+
+
+def community_csr(n: int, avg_deg: float, cmin: int, cmax: int, p_in: float, seed: int = 1234):
+    """Community-ordered stand-in for a rabbit-reordered graph (include/spmm_host.h)."""
+    rp, ci, nnz = c_void_p(), c_void_p(), c_int64(0)
+    if lib().spmm_host_gen_community_csr(n, avg_deg, cmin, cmax, p_in, seed, byref(rp), byref(ci),
+                                         byref(nnz)) != 0:
+        raise ValueError("spmm_host_gen_community_csr: invalid parameters")
+    return _take(rp, n + 1, np.int32), _take(ci, nnz.value, np.int32)

@@ -1,0 +1,182 @@
+"""Path B parity on the GPU: BSR x dense (fp32 MFMA, fp16 MFMA, generic)
+through the C ABI vs the oracle, with cusparseSbsrmm semantics."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from helpers import (TOL_F16_ACC, TOL_F32, assert_normwise, oracle_bsrmm_f64, oracle_csrmm_f64)
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _ops():
+    from spmm_hip import ops
+    return ops
+
+
+def _dev(*arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+def _rand_bsr(rng, mb, kb, bs, p, empty_rows=()):
+    rows = []
+    for br in range(mb):
+        cols = np.nonzero(rng.random(kb) < p)[0] if br not in empty_rows else np.zeros(0, int)
+        rows.append(cols)
+    rp = np.concatenate([[0], np.cumsum([len(c) for c in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32) if rp[-1] else np.zeros(0, np.int32)
+    val = rng.uniform(-1, 1, rp[-1] * bs * bs).astype(np.float32)
+    return rp, ci, val
+
+
+def test_kat_bsrmm_cu_via_sbsrmm(golden, device):
+    """bsrmm.cu:141-144: cusparseSbsrmm ROW, transB = N (col-major B, C)."""
+    from spmm_hip._lib import lib
+    k = golden["kats"]["bsrmm_cu"]
+    rp, ci, v = _dev(np.array(k["rowptr"], np.int32), np.array(k["colind"], np.int32),
+                     np.array(k["val"], np.float32))
+    B = torch.tensor(k["B_colmajor"], dtype=torch.float32, device=device)
+    C = torch.zeros(8, dtype=torch.float32, device=device)
+    h = _ops().default_handle()
+    d = ctypes.c_void_p()
+    lib().spmm_create_mat_descr(ctypes.byref(d))
+    one, zero = ctypes.c_float(1.0), ctypes.c_float(0.0)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    st = lib().spmm_sbsrmm(h.raw, 0, 0, 0, k["mb"], k["n"], k["kb"], 4, ctypes.byref(one), d,
+                           P(v), P(rp), P(ci), k["bs"], P(B), k["ldb"], ctypes.byref(zero), P(C),
+                           k["ldc"])
+    lib().spmm_destroy_mat_descr(d)
+    assert st == 0
+    assert C.cpu().tolist() == k["C_colmajor"]
+
+
+def test_kat_block_cublas(golden, device):
+    """block_cublas.cu:123-136 per-block cublasSgemm == dir COLUMN, row-major
+    B, col-major C, beta = 1 onto zeroed C."""
+    k = golden["kats"]["block_cublas_cu"]
+    rp, ci, v = _dev(np.array(k["rowptr"], np.int32), np.array(k["colind"], np.int32),
+                     np.array(k["val"], np.float32))
+    B = torch.tensor(k["B_rowmajor"], dtype=torch.float32, device=device)
+    C = torch.zeros(12, dtype=torch.float32, device=device)
+    _ops().bsrmm(rp, ci, v, B, mb=k["mb"], kb=k["kb"], n=k["n"], bs=k["bs"], ldb=k["ldb"],
+                 order_b=0, C=C, ldc=k["ldc"], order_c=1, beta=k["beta"], direction=k["dir"])
+    assert C.cpu().tolist() == k["C_colmajor"]
+
+
+@pytest.mark.parametrize("bs", [2, 3, 4, 8, 16, 32, 64])
+@pytest.mark.parametrize("direction", [0, 1])
+@pytest.mark.parametrize("orders", [(0, 0), (1, 1), (0, 1)])
+def test_bsrmm_f32(oracle, device, bs, direction, orders):
+    ob, oc = orders
+    rng = np.random.default_rng(bs * 10 + direction)
+    mb, kb = 23, 29
+    n = 130 if bs <= 16 else 96
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.2, empty_rows=(3, 4))
+    K = kb * bs
+    Bd = rng.uniform(-1, 1, (K, n)).astype(np.float32)
+    B = Bd if ob == 0 else np.ascontiguousarray(Bd.T)
+    ldb = n if ob == 0 else K
+    m = mb * bs
+    ldc = n if oc == 0 else m
+    drp, dci, dv, dB = _dev(rp, ci, v, B.reshape(-1))
+    C = torch.full((m * n,), float("nan"), device=device)
+    _ops().bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=ldb, order_b=ob, C=C, ldc=ldc,
+                 order_c=oc, direction=direction)
+    torch.cuda.synchronize()
+    got = C.cpu().numpy().reshape((m, n) if oc == 0 else (n, m))
+    got = got if oc == 0 else got.T
+    ref, absd = oracle_bsrmm_f64(oracle, direction, mb, n, bs, rp, ci, v, Bd, n, 0)
+    assert_normwise(got, ref, absd, TOL_F32, f"bsr bs={bs} dir={direction} orders={orders}")
+
+
+@pytest.mark.parametrize("bs", [16, 32])
+@pytest.mark.parametrize("n", [1, 16, 33, 128, 512])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.5, 2.0)])
+def test_bsrmm_mfma_shapes_alpha_beta(oracle, device, bs, n, alpha, beta):
+    rng = np.random.default_rng(n + bs)
+    mb, kb = 17, 21
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.3)
+    Bd = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (mb * bs, n)).astype(np.float32)
+    drp, dci, dv, dB, dC = _dev(rp, ci, v, Bd, C0)
+    _ops().bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n, alpha=alpha,
+                 beta=beta)
+    torch.cuda.synchronize()
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, Bd, n, 0)
+    assert_normwise(dC.cpu().numpy(), alpha * ref + beta * C0.astype(np.float64),
+                    abs(alpha) * absd + abs(beta) * np.abs(C0), TOL_F32,
+                    f"bs={bs} n={n} a={alpha} b={beta}")
+
+
+@pytest.mark.parametrize("n", [16, 64, 128, 512])
+@pytest.mark.parametrize("direction", [0, 1])
+@pytest.mark.parametrize("ob", [0, 1])
+def test_bsrmm_f16(oracle, device, n, direction, ob):
+    """fp16 A/B, fp32 accumulate: compared with the exact (f64) product of the
+    same fp16 values; odd block counts exercise the half-empty MFMA pair."""
+    rng = np.random.default_rng(n * 3 + direction)
+    mb, kb, bs = 19, 25, 16
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.27, empty_rows=(0,))
+    v16 = v.astype(np.float16)
+    Bd = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float16)
+    B = Bd if ob == 0 else np.ascontiguousarray(Bd.T)
+    ldb = n if ob == 0 else kb * bs
+    drp, dci, dv, dB = _dev(rp, ci, v16, B.reshape(-1))
+    C = torch.empty((mb * bs, n), dtype=torch.float32, device=device)
+    _ops().bsrmm_f16(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=ldb, order_b=ob, C=C,
+                     ldc=n, direction=direction)
+    torch.cuda.synchronize()
+    ref, absd = oracle_bsrmm_f64(oracle, direction, mb, n, bs, rp, ci, v16, Bd, n, 0, half=True)
+    assert_normwise(C.cpu().numpy(), ref, absd, TOL_F16_ACC, f"f16 n={n}")
+
+
+def test_csr_vs_bsr_differential(oracle, device):
+    """check_result.cu:103-116,233-246: csrmm2(T) vs bsrmm(T) after csr2bsr,
+    m = 32768, p = 0.01, bs = 4, K = 64, B = +-0.5 alternating, eps 1e-4."""
+    from spmm_hip import prep
+    prep.rng_seed(1234)
+    m, bs, K = 2 << 14, 4, 64
+    rp, ci, v = prep.random_csr(m, m, 0.01)
+    brp, bci, bval = prep.csr2bsr(m, m, rp, ci, v, bs)
+    B = np.where(np.arange(m * K) % 2 == 0, 0.5, -0.5).astype(np.float32)
+    drp, dci, dv, dB, dbrp, dbci, dbval = _dev(rp, ci, v, B, brp, bci, bval)
+    C1 = torch.empty((m, K), device=device)
+    C2 = torch.empty((m, K), device=device)
+    ops = _ops()
+    ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=C1, ldc=K)
+    ops.bsrmm(dbrp, dbci, dbval, dB, mb=m // bs, kb=m // bs, n=K, bs=bs, ldb=K, C=C2, ldc=K)
+    torch.cuda.synchronize()
+    assert float((C1 - C2).abs().max()) < 1e-4
+
+
+def test_bsr_status_codes(device):
+    """rocsparse_bsrmm.h:109-176 argument checks."""
+    from spmm_hip._lib import (INVALID_VALUE, MATRIX_TYPE_NOT_SUPPORTED, NOT_INITIALIZED,
+                               SUCCESS, lib)
+    L = lib()
+    h = _ops().default_handle()
+    d = ctypes.c_void_p()
+    L.spmm_create_mat_descr(ctypes.byref(d))
+    one = ctypes.c_float(1.0)
+    args = lambda **kw: dict(dict(handle=h.raw, dir=0, ta=0, tb=0, mb=2, n=2, kb=3, nnzb=4,
+                                  descr=d, bs=2, ldb=6, ldc=4), **kw)
+
+    def call(a, C=None):
+        return L.spmm_sbsrmm(a["handle"], a["dir"], a["ta"], a["tb"], a["mb"], a["n"], a["kb"],
+                             a["nnzb"], ctypes.byref(one), a["descr"], C, C, C, a["bs"], C,
+                             a["ldb"], ctypes.byref(one), C, a["ldc"])
+
+    assert call(args(handle=None)) == NOT_INITIALIZED
+    assert call(args(descr=None)) == INVALID_VALUE
+    assert call(args(ta=1)) == MATRIX_TYPE_NOT_SUPPORTED
+    assert call(args(tb=2)) == MATRIX_TYPE_NOT_SUPPORTED
+    assert call(args(mb=-1)) == INVALID_VALUE
+    assert call(args(bs=0)) == INVALID_VALUE
+    assert call(args(nnzb=0)) == SUCCESS  # quick return, nothing touched
+    assert call(args()) == INVALID_VALUE  # null pointers
+    L.spmm_destroy_mat_descr(d)

@@ -1,0 +1,246 @@
+"""Path A parity on the GPU: CSR x dense through the C ABI vs the oracle.
+
+Bar (north_star): within 1e-5 norm-wise relative of the reference semantics
+(sequential fp32 FMA in CSR order, gespmm_csrmm.h:124-129); in practice every
+row finished by one wave is bit-identical to the sequential oracle, which is
+asserted separately for small problems."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from helpers import TOL_F32, assert_normwise, oracle_csrmm_f32, oracle_csrmm_f64
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _ops():
+    from spmm_hip import ops
+    return ops
+
+
+def _rand_csr(rng, m, k, deg_hi, hub_rows=(), hub_deg=0, empty_frac=0.0):
+    deg = rng.integers(0, deg_hi + 1, m)
+    if empty_frac:
+        deg[rng.random(m) < empty_frac] = 0
+    for r in hub_rows:
+        deg[r] = min(hub_deg, k)
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    ci = np.concatenate([np.sort(rng.choice(k, d, replace=False)) for d in deg] or
+                        [np.zeros(0)]).astype(np.int32)
+    val = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    return rp, ci, val
+
+
+def _dev(*arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+def _check_rowmajor(oracle, rp, ci, val, B, C, what, exact_expected=False):
+    m, n = C.shape
+    ref32 = oracle_csrmm_f32(oracle, m, n, rp, ci, val, B, B.shape[1], 0).reshape(m, n)
+    ref64, absd = oracle_csrmm_f64(oracle, m, n, rp, ci, val, B, B.shape[1], 0)
+    got = C.cpu().numpy()
+    assert_normwise(got, ref64, absd, TOL_F32, what + " vs f64")
+    assert_normwise(got, ref32.astype(np.float64), absd, TOL_F32, what + " vs seq-f32")
+    if exact_expected:
+        assert np.array_equal(got, ref32), what + ": expected bit-exact sequential FMA"
+    return float(np.mean(got == ref32))
+
+
+def test_kat_csrmm_cu_via_scsrmm(oracle, golden, device):
+    """csrmm.cu:183-185 — cusparseScsrmm, col-major B and C."""
+    from spmm_hip._lib import lib
+    k = golden["kats"]["csrmm_cu"]
+    ops = _ops()
+    rp, ci, v = _dev(np.array(k["rowptr"], np.int32), np.array(k["colind"], np.int32),
+                     np.array(k["val"], np.float32))
+    B = torch.tensor(k["B_colmajor"], dtype=torch.float32, device=device)
+    C = torch.zeros(8, dtype=torch.float32, device=device)
+    h = ops.default_handle()
+    d = ctypes.c_void_p()
+    assert lib().spmm_create_mat_descr(ctypes.byref(d)) == 0
+    one, zero = ctypes.c_float(1.0), ctypes.c_float(0.0)
+    st = lib().spmm_scsrmm(h.raw, 0, 4, 2, 4, 9, ctypes.byref(one), d, ctypes.c_void_p(v.data_ptr()),
+                           ctypes.c_void_p(rp.data_ptr()), ctypes.c_void_p(ci.data_ptr()),
+                           ctypes.c_void_p(B.data_ptr()), 4, ctypes.byref(zero),
+                           ctypes.c_void_p(C.data_ptr()), 4)
+    lib().spmm_destroy_mat_descr(d)
+    assert st == 0
+    assert C.cpu().tolist() == k["C_colmajor"]
+
+
+def test_kat_try_cublas_dense_csr(golden, device):
+    k = golden["kats"]["try_cublas_cu"]
+    ops = _ops()
+    rp, ci, v = _dev(np.array(k["rowptr"], np.int32), np.array(k["colind"], np.int32),
+                     np.array(k["val"], np.float32))
+    B = torch.tensor(k["B_colmajor"], dtype=torch.float32, device=device)
+    C = torch.zeros(8, dtype=torch.float32, device=device)
+    ops.csrmm(rp, ci, v, B, m=2, n=4, k=3, ldb=3, order_b=1, C=C, ldc=2, order_c=1)
+    assert C.cpu().tolist() == k["C_colmajor"]
+
+
+@pytest.mark.parametrize("shape", [(64, 80, 0.1), (300, 257, 0.03), (1000, 1200, 0.01)])
+@pytest.mark.parametrize("K", [32, 64, 100, 128, 256, 512])
+def test_gespmm_reference_random_csr(oracle, golden, device, shape, K):
+    """randomCSRMatrix fixtures (the reference generator's own output)."""
+    m, n, p = shape
+    key = f"csr_{m}_{n}_{p}"
+    rp, ci, v = (golden["ref"][key + s] for s in ("_rowptr", "_colind", "_val"))
+    rng = np.random.default_rng(K)
+    B = rng.uniform(-1, 1, (n, K)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    C = _ops().gespmm_csrmm(drp, dci, dv, dB)
+    torch.cuda.synchronize()
+    _check_rowmajor(oracle, rp, ci, v, B, C, f"gespmm {key} K={K}")
+
+
+@pytest.mark.parametrize("K", [1, 2, 7, 64, 128, 130, 256, 512])
+def test_power_law_hubs_and_empty_rows(oracle, device, K):
+    """Merge-path carries: hub rows spanning many waves, runs of empty rows."""
+    rng = np.random.default_rng(100 + K)
+    m = 3000
+    rp, ci, v = _rand_csr(rng, m, 5000, 6, hub_rows=(0, 1, 1777, m - 1), hub_deg=4000,
+                          empty_frac=0.3)
+    B = rng.uniform(-1, 1, (5000, K)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    h = _ops().Handle()
+    h.set_csr_waves_per_cu(1)  # few waves -> long merge-path segments
+    C = torch.empty((m, K), dtype=torch.float32, device=device)
+    _ops().csrmm(drp, dci, dv, dB, n=K, k=5000, ldb=K, C=C, ldc=K, handle=h)
+    torch.cuda.synchronize()
+    _check_rowmajor(oracle, rp, ci, v, B, C, f"hubs K={K}")
+    # a second, differently cut grid gives the same answer up to carries
+    h.set_csr_waves_per_cu(32)
+    C2 = torch.empty_like(C)
+    _ops().csrmm(drp, dci, dv, dB, n=K, k=5000, ldb=K, C=C2, ldc=K, handle=h)
+    torch.cuda.synchronize()
+    _check_rowmajor(oracle, rp, ci, v, B, C2, f"hubs K={K} 32 waves/CU")
+
+
+def test_unsplit_rows_bit_exact(oracle, device):
+    """Small matrix, every row inside one wave: bit-identical to the
+    sequential fp32 FMA chain of the reference kernel."""
+    rng = np.random.default_rng(5)
+    rp, ci, v = _rand_csr(rng, 40, 300, 9)
+    B = rng.uniform(-1, 1, (300, 128)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    h = _ops().Handle()
+    h.set_csr_waves_per_cu(1)
+    C = torch.empty((40, 128), dtype=torch.float32, device=device)
+    # one wave for the whole matrix: no carries at all
+    _ops().csrmm(drp, dci, dv, dB, n=128, k=300, ldb=128, C=C, ldc=128, handle=h)
+    torch.cuda.synchronize()
+    frac = _check_rowmajor(oracle, rp, ci, v, B, C, "unsplit", exact_expected=True)
+    assert frac == 1.0
+
+
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (2.5, 0.0), (1.0, 1.0), (-0.5, 0.75)])
+@pytest.mark.parametrize("orders", [(0, 0), (1, 1), (0, 1), (1, 0)])
+def test_alpha_beta_and_layouts(oracle, device, alpha, beta, orders):
+    """cusparseScsrmm / csrmm2 semantics: C = alpha*A*B + beta*C for every
+    combination of B / C storage order (run_csrmm.cu:133-142)."""
+    ob, oc = orders
+    rng = np.random.default_rng(11)
+    m, k, n = 333, 401, 96
+    rp, ci, v = _rand_csr(rng, m, k, 12, empty_frac=0.1)
+    Bd = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    B = Bd if ob == 0 else np.ascontiguousarray(Bd.T)
+    ldb = n if ob == 0 else k
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    Cin = C0 if oc == 0 else np.ascontiguousarray(C0.T)
+    ldc = n if oc == 0 else m
+    drp, dci, dv, dB, dC = _dev(rp, ci, v, B.reshape(-1), Cin.reshape(-1))
+    _ops().csrmm(drp, dci, dv, dB, m=m, n=n, k=k, ldb=ldb, order_b=ob, C=dC, ldc=ldc,
+                 order_c=oc, alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    got = dC.cpu().numpy().reshape(Cin.shape)
+    got = got if oc == 0 else got.T
+    ref64, absd = oracle_csrmm_f64(oracle, m, n, rp, ci, v, Bd, n, 0)
+    ref = alpha * ref64 + beta * C0.astype(np.float64)
+    assert_normwise(got, ref, abs(alpha) * absd + abs(beta) * np.abs(C0), TOL_F32,
+                    f"alpha={alpha} beta={beta} orders={orders}")
+
+
+def test_index_base_one(oracle, device):
+    rng = np.random.default_rng(3)
+    m, k, n = 200, 150, 64
+    rp, ci, v = _rand_csr(rng, m, k, 7)
+    B = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp + 1, ci + 1, v, B)
+    C = torch.empty((m, n), dtype=torch.float32, device=device)
+    _ops().csrmm(drp, dci, dv, dB, n=n, k=k, ldb=n, C=C, ldc=n, base=1)
+    torch.cuda.synchronize()
+    _check_rowmajor(oracle, rp, ci, v, B, C, "base=1")
+
+
+def test_degenerate_shapes(oracle, device):
+    ops = _ops()
+    # nnz == 0: every row is an empty row -> zeros
+    rp = torch.zeros(51, dtype=torch.int32, device=device)
+    ci = torch.zeros(0, dtype=torch.int32, device=device)
+    v = torch.zeros(0, dtype=torch.float32, device=device)
+    B = torch.randn(10, 64, device=device)
+    C = torch.full((50, 64), 7.0, device=device)
+    ops.csrmm(rp, ci, v, B, n=64, k=10, ldb=64, C=C, ldc=64)
+    torch.cuda.synchronize()
+    assert torch.count_nonzero(C).item() == 0
+    # m == 0 is a quick return
+    C0 = torch.zeros(0, 64, device=device)
+    ops.csrmm(torch.zeros(1, dtype=torch.int32, device=device), ci, v, B, n=64, k=10, ldb=64,
+              C=C0, ldc=64)
+
+
+def test_status_codes(device):
+    from spmm_hip._lib import INVALID_VALUE, MATRIX_TYPE_NOT_SUPPORTED, NOT_INITIALIZED, lib
+    L = lib()
+    one = ctypes.c_float(1.0)
+    assert L.spmm_csrmm_ex_f32(None, 1, 1, 1, 0, 1.0, None, None, None, 0, None, 1, 0, 0.0,
+                               None, 1, 0) == NOT_INITIALIZED
+    h = _ops().default_handle()
+    assert L.spmm_csrmm_ex_f32(h.raw, -1, 1, 1, 0, 1.0, None, None, None, 0, None, 1, 0, 0.0,
+                               None, 1, 0) == INVALID_VALUE
+    d = ctypes.c_void_p()
+    L.spmm_create_mat_descr(ctypes.byref(d))
+    assert L.spmm_scsrmm(h.raw, 1, 4, 2, 4, 9, ctypes.byref(one), d, None, None, None, None, 4,
+                         ctypes.byref(one), None, 4) == MATRIX_TYPE_NOT_SUPPORTED
+    L.spmm_destroy_mat_descr(d)
+
+
+def test_products_scale_properties(oracle, device):
+    """BASELINE full size (ogbn-products stand-in, K=128): a sample of rows
+    against the oracle, determinism, and linearity A(B1+B2) = AB1 + AB2."""
+    from spmm_hip import prep
+    n, nnz, K = 2449029, 61859140, 128
+    rp, ci = prep.powerlaw_csr(n, nnz, 17481, 2.3, 1234)
+    rng = np.random.default_rng(0)
+    v = rng.uniform(-1, 1, nnz).astype(np.float32)
+    drp, dci, dv = _dev(rp, ci, v)
+    B1 = torch.rand((n, K), device=device) * 2 - 1
+    B2 = torch.rand((n, K), device=device) * 2 - 1
+    ops = _ops()
+    C1 = ops.gespmm_csrmm(drp, dci, dv, B1)
+    C1b = ops.gespmm_csrmm(drp, dci, dv, B1)
+    C2 = ops.gespmm_csrmm(drp, dci, dv, B2)
+    C12 = ops.gespmm_csrmm(drp, dci, dv, B1 + B2)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C1b), "not deterministic"
+    # sampled rows (hub rows included) vs the f64 oracle
+    deg = np.diff(rp)
+    rows = np.unique(np.concatenate([rng.choice(n, 2000, replace=False),
+                                     np.argsort(deg)[-20:]]))
+    sub_rp = np.concatenate([[0], np.cumsum(deg[rows])]).astype(np.int32)
+    sub_ci = np.concatenate([ci[rp[r]:rp[r + 1]] for r in rows]).astype(np.int32)
+    sub_v = np.concatenate([v[rp[r]:rp[r + 1]] for r in rows]).astype(np.float32)
+    Bh = B1.cpu().numpy()
+    ref64, absd = oracle_csrmm_f64(oracle, rows.size, K, sub_rp, sub_ci, sub_v, Bh, K, 0)
+    assert_normwise(C1.cpu().numpy()[rows], ref64, absd, TOL_F32, "products rows")
+    # linearity within the same tolerance (sum of the two magnitudes)
+    lin = (C1 + C2 - C12).abs()
+    absd_full = ops.gespmm_csrmm(drp, dci, dv.abs(), B1.abs() + B2.abs())
+    assert bool((lin <= 3 * TOL_F32 * absd_full + 1e-30).all())
