@@ -46,15 +46,11 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_gfx950_code_object_present():
+    """The fat binary embeds an amdgcn gfx950 code object (and no other ISA)."""
     from spmm_hip import _lib
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list",
-                          "--type=o", f"--input={_lib.LIB_PATH}"],
-                         capture_output=True, text=True)
-    if out.returncode != 0:  # fall back to scanning the fat binary
-        data = open(_lib.LIB_PATH, "rb").read()
-        assert b"gfx950" in data
-    else:
-        assert "gfx950" in out.stdout
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"amdgcn-amd-amdhsa--gfx906" not in data
 
 
 def test_status_strings_and_host_side_checks():
