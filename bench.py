@@ -1,16 +1,22 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE.json headline: SpMM GFLOP/s (2*nnz*K/t) + achieved HBM
-GB/s on ogbn-products at K = 128 (synthetic stand-in of the same n / nnz /
-max degree: the dataset is not reachable offline).
+GB/s on ogbn-products at K = 128 (synthetic stand-in with the same n / nnz /
+max degree: OGB data is not reachable offline).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--K 128]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-A step = one pass of the hot path over the resident inputs: the CSR x dense
-SpMM (merge-path kernel + carry fix-up) on this rank's rows, and for N > 1
-the RCCL all-gather of C (BASELINE config 4, strong scaling: the total graph
-is fixed, rows are split nnz-balanced). Inputs are in HBM before timing
-starts. Rank 0 prints ONE JSON line.
+Workloads (BASELINE.json configs; the default is the metric's own config):
+  products_csr       CSR x dense, ogbn-products stand-in, K=128   (metric; config 4 shape at N>1)
+  products_csr_k256  same graph, K=256                            (config 4)
+  arxiv_csr          ogbn-arxiv stand-in (169,343 / 1,166,243), K=128   (config 2)
+  reddit_bsr32       community-ordered reddit stand-in, csr2bsr bs=32, K=128, fp32 MFMA (config 3)
+  products_bsr16_f16 community-ordered products stand-in, bs=16, K=512, fp16 MFMA    (config 5)
+
+A step = one pass of the hot path over resident inputs. CSR: the merge-path
+kernel + carry fix-up on this rank's rows, plus (N > 1) the RCCL all-gather
+of C — strong scaling, the graph is fixed and rows are split nnz-balanced.
+BSR: one bsrmm. Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -25,83 +31,101 @@ sys.path.insert(0, os.path.join(ROOT, "spmm-denseblock_amd"))
 
 import numpy as np  # noqa: E402
 
-HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
-PRODUCTS = dict(n=2449029, nnz=61859140, max_deg=17481, gamma=2.3)
+HBM_PEAK_GBPS = 8000.0    # MI355X_MICROARCH.md chip table (spec)
+MFMA_PEAK_TFLOPS = {"fp32": 157.3, "fp16": 2500.0}  # dense (no sparsity)
+
+WORKLOADS = {
+    "products_csr": dict(kind="csr", n=2449029, nnz=61859140, max_deg=17481, K=128),
+    "products_csr_k256": dict(kind="csr", n=2449029, nnz=61859140, max_deg=17481, K=256),
+    "arxiv_csr": dict(kind="csr", n=169343, nnz=1166243, max_deg=13161, K=128),
+    "reddit_bsr32": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
+                         bs=32, K=128, dtype="fp32"),
+    "products_bsr16_f16": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                               p_in=0.97, bs=16, K=512, dtype="fp16"),
+}
+METRIC = "SpMM GFLOP/s (2*nnz*K/t) + achieved HBM GB/s, ogbn-products K=128"
 
 
-def algorithmic_bytes(n_rows: int, nnz: int, K: int) -> int:
-    """SURVEY.md §8(d) CSR gather model: rowptr + (colind, val) + one B row
-    per nnz + the C write."""
+def csr_bytes(n_rows: int, nnz: int, K: int) -> int:
+    """SURVEY.md §8(d) CSR gather model: rowptr + (colind, val) + one B row per
+    nnz + the C write."""
     return 4 * (n_rows + 1) + 8 * nnz + 4 * K * nnz + 4 * K * n_rows
 
 
-def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 12.0) -> dict:
+def bsr_bytes(mb: int, nnzb: int, bs: int, K: int, s: int) -> int:
+    """SURVEY.md §8(d) BSR model, s = value size."""
+    return 4 * (mb + 1) + 4 * nnzb + s * nnzb * bs * bs + s * nnzb * bs * K + 4 * mb * bs * K
+
+
+def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0) -> dict:
     """spmm.cc csr_spmm restated (oracle_spmm_cc_csr: OpenMP rows, k-outer,
-    double, unit values) timed on a growing row prefix of the SAME graph
-    until ~budget_s of CPU work; reports GFLOP/s = 2*nnz_sample*K/t."""
+    double, unit values) on the SAME graph: a growing row prefix until about
+    budget_s of CPU work, or the whole graph repeated, median of the repeats."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from helpers import load_oracle, ptr
     L = load_oracle()
     n = rp.size - 1
     Bd = np.random.default_rng(1).uniform(-1, 1, (n, K))  # double, as spmm.cc
-    ip64 = rp.astype(np.int64)
-    ix64 = ci.astype(np.int64)
-    rows = 1024
-    best = None
+    ip64, ix64 = rp.astype(np.int64), ci.astype(np.int64)
+    rows, spent = 1024, 0.0
     while True:
         rows = min(rows, n)
         out = np.empty((rows, K))
         t0 = time.perf_counter()
         L.oracle_spmm_cc_csr(rows, K, ptr(ip64), ptr(ix64), ptr(Bd), K, ptr(out))
         dt = time.perf_counter() - t0
-        nnz_s = int(rp[rows])
-        best = dict(rows=rows, nnz=nnz_s, seconds=dt)
-        if dt >= budget_s / 4 or rows == n:
+        spent += dt
+        if rows == n or dt >= budget_s / 3:
             break
-        rows = int(rows * min(8.0, max(2.0, (budget_s / 4) / max(dt, 1e-4))))
-    g = 2.0 * best["nnz"] * K / best["seconds"] / 1e9
-    return {"value": round(g, 3), "unit": "GFLOP/s", "cores": int(L.oracle_num_threads()),
-            "kind": "port",
-            "sample": (f"spmm.cc csr_spmm restated (double, unit values, k-outer) on the first "
-                       f"{best['rows']} rows ({best['nnz']} nnz) of the same synthetic "
-                       f"ogbn-products graph, K={K}, {best['seconds']:.2f} s")}
+        rows = int(rows * min(8.0, max(2.0, (budget_s / 3) / max(dt, 1e-4))))
+    times = [dt]
+    while spent < budget_s and len(times) < 15:
+        t0 = time.perf_counter()
+        L.oracle_spmm_cc_csr(rows, K, ptr(ip64), ptr(ix64), ptr(Bd), K, ptr(out))
+        times.append(time.perf_counter() - t0)
+        spent += times[-1]
+    med = float(np.median(times))
+    nnz_s = int(rp[rows])
+    return {"value": round(2.0 * nnz_s * K / med / 1e9, 3), "unit": "GFLOP/s",
+            "cores": int(L.oracle_num_threads()), "kind": "port",
+            "sample": (f"spmm.cc csr_spmm restated (double, unit values, k-outer, OpenMP) on "
+                       f"{'all' if rows == n else 'the first'} {rows} rows ({nnz_s} nnz) of the "
+                       f"same synthetic graph, K={K}; median of {len(times)} runs "
+                       f"({med:.3f} s each, {spent:.1f} s total)")}
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--K", type=int, default=128)
-    ap.add_argument("--waves-per-cu", type=int, default=0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (profiles/, see DESIGN.md §7)")
-    args = ap.parse_args()
-
+def timed_loop(step, h, steps, warmup, world, dist):
     import torch
-    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    h.kernel_times()
+    h.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    h.set_timing(False)
+    kt = h.kernel_times()
+    return elapsed, (float(np.mean(kt)) if kt else float("nan"))
+
+
+def run_csr(args, W, world, rank, dev, dist):
+    import torch
     from spmm_hip import dist as sdist
     from spmm_hip import ops, prep
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
-    K = args.K
-    P = PRODUCTS
+    K = args.K or W["K"]
     t_gen = time.perf_counter()
-    rp, ci = prep.powerlaw_csr(P["n"], P["nnz"], P["max_deg"], P["gamma"], 1234)
+    rp, ci = prep.powerlaw_csr(W["n"], W["nnz"], W["max_deg"], 2.3, 1234)
     val = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
     t_gen = time.perf_counter() - t_gen
     n, nnz = rp.size - 1, ci.size
-
     shard = sdist.make_shard(rp, ci, val, rank, world)
     d_rp = torch.from_numpy(shard.rowptr).to(dev)
     d_ci = torch.from_numpy(np.ascontiguousarray(shard.colind)).to(dev)
@@ -109,96 +133,158 @@ def main() -> None:
     g = torch.Generator(device=dev)
     g.manual_seed(1234)
     B = torch.rand((n, K), device=dev, generator=g) * 2 - 1
-    out = torch.empty((world * shard.max_rows, K), device=dev)
     mr = shard.max_rows
+    out = torch.empty((world * mr, K), device=dev)
     C_slot = out[rank * mr: rank * mr + shard.rows]
-
     h = ops.Handle()
     if args.waves_per_cu:
         h.set_csr_waves_per_cu(args.waves_per_cu)
-    local_nnz = int(shard.colind.size)
 
     def step():
         ops.csrmm(d_rp, d_ci, d_v, B, m=shard.rows, n=K, k=n, ldb=K, C=C_slot, ldc=K, handle=h)
         if world > 1:
             sdist.gather(out, shard, compact=False)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    h.kernel_times()  # drop warm-up records
-    h.set_timing(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    h.set_timing(False)
-    ktimes = h.kernel_times()
-    kms = float(np.mean(ktimes)) if ktimes else float("nan")
-
-    # max over ranks
+    elapsed, kms = timed_loop(step, h, args.steps, args.warmup, world, dist)
     t = torch.tensor([elapsed, kms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kms_max = float(t[0]), float(t[1])
-
-    ms_step = elapsed / args.steps * 1e3
-    flops = 2.0 * nnz * K
-    value = flops * args.steps / elapsed / 1e9
-    # dominant kernel = rank-local merge-path SpMM launch
-    kbytes = algorithmic_bytes(shard.rows, local_nnz, K)
-    achieved = kbytes / (kms / 1e3) / 1e9 if ktimes else None
+    kbytes = csr_bytes(shard.rows, int(shard.colind.size), K)
+    achieved = kbytes / (kms / 1e3) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("K") == K and tj.get("nnz") == local_nnz:
+            if tj.get("K") == K and tj.get("nnz") == int(shard.colind.size):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    vec = 4 if K > 128 and K % 4 == 0 else (2 if K > 64 and K % 2 == 0 else 1)
+    rec = dict(
+        value=2.0 * nnz * K * args.steps / elapsed / 1e9, ms_per_step=elapsed / args.steps * 1e3,
+        dtype="fp32",
+        data=("synthetic (Chung-Lu power-law digraph with the dataset's n / nnz / max degree, "
+              "U(-1,1) values and B; OGB data not reachable offline)"),
+        config={"workload": f"{args.workload}: csr_spmm K={K}" +
+                (" row-partitioned + RCCL all-gather" if world > 1 else ""),
+                "n": n, "nnz": nnz, "K": K, "max_deg": int(np.diff(rp).max()),
+                "parallelism": f"rows{world}" if world > 1 else "single",
+                "waves_per_cu": args.waves_per_cu or 16},
+        roofline={"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                  "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                  "traffic": traffic, "kernel": f"csr_mergepath_kernel<{vec}>",
+                  "kernel_ms": round(kms, 4), "kernel_ms_max_rank": round(kms_max, 4),
+                  "algorithmic_bytes_per_launch": kbytes},
+        gen_seconds=round(t_gen, 2))
+    return rec, (rp, ci, K)
+
+
+def run_bsr(args, W, world, rank, dev, dist):
+    import torch
+    from spmm_hip import ops, prep
+    if world > 1:
+        raise SystemExit("BSR workloads are single-GPU configs (BASELINE configs 3 and 5)")
+    K, bs, dt = args.K or W["K"], W["bs"], W["dtype"]
+    t_gen = time.perf_counter()
+    rp, ci = prep.community_csr(W["n"], W["avg_deg"], W["cmin"], W["cmax"], W["p_in"], 1234)
+    n, nnz = rp.size - 1, ci.size
+    val = np.random.default_rng(2).uniform(-1, 1, nnz).astype(np.float32)
+    t_gen = time.perf_counter() - t_gen
+    t_conv = time.perf_counter()
+    brp, bci, bval = prep.csr2bsr(n, n, rp, ci, val, bs, 0)  # host preprocessing
+    t_conv = time.perf_counter() - t_conv
+    mb = (n + bs - 1) // bs
+    nnzb = int(bci.size)
+    s = 4 if dt == "fp32" else 2
+    tdt = torch.float32 if dt == "fp32" else torch.float16
+    d_brp, d_bci = torch.from_numpy(brp).to(dev), torch.from_numpy(bci).to(dev)
+    d_bv = torch.from_numpy(bval).to(dev).to(tdt)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)
+    B = (torch.rand((mb * bs, K), device=dev, generator=g) * 2 - 1).to(tdt)
+    C = torch.empty((mb * bs, K), device=dev)
+    h = ops.Handle()
+    fn = ops.bsrmm if dt == "fp32" else ops.bsrmm_f16
+
+    def step():
+        fn(d_brp, d_bci, d_bv, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K, handle=h)
+
+    elapsed, kms = timed_loop(step, h, args.steps, args.warmup, 1, dist)
+    # The CSR path on the same matrix (the reference's question: does the
+    # reordered BSR beat CSR?), fp32.
+    d_rp, d_ci, d_v = (torch.from_numpy(a).to(dev) for a in (rp, ci, val))
+    B32 = B.float()
+    C2 = torch.empty((n, K), device=dev)
+    h2 = ops.Handle()
+    _, csr_ms = timed_loop(lambda: ops.csrmm(d_rp, d_ci, d_v, B32, m=n, n=K, k=mb * bs, ldb=K,
+                                             C=C2, ldc=K, handle=h2), h2, 5, 2, 1, dist)
+    mfma_flops = 2.0 * nnzb * bs * bs * K
+    achieved = mfma_flops / (kms / 1e3) / 1e12
+    peak = MFMA_PEAK_TFLOPS[dt]
+    kbytes = bsr_bytes(mb, nnzb, bs, K, s)
+    rec = dict(
+        value=2.0 * nnz * K * args.steps / elapsed / 1e9, ms_per_step=elapsed / args.steps * 1e3,
+        dtype=dt,
+        data=("synthetic community-ordered graph (stand-in for the reordered dataset: "
+              "rabbit_order / Gorder outputs are not reproducible offline), U(-1,1) values"),
+        config={"workload": f"{args.workload}: csr2bsr bs={bs} + bsrmm K={K} {dt}", "n": n,
+                "nnz": nnz, "K": K, "bs": bs, "nnzb": nnzb,
+                "block_fill": round(nnz / (nnzb * bs * bs), 4), "parallelism": "single"},
+        roofline={"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                  "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                  "kernel": f"bsr{bs}_{'f32' if dt == 'fp32' else 'f16'}_mfma_kernel",
+                  "kernel_ms": round(kms, 4), "mfma_flops_per_launch": mfma_flops,
+                  "algorithmic_bytes_per_launch": kbytes,
+                  "algorithmic_GBps": round(kbytes / (kms / 1e3) / 1e9, 1)},
+        csr_same_matrix_ms=round(csr_ms, 4), csr2bsr_host_seconds=round(t_conv, 2),
+        gen_seconds=round(t_gen, 2))
+    return rec, None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="products_csr", choices=sorted(WORKLOADS))
+    ap.add_argument("--K", type=int, default=0, help="override the workload's K")
+    ap.add_argument("--waves-per-cu", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (DESIGN.md §7)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    W = WORKLOADS[args.workload]
+    rec, csr_inputs = (run_csr if W["kind"] == "csr" else run_bsr)(args, W, world, rank, dev, dist)
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(rp, ci, K)
-        rec = {
-            "metric": "SpMM GFLOP/s (2*nnz*K/t) + achieved HBM GB/s, ogbn-products K=128",
-            "value": round(value, 2),
-            "unit": "GFLOP/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 4),
-            "higher_is_better": True,
-            "scaling": "strong" if world > 1 else "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic (Chung-Lu power-law graph with ogbn-products n/nnz/max-degree, "
-                    "U(-1,1) values and B; OGB data not reachable offline)",
-            "config": {"workload": "csr_spmm ogbn-products-synthetic K=%d%s" %
-                                   (K, " row-partitioned + RCCL all-gather" if world > 1 else ""),
-                       "n": n, "nnz": nnz, "K": K, "max_deg": int(np.diff(rp).max()),
-                       "parallelism": f"rows{world}" if world > 1 else "single",
-                       "waves_per_cu": args.waves_per_cu or 16},
-            "roofline": {"bound": "hbm",
-                         "achieved": round(achieved, 1) if achieved else None,
-                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-                         "traffic": traffic,
-                         "kernel": "csr_mergepath_kernel<2>",
-                         "kernel_ms": round(kms, 4), "kernel_ms_max_rank": round(kms_max, 4),
-                         "algorithmic_bytes_per_launch": kbytes},
-            "cpu_baseline": cpu,
-            "gen_seconds": round(t_gen, 2),
-        }
-        print(json.dumps(rec), flush=True)
+        if (csr_inputs is not None and world == 1 and not args.no_cpu_baseline):
+            cpu = cpu_baseline(*csr_inputs)
+        out = {"metric": METRIC if args.workload == "products_csr" else
+               f"SpMM GFLOP/s (2*nnz*K/t), {args.workload}",
+               "value": round(rec.pop("value"), 2), "unit": "GFLOP/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(rec.pop("ms_per_step"), 4), "higher_is_better": True,
+               "scaling": "strong" if world > 1 else "weak", "vs_baseline": None}
+        out.update(rec)
+        out["cpu_baseline"] = cpu
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
