@@ -139,6 +139,8 @@ def run_csr(args, W, world, rank, dev, dist):
     h = ops.Handle()
     if args.waves_per_cu:
         h.set_csr_waves_per_cu(args.waves_per_cu)
+    if args.csr_options is not None:
+        h.set_csr_options(args.csr_options)
 
     def step():
         ops.csrmm(d_rp, d_ci, d_v, B, m=shard.rows, n=K, k=n, ldb=K, C=C_slot, ldc=K, handle=h)
@@ -171,7 +173,8 @@ def run_csr(args, W, world, rank, dev, dist):
                 (" row-partitioned + RCCL all-gather" if world > 1 else ""),
                 "n": n, "nnz": nnz, "K": K, "max_deg": int(np.diff(rp).max()),
                 "parallelism": f"rows{world}" if world > 1 else "single",
-                "waves_per_cu": args.waves_per_cu or 16},
+                "waves_per_cu": args.waves_per_cu or 16,
+                "csr_options": args.csr_options},
         roofline={"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                   "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                   "traffic": traffic, "kernel": f"csr_mergepath_kernel<{vec}>",
@@ -251,6 +254,7 @@ def main() -> None:
     ap.add_argument("--workload", default="products_csr", choices=sorted(WORKLOADS))
     ap.add_argument("--K", type=int, default=0, help="override the workload's K")
     ap.add_argument("--waves-per-cu", type=int, default=0)
+    ap.add_argument("--csr-options", type=int, default=None, help="SPMM_CSR_* flags")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (DESIGN.md §7)")

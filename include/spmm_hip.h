@@ -98,6 +98,11 @@ spmm_status_t spmm_get_kernel_times(spmm_handle_t handle, float* ms, int max_cou
  * is sized for (0 = default). */
 spmm_status_t spmm_set_csr_waves_per_cu(spmm_handle_t handle, int waves_per_cu);
 
+/* CSR kernel options (bit flags). SPMM_CSR_NT_STREAMS: read colind/val and
+ * write C with non-temporal hints, keeping L2 / MALL for the B gathers. */
+#define SPMM_CSR_NT_STREAMS 1
+spmm_status_t spmm_set_csr_options(spmm_handle_t handle, int flags);
+
 /* ------------------------------------------------------------------------ */
 /* Path A: CSR x dense                                                         */
 /* ------------------------------------------------------------------------ */

@@ -117,7 +117,7 @@ __device__ __forceinline__ int merge_search2(const int* __restrict__ rowptr, int
   return lo;
 }
 
-template <int VEC>
+template <int VEC, bool NT>
 __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
     int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, int base, const float* __restrict__ B, int ldb, float alpha,
@@ -178,7 +178,16 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
       for (int c = 0; c < VEC; ++c)
         vset<VEC>(out, c, __builtin_fmaf(beta, vget<VEC>(old, c), alpha * acc[c]));
     }
-    if (col_ok) vstore<VEC>(cp, out);
+    if (col_ok) {
+      if constexpr (NT) {
+        // C is written once and never re-read here: stream it past the
+        // caches so hub rows of B keep their L2 / MALL residency.
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) __builtin_nontemporal_store(vget<VEC>(out, c), cp + c);
+      } else {
+        vstore<VEC>(cp, out);
+      }
+    }
 #pragma unroll
     for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
   };
@@ -210,8 +219,13 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
         const int idx = min(cb + r, A1 - 1);
-        colv[r] = colind[idx];
-        valv[r] = val[idx];
+        if constexpr (NT) {
+          colv[r] = __builtin_nontemporal_load(colind + idx);
+          valv[r] = __builtin_nontemporal_load(val + idx);
+        } else {
+          colv[r] = colind[idx];
+          valv[r] = val[idx];
+        }
       }
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
@@ -395,20 +409,18 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   dim3 grid((nw + kWavesPerWG - 1) / kWavesPerWG, ntiles);
   dim3 block(kWG);
   const int slot = timing_begin(ctx);
-  switch (vec) {
-    case 4:
-      hipLaunchKernelGGL(csr_mergepath_kernel<4>, grid, block, 0, ctx->stream, m, n, rowptr,
-                         colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw);
-      break;
-    case 2:
-      hipLaunchKernelGGL(csr_mergepath_kernel<2>, grid, block, 0, ctx->stream, m, n, rowptr,
-                         colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw);
-      break;
-    default:
-      hipLaunchKernelGGL(csr_mergepath_kernel<1>, grid, block, 0, ctx->stream, m, n, rowptr,
-                         colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw);
-      break;
+  const bool nt = (ctx->csr_flags & SPMM_CSR_NT_STREAMS) != 0;
+#define SPMM_LAUNCH_MP(V, N)                                                                   \
+  hipLaunchKernelGGL((csr_mergepath_kernel<V, N>), grid, block, 0, ctx->stream, m, n, rowptr, \
+                     colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw)
+  if (vec == 4) {
+    if (nt) SPMM_LAUNCH_MP(4, true); else SPMM_LAUNCH_MP(4, false);
+  } else if (vec == 2) {
+    if (nt) SPMM_LAUNCH_MP(2, true); else SPMM_LAUNCH_MP(2, false);
+  } else {
+    if (nt) SPMM_LAUNCH_MP(1, true); else SPMM_LAUNCH_MP(1, false);
   }
+#undef SPMM_LAUNCH_MP
   timing_end(ctx, slot);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return from_hip(e);

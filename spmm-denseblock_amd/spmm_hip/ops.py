@@ -67,6 +67,9 @@ class Handle:
     def set_csr_waves_per_cu(self, w: int) -> None:
         check(lib().spmm_set_csr_waves_per_cu(self._h, w), "spmm_set_csr_waves_per_cu")
 
+    def set_csr_options(self, flags: int) -> None:
+        check(lib().spmm_set_csr_options(self._h, flags), "spmm_set_csr_options")
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             lib().spmm_destroy(self._h)
