@@ -42,6 +42,9 @@ WORKLOADS = {
                          bs=32, K=128, dtype="fp32"),
     "products_bsr16_f16": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                p_in=0.97, bs=16, K=512, dtype="fp16"),
+    # §8f next row: dense-block + CSR remainder (divide.cu) on the reddit stand-in
+    "reddit_hybrid32": dict(kind="hybrid", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
+                            p_in=0.99, bs=32, K=128, density=1.0 / 32),
 }
 METRIC = "SpMM GFLOP/s (2*nnz*K/t) + achieved HBM GB/s, ogbn-products K=128"
 
@@ -189,7 +192,7 @@ def run_bsr(args, W, world, rank, dev, dist):
     from spmm_hip import ops, prep
     if world > 1:
         raise SystemExit("BSR workloads are single-GPU configs (BASELINE configs 3 and 5)")
-    K, bs, dt = args.K or W["K"], W["bs"], W["dtype"]
+    K, bs, dt = args.K or W["K"], W["bs"], args.dtype or W["dtype"]
     t_gen = time.perf_counter()
     rp, ci = prep.community_csr(W["n"], W["avg_deg"], W["cmin"], W["cmax"], W["p_in"], 1234)
     n, nnz = rp.size - 1, ci.size
@@ -207,12 +210,22 @@ def run_bsr(args, W, world, rank, dev, dist):
     g = torch.Generator(device=dev)
     g.manual_seed(1234)
     B = (torch.rand((mb * bs, K), device=dev, generator=g) * 2 - 1).to(tdt)
-    C = torch.empty((mb * bs, K), device=dev)
     h = ops.Handle()
     fn = ops.bsrmm if dt == "fp32" else ops.bsrmm_f16
+    if args.bsr_layout == "col":
+        # cusparseSbsrmm's transB = N layout (run_bsrmm.cu:70-71): B and C
+        # column-major with ld = mb*bs.
+        Bc = B.t().contiguous()
+        C = torch.empty((K, mb * bs), device=dev)
 
-    def step():
-        fn(d_brp, d_bci, d_bv, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K, handle=h)
+        def step():
+            fn(d_brp, d_bci, d_bv, Bc, mb=mb, kb=mb, n=K, bs=bs, ldb=mb * bs,
+               order_b=ops.ORDER_COL, C=C, ldc=mb * bs, order_c=ops.ORDER_COL, handle=h)
+    else:
+        C = torch.empty((mb * bs, K), device=dev)
+
+        def step():
+            fn(d_brp, d_bci, d_bv, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K, handle=h)
 
     elapsed, kms = timed_loop(step, h, args.steps, args.warmup, 1, dist)
     # The CSR path on the same matrix (the reference's question: does the
@@ -233,6 +246,7 @@ def run_bsr(args, W, world, rank, dev, dist):
         data=("synthetic community-ordered graph (stand-in for the reordered dataset: "
               "rabbit_order / Gorder outputs are not reproducible offline), U(-1,1) values"),
         config={"workload": f"{args.workload}: csr2bsr bs={bs} + bsrmm K={K} {dt}", "n": n,
+                "layout_BC": args.bsr_layout,
                 "nnz": nnz, "K": K, "bs": bs, "nnzb": nnzb,
                 "block_fill": round(nnz / (nnzb * bs * bs), 4), "parallelism": "single"},
         roofline={"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
@@ -246,6 +260,56 @@ def run_bsr(args, W, world, rank, dev, dist):
     return rec, None
 
 
+def run_hybrid(args, W, world, rank, dev, dist):
+    """divide_matrix + hybrid SpMM (divide.cu:348-373): blocks with fill >=
+    density on the BSR MFMA kernel, the remainder on the CSR kernel, one C.
+    Reported beside pure-BSR and pure-CSR on the same matrix."""
+    import torch
+    from spmm_hip import ops, prep
+    if world > 1:
+        raise SystemExit("hybrid workloads are single-GPU")
+    K, bs, dens = args.K or W["K"], W["bs"], W["density"]
+    rp, ci = prep.community_csr(W["n"], W["avg_deg"], W["cmin"], W["cmax"], W["p_in"], 1234)
+    n, nnz = rp.size - 1, ci.size
+    val = np.random.default_rng(2).uniform(-1, 1, nnz).astype(np.float32)
+    t_div = time.perf_counter()
+    crp, cci, cv, brp, bci, bv = prep.divide(n, rp, ci, val, bs, dens)
+    t_div = time.perf_counter() - t_div
+    mb = (n + bs - 1) // bs
+    d = [torch.from_numpy(a).to(dev) for a in (crp, cci, cv, brp, bci, bv, rp, ci, val)]
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)
+    B = torch.rand((mb * bs, K), device=dev, generator=g) * 2 - 1
+    C = torch.empty((mb * bs, K), device=dev)
+    h = ops.Handle()
+
+    def step():
+        ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=C,
+                         ldc=K, handle=h)
+
+    elapsed, _ = timed_loop(step, h, args.steps, args.warmup, 1, dist)
+    h2 = ops.Handle()
+    _, csr_ms = timed_loop(lambda: ops.csrmm(d[6], d[7], d[8], B, m=n, n=K, k=mb * bs, ldb=K,
+                                             C=C, ldc=K, handle=h2), h2, 5, 2, 1, dist)
+    ms = elapsed / args.steps * 1e3
+    useful = 2.0 * nnz * K
+    rec = dict(
+        value=useful * args.steps / elapsed / 1e9, ms_per_step=ms, dtype="fp32",
+        data="synthetic community-ordered graph (stand-in for a reordered dataset)",
+        config={"workload": f"{args.workload}: divide(bs={bs}, density={dens}) + hybrid "
+                            f"BSR-MFMA/CSR K={K}", "n": n, "nnz": nnz, "K": K, "bs": bs,
+                "nnzb": int(bci.size), "csr_remainder_nnz": int(cci.size),
+                "bsr_fill": round((nnz - cci.size) / max(1, bci.size * bs * bs), 4),
+                "parallelism": "single"},
+        roofline={"bound": "hbm", "achieved": round(
+            (csr_bytes(n, int(cci.size), K) + bsr_bytes(mb, int(bci.size), bs, K, 4)) /
+            (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": None, "traffic": None, "kernel": "bsr32_f32_mfma + csr_mergepath"},
+        csr_same_matrix_ms=round(csr_ms, 4), divide_host_seconds=round(t_div, 2))
+    rec["roofline"]["frac"] = round(rec["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
+    return rec, None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,6 +317,10 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="products_csr", choices=sorted(WORKLOADS))
     ap.add_argument("--K", type=int, default=0, help="override the workload's K")
+    ap.add_argument("--dtype", choices=["fp32", "fp16"], default=None,
+                    help="override a BSR workload's value type")
+    ap.add_argument("--bsr-layout", choices=["row", "col"], default="row",
+                    help="B/C storage for BSR workloads (col = cusparse transB=N)")
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--csr-options", type=int, default=None, help="SPMM_CSR_* flags")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -274,7 +342,8 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=dev)
 
     W = WORKLOADS[args.workload]
-    rec, csr_inputs = (run_csr if W["kind"] == "csr" else run_bsr)(args, W, world, rank, dev, dist)
+    runner = {"csr": run_csr, "bsr": run_bsr, "hybrid": run_hybrid}[W["kind"]]
+    rec, csr_inputs = runner(args, W, world, rank, dev, dist)
 
     if rank == 0:
         cpu = None

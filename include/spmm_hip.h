@@ -219,6 +219,38 @@ int64_t spmm_calculate_nnzb(int n, const int* csrRowPtr, const int* csrColInd, i
  * Minimises the max over parts of (nnz + rows) by a prefix search on rowptr. */
 spmm_status_t spmm_csr_partition_rows(int m, const int* csrRowPtr, int nparts, int* bounds);
 
+/* divide_matrix (divide.cu:52-127), with values: the n x n CSR is split into
+ * a BSR part (DIRECTION_ROW) holding every bs x bs block whose fill
+ * (entries / bs^2) is >= density, and a CSR remainder holding the other
+ * entries in their original order. As in the reference, density <= 0 admits
+ * every block, empty ones included (divide.cu:91). Host pointers, two
+ * phases: sizes (csrRowPtr[n+1], bsrRowPtr[mb+1], totals), then fill.
+ * Duplicate entries inside a BSR block are summed. */
+spmm_status_t spmm_divide_nnz(int n, const int* rowPtr, const int* colInd, int blockDim,
+                              float density, int* csrRowPtr, int* bsrRowPtr, int* csrNnz,
+                              int* nnzb);
+spmm_status_t spmm_sdivide(int n, const int* rowPtr, const int* colInd, const float* val,
+                           int blockDim, float density, const int* csrRowPtr,
+                           const int* bsrRowPtr, int* csrColInd, float* csrVal, int* bsrColInd,
+                           float* bsrVal);
+
+/* ------------------------------------------------------------------------ */
+/* Hybrid dense-block + CSR-remainder SpMM (divide.cu:348-373)                */
+/* ------------------------------------------------------------------------ */
+
+/* C(m x n) = alpha * (A_bsr + A_csr) * B(k x n) + beta * C, row-major B and C.
+ * A_bsr is the BSR part of spmm_sdivide (bs x bs blocks, mb = ceil(m/bs)
+ * block rows), A_csr the remainder. When nnzb > 0, B must hold
+ * ceil(k/bs)*bs rows and C ceil(m/bs)*bs rows (padded, as the reference's
+ * drivers allocate them, run_bsrmm.cu:86-94). The BSR part runs on MFMA
+ * (writing C with beta), then the CSR part accumulates (beta = 1). */
+spmm_status_t spmm_hybrid_csrmm_f32(spmm_handle_t handle, int m, int n, int k, float alpha,
+                                    const int* csrRowPtr, const int* csrColInd,
+                                    const float* csrVal, int csrNnz, int blockDim,
+                                    const int* bsrRowPtr, const int* bsrColInd,
+                                    const float* bsrVal, int nnzb, const float* B, int ldb,
+                                    float beta, float* C, int ldc);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -279,4 +279,54 @@ void oracle_bsr2csr(int dir, int mb, int bs, const int* bsr_rowptr, const int* b
     }
 }
 
+// divide_matrix (divide.cu:52-127) with values: per block row, block column
+// bc is admitted to the BSR part iff count(bc)/bs^2 >= density (every column,
+// empty ones too, when density <= 0: 0 >= 0). Other entries stay CSR in
+// row order. Caller capacities: csr arrays >= nnz, bsr blocks >= cap_blocks.
+// out[0] = csr nnz, out[1] = nnzb; returns -1 if a capacity is exceeded.
+int oracle_divide(int n, int bs, float density, const int* rowptr, const int* colind,
+                  const float* val, int* csr_rp, int* csr_ci, float* csr_v, int* bsr_rp,
+                  int* bsr_ci, float* bsr_v, int64_t cap_blocks, int64_t* out) {
+  const int nb = (n + bs - 1) / bs;
+  const size_t bs2 = (size_t)bs * bs;
+  int64_t cpos = 0, bpos = 0;
+  csr_rp[0] = 0;
+  bsr_rp[0] = 0;
+  for (int br = 0; br < nb; ++br) {
+    std::map<int, int> cnt;
+    const int r0 = br * bs, r1 = std::min(n, r0 + bs);
+    for (int r = r0; r < r1; ++r)
+      for (int j = rowptr[r]; j < rowptr[r + 1]; ++j) cnt[colind[j] / bs] += 1;
+    std::map<int, int64_t> slot;
+    for (int bc = 0; bc < nb; ++bc) {
+      const auto it = cnt.find(bc);
+      const float occupy = (float)((it == cnt.end() ? 0 : it->second) * 1.0 / (double)bs2);
+      if (occupy >= density) {
+        if (bpos >= cap_blocks) return -1;
+        slot[bc] = bpos;
+        bsr_ci[bpos] = bc;
+        std::fill(bsr_v + bpos * bs2, bsr_v + (bpos + 1) * bs2, 0.f);
+        ++bpos;
+      }
+    }
+    bsr_rp[br + 1] = (int)bpos;
+    for (int r = r0; r < r1; ++r) {
+      for (int j = rowptr[r]; j < rowptr[r + 1]; ++j) {
+        const auto it = slot.find(colind[j] / bs);
+        if (it == slot.end()) {
+          csr_ci[cpos] = colind[j];
+          csr_v[cpos] = val[j];
+          ++cpos;
+        } else {
+          bsr_v[it->second * bs2 + (size_t)(r - r0) * bs + colind[j] % bs] += val[j];
+        }
+      }
+      csr_rp[r + 1] = (int)cpos;
+    }
+  }
+  out[0] = cpos;
+  out[1] = bpos;
+  return 0;
+}
+
 }  // extern "C"

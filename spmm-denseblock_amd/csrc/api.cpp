@@ -195,3 +195,31 @@ spmm_status_t spmm_sbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_opera
 }
 
 }  // extern "C"
+
+extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
+    spmm_handle_t handle, int m, int n, int k, float alpha, const int* csrRowPtr,
+    const int* csrColInd, const float* csrVal, int csrNnz, int blockDim, const int* bsrRowPtr,
+    const int* bsrColInd, const float* bsrVal, int nnzb, const float* B, int ldb, float beta,
+    float* C, int ldc) {
+  // divide.cu:348-373 runs csrmm2 and bsrmm back to back with alpha = beta = 1
+  // onto a zeroed C; here the BSR part applies the caller's beta and the CSR
+  // remainder accumulates on top, both on the handle's stream.
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (m < 0 || n < 0 || k < 0 || csrNnz < 0 || nnzb < 0 || blockDim <= 0)
+    return SPMM_STATUS_INVALID_VALUE;
+  if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  if (!csrRowPtr || !C || ldb < n || ldc < n || (k > 0 && !B)) return SPMM_STATUS_INVALID_VALUE;
+  if (nnzb > 0 && (!bsrRowPtr || !bsrColInd || !bsrVal)) return SPMM_STATUS_INVALID_VALUE;
+  if (csrNnz > 0 && (!csrColInd || !csrVal)) return SPMM_STATUS_INVALID_VALUE;
+  float csr_beta = beta;
+  if (nnzb > 0) {
+    const int mb = (m + blockDim - 1) / blockDim, kb = (k + blockDim - 1) / blockDim;
+    spmm_status_t st = launch_bsrmm_f32(handle, SPMM_DIRECTION_ROW, mb, kb, n, nnzb, blockDim,
+                                        alpha, bsrRowPtr, bsrColInd, bsrVal, B, ldb,
+                                        SPMM_ORDER_ROW, beta, C, ldc, SPMM_ORDER_ROW);
+    if (st != SPMM_STATUS_SUCCESS) return st;
+    csr_beta = 1.f;
+  }
+  return csrmm_impl(handle, m, n, k, csrNnz, alpha, csrRowPtr, csrColInd, csrVal, 0, B, ldb,
+                    SPMM_ORDER_ROW, csr_beta, C, ldc, SPMM_ORDER_ROW);
+}

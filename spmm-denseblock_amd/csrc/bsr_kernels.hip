@@ -36,17 +36,57 @@ __device__ __forceinline__ float epi(float acc, float alpha, float beta, const f
   return beta == 0.f ? alpha * acc : __builtin_fmaf(beta, *p, alpha * acc);
 }
 
+// Wave-uniform block-column cursor over bsr_col_ind[k0, k1): 64 entries held
+// one per lane, read with v_readlane (no dependent scalar load per block) and
+// refilled in place every 64 blocks. The refill waits right away (asm use),
+// so the common path after the branch carries no conservative vmcnt(0).
+struct ColCursor {
+  const int* colind;
+  int k1, lane, base, vec;
+  __device__ __forceinline__ ColCursor(const int* ci, int k0, int k1_, int lane_)
+      : colind(ci), k1(k1_), lane(lane_), base(k0) {
+    refill();
+  }
+  __device__ __forceinline__ void refill() {
+    vec = colind[min(base + lane, max(k1 - 1, 0))];
+    asm volatile("" : "+v"(vec));
+  }
+  // k must be visited in non-decreasing order.
+  __device__ __forceinline__ int get(int k) {
+    if (k - base >= 64) {
+      base += 64 * ((k - base) >> 6);
+      refill();
+    }
+    return __builtin_amdgcn_readlane(vec, k - base);
+  }
+};
+
 // ---------------------------------------------------------------------------
 // bs = 32 fp32 MFMA. Block = 4 waves, each wave a 32-column slice.
 // ---------------------------------------------------------------------------
-template <bool ROWDIR, bool BROW, bool CROW>
-__global__ __launch_bounds__(256) void bsr32_f32_mfma_kernel(
+// VAR (tuning variants; kBsr32Default is the shipped one):
+//   VAR & 3  pipeline: 0 = prefetch block k+1 into a second register set,
+//            1 = fixed-role double buffer, 2 = load-use (no prefetch; the
+//            other resident waves hide the latency)
+//   VAR & 4  XCD-aware block-row order (neighbouring block rows share an L2)
+//   VAR >> 3 minimum waves per SIMD requested from the register allocator
+//            (0 = no bound). Measured on the reddit stand-in:
+//            this kernel is bound by B-panel traffic beyond L2, so resident
+//            waves (memory-level parallelism) decide its speed.
+template <bool ROWDIR, bool BROW, bool CROW, int VAR>
+__global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr32_f32_mfma_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc) {
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int br = blockIdx.x;
+  int br = blockIdx.x;
+  if constexpr ((VAR & 4) != 0) {
+    // Round-robin dispatch puts block b on XCD b % 8: give each XCD a
+    // contiguous range of block rows instead (bijective for any mb).
+    const int q = mb / 8, rem = mb % 8, x = br % 8, i = br / 8;
+    br = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + i;
+  }
   const int j0 = (blockIdx.y * (blockDim.x >> 6) + wv) * 32;
   if (j0 >= n) return;
   const int r = lane & 31;
@@ -60,9 +100,9 @@ __global__ __launch_bounds__(256) void bsr32_f32_mfma_kernel(
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 
-  float a[16], b[16], an[16], bn[16];
+  ColCursor cc(colind, k0, k1, lane);
   auto load_frags = [&](int k, float (&fa)[16], float (&fb)[16]) {
-    const int bc = colind[k];
+    const int bc = cc.get(k);
     const float* ab = val + (size_t)k * 1024;
     if constexpr (ROWDIR) {
       const f32x4* p = reinterpret_cast<const f32x4*>(ab + r * 32 + 16 * h);
@@ -89,13 +129,38 @@ __global__ __launch_bounds__(256) void bsr32_f32_mfma_kernel(
     }
   };
 
-  if (k0 < k1) load_frags(k0, a, b);
-  for (int k = k0; k < k1; ++k) {
-    if (k + 1 < k1) load_frags(k + 1, an, bn);
+  auto mfma16 = [&](const float (&fa)[16], const float (&fb)[16]) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+    for (int s = 0; s < 16; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s], fb[s], acc, 0, 0, 0);
+  };
+  // Two fragment buffers with fixed roles (loop unrolled by 2): block k+1's
+  // loads are in flight while block k's MFMAs issue, and no register copy
+  // ties the MFMAs to the loads just issued. Prefetches are unconditional
+  // (index clamped to the last block; the tail re-reads it and skips the
+  // MFMAs), so no branch around a load makes hipcc's counted waits collapse.
+  float a0[16], b0[16], a1[16], b1[16];
+  const int kl = k1 - 1;
+  if (k0 < k1) load_frags(k0, a0, b0);
+  if constexpr ((VAR & 3) == 1) {
+    for (int k = k0; k < k1; k += 2) {
+      load_frags(min(k + 1, kl), a1, b1);
+      mfma16(a0, b0);
+      load_frags(min(k + 2, kl), a0, b0);
+      if (k + 1 < k1) mfma16(a1, b1);
+    }
+  } else if constexpr ((VAR & 3) == 2) {
+    for (int k = k0; k < k1; ++k) {
+      if (k > k0) load_frags(k, a0, b0);
+      mfma16(a0, b0);
+    }
+  } else {
+    for (int k = k0; k < k1; ++k) {
+      if (k + 1 < k1) load_frags(k + 1, a1, b1);
+      mfma16(a0, b0);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) { a[s] = an[s]; b[s] = bn[s]; }
+      for (int s = 0; s < 16; ++s) { a0[s] = a1[s]; b0[s] = b1[s]; }
+    }
   }
 
   if (!jok) return;
@@ -114,8 +179,8 @@ __global__ __launch_bounds__(256) void bsr32_f32_mfma_kernel(
 // ---------------------------------------------------------------------------
 // bs = 16 fp32 MFMA. Each wave: 16 rows x 64 columns (4 tiles of 16).
 // ---------------------------------------------------------------------------
-template <bool ROWDIR, bool BROW, bool CROW>
-__global__ __launch_bounds__(256) void bsr16_f32_mfma_kernel(
+template <bool ROWDIR, bool BROW, bool CROW, int VAR>
+__global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f32_mfma_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc) {
@@ -140,9 +205,9 @@ __global__ __launch_bounds__(256) void bsr16_f32_mfma_kernel(
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  float a[4], b[NT][4], an[4], bn[NT][4];
+  ColCursor cc(colind, k0, k1, lane);
   auto load_frags = [&](int k, float (&fa)[4], float (&fb)[NT][4]) {
-    const int bc = colind[k];
+    const int bc = cc.get(k);
     const float* ab = val + (size_t)k * 256;
     if constexpr (ROWDIR) {
       const f32x4 x = *reinterpret_cast<const f32x4*>(ab + r * 16 + 4 * q);
@@ -164,19 +229,44 @@ __global__ __launch_bounds__(256) void bsr16_f32_mfma_kernel(
     }
   };
 
-  if (k0 < k1) load_frags(k0, a, b);
-  for (int k = k0; k < k1; ++k) {
-    if (k + 1 < k1) load_frags(k + 1, an, bn);
+  auto mfma = [&](const float (&fa)[4], const float (&fb)[NT][4]) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[t][s], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s], fb[t][s], acc[t], 0, 0, 0);
+  };
+  float a0[4], b0[NT][4];
+  if constexpr ((VAR & 3) == 0) {
+    // Rotation prefetch: next block loaded under a branch, copied down after use.
+    float a1[4], b1[NT][4];
+    if (k0 < k1) load_frags(k0, a0, b0);
+    for (int k = k0; k < k1; ++k) {
+      if (k + 1 < k1) load_frags(k + 1, a1, b1);
+      mfma(a0, b0);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      a[s] = an[s];
+      for (int s = 0; s < 4; ++s) {
+        a0[s] = a1[s];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) b[t][s] = bn[t][s];
+        for (int t = 0; t < NT; ++t) b0[t][s] = b1[t][s];
+      }
+    }
+  } else if constexpr ((VAR & 3) == 2) {
+    // Load-use: latency hidden by occupancy alone (fewest VGPRs).
+    for (int k = k0; k < k1; ++k) {
+      load_frags(k, a0, b0);
+      mfma(a0, b0);
+    }
+  } else {
+    // Fixed-role double buffer, unconditional clamped prefetch (as bs = 32).
+    float a1[4], b1[NT][4];
+    const int kl = k1 - 1;
+    if (k0 < k1) load_frags(k0, a0, b0);
+    for (int k = k0; k < k1; k += 2) {
+      load_frags(min(k + 1, kl), a1, b1);
+      mfma(a0, b0);
+      load_frags(min(k + 2, kl), a0, b0);
+      if (k + 1 < k1) mfma(a1, b1);
     }
   }
 
@@ -197,8 +287,8 @@ __global__ __launch_bounds__(256) void bsr16_f32_mfma_kernel(
 // bs = 16 fp16 MFMA (v_mfma_f32_16x16x32_f16): two blocks per instruction.
 // Lane quad q: q < 2 -> block b, k = 8q + e; q >= 2 -> block b+1, k = 8(q-2) + e.
 // ---------------------------------------------------------------------------
-template <bool ROWDIR, bool BROW, bool CROW>
-__global__ __launch_bounds__(256) void bsr16_f16_mfma_kernel(
+template <bool ROWDIR, bool BROW, bool CROW, int VAR>
+__global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f16_mfma_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
     float beta, float* __restrict__ C, int ldc) {
@@ -225,23 +315,23 @@ __global__ __launch_bounds__(256) void bsr16_f16_mfma_kernel(
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  f16x8 a, b[NT], an, bn[NT];
-  // k: first block of the pair; kk = k + half is this lane's block.
+  ColCursor cc(colind, k0, k1, lane);
+  // k: first block of the pair; kk = k + half is this lane's block. When the
+  // pair is incomplete the second half re-reads block k and is zeroed at use.
+  // k is clamped by the caller to <= k1 - 1; both cursor reads are
+  // unconditional (no branch around a load).
   auto load_frags = [&](int k, f16x8& fa, f16x8 (&fb)[NT]) {
-    const int kk = k + half;
-    const bool valid = kk < k1;
-    const int kl = valid ? kk : k;  // in-bounds block for the dummy half
-    const int bc = colind[kl];
+    const int k2 = min(k + 1, k1 - 1);
+    const int bc0 = cc.get(k);
+    const int bc1 = cc.get(k2);
+    const int kl = half ? k2 : k;
+    const int bc = half ? bc1 : bc0;
     const _Float16* ab = val + (size_t)kl * 256;
     if constexpr (ROWDIR) {
       fa = *reinterpret_cast<const f16x8*>(ab + r * 16 + kq);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) fa[e] = ab[(kq + e) * 16 + r];
-    }
-    if (!valid) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) fa[e] = (_Float16)0.f;
     }
     const size_t krow = (size_t)bc * 16 + kq;
 #pragma unroll
@@ -255,15 +345,42 @@ __global__ __launch_bounds__(256) void bsr16_f16_mfma_kernel(
     }
   };
 
-  if (k0 < k1) load_frags(k0, a, b);
-  for (int k = k0; k < k1; k += 2) {
-    if (k + 2 < k1) load_frags(k + 2, an, bn);
+  const f16x8 zero8 = {};
+  auto mfma = [&](const f16x8& fa, const f16x8 (&fb)[NT], int k) {
+    // Lanes of the missing second block of an odd tail contribute zero.
+    const f16x8 fz = (half && k + 1 >= k1) ? zero8 : fa;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[t], acc[t], 0, 0, 0);
-    a = an;
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fz, fb[t], acc[t], 0, 0, 0);
+  };
+  f16x8 a0, b0[NT];
+  if constexpr ((VAR & 3) == 0) {
+    // Rotation prefetch: next pair loaded under a branch, copied down after use.
+    f16x8 a1, b1[NT];
+    if (k0 < k1) load_frags(k0, a0, b0);
+    for (int k = k0; k < k1; k += 2) {
+      if (k + 2 < k1) load_frags(k + 2, a1, b1);
+      mfma(a0, b0, k);
+      a0 = a1;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) b[t] = bn[t];
+      for (int t = 0; t < NT; ++t) b0[t] = b1[t];
+    }
+  } else if constexpr ((VAR & 3) == 2) {
+    // Load-use over block pairs: latency hidden by occupancy alone.
+    for (int k = k0; k < k1; k += 2) {
+      load_frags(k, a0, b0);
+      mfma(a0, b0, k);
+    }
+  } else {
+    f16x8 a1, b1[NT];  // fixed-role double buffer over block pairs
+    const int kl = k1 - 1;
+    if (k0 < k1) load_frags(k0, a0, b0);
+    for (int k = k0; k < k1; k += 4) {
+      load_frags(min(k + 2, kl), a1, b1);
+      mfma(a0, b0, k);
+      load_frags(min(k + 4, kl), a0, b0);
+      if (k + 2 < k1) mfma(a1, b1, k + 2);
+    }
   }
 
   const size_t row0 = (size_t)br * 16 + 4 * q;
@@ -313,23 +430,38 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
   }
 }
 
-#define SPMM_BSR_DISPATCH(KERNEL, GRID, BLOCK, STREAM, ROWD, BR, CR, ...)                   \
+constexpr int kBsr32Default = 40;
+constexpr int kBsr16Default = 9;     // fp32 bs 16
+constexpr int kBsr16F16Default = 9;  // fp16 bs 16
+
+// SPMM_BSR_VARIANT=<v> overrides the variant of the row/row/row launch of
+// the bs 32 and bs 16 kernels (tuning sweeps only; tools/bsr_variants.sh).
+int variant_override() {
+  static const int var = [] {
+    const char* e = getenv("SPMM_BSR_VARIANT");
+    return e ? atoi(e) : -1;
+  }();
+  return var;
+}
+#define SPMM_COMMA ,
+
+#define SPMM_BSR_DISPATCH(KERNEL, TA, GRID, BLOCK, STREAM, ROWD, BR, CR, ...)                 \
   do {                                                                                    \
     if (ROWD) {                                                                           \
       if (BR) {                                                                           \
-        if (CR) hipLaunchKernelGGL((KERNEL<true, true, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);   \
-        else hipLaunchKernelGGL((KERNEL<true, true, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);     \
+        if (CR) hipLaunchKernelGGL((KERNEL<true, true, true TA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);   \
+        else hipLaunchKernelGGL((KERNEL<true, true, false TA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);     \
       } else {                                                                            \
-        if (CR) hipLaunchKernelGGL((KERNEL<true, false, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
-        else hipLaunchKernelGGL((KERNEL<true, false, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);    \
+        if (CR) hipLaunchKernelGGL((KERNEL<true, false, true TA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
+        else hipLaunchKernelGGL((KERNEL<true, false, false TA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);    \
       }                                                                                   \
     } else {                                                                              \
       if (BR) {                                                                           \
-        if (CR) hipLaunchKernelGGL((KERNEL<false, true, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
-        else hipLaunchKernelGGL((KERNEL<false, true, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);    \
+        if (CR) hipLaunchKernelGGL((KERNEL<false, true, true TA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
+        else hipLaunchKernelGGL((KERNEL<false, true, false TA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);    \
       } else {                                                                            \
-        if (CR) hipLaunchKernelGGL((KERNEL<false, false, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__); \
-        else hipLaunchKernelGGL((KERNEL<false, false, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);   \
+        if (CR) hipLaunchKernelGGL((KERNEL<false, false, true TA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__); \
+        else hipLaunchKernelGGL((KERNEL<false, false, false TA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);   \
       }                                                                                   \
     }                                                                                     \
   } while (0)
@@ -356,13 +488,33 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   if (bs == 32 && vec_ok) {
     const int waves = n <= 32 ? 1 : (n <= 64 ? 2 : 4);
     dim3 grid(mb, (n + 32 * waves - 1) / (32 * waves));
-    SPMM_BSR_DISPATCH(bsr32_f32_mfma_kernel, grid, dim3(64 * waves), ctx->stream, rowd, brow, crow,
-                      mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    const int var = variant_override();
+    if (var >= 0 && rowd && brow && crow) {
+      switch (var) {
+#define V(x) case x: hipLaunchKernelGGL((bsr32_f32_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
+        V(40) V(44) V(42) V(50) V(58) V(66) V(41) V(49)
+#undef V
+        default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
+      }
+    } else {
+      SPMM_BSR_DISPATCH(bsr32_f32_mfma_kernel, SPMM_COMMA kBsr32Default, grid, dim3(64 * waves), ctx->stream, rowd, brow,
+                        crow, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    }
   } else if (bs == 16 && vec_ok) {
     const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
     dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
-    SPMM_BSR_DISPATCH(bsr16_f32_mfma_kernel, grid, dim3(64 * waves), ctx->stream, rowd, brow, crow,
-                      mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    const int var = variant_override();
+    if (var >= 0 && rowd && brow && crow) {
+      switch (var) {
+#define V(x) case x: hipLaunchKernelGGL((bsr16_f32_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
+        V(8) V(9) V(10) V(24) V(32) V(40) V(34) V(66)
+#undef V
+        default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
+      }
+    } else {
+      SPMM_BSR_DISPATCH(bsr16_f32_mfma_kernel, SPMM_COMMA kBsr16Default, grid, dim3(64 * waves), ctx->stream,
+                        rowd, brow, crow, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    }
   } else {
     dim3 grid(mb, (n + 63) / 64);
     hipLaunchKernelGGL(bsr_generic_kernel<float>, grid, dim3(256), 0, ctx->stream, mb, n, bs,
@@ -390,8 +542,18 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   if (bs == 16 && vec_ok) {
     const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
     dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
-    SPMM_BSR_DISPATCH(bsr16_f16_mfma_kernel, grid, dim3(64 * waves), ctx->stream, rowd, brow, crow,
-                      mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    const int var = variant_override();
+    if (var >= 0 && rowd && brow && crow) {
+      switch (var) {
+#define V(x) case x: hipLaunchKernelGGL((bsr16_f16_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
+        V(8) V(9) V(10) V(24) V(32) V(40) V(34) V(66)
+#undef V
+        default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
+      }
+    } else {
+      SPMM_BSR_DISPATCH(bsr16_f16_mfma_kernel, SPMM_COMMA kBsr16F16Default, grid, dim3(64 * waves), ctx->stream,
+                        rowd, brow, crow, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    }
   } else {
     dim3 grid(mb, (n + 63) / 64);
     hipLaunchKernelGGL(bsr_generic_kernel<_Float16>, grid, dim3(256), 0, ctx->stream, mb, n, bs,

@@ -27,7 +27,7 @@ struct spmm_context {
   int device = 0;
   int num_cus = 256;
   int csr_waves_per_cu = 0;  // 0 = default
-  int csr_flags = 0;         // SPMM_CSR_* option bits
+  int csr_flags = SPMM_CSR_NT_STREAMS;  // SPMM_CSR_* option bits (default: nt streams)
 
   // Device workspace (grown, never shrunk; freed in spmm_destroy).
   void* ws = nullptr;

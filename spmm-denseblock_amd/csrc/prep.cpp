@@ -185,3 +185,130 @@ spmm_status_t spmm_csr_partition_rows(int m, const int* csrRowPtr, int nparts, i
 }
 
 }  // extern "C"
+
+// ----------------------------------------------------------------------------
+// divide_matrix (divide.cu:52-127) with values.
+// ----------------------------------------------------------------------------
+namespace {
+
+// Per block row: entry counts per block column (over the block row's rows),
+// and the admitted block columns in ascending order. `cnt` has nb entries,
+// zero on entry and on exit; `touched` lists the columns with a count.
+struct DivideScratch {
+  std::vector<int> cnt, touched, slot;
+  explicit DivideScratch(int nb) : cnt(std::max(nb, 1), 0), slot(std::max(nb, 1), -1) {}
+};
+
+// Returns false on an out-of-range column. Fills `adm` with the admitted
+// block columns (ascending).
+bool divide_block_row(int br, int bs, int n, int nb, const int* rowptr, const int* colind,
+                      int base, float density, DivideScratch& s, std::vector<int>& adm) {
+  adm.clear();
+  s.touched.clear();
+  const int r0 = br * bs, r1 = std::min(n, r0 + bs);
+  for (int r = r0; r < r1; ++r)
+    for (int j = rowptr[r] - base; j < rowptr[r + 1] - base; ++j) {
+      const int c = colind[j] - base;
+      if (c < 0 || c / bs >= nb) {
+        for (int t : s.touched) s.cnt[t] = 0;
+        return false;
+      }
+      if (s.cnt[c / bs]++ == 0) s.touched.push_back(c / bs);
+    }
+  const double bnum = (double)bs * bs;
+  if (density <= 0.f) {
+    // 0 >= 0: every block column is admitted, empty ones included (divide.cu:91).
+    for (int bc = 0; bc < nb; ++bc) adm.push_back(bc);
+  } else {
+    for (int bc : s.touched)
+      if ((float)(s.cnt[bc] / bnum) >= density) adm.push_back(bc);
+    std::sort(adm.begin(), adm.end());
+  }
+  for (int t : s.touched) s.cnt[t] = 0;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+spmm_status_t spmm_divide_nnz(int n, const int* rowPtr, const int* colInd, int blockDim,
+                              float density, int* csrRowPtr, int* bsrRowPtr, int* csrNnz,
+                              int* nnzb) {
+  if (n < 0 || blockDim <= 0) return SPMM_STATUS_INVALID_VALUE;
+  if (!rowPtr || !csrRowPtr || !bsrRowPtr || !csrNnz || !nnzb) return SPMM_STATUS_INVALID_VALUE;
+  const int bs = blockDim, nb = ceil_div(n, bs), mb = nb;
+  const int base = n > 0 ? rowPtr[0] : 0;
+  if (n > 0 && rowPtr[n] - base > 0 && !colInd) return SPMM_STATUS_INVALID_VALUE;
+  DivideScratch s(nb);
+  std::vector<int> adm;
+  long long nb_acc = 0, c_acc = 0;
+  csrRowPtr[0] = 0;
+  bsrRowPtr[0] = 0;
+  for (int br = 0; br < mb; ++br) {
+    if (!divide_block_row(br, bs, n, nb, rowPtr, colInd, base, density, s, adm))
+      return SPMM_STATUS_INVALID_VALUE;
+    nb_acc += (long long)adm.size();
+    for (int bc : adm) s.slot[bc] = 1;
+    const int r0 = br * bs, r1 = std::min(n, r0 + bs);
+    for (int r = r0; r < r1; ++r) {
+      for (int j = rowPtr[r] - base; j < rowPtr[r + 1] - base; ++j)
+        if (s.slot[(colInd[j] - base) / bs] < 0) ++c_acc;
+      csrRowPtr[r + 1] = (int)c_acc;
+    }
+    for (int bc : adm) s.slot[bc] = -1;
+    if (nb_acc > INT32_MAX || c_acc > INT32_MAX) return SPMM_STATUS_INVALID_VALUE;
+    bsrRowPtr[br + 1] = (int)nb_acc;
+  }
+  *csrNnz = (int)c_acc;
+  *nnzb = (int)nb_acc;
+  return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t spmm_sdivide(int n, const int* rowPtr, const int* colInd, const float* val,
+                           int blockDim, float density, const int* csrRowPtr,
+                           const int* bsrRowPtr, int* csrColInd, float* csrVal, int* bsrColInd,
+                           float* bsrVal) {
+  if (n < 0 || blockDim <= 0) return SPMM_STATUS_INVALID_VALUE;
+  if (!rowPtr || !csrRowPtr || !bsrRowPtr) return SPMM_STATUS_INVALID_VALUE;
+  const int bs = blockDim, nb = ceil_div(n, bs), mb = nb;
+  const int base = n > 0 ? rowPtr[0] : 0;
+  if (n > 0 && rowPtr[n] - base > 0 && (!colInd || !val)) return SPMM_STATUS_INVALID_VALUE;
+  if ((csrRowPtr[n] > 0 && (!csrColInd || !csrVal)) ||
+      (bsrRowPtr[mb] > 0 && (!bsrColInd || !bsrVal)))
+    return SPMM_STATUS_INVALID_VALUE;
+  const size_t bs2 = (size_t)bs * bs;
+  DivideScratch s(nb);
+  std::vector<int> adm;
+  for (int br = 0; br < mb; ++br) {
+    if (!divide_block_row(br, bs, n, nb, rowPtr, colInd, base, density, s, adm))
+      return SPMM_STATUS_INVALID_VALUE;
+    const int k0 = bsrRowPtr[br];
+    if (bsrRowPtr[br + 1] - k0 != (int)adm.size()) return SPMM_STATUS_INVALID_VALUE;
+    for (size_t t = 0; t < adm.size(); ++t) {
+      bsrColInd[k0 + t] = adm[t];
+      s.slot[adm[t]] = k0 + (int)t;
+    }
+    if (!adm.empty()) std::memset(bsrVal + (size_t)k0 * bs2, 0, adm.size() * bs2 * sizeof(float));
+    const int r0 = br * bs, r1 = std::min(n, r0 + bs);
+    for (int r = r0; r < r1; ++r) {
+      int pos = csrRowPtr[r];
+      for (int j = rowPtr[r] - base; j < rowPtr[r + 1] - base; ++j) {
+        const int c = colInd[j] - base;
+        const int k = s.slot[c / bs];
+        if (k < 0) {
+          csrColInd[pos] = c;
+          csrVal[pos] = val[j];
+          ++pos;
+        } else {
+          bsrVal[(size_t)k * bs2 + (size_t)(r - r0) * bs + c % bs] += val[j];
+        }
+      }
+      if (pos != csrRowPtr[r + 1]) return SPMM_STATUS_INVALID_VALUE;
+    }
+    for (int bc : adm) s.slot[bc] = -1;
+  }
+  return SPMM_STATUS_SUCCESS;
+}
+
+}  // extern "C"

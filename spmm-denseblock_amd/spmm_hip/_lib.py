@@ -82,6 +82,10 @@ _PROTOS = {
     "spmm_sbsr2csr": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, _P]),
     "spmm_calculate_nnzb": (c_int64, [c_int, _P, _P, c_int]),
     "spmm_csr_partition_rows": (c_int, [c_int, _P, c_int, _P]),
+    "spmm_divide_nnz": (c_int, [c_int, _P, _P, c_int, c_float, _P, _P, _PI, _PI]),
+    "spmm_sdivide": (c_int, [c_int, _P, _P, _P, c_int, c_float, _P, _P, _P, _P, _P, _P]),
+    "spmm_hybrid_csrmm_f32": (c_int, [_P, c_int, c_int, c_int, c_float, _P, _P, _P, c_int, c_int,
+                                      _P, _P, _P, c_int, _P, c_int, c_float, _P, c_int]),
     # spmm_host.h
     "spmm_host_free": (None, [_P]),
     "spmm_host_rng_seed": (None, [c_uint64]),

@@ -167,5 +167,27 @@ def bsrmm_f16(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: 
     return C
 
 
-__all__ = ["Handle", "default_handle", "gespmm_csrmm", "csrmm", "bsrmm", "bsrmm_f16",
+def hybrid_csrmm(csr: tuple, bsr: tuple, B: torch.Tensor, *, m: int, n: int, k: int, bs: int,
+                 ldb: int, C: torch.Tensor, ldc: int, alpha: float = 1.0, beta: float = 0.0,
+                 handle: Handle | None = None) -> torch.Tensor:
+    """Dense-block + CSR-remainder SpMM (divide.cu:348-373) on one stream:
+    csr = (rowptr, colind, val), bsr = (rowptr, colind, val) from
+    prep.divide; row-major B and C (padded to whole blocks when the BSR part
+    is non-empty)."""
+    crp, cci, cv = csr
+    brp, bci, bv = bsr
+    for t, dt, nm in ((crp, torch.int32, "csr_rowptr"), (cci, torch.int32, "csr_colind"),
+                      (cv, torch.float32, "csr_val"), (brp, torch.int32, "bsr_rowptr"),
+                      (bci, torch.int32, "bsr_colind"), (bv, torch.float32, "bsr_val"),
+                      (B, torch.float32, "B"), (C, torch.float32, "C")):
+        _need(t, dt, nm)
+    h = handle or default_handle()
+    check(lib().spmm_hybrid_csrmm_f32(h.raw, m, n, k, alpha, _ptr(crp), _ptr(cci), _ptr(cv),
+                                      cci.numel(), bs, _ptr(brp), _ptr(bci), _ptr(bv),
+                                      bci.numel(), _ptr(B), ldb, beta, _ptr(C), ldc),
+          "spmm_hybrid_csrmm_f32")
+    return C
+
+
+__all__ = ["Handle", "hybrid_csrmm", "default_handle", "gespmm_csrmm", "csrmm", "bsrmm", "bsrmm_f16",
            "SpmmError", "ORDER_ROW", "ORDER_COL"]

@@ -80,6 +80,26 @@ def calculate_nnzb(n: int, rowptr, colind, bs: int) -> int:
     return int(r)
 
 
+def divide(n: int, rowptr, colind, val, bs: int, density: float):
+    """divide_matrix (divide.cu:52-127) with values: blocks with fill >= density
+    -> BSR (DIRECTION_ROW), the rest -> CSR remainder. Returns
+    (csr_rowptr, csr_colind, csr_val, bsr_rowptr, bsr_colind, bsr_val)."""
+    rowptr, colind, val = _i32(rowptr), _i32(colind), _f32(val)
+    mb = (n + bs - 1) // bs
+    crp = np.zeros(n + 1, dtype=np.int32)
+    brp = np.zeros(mb + 1, dtype=np.int32)
+    cn, nb = c_int(0), c_int(0)
+    check(lib().spmm_divide_nnz(n, _p(rowptr), _p(colind), bs, density, _p(crp), _p(brp),
+                                byref(cn), byref(nb)), "spmm_divide_nnz")
+    cci = np.zeros(cn.value, dtype=np.int32)
+    cv = np.zeros(cn.value, dtype=np.float32)
+    bci = np.zeros(nb.value, dtype=np.int32)
+    bv = np.zeros(nb.value * bs * bs, dtype=np.float32)
+    check(lib().spmm_sdivide(n, _p(rowptr), _p(colind), _p(val), bs, density, _p(crp), _p(brp),
+                             _p(cci), _p(cv), _p(bci), _p(bv)), "spmm_sdivide")
+    return crp, cci, cv, brp, bci, bv
+
+
 def partition_rows(rowptr, nparts: int) -> np.ndarray:
     """nnz-balanced contiguous row split: bounds[nparts+1]."""
     rowptr = _i32(rowptr)

@@ -47,6 +47,7 @@ def load_oracle() -> ctypes.CDLL:
         "oracle_csr2bsr_nnz": (I64, [I, I, P, P, P]),
         "oracle_csr2bsr": (None, [I, I, I, P, P, P, P, P, P]),
         "oracle_bsr2csr": (None, [I, I, I, P, P, P, P, P, P]),
+        "oracle_divide": (I, [I, I, F, P, P, P, P, P, P, P, P, P, I64, P]),
     }
     for k, (r, a) in sig.items():
         f = getattr(L, k)
@@ -122,6 +123,24 @@ def oracle_bsrmm_f64(L, direction, mb, n, bs, rowptr, colind, val, B, ldb, order
     L.oracle_bsrmm_f64(direction, mb, n, bs, *[ptr(a) for a in args], ldb, order_b, int(half),
                        ptr(C), ptr(A))
     return C, A
+
+
+def oracle_divide(L, n, bs, density, rowptr, colind, val):
+    """divide_matrix with values -> (csr_rp, csr_ci, csr_v, bsr_rp, bsr_ci, bsr_v)."""
+    rowptr = np.ascontiguousarray(rowptr, np.int32)
+    colind = np.ascontiguousarray(colind, np.int32)
+    val = np.ascontiguousarray(val, np.float32)
+    nb = (n + bs - 1) // bs
+    cap = nb * nb if density <= 0 else max(colind.size, 1)
+    crp, cci, cv = (np.zeros(n + 1, np.int32), np.zeros(max(colind.size, 1), np.int32),
+                    np.zeros(max(colind.size, 1), np.float32))
+    brp, bci, bv = np.zeros(nb + 1, np.int32), np.zeros(cap, np.int32), \
+        np.zeros(cap * bs * bs, np.float32)
+    out = np.zeros(2, np.int64)
+    assert L.oracle_divide(n, bs, density, ptr(rowptr), ptr(colind), ptr(val), ptr(crp),
+                           ptr(cci), ptr(cv), ptr(brp), ptr(bci), ptr(bv), cap, ptr(out)) == 0
+    c, b = int(out[0]), int(out[1])
+    return crp, cci[:c].copy(), cv[:c].copy(), brp, bci[:b].copy(), bv[:b * bs * bs].copy()
 
 
 def assert_normwise(got, ref64, absdot, tol, what=""):

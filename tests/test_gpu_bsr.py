@@ -154,6 +154,31 @@ def test_csr_vs_bsr_differential(oracle, device):
     assert float((C1 - C2).abs().max()) < 1e-4
 
 
+@pytest.mark.parametrize("bs,density", [(16, 0.05), (32, 1.0 / 32), (32, 0.0), (8, 0.3)])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.5, 1.5)])
+def test_hybrid_divide_spmm(oracle, device, bs, density, alpha, beta):
+    """divide.cu:348-373: BSR part (fill >= density) on MFMA + CSR remainder,
+    one C; equals the plain CSR product of the whole matrix."""
+    from spmm_hip import prep
+    n, K = 700, 96
+    rp, ci = prep.community_csr(n, 40.0, 48, 160, 0.9, 3)
+    v = np.random.default_rng(4).uniform(-1, 1, ci.size).astype(np.float32)
+    parts = prep.divide(n, rp, ci, v, bs, density)
+    nb = (n + bs - 1) // bs
+    Bp = np.zeros((nb * bs, K), np.float32)
+    Bp[:n] = np.random.default_rng(5).uniform(-1, 1, (n, K))
+    C0 = np.random.default_rng(6).uniform(-1, 1, (nb * bs, K)).astype(np.float32)
+    d = _dev(*parts, Bp, C0)
+    _ops().hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), d[6], m=n, n=K, k=n, bs=bs, ldb=K,
+                        C=d[7], ldc=K, alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    ref, absd = oracle_csrmm_f64(oracle, n, K, rp, ci, v, Bp, K, 0)
+    got = d[7].cpu().numpy()[:n]
+    assert_normwise(got, alpha * ref + beta * C0[:n].astype(np.float64),
+                    abs(alpha) * absd + abs(beta) * np.abs(C0[:n]), TOL_F32,
+                    f"hybrid bs={bs} density={density}")
+
+
 def test_bsr_status_codes(device):
     """rocsparse_bsrmm.h:109-176 argument checks."""
     from spmm_hip._lib import (INVALID_VALUE, MATRIX_TYPE_NOT_SUPPORTED, NOT_INITIALIZED,

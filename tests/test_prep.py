@@ -78,6 +78,43 @@ def test_csr2bsr_bsr2csr_vs_oracle(oracle, golden, bs, direction):
     assert crp[-1] == nnzb * bs * bs  # bsr2csr.cu:177
 
 
+@pytest.mark.parametrize("g", ["rand300", "band200"])
+@pytest.mark.parametrize("bs", [2, 4, 16, 32])
+@pytest.mark.parametrize("tag,density", [("all", 1e-9), ("d25", 0.25)])
+def test_divide_bit_exact_vs_reference(oracle, golden, g, bs, tag, density):
+    """divide_matrix (divide.cu:52-127): BSR part and CSR remainder equal the
+    reference's own output on unit values, and the oracle's restatement."""
+    from helpers import oracle_divide
+    prep = _prep()
+    r = golden["ref"]
+    rp, ci = r[f"{g}_rowptr"], r[f"{g}_colind"]
+    n = rp.size - 1
+    ones = np.ones(ci.size, np.float32)
+    out = prep.divide(n, rp, ci, ones, bs, density)
+    ref = [r[f"{g}_bs{bs}_{tag}_{nm}"] for nm in ("csr_rp", "csr_ci", "bsr_rp", "bsr_ci",
+                                                  "bsr_val")]
+    crp, cci, cv, brp, bci, bv = out
+    for got, want in zip((crp, cci, brp, bci, bv), ref):
+        assert np.array_equal(got, want)
+    assert np.all(cv == 1.0)
+    for got, want in zip(out, oracle_divide(oracle, n, bs, density, rp, ci, ones)):
+        assert np.array_equal(got, want)
+
+
+def test_divide_density_zero_admits_empty_blocks(oracle):
+    """divide.cu:91: occupancy 0 >= density 0, so every block is admitted."""
+    from helpers import oracle_divide
+    prep = _prep()
+    rp = np.array([0, 1, 1, 2, 2], np.int32)
+    ci = np.array([0, 3], np.int32)
+    v = np.array([2.0, 3.0], np.float32)
+    crp, cci, cv, brp, bci, bv = prep.divide(4, rp, ci, v, 2, 0.0)
+    assert brp.tolist() == [0, 2, 4] and bci.tolist() == [0, 1, 0, 1] and cci.size == 0
+    assert bv.reshape(4, 4)[0, 0] == 2.0 and bv.reshape(4, 4)[3, 1] == 3.0
+    for got, want in zip((crp, cci, cv, brp, bci, bv), oracle_divide(oracle, 4, 2, 0.0, rp, ci, v)):
+        assert np.array_equal(got, want)
+
+
 def test_csr2bsr_duplicates_are_summed_and_errors():
     prep = _prep()
     rp = np.array([0, 3], np.int32)
