@@ -42,6 +42,12 @@ WORKLOADS = {
                          bs=32, K=128, dtype="fp32"),
     "products_bsr16_f16": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                p_in=0.97, bs=16, K=512, dtype="fp16"),
+    # north_star's BSR target (>= 40 % fp32 MFMA, products, K=128) on the
+    # community-ordered products stand-in
+    "products_bsr32": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                           p_in=0.97, bs=32, K=128, dtype="fp32"),
+    "products_hybrid32": dict(kind="hybrid", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                              p_in=0.97, bs=32, K=128, density=1.0 / 32),
     # §8f next row: dense-block + CSR remainder (divide.cu) on the reddit stand-in
     "reddit_hybrid32": dict(kind="hybrid", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
                             p_in=0.99, bs=32, K=128, density=1.0 / 32),

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f32_mf
 
   ColCursor cc(colind, k0, k1, lane);
   auto load_frags = [&](int k, float (&fa)[4], float (&fb)[NT][4]) {
-    const int bc = cc.get(k);
+    const int bc = (VAR & 4) != 0 ? colind[k] : cc.get(k);
     const float* ab = val + (size_t)k * 256;
     if constexpr (ROWDIR) {
       const f32x4 x = *reinterpret_cast<const f32x4*>(ab + r * 16 + 4 * q);
@@ -322,10 +322,15 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f16_mf
   // unconditional (no branch around a load).
   auto load_frags = [&](int k, f16x8& fa, f16x8 (&fb)[NT]) {
     const int k2 = min(k + 1, k1 - 1);
-    const int bc0 = cc.get(k);
-    const int bc1 = cc.get(k2);
     const int kl = half ? k2 : k;
-    const int bc = half ? bc1 : bc0;
+    int bc;
+    if constexpr ((VAR & 4) != 0) {
+      bc = colind[kl];  // per-lane load (two addresses per wave)
+    } else {
+      const int bc0 = cc.get(k);
+      const int bc1 = cc.get(k2);
+      bc = half ? bc1 : bc0;
+    }
     const _Float16* ab = val + (size_t)kl * 256;
     if constexpr (ROWDIR) {
       fa = *reinterpret_cast<const f16x8*>(ab + r * 16 + kq);
@@ -431,8 +436,8 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 }
 
 constexpr int kBsr32Default = 40;
-constexpr int kBsr16Default = 9;     // fp32 bs 16
-constexpr int kBsr16F16Default = 9;  // fp16 bs 16
+constexpr int kBsr16Default = 8;     // fp32 bs 16
+constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
 // SPMM_BSR_VARIANT=<v> overrides the variant of the row/row/row launch of
 // the bs 32 and bs 16 kernels (tuning sweeps only; tools/bsr_variants.sh).
@@ -507,7 +512,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     if (var >= 0 && rowd && brow && crow) {
       switch (var) {
 #define V(x) case x: hipLaunchKernelGGL((bsr16_f32_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
-        V(8) V(9) V(10) V(24) V(32) V(40) V(34) V(66)
+        V(8) V(9) V(10) V(12) V(13) V(14) V(40) V(66)
 #undef V
         default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
       }
@@ -546,7 +551,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
     if (var >= 0 && rowd && brow && crow) {
       switch (var) {
 #define V(x) case x: hipLaunchKernelGGL((bsr16_f16_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
-        V(8) V(9) V(10) V(24) V(32) V(40) V(34) V(66)
+        V(8) V(9) V(10) V(12) V(13) V(14) V(40) V(66)
 #undef V
         default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
       }
