@@ -329,4 +329,63 @@ int oracle_divide(int n, int bs, float density, const int* rowptr, const int* co
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Reorder front-end, restated on adjacency lists as the reference holds them.
+// kind 0: maxDegreeSort (reorder_strategy.cc:57-71) — descending degree,
+//         std::sort on (id, degree) records in id order (unstable, as there);
+// kind 1: BFSTraversal (:84-114) — FIFO over adjacency order, the smallest
+//         unvisited id starts each component;
+// kind 2: reverseCuthillMcKee (:73-82) — every list std::sort-ed by
+//         descending degree, then kind 1 (no final reversal, as there);
+// kind 3: permutate(old2new) (:42-55) — rename, move rows, sort lists.
+// Output: the reordered graph as CSR (out_rowptr[n+1], out_colind[nnz]).
+int oracle_reorder(int kind, int n, const int* rowptr, const int* colind, const int* perm,
+                   int* out_rowptr, int* out_colind) {
+  std::vector<std::vector<int>> e(n);
+  for (int i = 0; i < n; ++i) e[i].assign(colind + rowptr[i], colind + rowptr[i + 1]);
+  std::vector<int> old2new(n, -1);
+  if (kind == 0) {
+    std::vector<std::pair<int, int>> nodes;  // (id, degree)
+    for (int i = 0; i < n; ++i) nodes.emplace_back(i, (int)e[i].size());
+    std::sort(nodes.begin(), nodes.end(),
+              [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
+                return a.second > b.second;
+              });
+    for (int i = 0; i < n; ++i) old2new[nodes[i].first] = i;
+  } else if (kind == 1 || kind == 2) {
+    if (kind == 2)
+      for (auto& l : e)
+        std::sort(l.begin(), l.end(), [&e](int x, int y) { return e[x].size() > e[y].size(); });
+    int cnt = 0;
+    for (int root = 0; root < n; ++root) {
+      if (old2new[root] != -1) continue;
+      std::vector<int> q{root};
+      old2new[root] = cnt++;
+      for (size_t h = 0; h < q.size(); ++h)
+        for (int y : e[q[h]])
+          if (old2new[y] == -1) {
+            old2new[y] = cnt++;
+            q.push_back(y);
+          }
+    }
+  } else if (kind == 3) {
+    old2new.assign(perm, perm + n);
+  } else {
+    return -1;
+  }
+  std::vector<std::vector<int>> ne(n);
+  for (int i = 0; i < n; ++i) {
+    for (int& c : e[i]) c = old2new[c];
+    ne[old2new[i]] = std::move(e[i]);
+  }
+  out_rowptr[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    std::sort(ne[i].begin(), ne[i].end());
+    std::copy(ne[i].begin(), ne[i].end(), out_colind + out_rowptr[i]);
+    out_rowptr[i + 1] = out_rowptr[i] + (int)ne[i].size();
+  }
+  return 0;
+}
+
 }  // extern "C"
+

@@ -83,4 +83,52 @@ void ref_divide_fetch(int* csr_rp, int* csr_ci, int* bsr_rp, int* bsr_ci, float*
   std::copy(g_bsr_val.begin(), g_bsr_val.end(), bsr_val);
 }
 
+// --- reorder front-end (reorder_strategy.cc, utility.cc, rabbit_reorder.cc,
+// reorder_graph.cc). Reordered graphs come back as CSR via convertGraphToCSR.
+// kind: 0 = maxDegreeSort, 1 = BFSTraversal, 2 = reverseCuthillMcKee,
+// 3 = permutate(old2new), 4 = sortNeighbors. Output arrays hold n+1 / nnz.
+int ref_reorder(int kind, int n, const int* rowptr, const int* colind, const int* old2new,
+                int* out_rp, int* out_ci) {
+  std::vector<std::vector<int>> e = ref_harness::edges_of(n, rowptr, colind);
+  switch (kind) {
+    case 0: e = maxDegreeSort(std::move(e)); break;
+    case 1: e = BFSTraversal(std::move(e)); break;
+    case 2: e = reverseCuthillMcKee(std::move(e)); break;
+    case 3: e = permutate(std::vector<int>(old2new, old2new + n), std::move(e)); break;
+    case 4: e = sortNeighbors(std::move(e)); break;
+    default: return -1;
+  }
+  std::pair<int*, int*> p = convertGraphToCSR(e);
+  std::memcpy(out_rp, p.first, sizeof(int) * (n + 1));
+  std::memcpy(out_ci, p.second, sizeof(int) * (size_t)p.first[n]);
+  free(p.first); free(p.second);
+  return 0;
+}
+
+// getHeatmap (utility.cc:71-88) -> heatmap[nb * nb]
+void ref_heatmap(int n, const int* rowptr, const int* colind, int bs, int* out) {
+  auto h = getHeatmap(ref_harness::edges_of(n, rowptr, colind), bs);
+  const size_t nb = h.size();
+  for (size_t i = 0; i < nb; ++i) std::copy(h[i].begin(), h[i].end(), out + i * nb);
+}
+
+// loadPermutation (rabbit_reorder.cc:10-19)
+void ref_load_permutation(const char* filename, int n, int* out) {
+  std::vector<int> v = loadPermutation(filename, n);
+  std::copy(v.begin(), v.end(), out);
+}
+
+// analyzeBlockSparseMetrics (reorder_graph.cc:12-24): its stdout text.
+int ref_block_metrics_text(int n, const int* rowptr, const int* colind, int nnz, char* out,
+                           int cap) {
+  std::ostringstream os;
+  std::streambuf* old = std::cout.rdbuf(os.rdbuf());
+  analyzeBlockSparseMetrics(ref_harness::edges_of(n, rowptr, colind), nnz);
+  std::cout.rdbuf(old);
+  const std::string s = os.str();
+  if ((int)s.size() + 1 > cap) return -1;
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  return (int)s.size();
+}
+
 }  // extern "C"

@@ -104,7 +104,25 @@ _PROTOS = {
     "spmm_host_gen_community_csr": (c_int, [c_int, c_double, c_int, c_int, c_double, c_uint64,
                                             POINTER(c_void_p), POINTER(c_void_p),
                                             POINTER(c_int64)]),
+    # spmm_reorder.h
+    "spmm_reorder_degree": (c_int, [c_int, _P, _P, _P]),
+    "spmm_reorder_bfs": (c_int, [c_int, _P, _P, _P]),
+    "spmm_reorder_rcm": (c_int, [c_int, _P, _P, _P]),
+    "spmm_permute_csr": (c_int, [c_int, _P, _P, _P, _P, _P, _P, _P]),
+    "spmm_check_permutation": (c_int, [c_int, _P]),
+    "spmm_load_permutation": (c_int, [c_char_p, c_int, _P]),
+    "spmm_dump_permutation": (c_int, [c_char_p, c_int, _P]),
+    "spmm_block_metrics": (c_int, [c_int, _P, _P, c_int, _P]),
+    "spmm_block_heatmap": (c_int, [c_int, _P, _P, c_int, _P]),
+    "spmm_dump_heatmap": (c_int, [c_char_p, c_int, _P]),
 }
+
+
+class BlockMetrics(ctypes.Structure):
+    """spmm_block_metrics_t (include/spmm_reorder.h)."""
+    _fields_ = [("block_dim", c_int), ("nnzb", c_int64), ("density", c_double),
+                ("utilization", c_double), ("average", c_double)]
+
 
 # Symbols every build must export (tests/test_abi.py checks them against the
 # headers too).

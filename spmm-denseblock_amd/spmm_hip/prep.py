@@ -4,6 +4,8 @@ Thin wrappers over the C ABI of libspmm_hip.so:
   csr2bsr / bsr2csr / calculate_nnzb / partition_rows   (include/spmm_hip.h)
   rng_seed / random_array / random_csr / random_bsr /
   load_csr / dump_csr / load_graph / powerlaw_csr / community_csr (include/spmm_host.h)
+  reorder / permute_csr / load_permutation / dump_permutation /
+  block_metrics / block_heatmap / dump_heatmap                  (include/spmm_reorder.h)
 All conversion work happens in the library's C++ (north_star: CPU-side
 preprocessing), not in Python.
 """
@@ -14,7 +16,7 @@ from ctypes import byref, c_int, c_int64, c_void_p
 
 import numpy as np
 
-from ._lib import check, lib
+from ._lib import BlockMetrics, check, lib
 
 
 def _p(a: np.ndarray) -> c_void_p:
@@ -185,3 +187,86 @@ def community_csr(n: int, avg_deg: float, cmin: int, cmax: int, p_in: float, see
                                          byref(nnz)) != 0:
         raise ValueError("spmm_host_gen_community_csr: invalid parameters")
     return _take(rp, n + 1, np.int32), _take(ci, nnz.value, np.int32)
+
+
+# ------------------------------------------------------- reorder front-end
+_REORDER = {"degree": "spmm_reorder_degree", "bfs": "spmm_reorder_bfs",
+            "rcm": "spmm_reorder_rcm"}
+
+
+def _ok(rc: int, where: str) -> None:
+    if rc != 0:
+        raise ValueError(f"{where}: invalid input")
+
+
+def reorder(rowptr, colind, method: str = "rcm") -> np.ndarray:
+    """old2new permutation: "degree" (maxDegreeSort, reorder_strategy.cc:57-71),
+    "bfs" (BFSTraversal, :84-114) or "rcm" (reverseCuthillMcKee, :73-82)."""
+    if method not in _REORDER:
+        raise ValueError(f"unknown reorder method {method!r}; choose from {sorted(_REORDER)}")
+    rowptr, colind = _i32(rowptr), _i32(colind)
+    out = np.empty(rowptr.size - 1, dtype=np.int32)
+    _ok(getattr(lib(), _REORDER[method])(rowptr.size - 1, _p(rowptr), _p(colind), _p(out)),
+        _REORDER[method])
+    return out
+
+
+def permute_csr(rowptr, colind, old2new, val=None):
+    """permutate (reorder_strategy.cc:42-55): symmetric renumbering with sorted
+    columns; values follow their columns. Returns (rowptr, colind[, val])."""
+    rowptr, colind, old2new = _i32(rowptr), _i32(colind), _i32(old2new)
+    n = rowptr.size - 1
+    nrp = np.empty(n + 1, dtype=np.int32)
+    nci = np.empty(colind.size, dtype=np.int32)
+    if val is None:
+        _ok(lib().spmm_permute_csr(n, _p(rowptr), _p(colind), None, _p(old2new), _p(nrp),
+                                   _p(nci), None), "spmm_permute_csr")
+        return nrp, nci
+    val = _f32(val)
+    nv = np.empty(val.size, dtype=np.float32)
+    _ok(lib().spmm_permute_csr(n, _p(rowptr), _p(colind), _p(val), _p(old2new), _p(nrp),
+                               _p(nci), _p(nv)), "spmm_permute_csr")
+    return nrp, nci, nv
+
+
+def load_permutation(filename: str, n: int) -> np.ndarray:
+    """loadPermutation (rabbit_reorder.cc:10-19), validated as a permutation."""
+    out = np.empty(n, dtype=np.int32)
+    if lib().spmm_load_permutation(filename.encode(), n, _p(out)) != 0:
+        raise ValueError(f"load_permutation({filename}): unreadable or not a permutation of {n}")
+    return out
+
+
+def dump_permutation(filename: str, old2new) -> None:
+    old2new = _i32(old2new)
+    if lib().spmm_dump_permutation(filename.encode(), old2new.size, _p(old2new)) != 0:
+        raise OSError(f"dump_permutation({filename}) failed")
+
+
+def block_metrics(rowptr, colind, bs: int) -> dict:
+    """analyzeBlockSparseMetrics (reorder_graph.cc:12-24) at one block size."""
+    rowptr, colind = _i32(rowptr), _i32(colind)
+    m = BlockMetrics()
+    _ok(lib().spmm_block_metrics(rowptr.size - 1, _p(rowptr), _p(colind), bs,
+                                 c_void_p(ctypes.addressof(m))), "spmm_block_metrics")
+    return {"block_dim": m.block_dim, "nnzb": m.nnzb, "density": m.density,
+            "utilization": m.utilization, "average": m.average}
+
+
+def block_heatmap(rowptr, colind, bs: int) -> np.ndarray:
+    """getHeatmap (utility.cc:71-88): nnz per bs x bs block, shape (nb, nb)."""
+    rowptr, colind = _i32(rowptr), _i32(colind)
+    n = rowptr.size - 1
+    nb = (n + bs - 1) // bs
+    out = np.empty(nb * nb, dtype=np.int32)
+    _ok(lib().spmm_block_heatmap(n, _p(rowptr), _p(colind), bs, _p(out)), "spmm_block_heatmap")
+    return out.reshape(nb, nb)
+
+
+def dump_heatmap(filename: str, heatmap) -> None:
+    """dumpHeatmap (utility.cc:90-100) text format."""
+    h = np.ascontiguousarray(heatmap, dtype=np.int32)
+    if h.ndim != 2 or h.shape[0] != h.shape[1]:
+        raise ValueError("heatmap must be square")
+    if lib().spmm_dump_heatmap(filename.encode(), h.shape[0], _p(h)) != 0:
+        raise OSError(f"dump_heatmap({filename}) failed")

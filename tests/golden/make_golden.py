@@ -194,6 +194,74 @@ def ref_fixtures():
     return fx
 
 
+def reorder_graphs(fx_host: dict) -> dict:
+    """Inputs of the reorder fixtures: the two divide graphs, a power-law
+    graph with many equal degrees, isolated nodes and several components,
+    and a scrambled community graph (what a reorder should un-scramble)."""
+    g = {"rand300": (fx_host["rand300_rowptr"], fx_host["rand300_colind"]),
+         "band200": (fx_host["band200_rowptr"], fx_host["band200_colind"])}
+    rng = np.random.default_rng(77)
+    n = 2000
+    deg = np.minimum((rng.zipf(2.1, n) - 1) * 2, 400)
+    deg[rng.choice(n, 50, replace=False)] = 0  # isolated rows
+    rows = [np.sort(rng.choice(n, d, replace=False)) for d in deg]
+    g["pl2000"] = (np.concatenate([[0], np.cumsum(deg)]).astype(np.int32),
+                   np.concatenate(rows).astype(np.int32))
+    n, rows = 1500, []
+    comm = np.repeat(np.arange(15), 100)
+    for r in range(n):
+        inside = rng.choice(np.flatnonzero(comm == comm[r]), 12, replace=False)
+        outside = rng.choice(n, 2, replace=False)
+        rows.append(np.union1d(inside, outside))
+    perm = rng.permutation(n)  # scramble: old -> new
+    srows = [None] * n
+    for r in range(n):
+        srows[perm[r]] = np.sort(perm[rows[r]])
+    g["comm1500"] = (np.concatenate([[0], np.cumsum([len(x) for x in srows])]).astype(np.int32),
+                     np.concatenate(srows).astype(np.int32))
+    return g
+
+
+def reorder_fixtures(fx_host: dict, tmpdir: str) -> dict:
+    """The reference's own reorder front-end (reorder_strategy.cc,
+    utility.cc getHeatmap, rabbit_reorder.cc loadPermutation, reorder_graph.cc
+    analyzeBlockSparseMetrics) on reorder_graphs()."""
+    L = ctypes.CDLL(LIBREF)
+    L.ref_reorder.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 5
+    L.ref_heatmap.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                              ctypes.c_void_p]
+    L.ref_load_permutation.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p]
+    L.ref_block_metrics_text.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    fx = {}
+    for name, (rp, ci) in reorder_graphs(fx_host).items():
+        n, nnz = rp.size - 1, ci.size
+        fx[f"{name}_rowptr"], fx[f"{name}_colind"] = rp, ci
+        perm = np.random.default_rng(n).permutation(n).astype(np.int32)
+        fx[f"{name}_perm"] = perm
+        for kind, tag in ((0, "degree"), (1, "bfs"), (2, "rcm"), (3, "permute")):
+            orp, oci = np.zeros(n + 1, np.int32), np.zeros(nnz, np.int32)
+            assert L.ref_reorder(kind, n, _p(rp), _p(ci), _p(perm), _p(orp), _p(oci)) == 0
+            fx[f"{name}_{tag}_rowptr"], fx[f"{name}_{tag}_colind"] = orp, oci
+        for bs in (16, 64):
+            nb = (n + bs - 1) // bs
+            h = np.zeros(nb * nb, np.int32)
+            L.ref_heatmap(n, _p(rp), _p(ci), bs, _p(h))
+            fx[f"{name}_heatmap{bs}"] = h
+        buf = ctypes.create_string_buffer(1 << 14)
+        ln = L.ref_block_metrics_text(n, _p(rp), _p(ci), nnz, buf, len(buf))
+        assert ln > 0
+        fx[f"{name}_metrics_text"] = np.array(buf.value.decode())
+        # loadPermutation on a file in the rabbit/Gorder format.
+        f = os.path.join(tmpdir, f"{name}_perm.txt")
+        with open(f, "w") as fh:
+            fh.write("\n".join(str(x) for x in perm) + "\n")
+        got = np.zeros(n, np.int32)
+        L.ref_load_permutation(f.encode(), n, _p(got))
+        assert np.array_equal(got, perm)
+    return fx
+
+
 def big_digest():
     """Config 1 (BASELINE configs[0]): randomCSRMatrix(16384, 16384, 2^-10)
     from a fresh generator, followed by randomDenseMatrix(16384, 32):
@@ -227,7 +295,11 @@ def main():
         json.dump(kats(), f, indent=1)
     if not os.path.exists(LIBREF):
         sys.exit("oracle/_ref/libref.so missing: run `make -C oracle ref` first")
-    np.savez_compressed(os.path.join(HERE, "ref_host.npz"), **ref_fixtures())
+    host = ref_fixtures()
+    np.savez_compressed(os.path.join(HERE, "ref_host.npz"), **host)
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        np.savez_compressed(os.path.join(HERE, "ref_reorder.npz"), **reorder_fixtures(host, td))
     with open(os.path.join(HERE, "ref_config1.json"), "w") as f:
         json.dump(big_digest(), f, indent=1)
     print("golden fixtures written to", HERE)

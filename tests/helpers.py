@@ -42,6 +42,7 @@ def load_oracle() -> ctypes.CDLL:
         "oracle_csrmm_f64": (None, [I, I, P, P, P, I, P, I, I, P, P]),
         "oracle_spmm_cc_csr": (None, [I64, I64, P, P, P, I64, P]),
         "oracle_num_threads": (I, []),
+        "oracle_reorder": (I, [I, I, P, P, P, P, P]),
         "oracle_bsrmm_f32": (None, [I, I, I, I, P, P, P, P, I, I, F, F, P, I, I]),
         "oracle_bsrmm_f64": (None, [I, I, I, I, P, P, P, P, I, I, I, P, P]),
         "oracle_csr2bsr_nnz": (I64, [I, I, P, P, P]),
@@ -155,3 +156,19 @@ def assert_normwise(got, ref64, absdot, tol, what=""):
             f"{what}: {int(bad.sum())} / {bad.size} elements outside the norm-wise tolerance "
             f"{tol}; worst flat index {i}: got {got.flat[i]!r} ref {ref64.flat[i]!r} "
             f"|a||b| {absdot.flat[i]!r}")
+
+
+def oracle_reorder(L, kind: str, rowptr, colind, perm=None):
+    """Reordered CSR from the oracle's restatement of reorder_strategy.cc."""
+    k = {"degree": 0, "bfs": 1, "rcm": 2, "permute": 3}[kind]
+    rowptr = np.ascontiguousarray(rowptr, np.int32)
+    colind = np.ascontiguousarray(colind, np.int32)
+    n = rowptr.size - 1
+    perm = np.zeros(max(n, 1), np.int32) if perm is None else np.ascontiguousarray(perm, np.int32)
+    orp, oci = np.zeros(n + 1, np.int32), np.zeros(max(colind.size, 1), np.int32)
+    assert L.oracle_reorder(k, n, ptr(rowptr), ptr(colind), ptr(perm), ptr(orp), ptr(oci)) == 0
+    return orp, oci[:colind.size]
+
+
+def load_reorder_golden():
+    return np.load(os.path.join(GOLDEN, "ref_reorder.npz"), allow_pickle=False)

@@ -15,7 +15,7 @@ from conftest import ROOT
 
 def _declared() -> set[str]:
     names = set()
-    for h in ("spmm_hip.h", "spmm_host.h"):
+    for h in ("spmm_hip.h", "spmm_host.h", "spmm_reorder.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(spmm_[a-z0-9_]+)\s*\(", src))
