@@ -47,10 +47,10 @@ WORKLOADS = {
     "products_bsr32": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                            p_in=0.97, bs=32, K=128, dtype="fp32"),
     "products_hybrid32": dict(kind="hybrid", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
-                              p_in=0.97, bs=32, K=128, density=1.0 / 32),
+                              p_in=0.97, bs=32, K=128, density="auto"),
     # §8f next row: dense-block + CSR remainder (divide.cu) on the reddit stand-in
     "reddit_hybrid32": dict(kind="hybrid", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
-                            p_in=0.99, bs=32, K=128, density=1.0 / 32),
+                            p_in=0.99, bs=32, K=128, density="auto"),
 }
 METRIC = "SpMM GFLOP/s (2*nnz*K/t) + achieved HBM GB/s, ogbn-products K=128"
 
@@ -103,7 +103,7 @@ def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0)
                        f"({med:.3f} s each, {spent:.1f} s total)")}
 
 
-def timed_loop(step, h, steps, warmup, world, dist):
+def timed_loop(step, h, steps, warmup, world, dist, raw=False):
     import torch
     for _ in range(warmup):
         step()
@@ -122,6 +122,8 @@ def timed_loop(step, h, steps, warmup, world, dist):
     elapsed = time.perf_counter() - t0
     h.set_timing(False)
     kt = h.kernel_times()
+    if raw:
+        return elapsed, kt
     return elapsed, (float(np.mean(kt)) if kt else float("nan"))
 
 
@@ -278,6 +280,14 @@ def run_hybrid(args, W, world, rank, dev, dist):
     rp, ci = prep.community_csr(W["n"], W["avg_deg"], W["cmin"], W["cmax"], W["p_in"], 1234)
     n, nnz = rp.size - 1, ci.size
     val = np.random.default_rng(2).uniform(-1, 1, nnz).astype(np.float32)
+    plan = None
+    if args.density is None and dens == "auto":
+        args.density = "auto"
+    if args.density == "auto":
+        plan = prep.hybrid_plan(rp, ci, bs, K)
+        dens = plan["density"]
+    elif args.density is not None:
+        dens = float(args.density)
     t_div = time.perf_counter()
     crp, cci, cv, brp, bci, bv = prep.divide(n, rp, ci, val, bs, dens)
     t_div = time.perf_counter() - t_div
@@ -293,7 +303,10 @@ def run_hybrid(args, W, world, rank, dev, dist):
         ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=C,
                          ldc=K, handle=h)
 
-    elapsed, _ = timed_loop(step, h, args.steps, args.warmup, 1, dist)
+    elapsed, kt = timed_loop(step, h, args.steps, args.warmup, 1, dist, raw=True)
+    # launch order per step: the BSR kernel, then the CSR kernel (when both parts exist)
+    parts = int(bci.size > 0) + int(cci.size > 0)
+    kt = np.array(kt[: parts * args.steps]).reshape(args.steps, parts) if parts else None
     h2 = ops.Handle()
     _, csr_ms = timed_loop(lambda: ops.csrmm(d[6], d[7], d[8], B, m=n, n=K, k=mb * bs, ldb=K,
                                              C=C, ldc=K, handle=h2), h2, 5, 2, 1, dist)
@@ -311,7 +324,9 @@ def run_hybrid(args, W, world, rank, dev, dist):
             (csr_bytes(n, int(cci.size), K) + bsr_bytes(mb, int(bci.size), bs, K, 4)) /
             (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": None, "traffic": None, "kernel": "bsr32_f32_mfma + csr_mergepath"},
-        csr_same_matrix_ms=round(csr_ms, 4), divide_host_seconds=round(t_div, 2))
+        csr_same_matrix_ms=round(csr_ms, 4), divide_host_seconds=round(t_div, 2),
+        plan=plan,
+        part_kernel_ms=None if kt is None else [round(float(x), 4) for x in kt.mean(axis=0)])
     rec["roofline"]["frac"] = round(rec["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
     return rec, None
 
@@ -323,6 +338,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="products_csr", choices=sorted(WORKLOADS))
     ap.add_argument("--K", type=int, default=0, help="override the workload's K")
+    ap.add_argument("--density", default=None,
+                    help="hybrid workloads: divide threshold (a float, or 'auto' = spmm_hybrid_plan)")
     ap.add_argument("--dtype", choices=["fp32", "fp16"], default=None,
                     help="override a BSR workload's value type")
     ap.add_argument("--bsr-layout", choices=["row", "col"], default="row",

@@ -234,6 +234,21 @@ spmm_status_t spmm_sdivide(int n, const int* rowPtr, const int* colInd, const fl
                            const int* bsrRowPtr, int* csrColInd, float* csrVal, int* bsrColInd,
                            float* bsrVal);
 
+/* Threshold planner for divide (the reference takes `density` from the user,
+ * divide.cu:348): from the histogram of block fills it picks the count
+ * threshold T minimising a bytes-over-bandwidth model of the hybrid SpMM,
+ *   sum_{blocks, fill >= T} (s*(bs^2 + bs*K) + 4) / bsrBytesPerSec
+ * + sum_{blocks, fill <  T} fill * (8 + 4*K)    / csrBytesPerSec,
+ * s = valueBytes of the BSR part, and returns density = T / bs^2 (the value
+ * spmm_divide_nnz admits exactly those blocks for; T = bs^2 + 1 means "all
+ * CSR"). Bandwidths <= 0 take the defaults measured on MI355X with this
+ * library (BSR 7.0e12, CSR 7.5e12 algorithmic bytes/s).
+ * nnzb / csrNnz / estSeconds: the split and modelled time (may be NULL). */
+spmm_status_t spmm_hybrid_plan(int n, const int* rowPtr, const int* colInd, int blockDim, int K,
+                               int valueBytes, double bsrBytesPerSec, double csrBytesPerSec,
+                               float* density, int64_t* nnzb, int64_t* csrNnz,
+                               double* estSeconds);
+
 /* ------------------------------------------------------------------------ */
 /* Hybrid dense-block + CSR-remainder SpMM (divide.cu:348-373)                */
 /* ------------------------------------------------------------------------ */

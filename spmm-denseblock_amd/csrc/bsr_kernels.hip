@@ -36,6 +36,20 @@ __device__ __forceinline__ float epi(float acc, float alpha, float beta, const f
   return beta == 0.f ? alpha * acc : __builtin_fmaf(beta, *p, alpha * acc);
 }
 
+// Waits (once, before the block loop) for the loads that filled a fragment
+// buffer. Without it the loop header merges the prologue's loads with the
+// back edge, and hipcc's waitcnt pass puts a conservative counted wait on the
+// first MFMA that then also covers the prefetches issued in the same
+// iteration (measured: the prefetch hid nothing; hot-L2 and cold B panels ran
+// at the same 41 % of the MFMA peak).
+__device__ __forceinline__ void settle(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void settle(f16x8& x) { asm volatile("" : "+v"(x)); }
+template <typename T, int N>
+__device__ __forceinline__ void settle(T (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) settle(x[i]);
+}
+
 // Wave-uniform block-column cursor over bsr_col_ind[k0, k1): 64 entries held
 // one per lane, read with v_readlane (no dependent scalar load per block) and
 // refilled in place every 64 blocks. The refill waits right away (asm use),
@@ -102,8 +116,10 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr32_f32_mf
 
   ColCursor cc(colind, k0, k1, lane);
   auto load_frags = [&](int k, float (&fa)[16], float (&fb)[16]) {
-    const int bc = cc.get(k);
-    const float* ab = val + (size_t)k * 1024;
+    // VAR & 0x100 / 0x200: diagnostic variants (A always block 0 / B always
+    // panel 0, i.e. cache-resident operands); not used by the dispatch.
+    const int bc = (VAR & 0x200) ? 0 : cc.get(k);
+    const float* ab = val + ((VAR & 0x100) ? 0 : (size_t)k * 1024);
     if constexpr (ROWDIR) {
       const f32x4* p = reinterpret_cast<const f32x4*>(ab + r * 32 + 16 * h);
 #pragma unroll
@@ -141,7 +157,11 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr32_f32_mf
   // MFMAs), so no branch around a load makes hipcc's counted waits collapse.
   float a0[16], b0[16], a1[16], b1[16];
   const int kl = k1 - 1;
-  if (k0 < k1) load_frags(k0, a0, b0);
+  if (k0 < k1) {
+    load_frags(k0, a0, b0);
+    settle(a0);
+    settle(b0);
+  }
   if constexpr ((VAR & 3) == 1) {
     for (int k = k0; k < k1; k += 2) {
       load_frags(min(k + 1, kl), a1, b1);
@@ -154,6 +174,8 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr32_f32_mf
       if (k > k0) load_frags(k, a0, b0);
       mfma16(a0, b0);
     }
+  } else if constexpr ((VAR & 0x400) != 0) {
+    for (int k = k0; k < k1; ++k) mfma16(a0, b0);  // diagnostic: MFMA chain only
   } else {
     for (int k = k0; k < k1; ++k) {
       if (k + 1 < k1) load_frags(k + 1, a1, b1);
@@ -164,6 +186,131 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr32_f32_mf
   }
 
   if (!jok) return;
+  const size_t row0 = (size_t)br * 32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = row0 + 8 * g + 4 * h + e;
+      float* p = CROW ? C + row * ldc + jcol : C + (size_t)jcol * ldc + row;
+      *p = epi(acc[4 * g + e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 32 fp32, LDS-staged (ROW blocks, row-major B): the shipped bs = 32
+// kernel where the layout allows it.
+//
+// Fragment-shaped loads straight to VGPRs (the kernel above: per block and
+// wave 4 A loads touching 32 rows x 32 B and 16 B loads touching 2 rows each)
+// cap that kernel at ~41 % of the MFMA peak even when every operand is
+// L2-resident (tools/bsr_micro.py: hot / warm / cold B panels all 64-65
+// TFLOP/s; MFMA-only 105). Here a workgroup (4 waves, 128 output columns)
+// copies each block's A (4 KB) and B panel (32 rows x 512 B) into LDS with
+// global_load_lds_dwordx4 — whole 128-B lines, 20 wave-instructions per block
+// instead of 80, no VGPRs — D - 1 blocks ahead, then reads its fragments with
+// ds_read_b128 (A, XOR-swizzled 16-B chunks, conflict-free) and ds_read_b32
+// (B, 32 consecutive columns per half-wave, conflict-free).
+//
+// Per block k (stage k % D): wait for this wave's copies of block k (counted
+// vmcnt), raw s_barrier (every wave's copies landed and every wave is done
+// with stage (k-1) % D), issue the copies of block k + D - 1 into that stage
+// (index clamped to the row's last block so every iteration issues the same
+// count), then 4 + 16 LDS reads and 16 MFMAs.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef __attribute__((address_space(1))) void* gbl_void_t;
+
+// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4]<<14)
+constexpr int waitcnt_vm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+
+template <bool CROW, int D, bool XCD>
+__global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  constexpr int kStage = 1024 + 32 * 128;  // floats: A block + B panel (20 KB)
+  __shared__ __attribute__((aligned(16))) float smem[D * kStage];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  int br = blockIdx.x;
+  if constexpr (XCD) {
+    const int q = mb / 8, rem = mb % 8, x = br % 8, i = br / 8;
+    br = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + i;
+  }
+  const int jt = blockIdx.y * 128;  // first output column of the workgroup
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  if (k0 >= k1) {  // empty block row: C = beta * C (alpha * 0)
+    const int j = jt + 32 * wv + (lane & 31);
+    if (j < n)
+      for (int e = 0; e < 16; ++e) {
+        const size_t row = (size_t)br * 32 + 2 * e + (lane >> 5);
+        float* p = CROW ? C + row * ldc + j : C + (size_t)j * ldc + row;
+        *p = epi(0.f, alpha, beta, p);
+      }
+    return;
+  }
+
+  // Copy sources of this wave: A rows 8w .. 8w+7 (one instruction; lane l ->
+  // row 8w + l/8, LDS chunk l%8 holding logical chunk (l%8) ^ swz(row)), and
+  // B panel rows 8w .. 8w+7 (four instructions, two rows of 512 B each; the
+  // column chunk is clamped so every source stays inside B).
+  const int a_row = 8 * wv + (lane >> 3);
+  const int a_chunk = (lane & 7) ^ ((a_row >> 1) & 7);
+  const int a_src = a_row * 32 + 4 * a_chunk;
+  const int b_col = min(jt + 4 * (lane & 31), n - 4);
+  const int b_row = 8 * wv + (lane >> 5);
+  // bc: the block column of block k (wave-uniform).
+  auto issue = [&](int k, int bc, int st) {
+    const int kk = min(k, k1 - 1);
+    float* stage = smem + st * kStage;
+    __builtin_amdgcn_global_load_lds((gbl_void_t)(val + (size_t)kk * 1024 + a_src),
+                                     (lds_void_t)(stage + 256 * wv), 16, 0, 0);
+    const float* bsrc = B + ((size_t)bc * 32 + b_row) * ldb + b_col;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(bsrc + (size_t)(2 * i) * ldb),
+                                       (lds_void_t)(stage + 1024 + 128 * (8 * wv + 2 * i)), 16,
+                                       0, 0);
+  };
+
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  // Block columns through the readlane cursor: no load per block (a scalar
+  // load per block sat right before the copies it feeds), one refill per 64.
+  ColCursor cc(colind, k0, k1, lane);
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) issue(k0 + d, cc.get(min(k0 + d, k1 - 1)), d);
+
+  int st = 0;
+  for (int k = k0; k < k1; ++k) {
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(5 * (D - 2)));
+    __builtin_amdgcn_s_barrier();
+    issue(k + D - 1, cc.get(min(k + D - 1, k1 - 1)), st == 0 ? D - 1 : st - 1);
+    const float* stage = smem + st * kStage;
+    // A fragment: row r, logical chunks 4h .. 4h+3 (k = 16h + s).
+    float fa[16], fb[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int pc = (4 * h + q) ^ ((r >> 1) & 7);
+      const f32x4 x = *reinterpret_cast<const f32x4*>(stage + r * 32 + 4 * pc);
+      fa[4 * q] = x[0]; fa[4 * q + 1] = x[1]; fa[4 * q + 2] = x[2]; fa[4 * q + 3] = x[3];
+    }
+    const float* bs_ = stage + 1024 + (16 * h) * 128 + 32 * wv + r;
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) fb[s2] = bs_[s2 * 128];
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2], fb[s2], acc, 0, 0, 0);
+    st = st == D - 1 ? 0 : st + 1;
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // drain the clamped tail copies
+
+  const int jcol = jt + 32 * wv + r;
+  if (jcol >= n) return;
   const size_t row0 = (size_t)br * 32;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -240,7 +387,11 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f32_mf
   if constexpr ((VAR & 3) == 0) {
     // Rotation prefetch: next block loaded under a branch, copied down after use.
     float a1[4], b1[NT][4];
-    if (k0 < k1) load_frags(k0, a0, b0);
+    if (k0 < k1) {
+    load_frags(k0, a0, b0);
+    settle(a0);
+    settle(b0);
+  }
     for (int k = k0; k < k1; ++k) {
       if (k + 1 < k1) load_frags(k + 1, a1, b1);
       mfma(a0, b0);
@@ -261,7 +412,11 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f32_mf
     // Fixed-role double buffer, unconditional clamped prefetch (as bs = 32).
     float a1[4], b1[NT][4];
     const int kl = k1 - 1;
-    if (k0 < k1) load_frags(k0, a0, b0);
+    if (k0 < k1) {
+    load_frags(k0, a0, b0);
+    settle(a0);
+    settle(b0);
+  }
     for (int k = k0; k < k1; k += 2) {
       load_frags(min(k + 1, kl), a1, b1);
       mfma(a0, b0);
@@ -362,7 +517,11 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f16_mf
   if constexpr ((VAR & 3) == 0) {
     // Rotation prefetch: next pair loaded under a branch, copied down after use.
     f16x8 a1, b1[NT];
-    if (k0 < k1) load_frags(k0, a0, b0);
+    if (k0 < k1) {
+    load_frags(k0, a0, b0);
+    settle(a0);
+    settle(b0);
+  }
     for (int k = k0; k < k1; k += 2) {
       if (k + 2 < k1) load_frags(k + 2, a1, b1);
       mfma(a0, b0, k);
@@ -379,7 +538,11 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f16_mf
   } else {
     f16x8 a1, b1[NT];  // fixed-role double buffer over block pairs
     const int kl = k1 - 1;
-    if (k0 < k1) load_frags(k0, a0, b0);
+    if (k0 < k1) {
+    load_frags(k0, a0, b0);
+    settle(a0);
+    settle(b0);
+  }
     for (int k = k0; k < k1; k += 4) {
       load_frags(min(k + 2, kl), a1, b1);
       mfma(a0, b0, k);
@@ -436,6 +599,8 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 }
 
 constexpr int kBsr32Default = 40;
+// LDS-staged bs = 32 kernel: 4096 + D (+ 8 for the XCD-contiguous order).
+constexpr int kBsr32LdsDefault = 4107;
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -490,14 +655,32 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   const bool crow = orderC == SPMM_ORDER_ROW;
   const bool vec_ok = aligned(val, 16) && (brow || (aligned(B, 16) && ldb % 4 == 0));
   const int slot = timing_begin(ctx);
-  if (bs == 32 && vec_ok) {
+  const int var = variant_override();
+  if (bs == 32 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 && aligned(val, 16) &&
+      aligned(B, 16) && (var < 0 || var >= 4096)) {
+    dim3 grid(mb, (n + 127) / 128);
+    const int lv = var < 0 ? kBsr32LdsDefault : var;
+#define L(D, X)                                                                                   \
+  if (crow) hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, D, X>), grid, dim3(256), 0, ctx->stream,  \
+                               mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);          \
+  else hipLaunchKernelGGL((bsr32_f32_lds_kernel<false, D, X>), grid, dim3(256), 0, ctx->stream,      \
+                          mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    switch (lv) {
+      case 4098: L(2, false) break;
+      case 4099: L(3, false) break;
+      case 4100: L(4, false) break;
+      case 4106: L(2, true) break;
+      case 4107: L(3, true) break;
+      default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
+    }
+#undef L
+  } else if (bs == 32 && vec_ok) {
     const int waves = n <= 32 ? 1 : (n <= 64 ? 2 : 4);
     dim3 grid(mb, (n + 32 * waves - 1) / (32 * waves));
-    const int var = variant_override();
     if (var >= 0 && rowd && brow && crow) {
       switch (var) {
 #define V(x) case x: hipLaunchKernelGGL((bsr32_f32_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
-        V(40) V(44) V(42) V(50) V(58) V(66) V(41) V(49)
+        V(40) V(44) V(42) V(50) V(58) V(66) V(41) V(49) V(296) V(552) V(808) V(1064) V(298) V(554) V(810)
 #undef V
         default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
       }
@@ -508,7 +691,6 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   } else if (bs == 16 && vec_ok) {
     const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
     dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
-    const int var = variant_override();
     if (var >= 0 && rowd && brow && crow) {
       switch (var) {
 #define V(x) case x: hipLaunchKernelGGL((bsr16_f32_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;

@@ -10,7 +10,11 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <atomic>
+#include <thread>
 #include <vector>
+
+#include "host_util.hpp"
 
 #include "spmm_hip.h"
 
@@ -311,4 +315,77 @@ spmm_status_t spmm_sdivide(int n, const int* rowPtr, const int* colInd, const fl
   return SPMM_STATUS_SUCCESS;
 }
 
+spmm_status_t spmm_hybrid_plan(int n, const int* rowPtr, const int* colInd, int blockDim, int K,
+                               int valueBytes, double bsrBytesPerSec, double csrBytesPerSec,
+                               float* density, int64_t* nnzb, int64_t* csrNnz,
+                               double* estSeconds) {
+  if (n < 0 || blockDim <= 0 || K <= 0 || valueBytes <= 0 || !rowPtr || !density)
+    return SPMM_STATUS_INVALID_VALUE;
+  const int bs = blockDim, nb = ceil_div(n, bs);
+  const int64_t bs2 = (int64_t)bs * bs;
+  const int base = n > 0 ? rowPtr[0] : 0;
+  if (n > 0 && rowPtr[n] - base > 0 && !colInd) return SPMM_STATUS_INVALID_VALUE;
+  const double bw_b = bsrBytesPerSec > 0 ? bsrBytesPerSec : 7.0e12;
+  const double bw_c = csrBytesPerSec > 0 ? csrBytesPerSec : 7.5e12;
+  // hist[c] = number of blocks holding c entries (c = 1 .. bs^2; duplicates
+  // counted, as divide_matrix counts them).
+  const int nt = spmm_host::num_threads();
+  std::vector<std::vector<int64_t>> hist(nt, std::vector<int64_t>(bs2 + 1, 0));
+  std::atomic<bool> ok{true};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      DivideScratch s(nb);
+      auto& h = hist[t];
+      for (int br = (int)((int64_t)nb * t / nt); br < (int)((int64_t)nb * (t + 1) / nt); ++br) {
+        s.touched.clear();
+        const int r0 = br * bs, r1 = std::min(n, r0 + bs);
+        for (int r = r0; r < r1; ++r)
+          for (int j = rowPtr[r] - base; j < rowPtr[r + 1] - base; ++j) {
+            const int c = colInd[j] - base;
+            if (c < 0 || c / bs >= nb) {
+              ok = false;
+              for (int x : s.touched) s.cnt[x] = 0;
+              return;
+            }
+            if (s.cnt[c / bs]++ == 0) s.touched.push_back(c / bs);
+          }
+        for (int x : s.touched) {
+          ++h[std::min<int64_t>(s.cnt[x], bs2)];
+          s.cnt[x] = 0;
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  if (!ok) return SPMM_STATUS_INVALID_VALUE;
+  for (int t = 1; t < nt; ++t)
+    for (int64_t c = 0; c <= bs2; ++c) hist[0][c] += hist[t][c];
+  const auto& h = hist[0];
+  const double tb = ((double)valueBytes * (bs2 + (double)bs * K) + 4.0) / bw_b;
+  const double tn = (8.0 + 4.0 * K) / bw_c;
+  // T = bs^2 + 1 (all CSR) first; lowering T moves the blocks of fill T - 1
+  // from the CSR side to the BSR side.
+  int64_t total_nnz = 0;
+  for (int64_t c = 1; c <= bs2; ++c) total_nnz += c * h[c];
+  double cost = total_nnz * tn, best = cost;
+  int64_t bestT = bs2 + 1, blocks = 0, rem = total_nnz, best_blocks = 0, best_rem = rem;
+  for (int64_t T = bs2; T >= 1; --T) {
+    cost += h[T] * (tb - T * tn);
+    blocks += h[T];
+    rem -= T * h[T];
+    if (cost < best) {
+      best = cost;
+      bestT = T;
+      best_blocks = blocks;
+      best_rem = rem;
+    }
+  }
+  *density = (float)((double)bestT / (double)bs2);
+  if (nnzb) *nnzb = best_blocks;
+  if (csrNnz) *csrNnz = best_rem;
+  if (estSeconds) *estSeconds = best;
+  return SPMM_STATUS_SUCCESS;
+}
+
 }  // extern "C"
+

@@ -84,6 +84,9 @@ _PROTOS = {
     "spmm_csr_partition_rows": (c_int, [c_int, _P, c_int, _P]),
     "spmm_divide_nnz": (c_int, [c_int, _P, _P, c_int, c_float, _P, _P, _PI, _PI]),
     "spmm_sdivide": (c_int, [c_int, _P, _P, _P, c_int, c_float, _P, _P, _P, _P, _P, _P]),
+    "spmm_hybrid_plan": (c_int, [c_int, _P, _P, c_int, c_int, c_int, c_double, c_double,
+                                 POINTER(c_float), POINTER(c_int64), POINTER(c_int64),
+                                 POINTER(c_double)]),
     "spmm_hybrid_csrmm_f32": (c_int, [_P, c_int, c_int, c_int, c_float, _P, _P, _P, c_int, c_int,
                                       _P, _P, _P, c_int, _P, c_int, c_float, _P, c_int]),
     # spmm_host.h

@@ -102,6 +102,20 @@ def divide(n: int, rowptr, colind, val, bs: int, density: float):
     return crp, cci, cv, brp, bci, bv
 
 
+def hybrid_plan(rowptr, colind, bs: int, K: int, value_bytes: int = 4,
+                bsr_bytes_per_s: float = 0.0, csr_bytes_per_s: float = 0.0) -> dict:
+    """spmm_hybrid_plan: the divide density threshold minimising the modelled
+    hybrid time. Returns {density, nnzb, csr_nnz, est_seconds}."""
+    from ctypes import c_double, c_float
+    rowptr, colind = _i32(rowptr), _i32(colind)
+    d, nb, cn, est = c_float(0), c_int64(0), c_int64(0), c_double(0)
+    check(lib().spmm_hybrid_plan(rowptr.size - 1, _p(rowptr), _p(colind), bs, K, value_bytes,
+                                 bsr_bytes_per_s, csr_bytes_per_s, byref(d), byref(nb),
+                                 byref(cn), byref(est)), "spmm_hybrid_plan")
+    return {"density": d.value, "nnzb": nb.value, "csr_nnz": cn.value,
+            "est_seconds": est.value}
+
+
 def partition_rows(rowptr, nparts: int) -> np.ndarray:
     """nnz-balanced contiguous row split: bounds[nparts+1]."""
     rowptr = _i32(rowptr)

@@ -181,3 +181,26 @@ def test_load_graph_edge_list(tmp_path):
     f.write_text("4 5\n0 3\n0 1\n2 2\n3 0\n0 2\n")
     rp, ci = prep.load_graph(str(f))
     assert rp.tolist() == [0, 3, 3, 4, 5] and ci.tolist() == [1, 2, 3, 2, 0]
+
+
+@pytest.mark.parametrize("bs,K", [(16, 512), (32, 128)])
+def test_hybrid_plan_is_the_model_minimum(bs, K):
+    """The planner's threshold minimises its own cost model over every
+    threshold, and divide at the returned density yields the reported split."""
+    prep = _prep()
+    rp, ci = prep.community_csr(6000, 60.0, 64, 512, 0.95, 11)
+    n = rp.size - 1
+    v = np.ones(ci.size, np.float32)
+    plan = prep.hybrid_plan(rp, ci, bs, K)
+    crp, cci, cv, brp, bci, bv = prep.divide(n, rp, ci, v, bs, plan["density"])
+    assert bci.size == plan["nnzb"] and cci.size == plan["csr_nnz"]
+    tb = (4 * (bs * bs + bs * K) + 4) / 7.0e12
+    tn = (8 + 4 * K) / 7.5e12
+
+    def cost(T):
+        _, c2, _, _, b2, _ = prep.divide(n, rp, ci, v, bs, T / (bs * bs))
+        return b2.size * tb + c2.size * tn
+
+    best = min(cost(T) for T in range(1, bs * bs + 2, max(1, bs * bs // 64)))
+    assert plan["est_seconds"] <= best * (1 + 1e-9)
+    assert abs(plan["est_seconds"] - (bci.size * tb + cci.size * tn)) <= 1e-9 * best
