@@ -324,6 +324,149 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// bs = 16, LDS-staged (ROW blocks, row-major B), fp32 or fp16 A/B: the shipped
+// bs = 16 kernels where the layout allows it. Same scheme as the bs = 32
+// one: a workgroup (4 waves, 256 output columns, 64 per wave) copies each
+// block's A (16 x 16) and B panel (16 rows x 256 columns) into LDS with
+// global_load_lds_dwordx4, D - 1 blocks ahead, one raw barrier per block.
+//  * fp32: v_mfma_f32_16x16x4_f32 with k = 4g + s (lane group g = lane/16), so
+//    a lane's A fragment is one ds_read_b128; B by ds_read_b32.
+//  * fp16: v_mfma_f32_16x16x16_f16 (one block per instruction); the B
+//    fragment (4 consecutive k of one column) comes from the row-major panel
+//    through ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group,
+//    delivered column-wise) — the fragment-shaped 2-byte global loads of the
+//    kernel below are gone.
+// B panel rows are 16-byte-chunk XOR-swizzled (source side and read side) so
+// the reads are bank-conflict-free.
+// ---------------------------------------------------------------------------
+typedef short v4s __attribute__((vector_size(8)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ int bsr16_swz(int row) {
+  return sizeof(T) == 2 ? 2 * (row & 7) : 4 * ((row >> 2) & 1);
+}
+
+template <typename T, bool CROW, int D>
+__global__ __launch_bounds__(256) void bsr16_lds_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const T* __restrict__ val, const T* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  constexpr int kEpc = 16 / sizeof(T);             // elements per 16-B chunk
+  constexpr int kA = 256 * sizeof(T);              // A block bytes
+  constexpr int kRowB = 256 * sizeof(T);           // B panel row bytes (256 columns)
+  constexpr int kStage = kA + 16 * kRowB;          // bytes per stage
+  constexpr int kRpi = 1024 / kRowB;               // B rows per copy instruction (1 or 2)
+  constexpr int kCpr = kRowB / 16;                 // chunks per B row (64 or 32)
+  __shared__ __attribute__((aligned(16))) char smem[D * kStage];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int br = blockIdx.x;
+  const int jt = blockIdx.y * 256;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  if (k0 >= k1) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = jt + 64 * wv + 16 * t + c16;
+      if (j >= n) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const size_t row = (size_t)br * 16 + 4 * g + e;
+        float* p = CROW ? C + row * ldc + j : C + (size_t)j * ldc + row;
+        *p = epi(0.f, alpha, beta, p);
+      }
+    }
+    return;
+  }
+
+  // Copy sources of this wave: A rows 4w .. 4w+3 (lanes 0 .. kA/64 - 1, 16 B
+  // each, contiguous in the block) and B panel rows 4w .. 4w+3.
+  const bool a_lane = lane < kA / 64;
+  const int a_src = (4 * wv) * 16 + lane * kEpc;
+  int b_src[4 / kRpi];
+#pragma unroll
+  for (int i = 0; i < 4 / kRpi; ++i) {
+    const int row = 4 * wv + i * kRpi + lane / kCpr;
+    const int c = (lane % kCpr) ^ bsr16_swz<T>(row);
+    b_src[i] = row * ldb + min(jt + c * kEpc, n - kEpc);
+  }
+  auto issue = [&](int k, int bc, int st) {
+    const int kk = min(k, k1 - 1);
+    char* stage = smem + st * kStage;
+    if (a_lane)
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(val + (size_t)kk * 256 + a_src),
+                                       (lds_void_t)(stage + wv * (kA / 4)), 16, 0, 0);
+    const T* bp = B + (size_t)bc * 16 * ldb;
+#pragma unroll
+    for (int i = 0; i < 4 / kRpi; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(bp + b_src[i]),
+                                       (lds_void_t)(stage + kA + (4 * wv + i * kRpi) * kRowB),
+                                       16, 0, 0);
+  };
+  constexpr int kIssued = 1 + 4 / kRpi;  // copy instructions per wave and block
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  ColCursor cc(colind, k0, k1, lane);
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) issue(k0 + d, cc.get(min(k0 + d, k1 - 1)), d);
+
+  int st = 0;
+  for (int k = k0; k < k1; ++k) {
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(kIssued * (D - 2)));
+    __builtin_amdgcn_s_barrier();
+    issue(k + D - 1, cc.get(min(k + D - 1, k1 - 1)), st == 0 ? D - 1 : st - 1);
+    const char* stage = smem + st * kStage;
+    const char* bpan = stage + kA;
+    if constexpr (sizeof(T) == 2) {
+      // A: row c16, k = 4g .. 4g+3. B: group g reads rows 4g .. 4g+3 transposed.
+      const f16x4 fa = *reinterpret_cast<const f16x4*>(stage + c16 * 32 + 8 * g);
+      const int q = (lane >> 2) & 3, p = lane & 3;
+      const int row = 4 * g + q;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int col = 64 * wv + 16 * t + 4 * p;
+        const int off = row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2;
+        const v4s raw = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(bpan + off));
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, __builtin_bit_cast(f16x4, raw),
+                                                       acc[t], 0, 0, 0);
+      }
+    } else {
+      // A: row c16, k = 4g + s (s = 0..3) -> one 16-B read.
+      const f32x4 fa = *reinterpret_cast<const f32x4*>(stage + c16 * 64 + 16 * g);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int row = 4 * g + s2;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int col = 64 * wv + 16 * t + c16;
+          const int off = row * kRowB + (((col >> 2) ^ bsr16_swz<T>(row)) << 4) + (col & 3) * 4;
+          const float fb = *reinterpret_cast<const float*>(bpan + off);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s2], fb, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    st = st == D - 1 ? 0 : st + 1;
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int j = jt + 64 * wv + 16 * t + c16;
+    if (j >= n) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = (size_t)br * 16 + 4 * g + e;
+      float* p = CROW ? C + row * ldc + j : C + (size_t)j * ldc + row;
+      *p = epi(acc[t][e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // bs = 16 fp32 MFMA. Each wave: 16 rows x 64 columns (4 tiles of 16).
 // ---------------------------------------------------------------------------
 template <bool ROWDIR, bool BROW, bool CROW, int VAR>
@@ -601,6 +744,11 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 constexpr int kBsr32Default = 40;
 // LDS-staged bs = 32 kernel: 4096 + D (+ 8 for the XCD-contiguous order).
 constexpr int kBsr32LdsDefault = 4107;
+// LDS-staged bs = 16 kernels: 4096 + D (fp16: 6 waves/SIMD at D = 3 beat
+// deeper rings; fp32: D = 4). products_bsr16_f16: 9.39 ms vs 10.38 for the
+// register-fragment kernel; fp32 18.5 vs 21.4.
+constexpr int kBsr16LdsDefault = 4100;
+constexpr int kBsr16F16LdsDefault = 4099;
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -688,6 +836,22 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       SPMM_BSR_DISPATCH(bsr32_f32_mfma_kernel, SPMM_COMMA kBsr32Default, grid, dim3(64 * waves), ctx->stream, rowd, brow,
                         crow, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
     }
+  } else if (bs == 16 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 &&
+             aligned(val, 16) && aligned(B, 16) && (var < 0 || var >= 4096)) {
+    dim3 grid(mb, (n + 255) / 256);
+    const int lv = var < 0 ? kBsr16LdsDefault : var;
+#define L(D)                                                                                     \
+  if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<float, true, D>), grid, dim3(256), 0, ctx->stream, \
+                               mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);         \
+  else hipLaunchKernelGGL((bsr16_lds_kernel<float, false, D>), grid, dim3(256), 0, ctx->stream,     \
+                          mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    switch (lv) {
+      case 4099: L(3) break;
+      case 4100: L(4) break;
+      case 4102: L(6) break;
+      default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
+    }
+#undef L
   } else if (bs == 16 && vec_ok) {
     const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
     dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
@@ -726,10 +890,26 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   const bool crow = orderC == SPMM_ORDER_ROW;
   const bool vec_ok = aligned(val, 16) && (brow || (aligned(B, 16) && ldb % 8 == 0));
   const int slot = timing_begin(ctx);
-  if (bs == 16 && vec_ok) {
+  const int var = variant_override();
+  if (bs == 16 && rowd && brow && n >= 8 && n % 8 == 0 && ldb % 8 == 0 && aligned(val, 16) &&
+      aligned(B, 16) && (var < 0 || var >= 4096)) {
+    dim3 grid(mb, (n + 255) / 256);
+    const int lv = var < 0 ? kBsr16F16LdsDefault : var;
+#define L(D)                                                                                      \
+  if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, true, D>), grid, dim3(256), 0,          \
+                               ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
+  else hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, false, D>), grid, dim3(256), 0, ctx->stream,  \
+                          mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    switch (lv) {
+      case 4099: L(3) break;
+      case 4100: L(4) break;
+      case 4102: L(6) break;
+      default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
+    }
+#undef L
+  } else if (bs == 16 && vec_ok) {
     const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
     dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
-    const int var = variant_override();
     if (var >= 0 && rowd && brow && crow) {
       switch (var) {
 #define V(x) case x: hipLaunchKernelGGL((bsr16_f16_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;

@@ -205,3 +205,44 @@ def test_bsr_status_codes(device):
     assert call(args(nnzb=0)) == SUCCESS  # quick return, nothing touched
     assert call(args()) == INVALID_VALUE  # null pointers
     L.spmm_destroy_mat_descr(d)
+
+
+@pytest.mark.parametrize("bs,dtype", [(32, "f32"), (16, "f32"), (16, "f16")])
+@pytest.mark.parametrize("n", [8, 96, 264, 520])
+@pytest.mark.parametrize("oc", [0, 1])
+def test_lds_staged_kernels(oracle, device, bs, dtype, n, oc):
+    """The LDS-staged MFMA kernels (ROW blocks, row-major B): several column
+    tiles with a partial last one, ldb > n, empty block rows, one-block rows
+    (the clamped copy tail), long rows (cursor refills past 64 blocks), and
+    both C orders, with alpha/beta."""
+    rng = np.random.default_rng(n * 7 + bs + oc)
+    mb, kb = 23, 90
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.25, empty_rows=(0, 5))
+    # row 7: one block; row 9: every block column (90 > 64 blocks)
+    rows = [ci[rp[i]:rp[i + 1]] for i in range(mb)]
+    rows[7] = np.array([kb - 1])
+    rows[9] = np.arange(kb)
+    rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    v = rng.uniform(-1, 1, rp[-1] * bs * bs).astype(np.float32)
+    ldb = n + 8
+    Bfull = rng.uniform(-1, 1, (kb * bs, ldb)).astype(np.float32)
+    m = mb * bs
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    alpha, beta = 0.75, -0.5
+    if dtype == "f16":
+        v, Bfull = v.astype(np.float16), Bfull.astype(np.float16)
+    ldc = n if oc == 0 else m
+    Cinit = C0 if oc == 0 else np.ascontiguousarray(C0.T)
+    drp, dci, dv, dB, dC = _dev(rp, ci, v, Bfull.reshape(-1), Cinit.reshape(-1))
+    fn = _ops().bsrmm if dtype == "f32" else _ops().bsrmm_f16
+    fn(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=ldb, C=dC, ldc=ldc, order_c=oc,
+       alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    got = dC.cpu().numpy().reshape(Cinit.shape)
+    got = got if oc == 0 else got.T
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, Bfull[:, :n], n, 0,
+                                 half=dtype == "f16")
+    tol = TOL_F32 if dtype == "f32" else TOL_F16_ACC
+    assert_normwise(got, alpha * ref + beta * C0, abs(alpha) * absd + abs(beta) * np.abs(C0), tol,
+                    f"lds bs={bs} {dtype} n={n} oc={oc}")
