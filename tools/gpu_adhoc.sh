@@ -2,9 +2,13 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests/test_gpu_bsr.py -x -q > gpurun_out/pytest_bsr.log 2>&1; rc=$?
-tail -3 gpurun_out/pytest_bsr.log
-[ $rc -eq 0 ] || { grep -E "Error|assert|FAIL|mismatch" gpurun_out/pytest_bsr.log | head -30; exit $rc; }
-WL=products_bsr16_f16 VARS="4099 4100 4102 12" bash tools/bsr_variants.sh || exit 1
-WL=products_bsr16_f16 EXTRA="--dtype fp32" VARS="4099 4100 4102 8" bash tools/bsr_variants.sh || exit 1
-WL=products_bsr32 VARS="4099 4107" bash tools/bsr_variants.sh || exit 1
+bash tools/gpu_round.sh || exit 1
+SWEEP='--workload arxiv_csr|--workload products_csr_k256|--workload reddit_bsr32|--workload products_bsr32|--workload products_bsr16_f16|--workload reddit_hybrid32|--workload products_hybrid32'
+IFS='|' read -ra A <<< "$SWEEP"
+: > gpurun_out/sweep.jsonl
+for a in "${A[@]}"; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline $a --steps 10 --warmup 3 > gpurun_out/sweep_last.log 2>&1 || { tail -20 gpurun_out/sweep_last.log; exit 1; }
+  grep '^{' gpurun_out/sweep_last.log >> gpurun_out/sweep.jsonl
+done
+echo sweep done
+bash tools/profile_kt.sh || exit 1
