@@ -10,6 +10,8 @@
  *   randomBSRMatrix                   load_data.cc:81-113
  *   dumpCSRToFile / loadCSRFromFile   load_data.cc:125-165 (text CSR format)
  *   loadGraphFromFile                 load_data.cc:167-184 ("n nnz" + edge list)
+ * (text parsed and written by worker threads, host_io.cpp; same results as the
+ * reference's iostream loops on well-formed files, -1 on malformed ones)
  * All of them draw from ONE process-wide generator, as the reference's
  * `static std::mt19937_64 gen(1234)` (load_data.cc:12) does, so call order
  * matters exactly as it does there. Arrays returned through T** are
@@ -55,6 +57,23 @@ int spmm_host_load_csr(const char* prefix, int** rowptr, int** colind, int* n, i
 /* Edge list "n nnz\n src dst ..." -> CSR with sorted neighbours (duplicates
  * kept, as in the reference). Returns 0 on success. */
 int spmm_host_load_graph(const char* filename, int** rowptr, int** colind, int* n, int64_t* nnz);
+
+/* Binary sidecar cache: header (magic "SPMMCSR1",
+ * version, flags, n, nnz, one 64-bit checksum per array) + rowptr[n+1] +
+ * colind[nnz] (+ val[nnz] when given). Written under a temporary name and
+ * renamed. load returns 0, -1 (missing / not a cache / I/O error) or -2
+ * (checksum mismatch: the file is corrupt). *val is NULL when the file has no
+ * values; pass val = NULL to ignore them. */
+int spmm_host_save_csr_bin(const char* path, int n, int64_t nnz, const int* rowptr,
+                           const int* colind, const float* val);
+int spmm_host_load_csr_bin(const char* path, int** rowptr, int** colind, float** val, int* n,
+                           int64_t* nnz);
+
+/* loadCSRFromFile through the cache: <prefix>.csrbin is used when it is at
+ * least as new as both text files and intact; otherwise the text is parsed
+ * and the cache (re)written. The text format is unchanged. */
+int spmm_host_load_csr_cached(const char* prefix, int** rowptr, int** colind, int* n,
+                              int64_t* nnz);
 
 /* Chung-Lu power-law digraph: expected degree w_i = c*(i+s)^(-1/(gamma-1)),
  * w_0 = max_deg, sum w = nnz_target; row i draws d_i distinct columns with

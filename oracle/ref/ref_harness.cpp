@@ -131,4 +131,36 @@ int ref_block_metrics_text(int n, const int* rowptr, const int* colind, int nnz,
   return (int)s.size();
 }
 
+// dumpCSRToFile / loadCSRFromFile (load_data.cc:125-165), loadGraphFromFile
+// (:167-184) + convertGraphToCSR: the text formats as the reference writes
+// and reads them.
+void ref_dump_csr(const char* prefix, int n, int nnz, int* rowptr, int* colind) {
+  dumpCSRToFile(prefix, n, nnz, rowptr, colind);
+}
+
+int64_t ref_load_csr(const char* prefix, int* rowptr, int* colind, int64_t cap_n,
+                     int64_t cap_nnz) {
+  int *rp = nullptr, *ci = nullptr;
+  std::pair<int, int> nz = loadCSRFromFile(prefix, &rp, &ci);
+  if (nz.first + 1 > cap_n || nz.second > cap_nnz) return -1;
+  std::memcpy(rowptr, rp, sizeof(int) * (nz.first + 1));
+  std::memcpy(colind, ci, sizeof(int) * nz.second);
+  free(rp); free(ci);
+  return ((int64_t)nz.first << 32) | (uint32_t)nz.second;
+}
+
+int64_t ref_load_graph(const char* filename, int* rowptr, int* colind, int64_t cap_n,
+                       int64_t cap_nnz) {
+  std::vector<std::vector<int>> edges;
+  const int nnz = loadGraphFromFile(filename, edges);
+  const int n = (int)edges.size();
+  if (n + 1 > cap_n || nnz > cap_nnz) return -1;
+  std::pair<int*, int*> p = convertGraphToCSR(edges);
+  std::memcpy(rowptr, p.first, sizeof(int) * (n + 1));
+  std::memcpy(colind, p.second, sizeof(int) * nnz);
+  free(p.first); free(p.second);
+  return ((int64_t)n << 32) | (uint32_t)nnz;
+}
+
 }  // extern "C"
+

@@ -165,98 +165,7 @@ int64_t spmm_host_random_bsr(int mb, int nb, int blockDim, float p, float minVal
   return cnt;
 }
 
-int spmm_host_dump_csr(const char* prefix, int n, int64_t nnz, const int* rowptr,
-                       const int* colind) {
-  if (!prefix || n < 0 || !rowptr || (nnz > 0 && !colind)) return -1;
-  const std::string p(prefix);
-  FILE* f1 = std::fopen((p + "_indptr.txt").c_str(), "w");
-  FILE* f2 = std::fopen((p + "_indices.txt").c_str(), "w");
-  if (!f1 || !f2) {
-    if (f1) std::fclose(f1);
-    if (f2) std::fclose(f2);
-    return -1;
-  }
-  std::fprintf(f1, "%d\n", n + 1);
-  for (int i = 0; i <= n; ++i) std::fprintf(f1, "%d ", rowptr[i]);
-  std::fprintf(f1, "\n");
-  std::fprintf(f2, "%lld\n", (long long)nnz);
-  for (int64_t i = 0; i < nnz; ++i) std::fprintf(f2, "%d ", colind[i]);
-  std::fprintf(f2, "\n");
-  std::fclose(f1);
-  std::fclose(f2);
-  return 0;
-}
-
-int spmm_host_load_csr(const char* prefix, int** rowptr, int** colind, int* n, int64_t* nnz) {
-  if (!prefix || !rowptr || !colind || !n || !nnz) return -1;
-  const std::string p(prefix);
-  FILE* f1 = std::fopen((p + "_indptr.txt").c_str(), "r");
-  FILE* f2 = std::fopen((p + "_indices.txt").c_str(), "r");
-  if (!f1 || !f2) {
-    if (f1) std::fclose(f1);
-    if (f2) std::fclose(f2);
-    return -1;
-  }
-  int np1 = 0;
-  long long z = 0;
-  int rc = 0;
-  if (std::fscanf(f1, "%d", &np1) != 1 || np1 < 1) rc = -1;
-  int* rp = rc == 0 ? static_cast<int*>(std::malloc(sizeof(int) * (size_t)np1)) : nullptr;
-  for (int i = 0; rc == 0 && i < np1; ++i)
-    if (std::fscanf(f1, "%d", &rp[i]) != 1) rc = -1;
-  if (rc == 0 && (std::fscanf(f2, "%lld", &z) != 1 || z < 0)) rc = -1;
-  int* ci = rc == 0 ? static_cast<int*>(std::malloc(sizeof(int) * (size_t)std::max(1LL, z)))
-                    : nullptr;
-  for (long long i = 0; rc == 0 && i < z; ++i)
-    if (std::fscanf(f2, "%d", &ci[i]) != 1) rc = -1;
-  std::fclose(f1);
-  std::fclose(f2);
-  if (rc != 0) {
-    std::free(rp);
-    std::free(ci);
-    return -1;
-  }
-  *rowptr = rp;
-  *colind = ci;
-  *n = np1 - 1;
-  *nnz = z;
-  return 0;
-}
-
-int spmm_host_load_graph(const char* filename, int** rowptr, int** colind, int* n_out,
-                         int64_t* nnz_out) {
-  if (!filename || !rowptr || !colind || !n_out || !nnz_out) return -1;
-  FILE* f = std::fopen(filename, "r");
-  if (!f) return -1;
-  int n = 0;
-  long long nnz = 0;
-  if (std::fscanf(f, "%d %lld", &n, &nnz) != 2 || n < 0 || nnz < 0) {
-    std::fclose(f);
-    return -1;
-  }
-  std::vector<std::vector<int>> adj(n);
-  for (long long e = 0; e < nnz; ++e) {
-    int x, y;
-    if (std::fscanf(f, "%d %d", &x, &y) != 2 || x < 0 || x >= n) {
-      std::fclose(f);
-      return -1;
-    }
-    adj[x].push_back(y);
-  }
-  std::fclose(f);
-  std::vector<int> rp(n + 1, 0), ci;
-  ci.reserve(nnz);
-  for (int i = 0; i < n; ++i) {
-    std::sort(adj[i].begin(), adj[i].end());
-    ci.insert(ci.end(), adj[i].begin(), adj[i].end());
-    rp[i + 1] = (int)ci.size();
-  }
-  *rowptr = to_malloc(rp);
-  *colind = to_malloc(ci);
-  *n_out = n;
-  *nnz_out = nnz;
-  return 0;
-}
+// spmm_host_dump_csr / spmm_host_load_csr / spmm_host_load_graph: host_io.cpp.
 
 int spmm_host_gen_powerlaw_csr(int n, int64_t nnz_target, int max_deg, double gamma,
                                uint64_t seed, int** rowptr_out, int** colind_out) {

@@ -67,12 +67,13 @@ struct DeviceArena {
     exit(-1);                                     \
   }
 
-// loadCSRFromFile (load_data.cc:143-165) with the reference's "tmp/" prefix.
+// loadCSRFromFile (load_data.cc:143-165) with the reference's "tmp/" prefix, through the
+// binary sidecar cache (<prefix>.csrbin, rewritten whenever the text is newer).
 inline void load_csr_or_die(const std::string& prefix, std::vector<int>& rp,
                             std::vector<int>& ci) {
   int *r = nullptr, *c = nullptr, n = 0;
   int64_t nnz = 0;
-  if (spmm_host_load_csr(prefix.c_str(), &r, &c, &n, &nnz) != 0) {
+  if (spmm_host_load_csr_cached(prefix.c_str(), &r, &c, &n, &nnz) != 0) {
     printf("cannot read %s_indptr.txt / %s_indices.txt\n", prefix.c_str(), prefix.c_str());
     exit(-1);
   }

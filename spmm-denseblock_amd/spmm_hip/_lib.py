@@ -102,6 +102,11 @@ _PROTOS = {
                                    POINTER(c_int64)]),
     "spmm_host_load_graph": (c_int, [c_char_p, POINTER(c_void_p), POINTER(c_void_p), _PI,
                                      POINTER(c_int64)]),
+    "spmm_host_save_csr_bin": (c_int, [c_char_p, c_int, c_int64, _P, _P, _P]),
+    "spmm_host_load_csr_bin": (c_int, [c_char_p, POINTER(c_void_p), POINTER(c_void_p),
+                                       POINTER(c_void_p), _PI, POINTER(c_int64)]),
+    "spmm_host_load_csr_cached": (c_int, [c_char_p, POINTER(c_void_p), POINTER(c_void_p), _PI,
+                                          POINTER(c_int64)]),
     "spmm_host_gen_powerlaw_csr": (c_int, [c_int, c_int64, c_int, c_double, c_uint64,
                                            POINTER(c_void_p), POINTER(c_void_p)]),
     "spmm_host_gen_community_csr": (c_int, [c_int, c_double, c_int, c_int, c_double, c_uint64,

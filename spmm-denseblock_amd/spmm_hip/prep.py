@@ -3,7 +3,8 @@
 Thin wrappers over the C ABI of libspmm_hip.so:
   csr2bsr / bsr2csr / calculate_nnzb / partition_rows   (include/spmm_hip.h)
   rng_seed / random_array / random_csr / random_bsr /
-  load_csr / dump_csr / load_graph / powerlaw_csr / community_csr (include/spmm_host.h)
+  load_csr / dump_csr / load_graph / save_csr_bin / load_csr_bin / load_csr_cached /
+  powerlaw_csr / community_csr                                  (include/spmm_host.h)
   reorder / permute_csr / load_permutation / dump_permutation /
   block_metrics / block_heatmap / dump_heatmap                  (include/spmm_reorder.h)
 All conversion work happens in the library's C++ (north_star: CPU-side
@@ -174,6 +175,38 @@ def load_csr(prefix: str):
     rp, ci, n, nnz = c_void_p(), c_void_p(), c_int(0), c_int64(0)
     if lib().spmm_host_load_csr(prefix.encode(), byref(rp), byref(ci), byref(n), byref(nnz)) != 0:
         raise OSError(f"load_csr({prefix}) failed")
+    return _take(rp, n.value + 1, np.int32), _take(ci, nnz.value, np.int32)
+
+
+def save_csr_bin(path: str, rowptr, colind, val=None) -> None:
+    """Binary sidecar (magic SPMMCSR1 + per-array checksums), include/spmm_host.h."""
+    rowptr, colind = _i32(rowptr), _i32(colind)
+    v = None if val is None else _f32(val)
+    if lib().spmm_host_save_csr_bin(path.encode(), rowptr.size - 1, colind.size, _p(rowptr),
+                                    _p(colind), None if v is None else _p(v)) != 0:
+        raise OSError(f"save_csr_bin({path}) failed")
+
+
+def load_csr_bin(path: str):
+    """-> (rowptr, colind, val or None); raises on a missing or corrupt file."""
+    rp, ci, v, n, nnz = c_void_p(), c_void_p(), c_void_p(), c_int(0), c_int64(0)
+    rc = lib().spmm_host_load_csr_bin(path.encode(), byref(rp), byref(ci), byref(v), byref(n),
+                                      byref(nnz))
+    if rc == -2:
+        raise ValueError(f"load_csr_bin({path}): checksum mismatch (corrupt cache)")
+    if rc != 0:
+        raise OSError(f"load_csr_bin({path}) failed")
+    vals = _take(v, nnz.value, np.float32) if v.value else None
+    return _take(rp, n.value + 1, np.int32), _take(ci, nnz.value, np.int32), vals
+
+
+def load_csr_cached(prefix: str):
+    """loadCSRFromFile through <prefix>.csrbin (used when fresh and intact,
+    rewritten otherwise) -> (rowptr, colind)."""
+    rp, ci, n, nnz = c_void_p(), c_void_p(), c_int(0), c_int64(0)
+    if lib().spmm_host_load_csr_cached(prefix.encode(), byref(rp), byref(ci), byref(n),
+                                       byref(nnz)) != 0:
+        raise OSError(f"load_csr_cached({prefix}) failed")
     return _take(rp, n.value + 1, np.int32), _take(ci, nnz.value, np.int32)
 
 
