@@ -53,6 +53,8 @@ bool block_cols(int br, int bs, int m, const int* rowptr, const int* colind, int
 
 extern "C" {
 
+// Block rows are independent: counts and fills run on worker threads (each
+// with its own marker array), the prefix sums in between are sequential.
 spmm_status_t spmm_xcsr2bsr_nnz(spmm_direction_t dir, int m, int n, const int* csrRowPtr,
                                 const int* csrColInd, int blockDim, int* bsrRowPtr,
                                 int* nnzbTotal) {
@@ -62,13 +64,20 @@ spmm_status_t spmm_xcsr2bsr_nnz(spmm_direction_t dir, int m, int n, const int* c
   const int mb = ceil_div(m, blockDim), nb = ceil_div(n, blockDim);
   if (m > 0 && csrRowPtr[m] - csrRowPtr[0] > 0 && !csrColInd) return SPMM_STATUS_INVALID_VALUE;
   const int base = m > 0 ? csrRowPtr[0] : 0;
-  std::vector<int> mark(std::max(nb, 1), -1), cols;
+  std::vector<int> cnt(mb);
+  std::atomic<bool> ok{true};
+  spmm_host::parallel_for(mb, [&](int64_t lo, int64_t hi) {
+    std::vector<int> mark(std::max(nb, 1), -1), cols;
+    for (int64_t br = lo; br < hi && ok; ++br) {
+      if (!block_cols((int)br, blockDim, m, csrRowPtr, csrColInd, base, mark, cols)) ok = false;
+      cnt[br] = (int)cols.size();
+    }
+  });
+  if (!ok) return SPMM_STATUS_INVALID_VALUE;
   bsrRowPtr[0] = 0;
   long long acc = 0;
   for (int br = 0; br < mb; ++br) {
-    if (!block_cols(br, blockDim, m, csrRowPtr, csrColInd, base, mark, cols))
-      return SPMM_STATUS_INVALID_VALUE;
-    acc += (long long)cols.size();
+    acc += cnt[br];
     if (acc > INT32_MAX) return SPMM_STATUS_INVALID_VALUE;
     bsrRowPtr[br + 1] = (int)acc;
   }
@@ -89,32 +98,40 @@ spmm_status_t spmm_scsr2bsr(spmm_direction_t dir, int m, int n, const float* csr
     return SPMM_STATUS_INVALID_VALUE;
   const int base = m > 0 ? csrRowPtr[0] : 0;
   const size_t bs2 = (size_t)bs * bs;
-  std::vector<int> mark(std::max(nb, 1), -1), cols;
-  for (int br = 0; br < mb; ++br) {
-    if (!block_cols(br, bs, m, csrRowPtr, csrColInd, base, mark, cols))
-      return SPMM_STATUS_INVALID_VALUE;
-    const int k0 = bsrRowPtr[br];
-    if (bsrRowPtr[br + 1] - k0 != (int)cols.size()) return SPMM_STATUS_INVALID_VALUE;
-    for (size_t t = 0; t < cols.size(); ++t) {
-      bsrColInd[k0 + t] = cols[t];
-      mark[cols[t]] = k0 + (int)t;
-    }
-    std::memset(bsrVal + (size_t)k0 * bs2, 0, cols.size() * bs2 * sizeof(float));
-    const int r0 = br * bs, r1 = std::min(m, r0 + bs);
-    for (int r = r0; r < r1; ++r) {
-      const int rr = r - r0;
-      for (int j = csrRowPtr[r] - base; j < csrRowPtr[r + 1] - base; ++j) {
-        const int c = csrColInd[j] - base;
-        const int k = mark[c / bs], cc = c % bs;
-        const size_t off = (size_t)k * bs2 + (dir == SPMM_DIRECTION_ROW
-                                                  ? (size_t)rr * bs + cc
-                                                  : (size_t)cc * bs + rr);
-        bsrVal[off] += csrVal[j];
+  std::atomic<bool> ok{true};
+  spmm_host::parallel_for(mb, [&](int64_t lo, int64_t hi) {
+    std::vector<int> mark(std::max(nb, 1), -1), cols;
+    for (int64_t br = lo; br < hi && ok; ++br) {
+      if (!block_cols((int)br, bs, m, csrRowPtr, csrColInd, base, mark, cols)) {
+        ok = false;
+        return;
       }
+      const int k0 = bsrRowPtr[br];
+      if (bsrRowPtr[br + 1] - k0 != (int)cols.size()) {
+        ok = false;
+        return;
+      }
+      for (size_t t = 0; t < cols.size(); ++t) {
+        bsrColInd[k0 + t] = cols[t];
+        mark[cols[t]] = k0 + (int)t;
+      }
+      std::memset(bsrVal + (size_t)k0 * bs2, 0, cols.size() * bs2 * sizeof(float));
+      const int r0 = (int)br * bs, r1 = std::min(m, r0 + bs);
+      for (int r = r0; r < r1; ++r) {
+        const int rr = r - r0;
+        for (int j = csrRowPtr[r] - base; j < csrRowPtr[r + 1] - base; ++j) {
+          const int c = csrColInd[j] - base;
+          const int k = mark[c / bs], cc = c % bs;
+          const size_t off = (size_t)k * bs2 + (dir == SPMM_DIRECTION_ROW
+                                                    ? (size_t)rr * bs + cc
+                                                    : (size_t)cc * bs + rr);
+          bsrVal[off] += csrVal[j];  // duplicates summed, in CSR order
+        }
+      }
+      for (int bc : cols) mark[bc] = -1;
     }
-    for (int bc : cols) mark[bc] = -1;
-  }
-  return SPMM_STATUS_SUCCESS;
+  });
+  return ok ? SPMM_STATUS_SUCCESS : SPMM_STATUS_INVALID_VALUE;
 }
 
 spmm_status_t spmm_sbsr2csr(spmm_direction_t dir, int mb, int nb, const float* bsrVal,
@@ -244,24 +261,42 @@ spmm_status_t spmm_divide_nnz(int n, const int* rowPtr, const int* colInd, int b
   const int bs = blockDim, nb = ceil_div(n, bs), mb = nb;
   const int base = n > 0 ? rowPtr[0] : 0;
   if (n > 0 && rowPtr[n] - base > 0 && !colInd) return SPMM_STATUS_INVALID_VALUE;
-  DivideScratch s(nb);
-  std::vector<int> adm;
+  // Per block row (worker threads): admitted blocks, and per CSR row the
+  // entries left to the remainder (stored in csrRowPtr[r + 1], summed below).
+  std::vector<int> nb_row(mb);
+  std::atomic<bool> ok{true};
+  spmm_host::parallel_for(mb, [&](int64_t lo, int64_t hi) {
+    DivideScratch s(nb);
+    std::vector<int> adm;
+    for (int64_t br = lo; br < hi && ok; ++br) {
+      if (!divide_block_row((int)br, bs, n, nb, rowPtr, colInd, base, density, s, adm)) {
+        ok = false;
+        return;
+      }
+      nb_row[br] = (int)adm.size();
+      for (int bc : adm) s.slot[bc] = 1;
+      const int r0 = (int)br * bs, r1 = std::min(n, r0 + bs);
+      for (int r = r0; r < r1; ++r) {
+        int c = 0;
+        for (int j = rowPtr[r] - base; j < rowPtr[r + 1] - base; ++j)
+          if (s.slot[(colInd[j] - base) / bs] < 0) ++c;
+        csrRowPtr[r + 1] = c;
+      }
+      for (int bc : adm) s.slot[bc] = -1;
+    }
+  });
+  if (!ok) return SPMM_STATUS_INVALID_VALUE;
   long long nb_acc = 0, c_acc = 0;
   csrRowPtr[0] = 0;
   bsrRowPtr[0] = 0;
+  for (int r = 0; r < n; ++r) {
+    c_acc += csrRowPtr[r + 1];
+    if (c_acc > INT32_MAX) return SPMM_STATUS_INVALID_VALUE;
+    csrRowPtr[r + 1] = (int)c_acc;
+  }
   for (int br = 0; br < mb; ++br) {
-    if (!divide_block_row(br, bs, n, nb, rowPtr, colInd, base, density, s, adm))
-      return SPMM_STATUS_INVALID_VALUE;
-    nb_acc += (long long)adm.size();
-    for (int bc : adm) s.slot[bc] = 1;
-    const int r0 = br * bs, r1 = std::min(n, r0 + bs);
-    for (int r = r0; r < r1; ++r) {
-      for (int j = rowPtr[r] - base; j < rowPtr[r + 1] - base; ++j)
-        if (s.slot[(colInd[j] - base) / bs] < 0) ++c_acc;
-      csrRowPtr[r + 1] = (int)c_acc;
-    }
-    for (int bc : adm) s.slot[bc] = -1;
-    if (nb_acc > INT32_MAX || c_acc > INT32_MAX) return SPMM_STATUS_INVALID_VALUE;
+    nb_acc += nb_row[br];
+    if (nb_acc > INT32_MAX) return SPMM_STATUS_INVALID_VALUE;
     bsrRowPtr[br + 1] = (int)nb_acc;
   }
   *csrNnz = (int)c_acc;
@@ -282,37 +317,46 @@ spmm_status_t spmm_sdivide(int n, const int* rowPtr, const int* colInd, const fl
       (bsrRowPtr[mb] > 0 && (!bsrColInd || !bsrVal)))
     return SPMM_STATUS_INVALID_VALUE;
   const size_t bs2 = (size_t)bs * bs;
-  DivideScratch s(nb);
-  std::vector<int> adm;
-  for (int br = 0; br < mb; ++br) {
-    if (!divide_block_row(br, bs, n, nb, rowPtr, colInd, base, density, s, adm))
-      return SPMM_STATUS_INVALID_VALUE;
-    const int k0 = bsrRowPtr[br];
-    if (bsrRowPtr[br + 1] - k0 != (int)adm.size()) return SPMM_STATUS_INVALID_VALUE;
-    for (size_t t = 0; t < adm.size(); ++t) {
-      bsrColInd[k0 + t] = adm[t];
-      s.slot[adm[t]] = k0 + (int)t;
-    }
-    if (!adm.empty()) std::memset(bsrVal + (size_t)k0 * bs2, 0, adm.size() * bs2 * sizeof(float));
-    const int r0 = br * bs, r1 = std::min(n, r0 + bs);
-    for (int r = r0; r < r1; ++r) {
-      int pos = csrRowPtr[r];
-      for (int j = rowPtr[r] - base; j < rowPtr[r + 1] - base; ++j) {
-        const int c = colInd[j] - base;
-        const int k = s.slot[c / bs];
-        if (k < 0) {
-          csrColInd[pos] = c;
-          csrVal[pos] = val[j];
-          ++pos;
-        } else {
-          bsrVal[(size_t)k * bs2 + (size_t)(r - r0) * bs + c % bs] += val[j];
-        }
+  std::atomic<bool> ok{true};
+  spmm_host::parallel_for(mb, [&](int64_t lo, int64_t hi) {
+    DivideScratch s(nb);
+    std::vector<int> adm;
+    for (int64_t br = lo; br < hi && ok; ++br) {
+      if (!divide_block_row((int)br, bs, n, nb, rowPtr, colInd, base, density, s, adm)) {
+        ok = false;
+        return;
       }
-      if (pos != csrRowPtr[r + 1]) return SPMM_STATUS_INVALID_VALUE;
+      const int k0 = bsrRowPtr[br];
+      if (bsrRowPtr[br + 1] - k0 != (int)adm.size()) {
+        ok = false;
+        return;
+      }
+      for (size_t t = 0; t < adm.size(); ++t) {
+        bsrColInd[k0 + t] = adm[t];
+        s.slot[adm[t]] = k0 + (int)t;
+      }
+      if (!adm.empty())
+        std::memset(bsrVal + (size_t)k0 * bs2, 0, adm.size() * bs2 * sizeof(float));
+      const int r0 = (int)br * bs, r1 = std::min(n, r0 + bs);
+      for (int r = r0; r < r1; ++r) {
+        int pos = csrRowPtr[r];
+        for (int j = rowPtr[r] - base; j < rowPtr[r + 1] - base; ++j) {
+          const int c = colInd[j] - base;
+          const int k = s.slot[c / bs];
+          if (k < 0) {
+            csrColInd[pos] = c;
+            csrVal[pos] = val[j];
+            ++pos;
+          } else {
+            bsrVal[(size_t)k * bs2 + (size_t)(r - r0) * bs + c % bs] += val[j];
+          }
+        }
+        if (pos != csrRowPtr[r + 1]) ok = false;
+      }
+      for (int bc : adm) s.slot[bc] = -1;
     }
-    for (int bc : adm) s.slot[bc] = -1;
-  }
-  return SPMM_STATUS_SUCCESS;
+  });
+  return ok ? SPMM_STATUS_SUCCESS : SPMM_STATUS_INVALID_VALUE;
 }
 
 spmm_status_t spmm_hybrid_plan(int n, const int* rowPtr, const int* colInd, int blockDim, int K,
