@@ -2,13 +2,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-bash tools/gpu_round.sh || exit 1
-SWEEP='--workload arxiv_csr|--workload products_csr_k256|--workload reddit_bsr32|--workload products_bsr32|--workload products_bsr16_f16|--workload reddit_hybrid32|--workload products_hybrid32'
-IFS='|' read -ra A <<< "$SWEEP"
-: > gpurun_out/sweep.jsonl
-for a in "${A[@]}"; do
-  timeout -k 10 300 python bench.py --no-cpu-baseline $a --steps 10 --warmup 3 > gpurun_out/sweep_last.log 2>&1 || { tail -20 gpurun_out/sweep_last.log; exit 1; }
-  grep '^{' gpurun_out/sweep_last.log >> gpurun_out/sweep.jsonl
+for v in 4107 4172 4188 4164; do
+  SPMM_BSR_VARIANT=$v timeout -k 10 300 python tools/bsr_micro.py || exit 1
 done
-echo sweep done
-bash tools/profile_kt.sh || exit 1
+WL=reddit_bsr32 VARS="4107 4172" bash tools/bsr_variants.sh || exit 1
+SPMM_BSR_VARIANT=4172 timeout -k 10 400 python -m pytest tests/test_gpu_bsr.py -x -q -k "lds or mfma_shapes or hybrid" > gpurun_out/pt.log 2>&1; tail -2 gpurun_out/pt.log
