@@ -234,6 +234,31 @@ spmm_status_t spmm_sdivide(int n, const int* rowPtr, const int* colInd, const fl
                            const int* bsrRowPtr, int* csrColInd, float* csrVal, int* bsrColInd,
                            float* bsrVal);
 
+/* Device-pointer conversions: the argument order and
+ * meaning of cusparseXcsr2bsrNnz / cusparseScsr2bsr (run_bsrmm.cu:121-142) and
+ * cusparseSbsr2csr (bsr2csr.cu:186-188), on the handle's stream. The index
+ * bases come from the descriptors. csr2bsr needs rows sorted by column (the
+ * csrSorted* contract) and blockDim <= 64; duplicates are summed in CSR
+ * order, so every output is bit-identical to the host conversions above.
+ * nnzTotalHostPtr is a host pointer (the call synchronises, as cuSPARSE's host
+ * pointer mode does); a column outside [0, n) makes it return
+ * SPMM_STATUS_INVALID_VALUE. csr2bsr zero-fills bsrVal itself. */
+spmm_status_t spmm_xcsr2bsr_nnz_dev(spmm_handle_t handle, spmm_direction_t dir, int m, int n,
+                                    const spmm_mat_descr_t descrA, const int* csrRowPtr,
+                                    const int* csrColInd, int blockDim,
+                                    const spmm_mat_descr_t descrC, int* bsrRowPtr,
+                                    int* nnzTotalHostPtr);
+spmm_status_t spmm_scsr2bsr_dev(spmm_handle_t handle, spmm_direction_t dir, int m, int n,
+                                const spmm_mat_descr_t descrA, const float* csrVal,
+                                const int* csrRowPtr, const int* csrColInd, int blockDim,
+                                const spmm_mat_descr_t descrC, float* bsrVal,
+                                const int* bsrRowPtr, int* bsrColInd);
+spmm_status_t spmm_sbsr2csr_dev(spmm_handle_t handle, spmm_direction_t dir, int mb, int nb,
+                                const spmm_mat_descr_t descrA, const float* bsrVal,
+                                const int* bsrRowPtr, const int* bsrColInd, int blockDim,
+                                const spmm_mat_descr_t descrC, float* csrVal, int* csrRowPtr,
+                                int* csrColInd);
+
 /* Threshold planner for divide (the reference takes `density` from the user,
  * divide.cu:348): from the histogram of block fills it picks the count
  * threshold T minimising a bytes-over-bandwidth model of the hybrid SpMM,

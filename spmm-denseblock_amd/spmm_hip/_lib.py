@@ -84,6 +84,11 @@ _PROTOS = {
     "spmm_csr_partition_rows": (c_int, [c_int, _P, c_int, _P]),
     "spmm_divide_nnz": (c_int, [c_int, _P, _P, c_int, c_float, _P, _P, _PI, _PI]),
     "spmm_sdivide": (c_int, [c_int, _P, _P, _P, c_int, c_float, _P, _P, _P, _P, _P, _P]),
+    "spmm_xcsr2bsr_nnz_dev": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, _PI]),
+    "spmm_scsr2bsr_dev": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P,
+                                  _P]),
+    "spmm_sbsr2csr_dev": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P,
+                                  _P]),
     "spmm_hybrid_plan": (c_int, [c_int, _P, _P, c_int, c_int, c_int, c_double, c_double,
                                  POINTER(c_float), POINTER(c_int64), POINTER(c_int64),
                                  POINTER(c_double)]),

@@ -189,5 +189,66 @@ def hybrid_csrmm(csr: tuple, bsr: tuple, B: torch.Tensor, *, m: int, n: int, k: 
     return C
 
 
-__all__ = ["Handle", "hybrid_csrmm", "default_handle", "gespmm_csrmm", "csrmm", "bsrmm", "bsrmm_f16",
+class _Descr:
+    """spmm_mat_descr_t with an index base (cusparseMatDescr_t)."""
+
+    def __init__(self, base: int = 0):
+        self.raw = c_void_p()
+        check(lib().spmm_create_mat_descr(byref(self.raw)), "spmm_create_mat_descr")
+        check(lib().spmm_set_mat_index_base(self.raw, base), "spmm_set_mat_index_base")
+
+    def __del__(self):
+        try:
+            lib().spmm_destroy_mat_descr(self.raw)
+        except Exception:
+            pass
+
+
+def csr2bsr(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, *, m: int, n: int,
+            bs: int, direction: int = DIRECTION_ROW, base: int = 0,
+            handle: Handle | None = None):
+    """Device csr2bsr (cusparseXcsr2bsrNnz + cusparseScsr2bsr semantics, rows
+    sorted by column, bs <= 64) -> (bsr_rowptr, bsr_colind, bsr_val) tensors,
+    index base `base` on both sides."""
+    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                      (val, torch.float32, "val")):
+        _need(t, dt, nm)
+    h = handle or default_handle()
+    da, dc = _Descr(base), _Descr(base)
+    mb = (m + bs - 1) // bs
+    brp = torch.empty(mb + 1, dtype=torch.int32, device=rowptr.device)
+    nnzb = c_int(0)
+    check(lib().spmm_xcsr2bsr_nnz_dev(h.raw, direction, m, n, da.raw, _ptr(rowptr), _ptr(colind),
+                                      bs, dc.raw, _ptr(brp), byref(nnzb)),
+          "spmm_xcsr2bsr_nnz_dev")
+    bci = torch.empty(nnzb.value, dtype=torch.int32, device=rowptr.device)
+    bval = torch.empty(nnzb.value * bs * bs, dtype=torch.float32, device=rowptr.device)
+    if nnzb.value:
+        check(lib().spmm_scsr2bsr_dev(h.raw, direction, m, n, da.raw, _ptr(val), _ptr(rowptr),
+                                      _ptr(colind), bs, dc.raw, _ptr(bval), _ptr(brp),
+                                      _ptr(bci)), "spmm_scsr2bsr_dev")
+    return brp, bci, bval
+
+
+def bsr2csr(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, *, mb: int, nb: int,
+            bs: int, direction: int = DIRECTION_ROW, base: int = 0,
+            handle: Handle | None = None):
+    """Device bsr2csr (cusparseSbsr2csr semantics: every block expanded,
+    nnz = nnzb * bs^2) -> (csr_rowptr, csr_colind, csr_val) tensors."""
+    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                      (val, torch.float32, "val")):
+        _need(t, dt, nm)
+    h = handle or default_handle()
+    da, dc = _Descr(base), _Descr(base)
+    nnz = colind.numel() * bs * bs
+    crp = torch.empty(mb * bs + 1, dtype=torch.int32, device=rowptr.device)
+    cci = torch.empty(nnz, dtype=torch.int32, device=rowptr.device)
+    cv = torch.empty(nnz, dtype=torch.float32, device=rowptr.device)
+    check(lib().spmm_sbsr2csr_dev(h.raw, direction, mb, nb, da.raw, _ptr(val), _ptr(rowptr),
+                                  _ptr(colind), bs, dc.raw, _ptr(cv), _ptr(crp), _ptr(cci)),
+          "spmm_sbsr2csr_dev")
+    return crp, cci, cv
+
+
+__all__ = ["csr2bsr", "bsr2csr", "Handle", "hybrid_csrmm", "default_handle", "gespmm_csrmm", "csrmm", "bsrmm", "bsrmm_f16",
            "SpmmError", "ORDER_ROW", "ORDER_COL"]
