@@ -224,6 +224,8 @@ typedef __attribute__((address_space(1))) void* gbl_void_t;
 
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4]<<14)
 constexpr int waitcnt_vm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+// vmcnt(n) and lgkmcnt(0): also retires this wave's LDS writes before a barrier.
+constexpr int waitcnt_vm_lgkm0(int n) { return (n & 15) | (7 << 4) | ((n >> 4) << 14); }
 
 template <bool CROW, int D, bool XCD>
 __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
@@ -348,7 +350,7 @@ __device__ __forceinline__ int bsr16_swz(int row) {
   return sizeof(T) == 2 ? 2 * (row & 7) : 4 * ((row >> 2) & 1);
 }
 
-template <typename T, bool CROW, int D>
+template <typename T, bool CROW, int D, bool XCD = false>
 __global__ __launch_bounds__(256) void bsr16_lds_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const T* __restrict__ val, const T* __restrict__ B, int ldb, float alpha, float beta,
@@ -362,7 +364,11 @@ __global__ __launch_bounds__(256) void bsr16_lds_kernel(
   __shared__ __attribute__((aligned(16))) char smem[D * kStage];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int br = blockIdx.x;
+  int br = blockIdx.x;
+  if constexpr (XCD) {  // XCD-contiguous block rows (as bsr32_f32_lds_kernel)
+    const int q = mb / 8, rem = mb % 8, x = br % 8, i = br / 8;
+    br = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + i;
+  }
   const int jt = blockIdx.y * 256;
   const int g = lane >> 4, c16 = lane & 15;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
@@ -744,11 +750,12 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 constexpr int kBsr32Default = 40;
 // LDS-staged bs = 32 kernel: 4096 + D (+ 8 for the XCD-contiguous order).
 constexpr int kBsr32LdsDefault = 4107;
-// LDS-staged bs = 16 kernels: 4096 + D (fp16: 6 waves/SIMD at D = 3 beat
-// deeper rings; fp32: D = 4). products_bsr16_f16: 9.39 ms vs 10.38 for the
-// register-fragment kernel; fp32 18.5 vs 21.4.
+// LDS-staged bs = 16 kernels: 4096 + D (+ 8: XCD-contiguous block rows). fp16:
+// 6 waves/SIMD at D = 3 beat deeper rings, the XCD order 5 % more
+// (products_bsr16_f16 8.80 ms vs 10.38 for the register-fragment kernel);
+// fp32: D = 4, 18.4 vs 21.4.
 constexpr int kBsr16LdsDefault = 4100;
-constexpr int kBsr16F16LdsDefault = 4099;
+constexpr int kBsr16F16LdsDefault = 4107;  // D = 3, XCD-contiguous block rows
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -849,6 +856,10 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       case 4099: L(3) break;
       case 4100: L(4) break;
       case 4102: L(6) break;
+      case 4108:  // + 8: XCD-contiguous block rows
+        if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<float, true, 4, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+        else hipLaunchKernelGGL((bsr16_lds_kernel<float, false, 4, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+        break;
       default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
     }
 #undef L
@@ -904,6 +915,10 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       case 4099: L(3) break;
       case 4100: L(4) break;
       case 4102: L(6) break;
+      case 4107:  // + 8: XCD-contiguous block rows
+        if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, true, 3, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+        else hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, false, 3, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+        break;
       default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
     }
 #undef L
