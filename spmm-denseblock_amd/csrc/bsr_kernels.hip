@@ -116,10 +116,8 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr32_f32_mf
 
   ColCursor cc(colind, k0, k1, lane);
   auto load_frags = [&](int k, float (&fa)[16], float (&fb)[16]) {
-    // VAR & 0x100 / 0x200: diagnostic variants (A always block 0 / B always
-    // panel 0, i.e. cache-resident operands); not used by the dispatch.
-    const int bc = (VAR & 0x200) ? 0 : cc.get(k);
-    const float* ab = val + ((VAR & 0x100) ? 0 : (size_t)k * 1024);
+    const int bc = cc.get(k);
+    const float* ab = val + (size_t)k * 1024;
     if constexpr (ROWDIR) {
       const f32x4* p = reinterpret_cast<const f32x4*>(ab + r * 32 + 16 * h);
 #pragma unroll
@@ -174,8 +172,6 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr32_f32_mf
       if (k > k0) load_frags(k, a0, b0);
       mfma16(a0, b0);
     }
-  } else if constexpr ((VAR & 0x400) != 0) {
-    for (int k = k0; k < k1; ++k) mfma16(a0, b0);  // diagnostic: MFMA chain only
   } else {
     for (int k = k0; k < k1; ++k) {
       if (k + 1 < k1) load_frags(k + 1, a1, b1);
@@ -835,7 +831,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     if (var >= 0 && rowd && brow && crow) {
       switch (var) {
 #define V(x) case x: hipLaunchKernelGGL((bsr32_f32_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
-        V(40) V(44) V(42) V(50) V(58) V(66) V(41) V(49) V(296) V(552) V(808) V(1064) V(298) V(554) V(810)
+        V(40) V(44) V(42) V(50) V(58) V(66) V(41) V(49)
 #undef V
         default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
       }
