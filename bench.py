@@ -48,6 +48,9 @@ WORKLOADS = {
                            p_in=0.97, bs=32, K=128, dtype="fp32"),
     "products_hybrid32": dict(kind="hybrid", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                               p_in=0.97, bs=32, K=128, density="auto"),
+    # §8f rank 2 in the loop: scrambled ids -> in-repo RCM -> divide + hybrid
+    "reddit_rcm_hybrid32": dict(kind="hybrid", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
+                                p_in=0.99, bs=32, K=128, density="auto", reorder="rcm"),
     # §8f next row: dense-block + CSR remainder (divide.cu) on the reddit stand-in
     "reddit_hybrid32": dict(kind="hybrid", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
                             p_in=0.99, bs=32, K=128, density="auto"),
@@ -284,6 +287,21 @@ def run_hybrid(args, W, world, rank, dev, dist):
     K, bs, dens = args.K or W["K"], W["bs"], W["density"]
     rp, ci = prep.community_csr(W["n"], W["avg_deg"], W["cmin"], W["cmax"], W["p_in"], 1234)
     n, nnz = rp.size - 1, ci.size
+    reorder = None
+    if W.get("reorder"):
+        # The reorder-then-block pipeline of reorder_graph.cc / run_bsrmm.cu:
+        # node ids scrambled (the graph as downloaded), then the in-repo
+        # reorderer (spmm_reorder_*), then divide + hybrid SpMM.
+        scr = np.random.default_rng(9).permutation(n).astype(np.int32)
+        rp, ci = prep.permute_csr(rp, ci, scr)
+        before = prep.block_metrics(rp, ci, bs)["nnzb"]
+        t_ro = time.perf_counter()
+        o2n = prep.reorder(rp, ci, W["reorder"])
+        rp, ci = prep.permute_csr(rp, ci, o2n)
+        t_ro = time.perf_counter() - t_ro
+        reorder = {"method": W["reorder"], "host_seconds": round(t_ro, 2),
+                   "nnzb_scrambled": int(before),
+                   "nnzb_reordered": int(prep.block_metrics(rp, ci, bs)["nnzb"])}
     val = np.random.default_rng(2).uniform(-1, 1, nnz).astype(np.float32)
     plan = None
     if args.density is None and dens == "auto":
@@ -319,7 +337,9 @@ def run_hybrid(args, W, world, rank, dev, dist):
     useful = 2.0 * nnz * K
     rec = dict(
         value=useful * args.steps / elapsed / 1e9, ms_per_step=ms, dtype="fp32",
-        data="synthetic community-ordered graph (stand-in for a reordered dataset)",
+        data=("synthetic community graph, node ids scrambled, then reordered in-repo (" +
+              W["reorder"] + ")" if W.get("reorder") else
+              "synthetic community-ordered graph (stand-in for a reordered dataset)"),
         config={"workload": f"{args.workload}: divide(bs={bs}, density={dens}) + hybrid "
                             f"BSR-MFMA/CSR K={K}", "n": n, "nnz": nnz, "K": K, "bs": bs,
                 "nnzb": int(bci.size), "csr_remainder_nnz": int(cci.size),
@@ -330,7 +350,7 @@ def run_hybrid(args, W, world, rank, dev, dist):
             (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": None, "traffic": None, "kernel": "bsr32_f32_mfma + csr_mergepath"},
         csr_same_matrix_ms=round(csr_ms, 4), divide_host_seconds=round(t_div, 2),
-        plan=plan,
+        plan=plan, reorder=reorder,
         part_kernel_ms=None if kt is None else [round(float(x), 4) for x in kt.mean(axis=0)])
     rec["roofline"]["frac"] = round(rec["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
     return rec, None
