@@ -4,8 +4,9 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm).
 Every rank holds the full dense B (replicated: 2.5 GB for products at K=256,
 far under 288 GB), owns a contiguous nnz-balanced row range of A, computes
 its rows of C with the HIP kernel, and the ranks exchange C with ONE
-all-gather over xGMI. Output rows are independent, so the N-GPU result is
-bit-identical to the 1-GPU result of the same kernel on the same rows.
+all-gather over xGMI. Output rows are independent: a row that no merge-path
+wave splits is bit-identical to the 1-GPU result; a split row's carries are
+associated by where the wave boundaries fall (within the fp32 bar).
 
 Shards have unequal row counts; the all-gather runs on a padded
 [world, max_rows, K] buffer whose rank-r slot is written in place by the

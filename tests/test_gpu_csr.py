@@ -244,3 +244,63 @@ def test_products_scale_properties(oracle, device):
     lin = (C1 + C2 - C12).abs()
     absd_full = ops.gespmm_csrmm(drp, dci, dv.abs(), B1.abs() + B2.abs())
     assert bool((lin <= 3 * TOL_F32 * absd_full + 1e-30).all())
+
+
+def test_row_shards_match_whole_matrix(oracle, device):
+    """SURVEY §8e on one device: the rows of each nnz-balanced shard computed
+    alone equal the whole-matrix result — bit for bit where no wave splits
+    the row, within the fp32 bar everywhere."""
+    from spmm_hip import dist as sdist
+    rng = np.random.default_rng(21)
+    m, k, K = 6000, 6000, 128
+    rp, ci, v = _rand_csr(rng, m, k, 20, hub_rows=(10, 2500, 5999), hub_deg=3000)
+    B = rng.uniform(-1, 1, (k, K)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    Cw = torch.empty((m, K), dtype=torch.float32, device=device)
+    _ops().csrmm(drp, dci, dv, dB, n=K, k=k, ldb=K, C=Cw, ldc=K)
+    parts = []
+    for world in (2, 3, 8):
+        for r in range(world):
+            sh = sdist.make_shard(rp, ci, v, r, world)
+            srp, sci, sv = _dev(sh.rowptr, np.ascontiguousarray(sh.colind),
+                                np.ascontiguousarray(sh.val))
+            Cs = torch.empty((sh.rows, K), dtype=torch.float32, device=device)
+            if sh.rows:
+                _ops().csrmm(srp, sci, sv, dB, m=sh.rows, n=K, k=k, ldb=K, C=Cs, ldc=K)
+            parts.append((sh.row0, sh.row1, Cs))
+    torch.cuda.synchronize()
+    whole = Cw.cpu().numpy()
+    ref, absd = oracle_csrmm_f64(oracle, m, K, rp, ci, v, B, K, 0)
+    for r0, r1, Cs in parts:
+        got = Cs.cpu().numpy()
+        assert_normwise(got, ref[r0:r1], absd[r0:r1], TOL_F32, f"shard {r0}:{r1}")
+        # Rows differ only where a wave boundary cuts them in one run or the
+        # other (one row per boundary, ~1 boundary per 512 rows + nnz here).
+        same = np.all(got == whole[r0:r1], axis=1)
+        assert same.mean() > 0.9, (r0, r1, same.mean())
+
+
+def test_permutation_invariance(oracle, device):
+    """(P A P^T)(P B) = P (A B) through the reorder front-end."""
+    from spmm_hip import prep
+    rng = np.random.default_rng(22)
+    rp, ci = prep.community_csr(4000, 25.0, 32, 128, 0.9, 5)
+    v = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    n, K = rp.size - 1, 64
+    B = rng.uniform(-1, 1, (n, K)).astype(np.float32)
+    o2n = prep.reorder(rp, ci, "rcm")
+    prp, pci, pv = prep.permute_csr(rp, ci, o2n, v)
+    PB = np.empty_like(B)
+    PB[o2n] = B
+    d1 = _dev(rp, ci, v, B)
+    d2 = _dev(prp, pci, pv, PB)
+    C1 = torch.empty((n, K), dtype=torch.float32, device=device)
+    C2 = torch.empty((n, K), dtype=torch.float32, device=device)
+    _ops().csrmm(*d1, n=K, k=n, ldb=K, C=C1, ldc=K)
+    _ops().csrmm(*d2, n=K, k=n, ldb=K, C=C2, ldc=K)
+    torch.cuda.synchronize()
+    ref, absd = oracle_csrmm_f64(oracle, n, K, rp, ci, v, B, K, 0)
+    got = np.empty_like(B)
+    got[:] = C2.cpu().numpy()[o2n]  # row o2n[i] of the permuted product is row i
+    assert_normwise(got, ref, absd, TOL_F32, "P A P^T (P B)")
+    assert_normwise(C1.cpu().numpy(), ref, absd, TOL_F32, "A B")
