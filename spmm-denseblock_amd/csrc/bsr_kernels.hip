@@ -469,6 +469,142 @@ __global__ __launch_bounds__(256) void bsr16_lds_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// bs = 16 fp16, LDS-staged, TWO block rows per workgroup sharing B panels:
+// the workgroup walks the union of the two rows' block columns, copying each
+// B panel once (products stand-in: the union is 0.73 of the two rows' blocks).
+// Waves 0 / 1 copy the A block of row 0 / 1, all four copy a quarter of the
+// panel; the union element's row mask reaches the compute step through an
+// LDS header per stage. Past the end, "end" headers and dummy copies keep
+// every iteration's copy count fixed (counted vmcnt per wave).
+// ---------------------------------------------------------------------------
+template <bool CROW, int D>
+__global__ __launch_bounds__(256) void bsr16_f16_pair_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
+    float beta, float* __restrict__ C, int ldc) {
+  typedef _Float16 T;
+  constexpr int kEpc = 8, kA = 512, kRowB = 512, kStage = 2 * 1024 + 16 * kRowB;
+  __shared__ __attribute__((aligned(16))) char smem[D * kStage];
+  __shared__ int hdr[D];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int ng = (mb + 1) / 2;
+  int grp = blockIdx.x;
+  {  // XCD-contiguous groups
+    const int q = ng / 8, rem = ng % 8, x = grp % 8, i = grp / 8;
+    grp = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + i;
+  }
+  const int br0 = 2 * grp;
+  const int jt = blockIdx.y * 256;
+  const int g = lane >> 4, c16 = lane & 15;
+  int pos[2], end[2], head[2];
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int br = br0 + q;
+    pos[q] = br < mb ? rowptr[br] : 0;
+    end[q] = br < mb ? rowptr[br + 1] : 0;
+    any |= pos[q] < end[q];
+  }
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[q][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (any) {
+    ColCursor c0(colind, pos[0], end[0], lane), c1(colind, pos[1], end[1], lane);
+    head[0] = pos[0] < end[0] ? c0.get(pos[0]) : INT_MAX;
+    head[1] = pos[1] < end[1] ? c1.get(pos[1]) : INT_MAX;
+    const int safe_k = pos[0] < end[0] ? pos[0] : pos[1];
+    const int a_off = (lane * 16 % kA) / 2;  // lanes 32-63 duplicate lanes 0-31
+    int b_src[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 4 * wv + 2 * i + lane / 32;
+      const int c = (lane % 32) ^ bsr16_swz<T>(row);
+      b_src[i] = row * ldb + min(jt + c * kEpc, n - kEpc);
+    }
+    auto issue_next = [&](int st) {
+      const int c = min(head[0], head[1]);
+      int mask = 0, k0i = pos[0] < end[0] ? pos[0] : safe_k, k1i = pos[1] < end[1] ? pos[1] : safe_k;
+      if (c != INT_MAX && head[0] == c) {
+        mask |= 1;
+        ++pos[0];
+        head[0] = pos[0] < end[0] ? c0.get(pos[0]) : INT_MAX;
+      }
+      if (c != INT_MAX && head[1] == c) {
+        mask |= 2;
+        ++pos[1];
+        head[1] = pos[1] < end[1] ? c1.get(pos[1]) : INT_MAX;
+      }
+      char* stage = smem + st * kStage;
+      if (threadIdx.x == 0) hdr[st] = c == INT_MAX ? -1 : mask;
+      if (wv < 2)
+        __builtin_amdgcn_global_load_lds((gbl_void_t)(val + (size_t)(wv ? k1i : k0i) * 256 + a_off),
+                                         (lds_void_t)(stage + wv * 1024), 16, 0, 0);
+      const T* bp = B + (size_t)(c == INT_MAX ? 0 : c) * 16 * ldb;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((gbl_void_t)(bp + b_src[i]),
+                                         (lds_void_t)(stage + 2048 + (4 * wv + 2 * i) * kRowB),
+                                         16, 0, 0);
+    };
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) issue_next(d);
+    int st = 0;
+    while (true) {
+      if (wv < 2)
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(3 * (D - 2)));
+      else
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(2 * (D - 2)));
+      __builtin_amdgcn_s_barrier();
+      const int mask = __builtin_amdgcn_readfirstlane(hdr[st]);
+      if (mask < 0) break;
+      issue_next(st == 0 ? D - 1 : st - 1);
+      const char* stage = smem + st * kStage;
+      const char* bpan = stage + 2048;
+      const int q4 = (lane >> 2) & 3, p4 = lane & 3;
+      const int row = 4 * g + q4;
+      f16x4 fb[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int col = 64 * wv + 16 * t + 4 * p4;
+        const int off = row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2;
+        fb[t] = __builtin_bit_cast(
+            f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(bpan + off)));
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (!((mask >> q) & 1)) continue;
+        const f16x4 fa = *reinterpret_cast<const f16x4*>(stage + q * 1024 + c16 * 32 + 8 * g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[q][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[q][t], 0, 0, 0);
+      }
+      st = st == D - 1 ? 0 : st + 1;
+    }
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int br = br0 + q;
+    if (br >= mb) break;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = jt + 64 * wv + 16 * t + c16;
+      if (j >= n) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const size_t r = (size_t)br * 16 + 4 * g + e;
+        float* p = CROW ? C + r * ldc + j : C + (size_t)j * ldc + r;
+        *p = epi(acc[q][t][e], alpha, beta, p);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // bs = 16 fp32 MFMA. Each wave: 16 rows x 64 columns (4 tiles of 16).
 // ---------------------------------------------------------------------------
 template <bool ROWDIR, bool BROW, bool CROW, int VAR>
@@ -751,7 +887,7 @@ constexpr int kBsr32LdsDefault = 4107;
 // (products_bsr16_f16 8.80 ms vs 10.38 for the register-fragment kernel);
 // fp32: D = 4, 18.4 vs 21.4.
 constexpr int kBsr16LdsDefault = 4100;
-constexpr int kBsr16F16LdsDefault = 4107;  // D = 3, XCD-contiguous block rows
+constexpr int kBsr16F16LdsDefault = 4303;  // block-row pairs, D = 3 (4107: single rows)
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -915,6 +1051,17 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
         if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, true, 3, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
         else hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, false, 3, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
         break;
+      case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4
+        const dim3 gp((mb + 1) / 2, (n + 255) / 256);
+        if (lv == 4303) {
+          if (crow) hipLaunchKernelGGL((bsr16_f16_pair_kernel<true, 3>), gp, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+          else hipLaunchKernelGGL((bsr16_f16_pair_kernel<false, 3>), gp, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+        } else {
+          if (crow) hipLaunchKernelGGL((bsr16_f16_pair_kernel<true, 4>), gp, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+          else hipLaunchKernelGGL((bsr16_f16_pair_kernel<false, 4>), gp, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+        }
+        break;
+      }
       default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
     }
 #undef L
