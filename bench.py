@@ -295,7 +295,7 @@ def run_hybrid(args, W, world, rank, dev, dist):
     from spmm_hip import ops, prep
     if world > 1:
         raise SystemExit("hybrid workloads are single-GPU")
-    K, bs, dens = args.K or W["K"], W["bs"], W["density"]
+    K, bs, dens = args.K or W["K"], args.bs or W["bs"], W["density"]
     rp, ci = prep.community_csr(W["n"], W["avg_deg"], W["cmin"], W["cmax"], W["p_in"], 1234)
     n, nnz = rp.size - 1, ci.size
     reorder = None
@@ -376,6 +376,7 @@ def main() -> None:
     ap.add_argument("--K", type=int, default=0, help="override the workload's K")
     ap.add_argument("--density", default=None,
                     help="hybrid workloads: divide threshold (a float, or 'auto' = spmm_hybrid_plan)")
+    ap.add_argument("--bs", type=int, default=0, help="override a hybrid workload's block size")
     ap.add_argument("--dtype", choices=["fp32", "fp16"], default=None,
                     help="override a BSR workload's value type")
     ap.add_argument("--bsr-layout", choices=["row", "col"], default="row",

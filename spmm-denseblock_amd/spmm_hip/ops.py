@@ -12,7 +12,6 @@ through the C ABI. The functions mirror the reference's operator interfaces:
 """
 from __future__ import annotations
 
-import ctypes
 from ctypes import byref, c_float, c_int, c_void_p
 
 import torch

@@ -3,8 +3,6 @@ reference's own outputs (golden fixtures) and the oracle: bit-exact index
 arrays and values. CPU only."""
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import pytest
 

@@ -2,6 +2,11 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-SPMM_BSR_VARIANT=4303 timeout -k 10 300 python -m pytest tests/test_gpu_bsr.py -x -q -k "16-f16 or test_bsrmm_f16" > gpurun_out/pt.log 2>&1; rc=$?
-echo "$(tail -1 gpurun_out/pt.log)"; [ $rc -eq 0 ] || { grep -E "Error|assert" gpurun_out/pt.log | head; exit 1; }
-WL=products_bsr16_f16 VARS="4107 4303 4304 4107 4303" bash tools/bsr_variants.sh || exit 1
+for wl in reddit_hybrid32 products_hybrid32; do
+  for bs in 16 32; do
+    for d in auto 0.0625 0.125; do
+      timeout -k 10 300 python bench.py --workload $wl --bs $bs --density $d --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/h.log 2>&1 || { tail -20 gpurun_out/h.log; exit 1; }
+      grep '^{' gpurun_out/h.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); c=r['config']; print('$wl bs=$bs d=$d', r['ms_per_step'], r['part_kernel_ms'], c['nnzb'], c['csr_remainder_nnz'], (r.get('plan') or {}).get('density'))"
+    done
+  done
+done
