@@ -101,6 +101,10 @@ spmm_status_t spmm_set_csr_waves_per_cu(spmm_handle_t handle, int waves_per_cu);
 /* CSR kernel options (bit flags). SPMM_CSR_NT_STREAMS: read colind/val and
  * write C with non-temporal hints, keeping L2 / MALL for the B gathers. */
 #define SPMM_CSR_NT_STREAMS 1
+/* K <= 32: use the one-nnz-per-wave-instruction kernel (one sequential FMA
+ * chain per unsplit row, the reference's order) instead of the default
+ * several-rows-per-instruction kernel (interleaved chains per row). */
+#define SPMM_CSR_SEQUENTIAL_ROWS 2
 spmm_status_t spmm_set_csr_options(spmm_handle_t handle, int flags);
 
 /* ------------------------------------------------------------------------ */

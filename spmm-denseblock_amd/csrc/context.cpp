@@ -191,7 +191,7 @@ spmm_status_t spmm_set_csr_waves_per_cu(spmm_handle_t h, int w) {
 
 spmm_status_t spmm_set_csr_options(spmm_handle_t h, int flags) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
-  if (flags & ~SPMM_CSR_NT_STREAMS) return SPMM_STATUS_INVALID_VALUE;
+  if (flags & ~(SPMM_CSR_NT_STREAMS | SPMM_CSR_SEQUENTIAL_ROWS)) return SPMM_STATUS_INVALID_VALUE;
   h->csr_flags = flags;
   return SPMM_STATUS_SUCCESS;
 }

@@ -299,6 +299,169 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   }
 }
 
+// Small-K form (K <= 32, K % 4 == 0): the wave is cut into G = 64 / LPG lane
+// groups of LPG lanes (LPG = 2 / 4 / 8 for K <= 8 / 16 / 32; lane l: group
+// l / LPG, columns 4 (l % LPG) .. +3), each group a different nnz of the
+// wave's merge-path range per step. A step is one G-row gather with per-lane
+// colind / val loads instead of per-nnz v_readlane and scalar address
+// arithmetic, which is what bounds the main kernel at small K.
+// Each group accumulates its own partial of the current row; at a row end the
+// groups before the end position are folded in and the G partials summed
+// across groups (log2 G cross-lane steps). Products of a row are thus summed
+// in G interleaved chains — within the fp32 bar, not bit-identical to the
+// sequential order (SPMM_CSR_SEQUENTIAL_ROWS keeps the main kernel).
+// Carries use the VEC = 1 fix-up (columns 0..31 of a slot).
+template <bool NT, int LPG>
+__global__ __launch_bounds__(kWG) void csr_group_kernel(
+    int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, int base, const float* __restrict__ B, int ldb, float alpha,
+    float beta, float* __restrict__ C, int ldc, float* __restrict__ carry_val,
+    int* __restrict__ carry_row, int nwaves) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
+  if (w >= nwaves) return;
+  constexpr int G = kWave / LPG;  // nnz per step (lane groups)
+  const int grp = lane / LPG;
+  const int col = 4 * (lane % LPG);
+  const bool col_ok = col < n;
+  const int col_ld = col_ok ? col : 0;
+
+  const int rp0 = rowptr[0];
+  const long long nnz = (long long)rowptr[m] - rp0;
+  const long long total = (long long)m + nnz;
+  const long long per = (total + nwaves - 1) / nwaves;
+  const long long d0 = min((long long)w * per, total);
+  const long long d1 = min(d0 + per, total);
+  const int ires = merge_search2(rowptr, rp0, m, nnz, d0, d1, lane);
+  const int i0 = rdlane(ires, 0);
+  const int i1 = rdlane(ires, 32);
+  const int j0 = (int)(d0 - i0);
+  const int j1 = (int)(d1 - i1);
+  const int aoff = rp0 - base;
+  const int slot = w;
+
+  auto load_rowends = [&](int rb) -> int { return rowptr[min(rb + 1 + lane, m)]; };
+  int rbase = i0;
+  int rev = load_rowends(rbase);
+  int i = i0;
+  int cur_end = (i < i1) ? rdlane(rev, 0) - rp0 : INT_MAX;
+  auto advance_row = [&]() {
+    ++i;
+    if (i - rbase == kWave) {
+      rbase += kWave;
+      rev = load_rowends(rbase);
+      settle(rev);
+    }
+    cur_end = (i < i1) ? rdlane(rev, i - rbase) - rp0 : INT_MAX;
+  };
+
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float* Bb = B - (size_t)base * ldb;
+  // Sum of the G group partials, in every lane of the same column slot.
+  auto fold = [&](f32x4 v) {
+#pragma unroll
+    for (int o = LPG; o < 64; o <<= 1)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] += __shfl_xor(v[c], o);
+    return v;
+  };
+  auto emit = [&](int row) {
+    const f32x4 t = fold(acc);
+    if (grp == 0 && col_ok) {
+      float* cp = C + (size_t)row * ldc + col;
+      f32x4 out;
+      if (beta == 0.f) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) out[c] = alpha * t[c];
+      } else {
+        const f32x4 old = *reinterpret_cast<const f32x4*>(cp);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) out[c] = __builtin_fmaf(beta, old[c], alpha * t[c]);
+      }
+      if constexpr (NT) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) __builtin_nontemporal_store(out[c], cp + c);
+      } else {
+        *reinterpret_cast<f32x4*>(cp) = out;
+      }
+    }
+    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // Steps of G nnz aligned to absolute array positions (as the main kernel):
+  // step s covers [gs + G s, gs + G s + G); lane group g takes position + g.
+  const int A0 = aoff + j0, A1 = aoff + j1;
+  const int gs = A0 & ~(G - 1);
+  const int S = j1 > j0 ? (A1 - gs + G - 1) / G : 0;
+  auto load_idx = [&](int s, int& c, float& v) {
+    const int p = min(max(gs + G * s + grp, A0), A1 - 1);  // clamped: always a valid index
+    if constexpr (NT) {
+      c = __builtin_nontemporal_load(colind + p);
+      v = __builtin_nontemporal_load(val + p);
+    } else {
+      c = colind[p];
+      v = val[p];
+    }
+  };
+  auto load_b = [&](int c) {
+    return *reinterpret_cast<const f32x4*>(Bb + (size_t)c * ldb + col_ld);
+  };
+  if (S > 0) {
+    // Pipeline: indices two steps ahead, B rows one step ahead.
+    int cA, cB;
+    float vA, vB;
+    load_idx(0, cA, vA);
+    load_idx(min(1, S - 1), cB, vB);
+    f32x4 b = load_b(cA);
+    float vcur = vA;
+    for (int s = 0; s < S; ++s) {
+      // next B row (step s+1) from the indices loaded one step ago
+      const f32x4 bn = load_b(cB);
+      const float vn = vB;
+      load_idx(min(s + 2, S - 1), cB, vB);
+      const int q0 = gs + G * s;
+      const int p = q0 + grp;
+      const bool ok = p >= A0 && p < A1;
+      f32x4 prod;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) prod[c] = ok ? vcur * b[c] : 0.f;
+      // Row ends inside this step: groups before the end position belong to
+      // the ending row.
+      while (cur_end - (q0 - aoff) < G) {  // cur_end is INT_MAX once i reaches i1
+        const int e = cur_end - (q0 - aoff);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bool mine = grp < e;
+          acc[c] += mine ? prod[c] : 0.f;
+          prod[c] = mine ? 0.f : prod[c];
+        }
+        emit(i);
+        advance_row();
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] += prod[c];
+      b = bn;
+      vcur = vn;
+    }
+  }
+  while (i < i1) {
+    emit(i);
+    advance_row();
+  }
+  bool has_carry = false;
+  if (i1 < m && j1 > j0) {
+    const int rs1 = rowptr[i1] - rp0;
+    has_carry = j1 > rs1;
+  }
+  if (has_carry) {
+    if (lane == 0) carry_row[slot] = i1;
+    const f32x4 t = fold(acc);
+    if (grp == 0) *reinterpret_cast<f32x4*>(carry_val + (size_t)slot * kWave + col) = t;
+  } else if (lane == 0) {
+    carry_row[slot] = -1;
+  }
+}
+
 // Adds the carries of rows split across waves, summed in wave order. One
 // wave per carry slot; only the first slot of a run of equal rows works.
 template <int VEC>
@@ -410,6 +573,35 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   dim3 block(kWG);
   const int slot = timing_begin(ctx);
   const bool nt = (ctx->csr_flags & SPMM_CSR_NT_STREAMS) != 0;
+  const bool grouped = n <= 32 && n % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
+                      reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
+                      reinterpret_cast<uintptr_t>(C) % 16 == 0 &&
+                      (ctx->csr_flags & SPMM_CSR_SEQUENTIAL_ROWS) == 0;
+  if (grouped) {
+    dim3 g8((nw + kWavesPerWG - 1) / kWavesPerWG, 1);
+#define SPMM_LAUNCH_GRP(L)                                                                      \
+  if (nt)                                                                                      \
+    hipLaunchKernelGGL((csr_group_kernel<true, L>), g8, block, 0, ctx->stream, m, n, rowptr,    \
+                       colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw); \
+  else                                                                                         \
+    hipLaunchKernelGGL((csr_group_kernel<false, L>), g8, block, 0, ctx->stream, m, n, rowptr,   \
+                       colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw);
+    // lanes per nnz: 4 columns each, so 2 / 4 / 8 lanes cover K <= 8 / 16 / 32
+    if (n <= 8) {
+      SPMM_LAUNCH_GRP(2)
+    } else if (n <= 16) {
+      SPMM_LAUNCH_GRP(4)
+    } else {
+      SPMM_LAUNCH_GRP(8)
+    }
+#undef SPMM_LAUNCH_GRP
+    timing_end(ctx, slot);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return from_hip(e);
+    hipLaunchKernelGGL(csr_carry_fixup_kernel<1>, g8, block, 0, ctx->stream, n, alpha, C, ldc,
+                       carry_val, carry_row, nw);
+    return from_hip(hipGetLastError());
+  }
 #define SPMM_LAUNCH_MP(V, N)                                                                   \
   hipLaunchKernelGGL((csr_mergepath_kernel<V, N>), grid, block, 0, ctx->stream, m, n, rowptr, \
                      colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw)

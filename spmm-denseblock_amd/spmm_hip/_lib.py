@@ -30,6 +30,7 @@ OPERATION_NON_TRANSPOSE, OPERATION_TRANSPOSE = 0, 1
 ORDER_ROW, ORDER_COL = 0, 1
 INDEX_BASE_ZERO, INDEX_BASE_ONE = 0, 1
 CSR_NT_STREAMS = 1
+CSR_SEQUENTIAL_ROWS = 2
 
 
 class SpmmError(RuntimeError):

@@ -100,7 +100,7 @@ def test_gespmm_reference_random_csr(oracle, golden, device, shape, K):
     _check_rowmajor(oracle, rp, ci, v, B, C, f"gespmm {key} K={K}")
 
 
-@pytest.mark.parametrize("K", [1, 2, 7, 64, 128, 130, 256, 512])
+@pytest.mark.parametrize("K", [1, 2, 4, 7, 8, 16, 28, 32, 64, 128, 130, 256, 512])
 def test_power_law_hubs_and_empty_rows(oracle, device, K):
     """Merge-path carries: hub rows spanning many waves, runs of empty rows."""
     rng = np.random.default_rng(100 + K)
@@ -138,6 +138,60 @@ def test_unsplit_rows_bit_exact(oracle, device):
     torch.cuda.synchronize()
     frac = _check_rowmajor(oracle, rp, ci, v, B, C, "unsplit", exact_expected=True)
     assert frac == 1.0
+
+
+@pytest.mark.parametrize("K", [32, 8])
+def test_small_k_sequential_rows_option(oracle, device, K):
+    """K <= 32 runs the several-rows-per-instruction kernel by default
+    (interleaved chains per row, within the fp32 bar); SPMM_CSR_SEQUENTIAL_ROWS
+    selects the main kernel, whose unsplit rows are bit-identical to the
+    reference's sequential order."""
+    from spmm_hip._lib import CSR_NT_STREAMS, CSR_SEQUENTIAL_ROWS
+    rng = np.random.default_rng(7)
+    rp, ci, v = _rand_csr(rng, 40, 300, 9)
+    B = rng.uniform(-1, 1, (300, K)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    h = _ops().Handle()
+    h.set_csr_waves_per_cu(1)
+    C = torch.empty((40, K), dtype=torch.float32, device=device)
+    h.set_csr_options(CSR_NT_STREAMS | CSR_SEQUENTIAL_ROWS)
+    _ops().csrmm(drp, dci, dv, dB, n=K, k=300, ldb=K, C=C, ldc=K, handle=h)
+    torch.cuda.synchronize()
+    assert _check_rowmajor(oracle, rp, ci, v, B, C, "sequential", exact_expected=True) == 1.0
+    h.set_csr_options(CSR_NT_STREAMS)
+    C2 = torch.empty_like(C)
+    _ops().csrmm(drp, dci, dv, dB, n=K, k=300, ldb=K, C=C2, ldc=K, handle=h)
+    torch.cuda.synchronize()
+    _check_rowmajor(oracle, rp, ci, v, B, C2, "grouped rows")
+
+
+@pytest.mark.parametrize("alpha,beta", [(1.0, -0.5), (0.25, 1.0)])
+@pytest.mark.parametrize("orders", [(0, 0), (1, 1)])
+@pytest.mark.parametrize("K", [4, 12, 32])
+def test_small_k_alpha_beta_layouts(oracle, device, alpha, beta, orders, K):
+    """The K <= 32 kernel under csrmm semantics: alpha, beta, both storage
+    orders, hub rows split across waves (carries), empty rows."""
+    ob, oc = orders
+    rng = np.random.default_rng(12 + K)
+    m, k = 1500, 900
+    rp, ci, v = _rand_csr(rng, m, k, 10, hub_rows=(3, 700), hub_deg=800, empty_frac=0.2)
+    Bd = rng.uniform(-1, 1, (k, K)).astype(np.float32)
+    B = Bd if ob == 0 else np.ascontiguousarray(Bd.T)
+    ldb = K if ob == 0 else k
+    C0 = rng.uniform(-1, 1, (m, K)).astype(np.float32)
+    Cin = C0 if oc == 0 else np.ascontiguousarray(C0.T)
+    ldc = K if oc == 0 else m
+    drp, dci, dv, dB, dC = _dev(rp, ci, v, B.reshape(-1), Cin.reshape(-1))
+    h = _ops().Handle()
+    h.set_csr_waves_per_cu(2)
+    _ops().csrmm(drp, dci, dv, dB, n=K, k=k, ldb=ldb, order_b=ob, C=dC, ldc=ldc, order_c=oc,
+                 alpha=alpha, beta=beta, handle=h)
+    torch.cuda.synchronize()
+    got = dC.cpu().numpy().reshape(Cin.shape)
+    got = got if oc == 0 else got.T
+    ref, absd = oracle_csrmm_f64(oracle, m, K, rp, ci, v, Bd, K, 0)
+    assert_normwise(got, alpha * ref + beta * C0, abs(alpha) * absd + abs(beta) * np.abs(C0),
+                    TOL_F32, f"small K={K} a={alpha} b={beta} orders={orders}")
 
 
 @pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (2.5, 0.0), (1.0, 1.0), (-0.5, 0.75)])
