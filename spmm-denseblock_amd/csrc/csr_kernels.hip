@@ -45,6 +45,7 @@ constexpr int kU = 8;            // nnz per pipeline group
 constexpr int kR = 4;            // colind/val registers per lane per chunk
 constexpr int kChunk = kWave * kR / kU;  // groups per chunk (32)
 constexpr int kMinItemsPerWave = 512;
+constexpr int kGroupMaxK = 32;  // K handled by csr_group_kernel (K = 48 / 64: main kernel faster)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -573,7 +574,7 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   dim3 block(kWG);
   const int slot = timing_begin(ctx);
   const bool nt = (ctx->csr_flags & SPMM_CSR_NT_STREAMS) != 0;
-  const bool grouped = n <= 32 && n % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
+  const bool grouped = n <= kGroupMaxK && n % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
                       reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
                       reinterpret_cast<uintptr_t>(C) % 16 == 0 &&
                       (ctx->csr_flags & SPMM_CSR_SEQUENTIAL_ROWS) == 0;
