@@ -81,6 +81,12 @@ __device__ __forceinline__ void settle(T& x) {
 }
 
 __device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// x from lane (l - N) mod 16 of the same 16-lane row (DPP row_ror:N).
+template <int N>
+__device__ __forceinline__ float dpp_ror(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x120 + N, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float rdlanef(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -358,12 +364,19 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const float* Bb = B - (size_t)base * ldb;
-  // Sum of the G group partials, in every lane of the same column slot.
+  // Sum of the G group partials, in every lane of the same column slot:
+  // rotations inside 16-lane rows (v_add_f32_dpp row_ror: one instruction per
+  // step), then the rows with two cross-lane shuffles.
   auto fold = [&](f32x4 v) {
 #pragma unroll
-    for (int o = LPG; o < 64; o <<= 1)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] += __shfl_xor(v[c], o);
+    for (int c = 0; c < 4; ++c) {
+      float x = v[c];
+      if constexpr (LPG <= 2) x += dpp_ror<2>(x);
+      if constexpr (LPG <= 4) x += dpp_ror<4>(x);
+      if constexpr (LPG <= 8) x += dpp_ror<8>(x);
+      x += __shfl_xor(x, 16);
+      v[c] = x + __shfl_xor(x, 32);
+    }
     return v;
   };
   auto emit = [&](int row) {
