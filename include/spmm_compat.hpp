@@ -25,6 +25,12 @@ inline void gespmm_csrmm<float>(int A_nrows, int B_ncols, int* A_rowPtr, int* A_
   (void)spmm_gespmm_csrmm_f32(A_nrows, B_ncols, A_rowPtr, A_colInd, A_val, B, C, nullptr);
 }
 
+template <>
+inline void gespmm_csrmm<double>(int A_nrows, int B_ncols, int* A_rowPtr, int* A_colInd,
+                                 double* A_val, double* B, double* C) {
+  (void)spmm_gespmm_csrmm_f64(A_nrows, B_ncols, A_rowPtr, A_colInd, A_val, B, C, nullptr);
+}
+
 template <class T>
 spmm_status_t rocsparse_bsrmm_template(spmm_handle_t handle, spmm_direction_t dir,
                                        spmm_operation_t trans_A, spmm_operation_t trans_B,
@@ -40,6 +46,16 @@ inline spmm_status_t rocsparse_bsrmm_template<float>(
     const spmm_mat_descr_t descr, const float* bsr_val, const int* bsr_row_ptr,
     const int* bsr_col_ind, int block_dim, float* B, int ldb, float beta, float* C, int ldc) {
   return spmm_sbsrmm(handle, dir, trans_A, trans_B, mb, n, kb, nnzb, &alpha, descr, bsr_val,
+                     bsr_row_ptr, bsr_col_ind, block_dim, B, ldb, &beta, C, ldc);
+}
+
+template <>
+inline spmm_status_t rocsparse_bsrmm_template<double>(
+    spmm_handle_t handle, spmm_direction_t dir, spmm_operation_t trans_A,
+    spmm_operation_t trans_B, int mb, int n, int kb, int nnzb, double alpha,
+    const spmm_mat_descr_t descr, const double* bsr_val, const int* bsr_row_ptr,
+    const int* bsr_col_ind, int block_dim, double* B, int ldb, double beta, double* C, int ldc) {
+  return spmm_dbsrmm(handle, dir, trans_A, trans_B, mb, n, kb, nnzb, &alpha, descr, bsr_val,
                      bsr_row_ptr, bsr_col_ind, block_dim, B, ldb, &beta, C, ldc);
 }
 

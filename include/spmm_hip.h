@@ -279,6 +279,39 @@ spmm_status_t spmm_hybrid_plan(int n, const int* rowPtr, const int* colInd, int 
                                double* estSeconds);
 
 /* ------------------------------------------------------------------------ */
+/* fp64 (T = double in gespmm_csrmm<T> / rocsparse_bsrmm_template<T>,          */
+/* gespmm_csrmm.h:422, rocsparse_bsrmm.h:102): same semantics and checks as    */
+/* the fp32 entry points, VALU fp64 kernels (one sequential FMA chain per CSR  */
+/* output element in CSR order).                                              */
+/* ------------------------------------------------------------------------ */
+spmm_status_t spmm_gespmm_csrmm_f64(int A_nrows, int B_ncols, const int* A_rowPtr,
+                                    const int* A_colInd, const double* A_val, const double* B,
+                                    double* C, void* stream);
+spmm_status_t spmm_csrmm_ex_f64(spmm_handle_t handle, int m, int n, int k, int nnz, double alpha,
+                                const int* csrRowPtr, const int* csrColInd, const double* csrVal,
+                                spmm_index_base_t base, const double* B, int ldb,
+                                spmm_order_t orderB, double beta, double* C, int ldc,
+                                spmm_order_t orderC);
+/* cusparseDcsrmm2 */
+spmm_status_t spmm_dcsrmm2(spmm_handle_t handle, spmm_operation_t transA,
+                           spmm_operation_t transB, int m, int n, int k, int nnz,
+                           const double* alpha, const spmm_mat_descr_t descrA,
+                           const double* csrValA, const int* csrRowPtrA, const int* csrColIndA,
+                           const double* B, int ldb, const double* beta, double* C, int ldc);
+spmm_status_t spmm_bsrmm_ex_f64(spmm_handle_t handle, spmm_direction_t dir, int mb, int kb, int n,
+                                int nnzb, int blockDim, double alpha, const int* bsrRowPtr,
+                                const int* bsrColInd, const double* bsrVal, const double* B,
+                                int ldb, spmm_order_t orderB, double beta, double* C, int ldc,
+                                spmm_order_t orderC);
+/* cusparseDbsrmm / rocsparse_bsrmm_template<double> */
+spmm_status_t spmm_dbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_operation_t transA,
+                          spmm_operation_t transB, int mb, int n, int kb, int nnzb,
+                          const double* alpha, const spmm_mat_descr_t descrA,
+                          const double* bsrValA, const int* bsrRowPtrA, const int* bsrColIndA,
+                          int blockDim, const double* B, int ldb, const double* beta, double* C,
+                          int ldc);
+
+/* ------------------------------------------------------------------------ */
 /* Hybrid dense-block + CSR-remainder SpMM (divide.cu:348-373)                */
 /* ------------------------------------------------------------------------ */
 

@@ -81,20 +81,36 @@ int64_t oracle_random_csr(int m, int n, float p, float lo, float hi, int* rowptr
 // contracted to FMA by nvcc) generalised with cusparseScsrmm's alpha/beta and
 // storage orders (run_csrmm.cu:135-142), epilogue as rocsparse_bsrmm_impl.h:
 // 381-388 (beta == 0 -> alpha*sum without reading C, else fma(beta, C, alpha*sum)).
-void oracle_csrmm_f32(int m, int n, const int* rowptr, const int* colind, const float* val,
-                      int base, const float* B, int ldb, int orderB, float alpha, float beta,
-                      float* C, int ldc, int orderC) {
+// T = double is gespmm_csrmm<double> (the template's T, gespmm_csrmm.h:422).
+extern "C++" {
+template <class T>
+static void csrmm_seq(int m, int n, const int* rowptr, const int* colind, const T* val, int base,
+                      const T* B, int ldb, int orderB, T alpha, T beta, T* C, int ldc,
+                      int orderC) {
 #pragma omp parallel for schedule(dynamic, 64)
   for (int r = 0; r < m; ++r) {
     const int j0 = rowptr[r] - base, j1 = rowptr[r + 1] - base;
     for (int c = 0; c < n; ++c) {
-      float acc = 0.f;
+      T acc = 0;
       for (int j = j0; j < j1; ++j)
         acc = std::fma(val[j], B[at(colind[j] - base, c, ldb, orderB)], acc);
-      float& out = C[at(r, c, ldc, orderC)];
-      out = beta == 0.f ? alpha * acc : std::fma(beta, out, alpha * acc);
+      T& out = C[at(r, c, ldc, orderC)];
+      out = beta == T(0) ? alpha * acc : std::fma(beta, out, alpha * acc);
     }
   }
+}
+}  // extern "C++"
+
+void oracle_csrmm_f32(int m, int n, const int* rowptr, const int* colind, const float* val,
+                      int base, const float* B, int ldb, int orderB, float alpha, float beta,
+                      float* C, int ldc, int orderC) {
+  csrmm_seq<float>(m, n, rowptr, colind, val, base, B, ldb, orderB, alpha, beta, C, ldc, orderC);
+}
+
+void oracle_csrmm_d(int m, int n, const int* rowptr, const int* colind, const double* val,
+                    int base, const double* B, int ldb, int orderB, double alpha, double beta,
+                    double* C, int ldc, int orderC) {
+  csrmm_seq<double>(m, n, rowptr, colind, val, base, B, ldb, orderB, alpha, beta, C, ldc, orderC);
 }
 
 // Same product in double, plus the per-element magnitude sum |a|.|b| used by
@@ -148,28 +164,47 @@ int oracle_num_threads(void) {
 // C = alpha * A_bsr * B + beta * C, A block b stored row-major (dir 0,
 // DIRECTION_ROW: val[b*bs*bs + r*bs + c]) or column-major (dir 1). Sum order:
 // blocks of the block row in order, k = 0..bs-1 inside a block.
-void oracle_bsrmm_f32(int dir, int mb, int n, int bs, const int* rowptr, const int* colind,
-                      const float* val, const float* B, int ldb, int orderB, float alpha,
-                      float beta, float* C, int ldc, int orderC) {
+extern "C++" {
+template <class T>
+static void bsrmm_seq(int dir, int mb, int n, int bs, const int* rowptr, const int* colind,
+                      const T* val, const T* B, int ldb, int orderB, T alpha, T beta, T* C,
+                      int ldc, int orderC) {
   const size_t bs2 = (size_t)bs * bs;
 #pragma omp parallel for schedule(dynamic, 4)
   for (int br = 0; br < mb; ++br) {
     for (int rr = 0; rr < bs; ++rr) {
       const int r = br * bs + rr;
       for (int c = 0; c < n; ++c) {
-        float acc = 0.f;
+        T acc = 0;
         for (int k = rowptr[br]; k < rowptr[br + 1]; ++k) {
-          const float* blk = val + (size_t)k * bs2;
+          const T* blk = val + (size_t)k * bs2;
           for (int q = 0; q < bs; ++q) {
-            const float a = dir == 0 ? blk[(size_t)rr * bs + q] : blk[(size_t)q * bs + rr];
+            const T a = dir == 0 ? blk[(size_t)rr * bs + q] : blk[(size_t)q * bs + rr];
             acc = std::fma(a, B[at(colind[k] * bs + q, c, ldb, orderB)], acc);
           }
         }
-        float& out = C[at(r, c, ldc, orderC)];
-        out = beta == 0.f ? alpha * acc : std::fma(beta, out, alpha * acc);
+        T& out = C[at(r, c, ldc, orderC)];
+        out = beta == T(0) ? alpha * acc : std::fma(beta, out, alpha * acc);
       }
     }
   }
+}
+}  // extern "C++"
+
+void oracle_bsrmm_f32(int dir, int mb, int n, int bs, const int* rowptr, const int* colind,
+                      const float* val, const float* B, int ldb, int orderB, float alpha,
+                      float beta, float* C, int ldc, int orderC) {
+  bsrmm_seq<float>(dir, mb, n, bs, rowptr, colind, val, B, ldb, orderB, alpha, beta, C, ldc,
+                   orderC);
+}
+
+// rocsparse_bsrmm_template<double> (rocsparse_bsrmm.h:102; the double myfma
+// overload, rocsparse_bsrmm_impl.h:10).
+void oracle_bsrmm_d(int dir, int mb, int n, int bs, const int* rowptr, const int* colind,
+                    const double* val, const double* B, int ldb, int orderB, double alpha,
+                    double beta, double* C, int ldc, int orderC) {
+  bsrmm_seq<double>(dir, mb, n, bs, rowptr, colind, val, B, ldb, orderB, alpha, beta, C, ldc,
+                    orderC);
 }
 
 // Double-precision BSR product + |a|.|b| (row-major outputs, m = mb*bs rows).

@@ -172,6 +172,95 @@ spmm_status_t spmm_bsrmm_ex_f16(spmm_handle_t handle, spmm_direction_t dir, int 
                           bsrVal, B, ldb, orderB, beta, C, ldc, orderC);
 }
 
+spmm_status_t spmm_csrmm_ex_f64(spmm_handle_t handle, int m, int n, int k, int nnz, double alpha,
+                                const int* csrRowPtr, const int* csrColInd, const double* csrVal,
+                                spmm_index_base_t base, const double* B, int ldb,
+                                spmm_order_t orderB, double beta, double* C, int ldc,
+                                spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (m < 0 || n < 0 || k < 0 || nnz < 0) return SPMM_STATUS_INVALID_VALUE;
+  if (base != SPMM_INDEX_BASE_ZERO && base != SPMM_INDEX_BASE_ONE)
+    return SPMM_STATUS_INVALID_VALUE;
+  if ((orderB != SPMM_ORDER_ROW && orderB != SPMM_ORDER_COL) ||
+      (orderC != SPMM_ORDER_ROW && orderC != SPMM_ORDER_COL))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  if (!csrRowPtr || !C || (k > 0 && !B) || (nnz > 0 && (!csrColInd || !csrVal)))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (orderB == SPMM_ORDER_ROW ? ldb < n : ldb < (k > 0 ? k : 1)) return SPMM_STATUS_INVALID_VALUE;
+  if (orderC == SPMM_ORDER_ROW ? ldc < n : ldc < m) return SPMM_STATUS_INVALID_VALUE;
+  return launch_csrmm_f64(handle, m, n, csrRowPtr, csrColInd, csrVal, (int)base, B, ldb,
+                          orderB == SPMM_ORDER_ROW, alpha, beta, C, ldc, orderC == SPMM_ORDER_ROW);
+}
+
+spmm_status_t spmm_dcsrmm2(spmm_handle_t handle, spmm_operation_t transA,
+                           spmm_operation_t transB, int m, int n, int k, int nnz,
+                           const double* alpha, const spmm_mat_descr_t descrA,
+                           const double* csrValA, const int* csrRowPtrA, const int* csrColIndA,
+                           const double* B, int ldb, const double* beta, double* C, int ldc) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (!descrA || !alpha || !beta) return SPMM_STATUS_INVALID_VALUE;
+  if (transA != SPMM_OPERATION_NON_TRANSPOSE) return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  if (transB != SPMM_OPERATION_NON_TRANSPOSE && transB != SPMM_OPERATION_TRANSPOSE)
+    return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  const spmm_order_t ob =
+      transB == SPMM_OPERATION_NON_TRANSPOSE ? SPMM_ORDER_COL : SPMM_ORDER_ROW;
+  return spmm_csrmm_ex_f64(handle, m, n, k, nnz, *alpha, csrRowPtrA, csrColIndA, csrValA,
+                           descrA->base, B, ldb, ob, *beta, C, ldc, SPMM_ORDER_COL);
+}
+
+spmm_status_t spmm_gespmm_csrmm_f64(int A_nrows, int B_ncols, const int* A_rowPtr,
+                                    const int* A_colInd, const double* A_val, const double* B,
+                                    double* C, void* stream) {
+  spmm_context* ctx = default_context();
+  if (!ctx) return SPMM_STATUS_NOT_INITIALIZED;
+  if (A_nrows < 0 || B_ncols < 0) return SPMM_STATUS_INVALID_VALUE;
+  if (A_nrows == 0 || B_ncols == 0) return SPMM_STATUS_SUCCESS;
+  if (!A_rowPtr || !C || !B) return SPMM_STATUS_INVALID_VALUE;
+  hipStream_t saved = ctx->stream;
+  ctx->stream = reinterpret_cast<hipStream_t>(stream);
+  const spmm_status_t st = launch_csrmm_f64(ctx, A_nrows, B_ncols, A_rowPtr, A_colInd, A_val, 0,
+                                            B, B_ncols, true, 1.0, 0.0, C, B_ncols, true);
+  ctx->stream = saved;
+  return st;
+}
+
+spmm_status_t spmm_bsrmm_ex_f64(spmm_handle_t handle, spmm_direction_t dir, int mb, int kb, int n,
+                                int nnzb, int blockDim, double alpha, const int* bsrRowPtr,
+                                const int* bsrColInd, const double* bsrVal, const double* B,
+                                int ldb, spmm_order_t orderB, double beta, double* C, int ldc,
+                                spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) return SPMM_STATUS_INVALID_VALUE;
+  bool quick = false;
+  spmm_status_t st = bsr_checks(mb, kb, n, nnzb, blockDim, bsrRowPtr, bsrColInd, bsrVal, B, ldb,
+                                orderB, C, ldc, orderC, &quick);
+  if (st != SPMM_STATUS_SUCCESS || quick) return st;
+  return launch_bsrmm_f64(handle, dir, mb, n, blockDim, bsrRowPtr, bsrColInd, bsrVal, B, ldb,
+                          orderB == SPMM_ORDER_ROW, alpha, beta, C, ldc, orderC == SPMM_ORDER_ROW);
+}
+
+spmm_status_t spmm_dbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_operation_t transA,
+                          spmm_operation_t transB, int mb, int n, int kb, int nnzb,
+                          const double* alpha, const spmm_mat_descr_t descrA,
+                          const double* bsrValA, const int* bsrRowPtrA, const int* bsrColIndA,
+                          int blockDim, const double* B, int ldb, const double* beta, double* C,
+                          int ldc) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (!descrA) return SPMM_STATUS_INVALID_VALUE;
+  if (transA != SPMM_OPERATION_NON_TRANSPOSE) return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  if (transB != SPMM_OPERATION_NON_TRANSPOSE && transB != SPMM_OPERATION_TRANSPOSE)
+    return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  if (mb < 0 || n < 0 || kb < 0 || nnzb < 0 || blockDim <= 0) return SPMM_STATUS_INVALID_VALUE;
+  if (mb == 0 || n == 0 || kb == 0 || nnzb == 0) return SPMM_STATUS_SUCCESS;
+  if (!alpha || !beta) return SPMM_STATUS_INVALID_VALUE;
+  if (descrA->base != SPMM_INDEX_BASE_ZERO) return SPMM_STATUS_MATRIX_TYPE_NOT_SUPPORTED;
+  const spmm_order_t ob =
+      transB == SPMM_OPERATION_NON_TRANSPOSE ? SPMM_ORDER_COL : SPMM_ORDER_ROW;
+  return spmm_bsrmm_ex_f64(handle, dir, mb, kb, n, nnzb, blockDim, *alpha, bsrRowPtrA, bsrColIndA,
+                           bsrValA, B, ldb, ob, *beta, C, ldc, SPMM_ORDER_COL);
+}
+
 spmm_status_t spmm_sbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_operation_t transA,
                           spmm_operation_t transB, int mb, int n, int kb, int nnzb,
                           const float* alpha, const spmm_mat_descr_t descrA,

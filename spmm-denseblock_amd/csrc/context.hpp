@@ -79,6 +79,14 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                spmm_order_t orderB, float beta, float* C, int ldc,
                                spmm_order_t orderC);
 
+spmm_status_t launch_csrmm_f64(spmm_context* ctx, int m, int n, const int* rowptr,
+                               const int* colind, const double* val, int base, const double* B,
+                               int ldb, bool brow, double alpha, double beta, double* C, int ldc,
+                               bool crow);
+spmm_status_t launch_bsrmm_f64(spmm_context* ctx, spmm_direction_t dir, int mb, int n, int bs,
+                               const int* rowptr, const int* colind, const double* val,
+                               const double* B, int ldb, bool brow, double alpha, double beta,
+                               double* C, int ldc, bool crow);
 spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, int kb, int n,
                                int nnzb, int bs, float alpha, const int* rowptr,
                                const int* colind, const uint16_t* val, const uint16_t* B,

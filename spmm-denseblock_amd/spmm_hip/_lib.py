@@ -78,6 +78,16 @@ _PROTOS = {
                                   _P, _P, c_int, c_int, c_float, _P, c_int, c_int]),
     "spmm_bsrmm_ex_f16": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, _P, _P,
                                   _P, _P, c_int, c_int, c_float, _P, c_int, c_int]),
+    "spmm_gespmm_csrmm_f64": (c_int, [c_int, c_int, _P, _P, _P, _P, _P, _P]),
+    "spmm_csrmm_ex_f64": (c_int, [_P, c_int, c_int, c_int, c_int, c_double, _P, _P, _P, c_int,
+                                  _P, c_int, c_int, c_double, _P, c_int, c_int]),
+    "spmm_dcsrmm2": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, POINTER(c_double), _P,
+                             _P, _P, _P, _P, c_int, POINTER(c_double), _P, c_int]),
+    "spmm_bsrmm_ex_f64": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, c_double, _P, _P,
+                                  _P, _P, c_int, c_int, c_double, _P, c_int, c_int]),
+    "spmm_dbsrmm": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                            POINTER(c_double), _P, _P, _P, _P, c_int, _P, c_int,
+                            POINTER(c_double), _P, c_int]),
     "spmm_xcsr2bsr_nnz": (c_int, [c_int, c_int, c_int, _P, _P, c_int, _P, _PI]),
     "spmm_scsr2bsr": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, _P]),
     "spmm_sbsr2csr": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, _P]),

@@ -93,24 +93,35 @@ def default_handle() -> Handle:
     return h
 
 
+_SUFFIX = {torch.float32: "f32", torch.float64: "f64"}
+
+
+def _value_type(val: torch.Tensor) -> torch.dtype:
+    """fp32 or fp64 (the T of gespmm_csrmm<T> / rocsparse_bsrmm_template<T>)."""
+    if val.dtype not in _SUFFIX:
+        raise TypeError(f"val must be float32 or float64, got {val.dtype}")
+    return val.dtype
+
+
 def gespmm_csrmm(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor,
                  B: torch.Tensor, C: torch.Tensor | None = None) -> torch.Tensor:
-    """Drop-in for gespmm_csrmm<float> (gespmm_csrmm.h:422-426).
-    rowptr int32[m+1], colind int32[nnz], val f32[nnz], B f32[k, K] row-major;
-    returns C f32[m, K] (overwritten, no alpha/beta)."""
-    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
-                      (val, torch.float32, "val"), (B, torch.float32, "B")):
-        _need(t, dt, nm)
+    """Drop-in for gespmm_csrmm<T> (gespmm_csrmm.h:422-426), T = float or double
+    from val's dtype. rowptr int32[m+1], colind int32[nnz], val T[nnz], B T[k, K]
+    row-major; returns C T[m, K] (overwritten, no alpha/beta)."""
+    dt = _value_type(val)
+    for t, d, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                     (val, dt, "val"), (B, dt, "B")):
+        _need(t, d, nm)
     m = rowptr.numel() - 1
     K = B.shape[1]
     if C is None:
-        C = torch.empty((m, K), dtype=torch.float32, device=B.device)
-    _need(C, torch.float32, "C")
+        C = torch.empty((m, K), dtype=dt, device=B.device)
+    _need(C, dt, "C")
     if C.shape != (m, K):
         raise ValueError(f"C must be {(m, K)}, got {tuple(C.shape)}")
-    check(lib().spmm_gespmm_csrmm_f32(m, K, _ptr(rowptr), _ptr(colind), _ptr(val), _ptr(B),
-                                      _ptr(C), c_void_p(torch.cuda.current_stream().cuda_stream)),
-          "spmm_gespmm_csrmm_f32")
+    fn = "spmm_gespmm_csrmm_" + _SUFFIX[dt]
+    check(getattr(lib(), fn)(m, K, _ptr(rowptr), _ptr(colind), _ptr(val), _ptr(B), _ptr(C),
+                             c_void_p(torch.cuda.current_stream().cuda_stream)), fn)
     return C
 
 
@@ -119,16 +130,17 @@ def csrmm(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torc
           C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW, alpha: float = 1.0,
           beta: float = 0.0, base: int = 0, handle: Handle | None = None) -> torch.Tensor:
     """C(m x n) = alpha * A(m x k, csr) * B(k x n) + beta * C with explicit
-    storage orders and leading dimensions (spmm_csrmm_ex_f32)."""
-    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
-                      (val, torch.float32, "val"), (B, torch.float32, "B"),
-                      (C, torch.float32, "C")):
-        _need(t, dt, nm)
+    storage orders and leading dimensions (spmm_csrmm_ex_f32 / _f64 by val's dtype)."""
+    dt = _value_type(val)
+    for t, d, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                     (val, dt, "val"), (B, dt, "B"), (C, dt, "C")):
+        _need(t, d, nm)
     h = handle or default_handle()
     m = rowptr.numel() - 1 if m is None else m
-    check(lib().spmm_csrmm_ex_f32(h.raw, m, n, k, colind.numel(), alpha, _ptr(rowptr),
-                                  _ptr(colind), _ptr(val), base, _ptr(B), ldb, order_b, beta,
-                                  _ptr(C), ldc, order_c), "spmm_csrmm_ex_f32")
+    fn = "spmm_csrmm_ex_" + _SUFFIX[dt]
+    check(getattr(lib(), fn)(h.raw, m, n, k, colind.numel(), alpha, _ptr(rowptr), _ptr(colind),
+                             _ptr(val), base, _ptr(B), ldb, order_b, beta, _ptr(C), ldc,
+                             order_c), fn)
     return C
 
 
@@ -137,15 +149,17 @@ def bsrmm(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torc
           C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW, alpha: float = 1.0,
           beta: float = 0.0, direction: int = DIRECTION_ROW,
           handle: Handle | None = None) -> torch.Tensor:
-    """C(mb*bs x n) = alpha * A(bsr) * B(kb*bs x n) + beta * C (spmm_bsrmm_ex_f32)."""
-    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
-                      (val, torch.float32, "val"), (B, torch.float32, "B"),
-                      (C, torch.float32, "C")):
-        _need(t, dt, nm)
+    """C(mb*bs x n) = alpha * A(bsr) * B(kb*bs x n) + beta * C
+    (spmm_bsrmm_ex_f32 / _f64 by val's dtype)."""
+    dt = _value_type(val)
+    for t, d, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                     (val, dt, "val"), (B, dt, "B"), (C, dt, "C")):
+        _need(t, d, nm)
     h = handle or default_handle()
-    check(lib().spmm_bsrmm_ex_f32(h.raw, direction, mb, kb, n, colind.numel(), bs, alpha,
-                                  _ptr(rowptr), _ptr(colind), _ptr(val), _ptr(B), ldb, order_b,
-                                  beta, _ptr(C), ldc, order_c), "spmm_bsrmm_ex_f32")
+    fn = "spmm_bsrmm_ex_" + _SUFFIX[dt]
+    check(getattr(lib(), fn)(h.raw, direction, mb, kb, n, colind.numel(), bs, alpha,
+                             _ptr(rowptr), _ptr(colind), _ptr(val), _ptr(B), ldb, order_b, beta,
+                             _ptr(C), ldc, order_c), fn)
     return C
 
 

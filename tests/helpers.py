@@ -40,6 +40,10 @@ def load_oracle() -> ctypes.CDLL:
         "oracle_random_csr": (I64, [I, I, F, F, F, P, P, P, I64]),
         "oracle_csrmm_f32": (None, [I, I, P, P, P, I, P, I, I, F, F, P, I, I]),
         "oracle_csrmm_f64": (None, [I, I, P, P, P, I, P, I, I, P, P]),
+        "oracle_csrmm_d": (None, [I, I, P, P, P, I, P, I, I, ctypes.c_double, ctypes.c_double,
+                                  P, I, I]),
+        "oracle_bsrmm_d": (None, [I, I, I, I, P, P, P, P, I, I, ctypes.c_double,
+                                  ctypes.c_double, P, I, I]),
         "oracle_spmm_cc_csr": (None, [I64, I64, P, P, P, I64, P]),
         "oracle_num_threads": (I, []),
         "oracle_reorder": (I, [I, I, P, P, P, P, P]),
@@ -84,6 +88,39 @@ def oracle_csrmm_f32(L, m, n, rowptr, colind, val, B, ldb, order_b, alpha=1.0, b
     C = np.ascontiguousarray(C, np.float32).copy()
     L.oracle_csrmm_f32(m, n, ptr(rowptr), ptr(colind), ptr(val), base, ptr(B), ldb, order_b,
                        alpha, beta, ptr(C), ldc, order_c)
+    return C
+
+
+def oracle_csrmm_d(L, m, n, rowptr, colind, val, B, ldb, order_b, alpha=1.0, beta=0.0,
+                   C=None, ldc=None, order_c=0, base=0):
+    """gespmm_csrmm<double> semantics: sequential fp64 FMA in CSR order."""
+    rowptr = np.ascontiguousarray(rowptr, np.int32)
+    colind = np.ascontiguousarray(colind, np.int32)
+    val = np.ascontiguousarray(val, np.float64)
+    B = np.ascontiguousarray(B, np.float64)
+    if ldc is None:
+        ldc = n if order_c == 0 else m
+    if C is None:
+        C = np.zeros(m * ldc if order_c == 0 else n * ldc, np.float64)
+    C = np.ascontiguousarray(C, np.float64).copy()
+    L.oracle_csrmm_d(m, n, ptr(rowptr), ptr(colind), ptr(val), base, ptr(B), ldb, order_b,
+                     alpha, beta, ptr(C), ldc, order_c)
+    return C
+
+
+def oracle_bsrmm_d(L, direction, mb, n, bs, rowptr, colind, val, B, ldb, order_b, alpha=1.0,
+                   beta=0.0, C=None, ldc=None, order_c=0):
+    """rocsparse_bsrmm_template<double> semantics: blocks in order, q = 0..bs-1."""
+    m = mb * bs
+    if ldc is None:
+        ldc = n if order_c == 0 else m
+    if C is None:
+        C = np.zeros(m * ldc if order_c == 0 else n * ldc, np.float64)
+    C = np.ascontiguousarray(C, np.float64).copy()
+    args = [np.ascontiguousarray(a, t) for a, t in
+            ((rowptr, np.int32), (colind, np.int32), (val, np.float64), (B, np.float64))]
+    L.oracle_bsrmm_d(direction, mb, n, bs, *[ptr(a) for a in args], ldb, order_b, alpha, beta,
+                     ptr(C), ldc, order_c)
     return C
 
 

@@ -11,7 +11,8 @@ import os
 import numpy as np
 import pytest
 
-from helpers import (REF_SO, oracle_bsrmm_f32, oracle_csrmm_f32, ptr)
+from helpers import (REF_SO, oracle_bsrmm_d, oracle_bsrmm_f32, oracle_csrmm_d, oracle_csrmm_f32,
+                     ptr)
 
 
 def test_rng_stream_matches_reference(oracle, golden):
@@ -88,6 +89,46 @@ def test_kat_block_cublas_cu(oracle, golden):
                          k["val"], np.array(k["B_rowmajor"], np.float32), k["ldb"], 0,
                          beta=k["beta"], C=np.zeros(12, np.float32), ldc=k["ldc"], order_c=1)
     assert C.tolist() == k["C_colmajor"]
+
+
+def test_kat_fp64_forms(oracle, golden):
+    """T = double (gespmm_csrmm<T>, rocsparse_bsrmm_template<T>): the KAT
+    programs' integer-valued operands give the same answers in fp64."""
+    k = golden["kats"]["csrmm_cu"]
+    C = oracle_csrmm_d(oracle, k["m"], k["n"], k["rowptr"], k["colind"], k["val"],
+                       np.array(k["B_colmajor"], np.float64), k["ldb"], 1, ldc=k["ldc"],
+                       order_c=1)
+    assert C.tolist() == k["C_colmajor"]
+    k = golden["kats"]["bsrmm_cu"]
+    C = oracle_bsrmm_d(oracle, k["dir"], k["mb"], k["n"], k["bs"], k["rowptr"], k["colind"],
+                       k["val"], np.array(k["B_colmajor"], np.float64), k["ldb"], 1,
+                       ldc=k["ldc"], order_c=1)
+    assert C.tolist() == k["C_colmajor"]
+
+
+@pytest.mark.parametrize("bs,direction", [(1, 0), (3, 1), (8, 0)])
+def test_fp64_oracles_vs_dense(oracle, bs, direction):
+    """fp64 oracles against a dense numpy product (alpha/beta epilogue too)."""
+    rng = np.random.default_rng(5)
+    mb, kb, n = 13, 11, 7
+    mask = rng.random((mb, kb)) < 0.3
+    brp = np.concatenate([[0], np.cumsum(mask.sum(1))]).astype(np.int32)
+    bci = np.nonzero(mask)[1].astype(np.int32)
+    blocks = rng.standard_normal((bci.size, bs, bs))
+    A = np.zeros((mb * bs, kb * bs))
+    for r in range(mb):
+        for k in range(brp[r], brp[r + 1]):
+            A[r * bs:(r + 1) * bs, bci[k] * bs:(bci[k] + 1) * bs] = blocks[k]
+    vals = blocks if direction == 0 else blocks.transpose(0, 2, 1)
+    B = rng.standard_normal((kb * bs, n))
+    C0 = rng.standard_normal((mb * bs, n))
+    got = oracle_bsrmm_d(oracle, direction, mb, n, bs, brp, bci, vals.ravel(), B, n, 0,
+                         alpha=0.5, beta=2.0, C=C0.ravel()).reshape(mb * bs, n)
+    np.testing.assert_allclose(got, 0.5 * A @ B + 2.0 * C0, rtol=1e-12, atol=1e-12)
+    rows, cols = np.nonzero(A)
+    rp = np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=A.shape[0]))])
+    got = oracle_csrmm_d(oracle, A.shape[0], n, rp, cols, A[rows, cols], B, n, 0)
+    np.testing.assert_allclose(got.reshape(-1, n), A @ B, rtol=1e-12, atol=1e-12)
 
 
 def test_kat_spmm_cc_small(oracle, golden):
