@@ -337,9 +337,14 @@ def run_hybrid(args, W, world, rank, dev, dist):
         ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=C,
                          ldc=K, handle=h)
 
+    hopt = args.hybrid_options or 0
+    if hopt:
+        h.set_hybrid_options(hopt)
+    # SPMM_HYBRID_FUSED: both parts in one bs = 32 launch
+    fused = bs == 32 and bci.size > 0 and cci.size > 0 and K % 4 == 0 and bool(hopt & 1)
     elapsed, kt = timed_loop(step, h, args.steps, args.warmup, 1, dist, raw=True)
     # launch order per step: the BSR kernel, then the CSR kernel (when both parts exist)
-    parts = int(bci.size > 0) + int(cci.size > 0)
+    parts = 1 if fused else int(bci.size > 0) + int(cci.size > 0)
     kt = np.array(kt[: parts * args.steps]).reshape(args.steps, parts) if parts else None
     h2 = ops.Handle()
     _, csr_ms = timed_loop(lambda: ops.csrmm(d[6], d[7], d[8], B, m=n, n=K, k=mb * bs, ldb=K,
@@ -355,11 +360,13 @@ def run_hybrid(args, W, world, rank, dev, dist):
                             f"BSR-MFMA/CSR K={K}", "n": n, "nnz": nnz, "K": K, "bs": bs,
                 "nnzb": int(bci.size), "csr_remainder_nnz": int(cci.size),
                 "bsr_fill": round((nnz - cci.size) / max(1, bci.size * bs * bs), 4),
-                "parallelism": "single"},
+                "parallelism": "single", "hybrid_options": hopt, "fused": bool(fused)},
         roofline={"bound": "hbm", "achieved": round(
             (csr_bytes(n, int(cci.size), K) + bsr_bytes(mb, int(bci.size), bs, K, 4)) /
             (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": None, "traffic": None, "kernel": "bsr32_f32_mfma + csr_mergepath"},
+            "frac": None, "traffic": None,
+            "kernel": ("bsr32_f32_lds_kernel<HYB> (fused)" if fused else
+                       "bsr MFMA kernel + csr_mergepath")},
         csr_same_matrix_ms=round(csr_ms, 4), divide_host_seconds=round(t_div, 2),
         plan=plan, reorder=reorder,
         part_kernel_ms=None if kt is None else [round(float(x), 4) for x in kt.mean(axis=0)])
@@ -383,6 +390,8 @@ def main() -> None:
                     help="B/C storage for BSR workloads (col = cusparse transB=N)")
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--csr-options", type=int, default=None, help="SPMM_CSR_* flags")
+    ap.add_argument("--hybrid-options", type=int, default=None,
+                    help="SPMM_HYBRID_* flags (1 = fused single launch, bs = 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (DESIGN.md §7)")

@@ -315,6 +315,14 @@ spmm_status_t spmm_dbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_opera
 /* Hybrid dense-block + CSR-remainder SpMM (divide.cu:348-373)                */
 /* ------------------------------------------------------------------------ */
 
+/* Hybrid options (per handle): SPMM_HYBRID_FUSED computes both parts in one
+ * bs = 32 launch (MFMA part, then each block row's CSR remainder in the same
+ * workgroup) instead of two stream-ordered launches. Same result up to the
+ * CSR kernel's split-row carries; measured no faster on bandwidth-bound
+ * inputs, hence opt-in. */
+#define SPMM_HYBRID_FUSED 1
+spmm_status_t spmm_set_hybrid_options(spmm_handle_t handle, int flags);
+
 /* C(m x n) = alpha * (A_bsr + A_csr) * B(k x n) + beta * C, row-major B and C.
  * A_bsr is the BSR part of spmm_sdivide (bs x bs blocks, mb = ceil(m/bs)
  * block rows), A_csr the remainder. When nnzb > 0, B must hold

@@ -291,8 +291,9 @@ extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
     const int* bsrColInd, const float* bsrVal, int nnzb, const float* B, int ldb, float beta,
     float* C, int ldc) {
   // divide.cu:348-373 runs csrmm2 and bsrmm back to back with alpha = beta = 1
-  // onto a zeroed C; here the BSR part applies the caller's beta and the CSR
-  // remainder accumulates on top, both on the handle's stream.
+  // onto a zeroed C. Here the BSR part applies the caller's beta and the CSR
+  // remainder accumulates on top, both on the handle's stream; with
+  // SPMM_HYBRID_FUSED (bs = 32) one launch does both per block row (§4a).
   if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
   if (m < 0 || n < 0 || k < 0 || csrNnz < 0 || nnzb < 0 || blockDim <= 0)
     return SPMM_STATUS_INVALID_VALUE;
@@ -300,6 +301,10 @@ extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
   if (!csrRowPtr || !C || ldb < n || ldc < n || (k > 0 && !B)) return SPMM_STATUS_INVALID_VALUE;
   if (nnzb > 0 && (!bsrRowPtr || !bsrColInd || !bsrVal)) return SPMM_STATUS_INVALID_VALUE;
   if (csrNnz > 0 && (!csrColInd || !csrVal)) return SPMM_STATUS_INVALID_VALUE;
+  if (blockDim == 32 && nnzb > 0 && csrNnz > 0 && (handle->hybrid_flags & SPMM_HYBRID_FUSED) &&
+      hybrid32_fusable(n, ldb, ldc, bsrVal, B, C))
+    return launch_hybrid32_fused(handle, m, n, alpha, csrRowPtr, csrColInd, csrVal, bsrRowPtr,
+                                 bsrColInd, bsrVal, B, ldb, beta, C, ldc);
   float csr_beta = beta;
   if (nnzb > 0) {
     const int mb = (m + blockDim - 1) / blockDim, kb = (k + blockDim - 1) / blockDim;

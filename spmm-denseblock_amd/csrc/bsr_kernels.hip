@@ -223,23 +223,134 @@ constexpr int waitcnt_vm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >
 // vmcnt(n) and lgkmcnt(0): also retires this wave's LDS writes before a barrier.
 constexpr int waitcnt_vm_lgkm0(int n) { return (n & 15) | (7 << 4) | ((n >> 4) << 14); }
 
-template <bool CROW, int D, bool XCD>
+// Fused-hybrid epilogue (spmm_hybrid_csrmm_f32). The MFMA tile
+// (32 rows x 128 columns, raw sums) goes to LDS; then the 4 waves split the
+// block row's 32 rows into contiguous ranges balanced on rows + remainder nnz
+// (a merge-path cut over the 33 row pointers, one ballot per wave). A wave
+// walks its rows with wave-uniform (scalar) colind/val loads, lanes across the
+// 128 columns (one float2 of each B row per lane, 512 B per wave-instruction),
+// 8 entries in flight per batch, one sequential FMA chain per element in CSR
+// order, and writes each row once:
+//   C = epi(tile, alpha, beta, C) + alpha * remainder
+// which is the two-launch result (BSR kernel, then the CSR kernel with
+// beta = 1) bit for bit on every row the CSR kernel keeps in one wave.
+// The remainder's HBM gathers of one workgroup overlap other workgroups' MFMA
+// phases on the same CU.
+constexpr int kHybBatch = 32;
+constexpr int kHybTs = 136;  // tile row stride (floats): the two half-waves' rows
+                             // land 32 banks apart when the tile is written
+template <int D>
+__device__ __forceinline__ void hyb_remainder(float* smem, const f32x16& acc, int br, int jt,
+                                              int n, const int* __restrict__ rrp,
+                                              const int* __restrict__ rci,
+                                              const float* __restrict__ rv, int m,
+                                              const float* __restrict__ B, int ldb, float alpha,
+                                              float beta, float* __restrict__ C, int ldc) {
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  __syncthreads();  // every wave is done with the stages (copies drained before)
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) smem[(8 * g + 4 * h + e) * kHybTs + 32 * wv + r] = acc[4 * g + e];
+  __syncthreads();
+
+  const int R0 = br * 32;
+  // lane i (0..32) holds the row pointer of local row i (rows >= m: empty)
+  const int rpv = rrp[min(R0 + min(lane, 32), m)];
+  const int s0 = __builtin_amdgcn_readlane(rpv, 0);
+  const int tot = __builtin_amdgcn_readlane(rpv, 32) - s0;
+  const int pos = rpv - s0 + lane;  // merge-path coordinate of row i's start
+  auto cut = [&](int w) -> int {
+    const int t = (int)(((long long)(tot + 32) * w) / 4);
+    return __builtin_popcountll(__ballot(lane <= 32 && pos < t));
+  };
+  const int i0 = cut(wv), i1 = wv == 3 ? 32 : cut(wv + 1);
+  const int j = jt + 2 * lane;
+  const bool jok = j < n;
+  const int jl = jok ? j : 0;
+  // The wave's entries [p, pend) as one stream across its rows, kHybBatch
+  // gathers in flight per step (rows average a few entries on power-law
+  // graphs, so per-row batches would serialise on latency); a row is written
+  // when the stream passes its end.
+  int i = i0;
+  int next = __builtin_amdgcn_readlane(rpv, i0 + 1);
+  float ax = 0.f, ay = 0.f;
+  auto flush = [&]() {
+    if (jok) {
+      const float2 t = *reinterpret_cast<const float2*>(smem + i * kHybTs + 2 * lane);
+      float* out = C + (size_t)(R0 + i) * ldc + j;
+      float2 o;
+      o.x = epi(t.x, alpha, beta, out) + alpha * ax;
+      o.y = epi(t.y, alpha, beta, out + 1) + alpha * ay;
+      *reinterpret_cast<float2*>(out) = o;
+    }
+    ax = ay = 0.f;
+    ++i;
+    next = __builtin_amdgcn_readlane(rpv, min(i + 1, 32));
+  };
+  int p = __builtin_amdgcn_readlane(rpv, i0);
+  const int pend = __builtin_amdgcn_readlane(rpv, i1);
+  while (p < pend) {
+    const int nb = min(kHybBatch, pend - p);
+    float2 b[kHybBatch];
+    float a[kHybBatch];
+#pragma unroll
+    for (int u = 0; u < kHybBatch; ++u) {
+      const int q = min(p + u, pend - 1);  // clamped: same count every step
+      a[u] = rv[q];
+      b[u] = *reinterpret_cast<const float2*>(B + (size_t)rci[q] * ldb + jl);
+    }
+#pragma unroll
+    for (int u = 0; u < kHybBatch; ++u) {
+      if (u < nb) {
+        while (i < i1 && p + u >= next) flush();
+        ax = __builtin_fmaf(a[u], b[u].x, ax);
+        ay = __builtin_fmaf(a[u], b[u].y, ay);
+      }
+    }
+    p += nb;
+  }
+  while (i < i1) flush();
+}
+
+// HYB (the fused hybrid, §4a): after the block loop the workgroup adds its
+// 32 rows' CSR remainder (rrp/rci/rv, m rows) — see hyb_remainder below.
+// Only CROW is instantiated with HYB.
+// XM: block-row order across the 8 XCDs (dispatch puts workgroup b on XCD
+// b % 8). 0 = as dispatched; 1 = each XCD a contiguous eighth (neighbouring
+// block rows share that XCD's L2); XM >= 2 = chunks of XM block rows dealt
+// round-robin to the XCDs (L2 locality inside a chunk, and a heavy region of
+// the matrix spread over all XCDs instead of landing on one).
+__device__ __forceinline__ int xcd_block_row(int b, int mb, int xm) {
+  if (xm == 1) {
+    const int q = mb / 8, rem = mb % 8, x = b % 8, i = b / 8;
+    return (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + i;
+  }
+  if (xm >= 2) {
+    const int full = mb / (8 * xm) * (8 * xm);
+    if (b >= full) return b;
+    const int x = b % 8, i = b / 8;
+    return ((i / xm) * 8 + x) * xm + i % xm;
+  }
+  return b;
+}
+
+template <bool CROW, int D, int XM, bool HYB = false>
 __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
-    float* __restrict__ C, int ldc) {
+    float* __restrict__ C, int ldc, const int* __restrict__ rrp, const int* __restrict__ rci,
+    const float* __restrict__ rv, int m) {
   constexpr int kStage = 1024 + 32 * 128;  // floats: A block + B panel (20 KB)
   __shared__ __attribute__((aligned(16))) float smem[D * kStage];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  int br = blockIdx.x;
-  if constexpr (XCD) {
-    const int q = mb / 8, rem = mb % 8, x = br % 8, i = br / 8;
-    br = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + i;
-  }
+  const int br = xcd_block_row(blockIdx.x, mb, XM);
   const int jt = blockIdx.y * 128;  // first output column of the workgroup
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
-  if (k0 >= k1) {  // empty block row: C = beta * C (alpha * 0)
+  if (!HYB && k0 >= k1) {  // empty block row: C = beta * C (alpha * 0)
     const int j = jt + 32 * wv + (lane & 31);
     if (j < n)
       for (int e = 0; e < 16; ++e) {
@@ -279,6 +390,7 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
   // Block columns through the readlane cursor: no load per block (a scalar
   // load per block sat right before the copies it feeds), one refill per 64.
+  if (!HYB || k0 < k1) {
   ColCursor cc(colind, k0, k1, lane);
 #pragma unroll
   for (int d = 0; d < D - 1; ++d) issue(k0 + d, cc.get(min(k0 + d, k1 - 1)), d);
@@ -306,7 +418,12 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
     st = st == D - 1 ? 0 : st + 1;
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // drain the clamped tail copies
+  }
 
+  if constexpr (HYB) {
+    hyb_remainder<D>(smem, acc, br, jt, n, rrp, rci, rv, m, B, ldb, alpha, beta, C, ldc);
+    return;
+  }
   const int jcol = jt + 32 * wv + r;
   if (jcol >= n) return;
   const size_t row0 = (size_t)br * 32;
@@ -360,11 +477,7 @@ __global__ __launch_bounds__(256) void bsr16_lds_kernel(
   __shared__ __attribute__((aligned(16))) char smem[D * kStage];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  int br = blockIdx.x;
-  if constexpr (XCD) {  // XCD-contiguous block rows (as bsr32_f32_lds_kernel)
-    const int q = mb / 8, rem = mb % 8, x = br % 8, i = br / 8;
-    br = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + i;
-  }
+  const int br = xcd_block_row(blockIdx.x, mb, XCD ? 1 : 0);  // XCD-contiguous option
   const int jt = blockIdx.y * 256;
   const int g = lane >> 4, c16 = lane & 15;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
@@ -880,8 +993,9 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 }
 
 constexpr int kBsr32Default = 40;
-// LDS-staged bs = 32 kernel: 4096 + D (+ 8 for the XCD-contiguous order).
-constexpr int kBsr32LdsDefault = 4107;
+// LDS-staged bs = 32 kernel: 4096 + D (+ 8: XCD-contiguous order; 4123-4125:
+// XCD order in chunks of 16 / 32 / 64 block rows).
+constexpr int kBsr32LdsDefault = 4124;
 // LDS-staged bs = 16 kernels: 4096 + D (+ 8: XCD-contiguous block rows). fp16:
 // 6 waves/SIMD at D = 3 beat deeper rings, the XCD order 5 % more
 // (products_bsr16_f16 8.80 ms vs 10.38 for the register-fragment kernel);
@@ -949,15 +1063,20 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     const int lv = var < 0 ? kBsr32LdsDefault : var;
 #define L(D, X)                                                                                   \
   if (crow) hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, D, X>), grid, dim3(256), 0, ctx->stream,  \
-                               mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);          \
+                               mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, nullptr,  \
+                               nullptr, nullptr, 0);                                              \
   else hipLaunchKernelGGL((bsr32_f32_lds_kernel<false, D, X>), grid, dim3(256), 0, ctx->stream,      \
-                          mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+                          mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, nullptr,       \
+                          nullptr, nullptr, 0);
     switch (lv) {
-      case 4098: L(2, false) break;
-      case 4099: L(3, false) break;
-      case 4100: L(4, false) break;
-      case 4106: L(2, true) break;
-      case 4107: L(3, true) break;
+      case 4098: L(2, 0) break;
+      case 4099: L(3, 0) break;
+      case 4100: L(4, 0) break;
+      case 4106: L(2, 1) break;
+      case 4107: L(3, 1) break;
+      case 4123: L(3, 16) break;  // 4123-4125: XCD order in chunks of 16 / 32 / 64
+      case 4124: L(3, 32) break;
+      case 4125: L(3, 64) break;
       default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
     }
 #undef L
@@ -1014,6 +1133,30 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     hipLaunchKernelGGL(bsr_generic_kernel<float>, grid, dim3(256), 0, ctx->stream, mb, n, bs,
                        rowd, rowptr, colind, val, B, ldb, brow, alpha, beta, C, ldc, crow);
   }
+  timing_end(ctx, slot);
+  return from_hip(hipGetLastError());
+}
+
+bool hybrid32_fusable(int n, int ldb, int ldc, const float* bval, const float* B, const float* C) {
+  return n >= 4 && n % 4 == 0 && ldb % 4 == 0 && ldc % 2 == 0 && aligned(bval, 16) &&
+         aligned(B, 16) && aligned(C, 8);
+}
+
+spmm_status_t launch_hybrid32_fused(spmm_context* ctx, int m, int n, float alpha,
+                                    const int* crp, const int* cci, const float* cv,
+                                    const int* brp, const int* bci, const float* bval,
+                                    const float* B, int ldb, float beta, float* C, int ldc) {
+  const int mb = (m + 31) / 32;
+  if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  const int slot = timing_begin(ctx);
+  const dim3 grid(mb, (n + 127) / 128);
+  const int var = variant_override();
+  if (var == 4107)
+    hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 3, 1, true>), grid, dim3(256), 0, ctx->stream,
+                       mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+  else
+    hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 3, 32, true>), grid, dim3(256), 0, ctx->stream,
+                       mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
   timing_end(ctx, slot);
   return from_hip(hipGetLastError());
 }

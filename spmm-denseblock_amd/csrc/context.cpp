@@ -196,4 +196,11 @@ spmm_status_t spmm_set_csr_options(spmm_handle_t h, int flags) {
   return SPMM_STATUS_SUCCESS;
 }
 
+spmm_status_t spmm_set_hybrid_options(spmm_handle_t h, int flags) {
+  if (!h) return SPMM_STATUS_NOT_INITIALIZED;
+  if (flags & ~SPMM_HYBRID_FUSED) return SPMM_STATUS_INVALID_VALUE;
+  h->hybrid_flags = flags;
+  return SPMM_STATUS_SUCCESS;
+}
+
 }  // extern "C"

@@ -28,6 +28,7 @@ struct spmm_context {
   int num_cus = 256;
   int csr_waves_per_cu = 0;  // 0 = default
   int csr_flags = SPMM_CSR_NT_STREAMS;  // SPMM_CSR_* option bits (default: nt streams)
+  int hybrid_flags = 0;                 // SPMM_HYBRID_* option bits
 
   // Device workspace (grown, never shrunk; freed in spmm_destroy).
   void* ws = nullptr;
@@ -79,6 +80,13 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                spmm_order_t orderB, float beta, float* C, int ldc,
                                spmm_order_t orderC);
 
+// Fused hybrid (bs = 32, row-major B and C): one launch, BSR MFMA part plus the
+// CSR remainder per block row (bsr_kernels.hip). C holds ceil(m/32)*32 rows.
+bool hybrid32_fusable(int n, int ldb, int ldc, const float* bval, const float* B, const float* C);
+spmm_status_t launch_hybrid32_fused(spmm_context* ctx, int m, int n, float alpha,
+                                    const int* crp, const int* cci, const float* cv,
+                                    const int* brp, const int* bci, const float* bval,
+                                    const float* B, int ldb, float beta, float* C, int ldc);
 spmm_status_t launch_csrmm_f64(spmm_context* ctx, int m, int n, const int* rowptr,
                                const int* colind, const double* val, int base, const double* B,
                                int ldb, bool brow, double alpha, double beta, double* C, int ldc,

@@ -31,6 +31,7 @@ ORDER_ROW, ORDER_COL = 0, 1
 INDEX_BASE_ZERO, INDEX_BASE_ONE = 0, 1
 CSR_NT_STREAMS = 1
 CSR_SEQUENTIAL_ROWS = 2
+HYBRID_FUSED = 1
 
 
 class SpmmError(RuntimeError):
@@ -64,6 +65,7 @@ _PROTOS = {
     "spmm_get_kernel_times": (c_int, [_P, POINTER(c_float), c_int, _PI]),
     "spmm_set_csr_waves_per_cu": (c_int, [_P, c_int]),
     "spmm_set_csr_options": (c_int, [_P, c_int]),
+    "spmm_set_hybrid_options": (c_int, [_P, c_int]),
     "spmm_gespmm_csrmm_f32": (c_int, [c_int, c_int, _P, _P, _P, _P, _P, _P]),
     "spmm_scsrmm": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, POINTER(c_float), _P,
                             _P, _P, _P, _P, c_int, POINTER(c_float), _P, c_int]),

@@ -69,6 +69,9 @@ class Handle:
     def set_csr_options(self, flags: int) -> None:
         check(lib().spmm_set_csr_options(self._h, flags), "spmm_set_csr_options")
 
+    def set_hybrid_options(self, flags: int) -> None:
+        check(lib().spmm_set_hybrid_options(self._h, flags), "spmm_set_hybrid_options")
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             lib().spmm_destroy(self._h)

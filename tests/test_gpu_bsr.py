@@ -179,6 +179,57 @@ def test_hybrid_divide_spmm(oracle, device, bs, density, alpha, beta):
                     f"hybrid bs={bs} density={density}")
 
 
+@pytest.mark.parametrize("n,K", [(700, 96), (1000, 4), (963, 132), (2048, 256)])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.5, 1.5)])
+def test_hybrid_fused_vs_two_launch(oracle, device, n, K, alpha, beta):
+    """The fused bs = 32 hybrid (SPMM_HYBRID_FUSED: one launch, MFMA part +
+    per-block-row CSR remainder) against the oracle, and against the default
+    two-launch form: identical on every row the CSR kernel keeps in one wave.
+    Hub rows give remainders far longer than the 32-entry batch, sparse rows
+    give block rows with no dense block at all."""
+    from spmm_hip import prep
+    from spmm_hip._lib import CSR_NT_STREAMS, CSR_SEQUENTIAL_ROWS, HYBRID_FUSED
+    rp, ci = prep.community_csr(n, 30.0, 48, 160, 0.9, 7)
+    rng = np.random.default_rng(8)
+    rows = [ci[rp[i]:rp[i + 1]] for i in range(n)]
+    rows[1] = np.arange(0, n, 2)                      # hub: long remainder
+    rows[n // 2] = np.sort(rng.choice(n, n // 3, replace=False))
+    for i in range(n - 40, n):                        # tail rows: remainder only
+        rows[i] = np.sort(rng.choice(n, 3, replace=False))
+    rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    v = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    parts = prep.divide(n, rp, ci, v, 32, 0.1)
+    assert parts[4].size > 0 and parts[1].size > 0
+    nb = (n + 31) // 32
+    Bp = np.zeros((nb * 32, K), np.float32)
+    Bp[:n] = rng.uniform(-1, 1, (n, K))
+    C0 = rng.uniform(-1, 1, (nb * 32, K)).astype(np.float32)
+    d = _dev(*parts, Bp)
+    ops = _ops()
+    outs = []
+    for flags in (HYBRID_FUSED, 0):
+        h = ops.Handle()
+        h.set_hybrid_options(flags)
+        # the small-K lane-group CSR kernel folds partial sums: compare
+        # against the sequential-row kernel
+        h.set_csr_options(CSR_NT_STREAMS | CSR_SEQUENTIAL_ROWS)
+        C = torch.from_numpy(C0.copy()).cuda()
+        ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), d[6], m=n, n=K, k=n, bs=32, ldb=K, C=C,
+                         ldc=K, alpha=alpha, beta=beta, handle=h)
+        torch.cuda.synchronize()
+        outs.append(C.cpu().numpy())
+        h.close()
+    fused, two = outs
+    ref, absd = oracle_csrmm_f64(oracle, n, K, rp, ci, v, Bp, K, 0)
+    assert_normwise(fused[:n], alpha * ref + beta * C0[:n].astype(np.float64),
+                    abs(alpha) * absd + abs(beta) * np.abs(C0[:n]), TOL_F32, "fused hybrid")
+    same = np.mean(np.all(fused[:n] == two[:n], axis=1))
+    assert same > 0.9, f"only {same:.3f} of rows identical to the two-launch form"
+    # padding rows (n .. nb*32): the BSR epilogue of an empty tail
+    np.testing.assert_allclose(fused[n:], two[n:], rtol=0, atol=0)
+
+
 def test_bsr_status_codes(device):
     """rocsparse_bsrmm.h:109-176 argument checks."""
     from spmm_hip._lib import (INVALID_VALUE, MATRIX_TYPE_NOT_SUPPORTED, NOT_INITIALIZED,
