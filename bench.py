@@ -250,6 +250,8 @@ def run_bsr(args, W, world, rank, dev, dist):
     B32 = B.float()
     C2 = torch.empty((n, K), device=dev)
     h2 = ops.Handle()
+    if args.csr_options is not None:
+        h2.set_csr_options(args.csr_options)
     _, csr_ms = timed_loop(lambda: ops.csrmm(d_rp, d_ci, d_v, B32, m=n, n=K, k=mb * bs, ldb=K,
                                              C=C2, ldc=K, handle=h2), h2, 5, 2, 1, dist)
     mfma_flops = 2.0 * nnzb * bs * bs * K
