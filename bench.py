@@ -148,20 +148,37 @@ def run_csr(args, W, world, rank, dev, dist):
     g.manual_seed(1234)
     B = torch.rand((n, K), device=dev, generator=g) * 2 - 1
     mr = shard.max_rows
-    out = torch.empty((world * mr, K), device=dev)
-    C_slot = out[rank * mr: rank * mr + shard.rows]
     h = ops.Handle()
     if args.waves_per_cu:
         h.set_csr_waves_per_cu(args.waves_per_cu)
     if args.csr_options is not None:
         h.set_csr_options(args.csr_options)
+    nch = args.chunks or (4 if world > 1 else 1)
+    if nch > 1 and not dist.is_initialized():
+        raise SystemExit("--chunks > 1 at N = 1 needs a torch.distributed launcher")
+    if nch > 1:
+        # the all-gather of chunk c overlaps the compute of chunk c + 1
+        out = torch.empty((nch, world, sdist.chunk_rows(shard, nch), K), device=dev)
 
-    def step():
-        ops.csrmm(d_rp, d_ci, d_v, B, m=shard.rows, n=K, k=n, ldb=K, C=C_slot, ldc=K, handle=h)
-        if world > 1:
-            sdist.gather(out, shard, compact=False)
+        def compute_chunk(r0, r1, dest):
+            ops.csrmm(d_rp[r0:r1 + 1], d_ci, d_v, B, m=r1 - r0, n=K, k=n, ldb=K, C=dest,
+                      ldc=K, handle=h)
 
-    elapsed, kms = timed_loop(step, h, args.steps, args.warmup, world, dist)
+        def step():
+            sdist.chunked_spmm(shard, out, compute_chunk, nch, compact=False)
+    else:
+        out = torch.empty((world * mr, K), device=dev)
+        C_slot = out[rank * mr: rank * mr + shard.rows]
+
+        def step():
+            ops.csrmm(d_rp, d_ci, d_v, B, m=shard.rows, n=K, k=n, ldb=K, C=C_slot, ldc=K,
+                      handle=h)
+            if world > 1:
+                sdist.gather(out, shard, compact=False)
+
+    elapsed, kt = timed_loop(step, h, args.steps, args.warmup, world, dist, raw=True)
+    # kernel time per step (all chunks of a step; one launch when unchunked)
+    kms = float(np.sum(kt)) / args.steps if kt else float("nan")
     t = torch.tensor([elapsed, kms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -187,6 +204,7 @@ def run_csr(args, W, world, rank, dev, dist):
                 (" row-partitioned + RCCL all-gather" if world > 1 else ""),
                 "n": n, "nnz": nnz, "K": K, "max_deg": int(np.diff(rp).max()),
                 "parallelism": f"rows{world}" if world > 1 else "single",
+                "exchange_chunks": nch,
                 "waves_per_cu": args.waves_per_cu or 16,
                 "csr_options": args.csr_options},
         roofline={"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
@@ -197,7 +215,8 @@ def run_csr(args, W, world, rank, dev, dist):
         gen_seconds=round(t_gen, 2))
     if world > 1:
         # compute and collective reported separately (the step
-        # minus the slowest rank's kernel time; the fix-up kernel is ~4 us).
+        # minus the slowest rank's kernel time, i.e. the collective time not
+        # hidden behind compute; the fix-up kernel is ~4 us).
         rec["collective_ms_est"] = round(rec["ms_per_step"] - kms_max, 4)
         rec["rows_per_rank"] = [int(b) for b in np.diff(shard.bounds)]
     return rec, (rp, ci, K)
@@ -392,6 +411,10 @@ def main() -> None:
                     help="B/C storage for BSR workloads (col = cusparse transB=N)")
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--csr-options", type=int, default=None, help="SPMM_CSR_* flags")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="row chunks per rank whose all-gathers overlap the next chunk's compute "
+                         "(default 4 when N > 1; 1 = compute, then one all-gather; > 1 at N = 1 "
+                         "needs a torch.distributed launcher)")
     ap.add_argument("--hybrid-options", type=int, default=None,
                     help="SPMM_HYBRID_* flags (1 = fused single launch, bs = 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -409,7 +432,7 @@ def main() -> None:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or (args.chunks > 1 and "WORLD_SIZE" in os.environ):
         dist.init_process_group("nccl", device_id=dev)
 
     W = WORKLOADS[args.workload]
@@ -433,7 +456,7 @@ def main() -> None:
                           "(SURVEY.md §8d)")
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -13,6 +13,12 @@ Shards have unequal row counts; the all-gather runs on a padded
 kernel (no staging copy). ``gather(..., compact=True)`` returns the dense
 [m, K] matrix (one extra device copy); the padded buffer plus ``bounds`` is
 the zero-copy form.
+
+``chunked_spmm`` overlaps the exchange with the compute: each rank's rows are
+cut into ``nchunks`` pieces, and piece c's all-gather (RCCL on its own
+stream, ``async_op``) runs while piece c+1 is computed. The buffer is
+chunk-major, [nchunks, world, rows_per_chunk, K], so every piece's gather is
+one contiguous in-place all-gather.
 """
 from __future__ import annotations
 
@@ -80,3 +86,48 @@ def partitioned_spmm(shard: Shard, B, out, compute: Callable, group=None, compac
     slot = out[shard.rank * mr:shard.rank * mr + shard.rows]
     compute(shard, B, slot)
     return gather(out, shard, group=group, compact=compact)
+
+
+def chunk_rows(shard: Shard, nchunks: int) -> int:
+    """Rows per chunk (same on every rank: derived from the shared bounds)."""
+    return max(1, -(-shard.max_rows // nchunks))
+
+
+def chunk_range(shard: Shard, rank: int, c: int, nchunks: int) -> tuple[int, int]:
+    """Local row range [r0, r1) of rank's chunk c (possibly empty)."""
+    cr = chunk_rows(shard, nchunks)
+    rows = int(shard.bounds[rank + 1] - shard.bounds[rank])
+    r0 = min(c * cr, rows)
+    return r0, min(r0 + cr, rows)
+
+
+def chunked_spmm(shard: Shard, out, compute_chunk: Callable, nchunks: int, group=None,
+                 compact: bool = True):
+    """C = A @ B across ranks with the all-gather of chunk c overlapping the
+    compute of chunk c+1. `out` is [nchunks, world, chunk_rows, K];
+    compute_chunk(r0, r1, dest) writes local rows [r0, r1) into dest (a
+    [r1-r0, K] view of this rank's slot of chunk c). Returns the dense [m, K]
+    C if compact, else `out`."""
+    import torch
+    import torch.distributed as dist
+    nch, world, cr, K = out.shape
+    assert nch == nchunks and world == shard.world and cr == chunk_rows(shard, nchunks)
+    works = []
+    for c in range(nchunks):
+        r0, r1 = chunk_range(shard, shard.rank, c, nchunks)
+        if r1 > r0:
+            compute_chunk(r0, r1, out[c, shard.rank, :r1 - r0])
+        works.append(dist.all_gather_into_tensor(out[c].view(world * cr, K),
+                                                 out[c, shard.rank], group=group,
+                                                 async_op=True))
+    for w in works:
+        w.wait()
+    if not compact:
+        return out
+    parts = []
+    for r in range(world):
+        for c in range(nchunks):
+            r0, r1 = chunk_range(shard, r, c, nchunks)
+            if r1 > r0:
+                parts.append(out[c, r, :r1 - r0])
+    return torch.cat(parts, 0) if parts else out.new_zeros((0, K))

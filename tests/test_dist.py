@@ -48,8 +48,21 @@ def _worker(rank, world, port, q):
         out = torch.zeros((world * sh.max_rows, K))
         C = sdist.partitioned_spmm(sh, torch.from_numpy(B), out, compute, compact=True)
         full = oracle_csrmm_f32(L, n, K, rp, ci, val, B, K, 0).reshape(n, K)
-        q.put((rank, bool(np.array_equal(C.numpy(), full)), sh.bounds.tolist(),
-               int(sh.colind.size)))
+        ok = bool(np.array_equal(C.numpy(), full))
+
+        # chunked exchange: chunk c's all-gather in flight while c+1 computes
+        def compute_chunk(r0, r1, dest):
+            lrp = (sh.rowptr[r0:r1 + 1] - sh.rowptr[r0]).astype(np.int32)
+            j0, j1 = int(sh.rowptr[r0]), int(sh.rowptr[r1])
+            c = oracle_csrmm_f32(L, r1 - r0, K, lrp, sh.colind[j0:j1], sh.val[j0:j1],
+                                 B, K, 0)
+            dest.copy_(torch.from_numpy(c.reshape(r1 - r0, K)))
+
+        for nch in (1, 3, 7):
+            buf = torch.full((nch, world, sdist.chunk_rows(sh, nch), K), float("nan"))
+            Cc = sdist.chunked_spmm(sh, buf, compute_chunk, nch, compact=True)
+            ok = ok and bool(np.array_equal(Cc.numpy(), full))
+        q.put((rank, ok, sh.bounds.tolist(), int(sh.colind.size)))
     finally:
         dist.destroy_process_group()
 
