@@ -106,12 +106,41 @@ def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0)
                        f"({med:.3f} s each, {spent:.1f} s total)")}
 
 
+GRAPH = False  # --graph: replay the step as a captured HIP graph (N = 1)
+
+
 def timed_loop(step, h, steps, warmup, world, dist, raw=False):
     import torch
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     h.kernel_times()
+    if GRAPH and world == 1:
+        # The launches of one step captured once (workspace already sized by
+        # the warm-up, so nothing allocates or syncs inside), replayed K
+        # times; the kernel durations come from an event-timed eager pass
+        # right after, over the same number of steps.
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            h.set_stream(torch.cuda.current_stream())  # the capture stream
+            step()
+        h.set_stream(torch.cuda.current_stream())
+        g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        h.set_timing(True)
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        h.set_timing(False)
+        kt = h.kernel_times()
+        if raw:
+            return elapsed, kt
+        return elapsed, (float(np.mean(kt)) if kt else float("nan"))
     h.set_timing(True)
     if world > 1:
         dist.barrier()
@@ -204,7 +233,7 @@ def run_csr(args, W, world, rank, dev, dist):
                 (" row-partitioned + RCCL all-gather" if world > 1 else ""),
                 "n": n, "nnz": nnz, "K": K, "max_deg": int(np.diff(rp).max()),
                 "parallelism": f"rows{world}" if world > 1 else "single",
-                "exchange_chunks": nch,
+                "exchange_chunks": nch, "hip_graph": bool(GRAPH and world == 1),
                 "waves_per_cu": args.waves_per_cu or 16,
                 "csr_options": args.csr_options},
         roofline={"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
@@ -420,7 +449,11 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (DESIGN.md §7)")
+    ap.add_argument("--graph", action="store_true",
+                    help="N = 1: time the step as a replayed HIP graph (launch overhead out)")
     args = ap.parse_args()
+    global GRAPH
+    GRAPH = args.graph
 
     import torch
     import torch.distributed as dist
