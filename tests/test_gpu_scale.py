@@ -1,0 +1,88 @@
+"""Path B at BASELINE's full sizes, through
+size-independent properties: the BSR, hybrid and CSR kernels are three
+independent implementations of the same product, so at full scale each BSR
+result must agree with the CSR kernel's within the fp32 bar, with the
+magnitude bound |A|.|B| itself computed on the device (the CSR kernel on
+|val|, |B|). The small-size tests pin each kernel to the oracle; these check
+that nothing breaks at 10^8 nonzeros (index widths, grid sizes, tails)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from helpers import TOL_F16_ACC, TOL_F32
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _ops():
+    from spmm_hip import ops
+    return ops
+
+
+def _dev(*arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+def _within(got, ref, absd, tol, what):
+    err = (got - ref).abs()
+    bound = tol * absd + 1e-30
+    bad = int((err > bound).sum())
+    assert bad == 0, f"{what}: {bad} elements outside {tol} x |A||B| (max err {float(err.max())})"
+
+
+def test_reddit_scale_bsr32_and_hybrid_vs_csr(device):
+    """Config 3 (reddit stand-in, 115 M nnz, bs = 32, K = 128): device csr2bsr
+    -> LDS MFMA kernel, and divide -> hybrid, both against the CSR kernel."""
+    from spmm_hip import prep
+    ops = _ops()
+    n, K, bs = 232965, 128, 32
+    rp, ci = prep.community_csr(n, 670.0, 512, 2048, 0.99, 1234)
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
+    drp, dci, dv = _dev(rp, ci, v)
+    mb = (n + bs - 1) // bs
+    B = torch.rand((mb * bs, K), device=device) * 2 - 1
+    Cc = ops.gespmm_csrmm(drp, dci, dv, B[:n].contiguous())
+    absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B[:n].abs().contiguous())
+    brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
+    Cb = torch.empty((mb * bs, K), device=device)
+    ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=Cb, ldc=K)
+    torch.cuda.synchronize()
+    assert int(bci.numel()) > 1_000_000
+    _within(Cb[:n], Cc, absd, 2 * TOL_F32, "reddit bs32 BSR vs CSR")
+    assert not bool(Cb[n:].any()), "padding rows of C must be zero"
+    del brp, bci, bval
+    parts = prep.divide(n, rp, ci, v, bs, prep.hybrid_plan(rp, ci, bs, K)["density"])
+    d = _dev(*parts)
+    Ch = torch.empty((mb * bs, K), device=device)
+    ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=Ch, ldc=K)
+    torch.cuda.synchronize()
+    _within(Ch[:n], Cc, absd, 2 * TOL_F32, "reddit hybrid vs CSR")
+
+
+def test_products_scale_bsr16_f16_vs_csr(device):
+    """Config 5 (products stand-in, bs = 16, fp16 A and B, K = 512): the
+    fp16 MFMA kernel against the CSR kernel run on the same fp16-rounded
+    values in fp32 (both accumulate in fp32)."""
+    from spmm_hip import prep
+    ops = _ops()
+    n, K, bs = 2449029, 512, 16
+    rp, ci = prep.community_csr(n, 27.0, 32, 512, 0.97, 1234)
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float16).astype(np.float32)
+    drp, dci, dv = _dev(rp, ci, v)
+    mb = (n + bs - 1) // bs
+    B16 = (torch.rand((mb * bs, K), device=device) * 2 - 1).half()
+    Bf = B16[:n].float().contiguous()
+    Cc = ops.gespmm_csrmm(drp, dci, dv, Bf)
+    absd = ops.gespmm_csrmm(drp, dci, dv.abs(), Bf.abs())
+    del Bf
+    brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
+    bval16 = bval.half()
+    del bval
+    Cb = torch.empty((mb * bs, K), device=device)
+    ops.bsrmm_f16(brp, bci, bval16, B16, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=Cb, ldc=K)
+    torch.cuda.synchronize()
+    assert int(bci.numel()) > 4_000_000
+    _within(Cb[:n], Cc, absd, 2 * TOL_F16_ACC, "products bs16 fp16 BSR vs CSR")
