@@ -69,22 +69,14 @@ def bsr_bytes(mb: int, nnzb: int, bs: int, K: int, s: int) -> int:
     return 4 * (mb + 1) + 4 * nnzb + s * nnzb * bs * bs + s * nnzb * bs * K + 4 * mb * bs * K
 
 
-def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0) -> dict:
-    """spmm.cc csr_spmm restated (oracle_spmm_cc_csr: OpenMP rows, k-outer,
-    double, unit values) on the SAME graph: a growing row prefix until about
-    budget_s of CPU work, or the whole graph repeated, median of the repeats."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from helpers import load_oracle, ptr
-    L = load_oracle()
-    n = rp.size - 1
-    Bd = np.random.default_rng(1).uniform(-1, 1, (n, K))  # double, as spmm.cc
-    ip64, ix64 = rp.astype(np.int64), ci.astype(np.int64)
+def _time_prefix(run, n: int, budget_s: float):
+    """Grow a row prefix until one run takes about budget_s / 3 (or covers all
+    n rows), then repeat it within budget_s; returns (rows, run times)."""
     rows, spent = 1024, 0.0
     while True:
         rows = min(rows, n)
-        out = np.empty((rows, K))
         t0 = time.perf_counter()
-        L.oracle_spmm_cc_csr(rows, K, ptr(ip64), ptr(ix64), ptr(Bd), K, ptr(out))
+        run(rows)
         dt = time.perf_counter() - t0
         spent += dt
         if rows == n or dt >= budget_s / 3:
@@ -93,17 +85,62 @@ def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0)
     times = [dt]
     while spent < budget_s and len(times) < 15:
         t0 = time.perf_counter()
-        L.oracle_spmm_cc_csr(rows, K, ptr(ip64), ptr(ix64), ptr(Bd), K, ptr(out))
+        run(rows)
         times.append(time.perf_counter() - t0)
         spent += times[-1]
+    return rows, times
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0) -> dict:
+    """spmm.cc csr_spmm restated (oracle_spmm_cc_csr: OpenMP rows, k-outer,
+    double, unit values) on the SAME graph: a growing row prefix until about
+    budget_s of CPU work, or the whole graph repeated, median of the repeats.
+    Also the fp32-weighted variant at the same shape: the
+    oracle's sequential-FMA csrmm on U(-1,1) values, same prefix rule."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import load_oracle, ptr
+    L = load_oracle()
+    n = rp.size - 1
+    Bd = np.random.default_rng(1).uniform(-1, 1, (n, K))  # double, as spmm.cc
+    ip64, ix64 = rp.astype(np.int64), ci.astype(np.int64)
+    out = np.empty((n, K))
+    rows, times = _time_prefix(
+        lambda r: L.oracle_spmm_cc_csr(r, K, ptr(ip64), ptr(ix64), ptr(Bd), K, ptr(out)),
+        n, budget_s)
+    del out, Bd
     med = float(np.median(times))
     nnz_s = int(rp[rows])
-    return {"value": round(2.0 * nnz_s * K / med / 1e9, 3), "unit": "GFLOP/s",
-            "cores": int(L.oracle_num_threads()), "kind": "port",
-            "sample": (f"spmm.cc csr_spmm restated (double, unit values, k-outer, OpenMP) on "
-                       f"{'all' if rows == n else 'the first'} {rows} rows ({nnz_s} nnz) of the "
-                       f"same synthetic graph, K={K}; median of {len(times)} runs "
-                       f"({med:.3f} s each, {spent:.1f} s total)")}
+    res = {"value": round(2.0 * nnz_s * K / med / 1e9, 3), "unit": "GFLOP/s",
+           "cores": int(L.oracle_num_threads()), "kind": "port", "cpu_model": _cpu_model(),
+           "sample": (f"spmm.cc csr_spmm restated (double, unit values, k-outer, OpenMP) on "
+                      f"{'all' if rows == n else 'the first'} {rows} rows ({nnz_s} nnz) of the "
+                      f"same synthetic graph, K={K}; median of {len(times)} runs "
+                      f"({med:.3f} s each, {sum(times):.1f} s total)")}
+    Bf = np.random.default_rng(1).uniform(-1, 1, (n, K)).astype(np.float32)
+    vf = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
+    outf = np.empty((n, K), np.float32)
+    rows, times = _time_prefix(
+        lambda r: L.oracle_csrmm_f32(r, K, ptr(rp), ptr(ci), ptr(vf), 0, ptr(Bf), K, 0, 1.0, 0.0,
+                                     ptr(outf), K, 0), n, budget_s)
+    med = float(np.median(times))
+    nnz_s = int(rp[rows])
+    res["fp32_weighted"] = {
+        "value": round(2.0 * nnz_s * K / med / 1e9, 3), "unit": "GFLOP/s",
+        "sample": (f"fp32 values, sequential FMA per element (oracle_csrmm_f32, OpenMP rows) on "
+                   f"{'all' if rows == n else 'the first'} {rows} rows ({nnz_s} nnz), K={K}; "
+                   f"median of {len(times)} runs ({med:.3f} s each)")}
+    return res
 
 
 GRAPH = False  # --graph: replay the step as a captured HIP graph (N = 1)
