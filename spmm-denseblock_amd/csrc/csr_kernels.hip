@@ -318,7 +318,7 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
 // in G interleaved chains — within the fp32 bar, not bit-identical to the
 // sequential order (SPMM_CSR_SEQUENTIAL_ROWS keeps the main kernel).
 // Carries use the VEC = 1 fix-up (columns 0..31 of a slot).
-template <bool NT, int LPG>
+template <bool NT, int LPG, int PD>
 __global__ __launch_bounds__(kWG) void csr_group_kernel(
     int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, int base, const float* __restrict__ B, int ldb, float alpha,
@@ -420,42 +420,56 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
   auto load_b = [&](int c) {
     return *reinterpret_cast<const f32x4*>(Bb + (size_t)c * ldb + col_ld);
   };
-  if (S > 0) {
-    // Pipeline: indices two steps ahead, B rows one step ahead.
-    int cA, cB;
-    float vA, vB;
-    load_idx(0, cA, vA);
-    load_idx(min(1, S - 1), cB, vB);
-    f32x4 b = load_b(cA);
-    float vcur = vA;
-    for (int s = 0; s < S; ++s) {
-      // next B row (step s+1) from the indices loaded one step ago
-      const f32x4 bn = load_b(cB);
-      const float vn = vB;
-      load_idx(min(s + 2, S - 1), cB, vB);
-      const int q0 = gs + G * s;
-      const int p = q0 + grp;
-      const bool ok = p >= A0 && p < A1;
-      f32x4 prod;
+  // One step's products: groups before a row end inside the step belong to
+  // the ending row(s).
+  auto consume = [&](int s, const f32x4& b, float v) {
+    const int q0 = gs + G * s;
+    const int p = q0 + grp;
+    const bool ok = p >= A0 && p < A1;
+    f32x4 prod;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) prod[c] = ok ? vcur * b[c] : 0.f;
-      // Row ends inside this step: groups before the end position belong to
-      // the ending row.
-      while (cur_end - (q0 - aoff) < G) {  // cur_end is INT_MAX once i reaches i1
-        const int e = cur_end - (q0 - aoff);
+    for (int c = 0; c < 4; ++c) prod[c] = ok ? v * b[c] : 0.f;
+    while (cur_end - (q0 - aoff) < G) {  // cur_end is INT_MAX once i reaches i1
+      const int e = cur_end - (q0 - aoff);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const bool mine = grp < e;
-          acc[c] += mine ? prod[c] : 0.f;
-          prod[c] = mine ? 0.f : prod[c];
-        }
-        emit(i);
-        advance_row();
+      for (int c = 0; c < 4; ++c) {
+        const bool mine = grp < e;
+        acc[c] += mine ? prod[c] : 0.f;
+        prod[c] = mine ? 0.f : prod[c];
       }
+      emit(i);
+      advance_row();
+    }
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] += prod[c];
-      b = bn;
-      vcur = vn;
+    for (int c = 0; c < 4; ++c) acc[c] += prod[c];
+  };
+  if (S > 0) {
+    // Pipeline: PD B-row gathers in flight (ring slot u = s % PD holds step
+    // s's row and value), indices PD steps ahead of their gather. Step
+    // indices past the end are clamped (valid, never consumed).
+    f32x4 bq[PD];
+    float vq[PD], vi[PD];
+    int ci[PD];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      int c;
+      load_idx(min(u, S - 1), c, vq[u]);
+      bq[u] = load_b(c);
+    }
+#pragma unroll
+    for (int u = 0; u < PD; ++u) load_idx(min(PD + u, S - 1), ci[u], vi[u]);
+    for (int s0 = 0; s0 < S; s0 += PD) {
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {
+        const int s = s0 + u;
+        if (s >= S) break;
+        const f32x4 b = bq[u];
+        const float v = vq[u];
+        bq[u] = load_b(ci[u]);  // step s + PD
+        vq[u] = vi[u];
+        load_idx(min(s + 2 * PD, S - 1), ci[u], vi[u]);
+        consume(s, b, v);
+      }
     }
   }
   while (i < i1) {
@@ -593,13 +607,26 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
                       (ctx->csr_flags & SPMM_CSR_SEQUENTIAL_ROWS) == 0;
   if (grouped) {
     dim3 g8((nw + kWavesPerWG - 1) / kWavesPerWG, 1);
-#define SPMM_LAUNCH_GRP(L)                                                                      \
+    static const int pd_env = [] {
+      const char* e = getenv("SPMM_CSR_GROUP_PD");  // tuning only
+      return e ? atoi(e) : 0;
+    }();
+#define SPMM_LAUNCH_GRP_PD(L, PD)                                                              \
   if (nt)                                                                                      \
-    hipLaunchKernelGGL((csr_group_kernel<true, L>), g8, block, 0, ctx->stream, m, n, rowptr,    \
-                       colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw); \
+    hipLaunchKernelGGL((csr_group_kernel<true, L, PD>), g8, block, 0, ctx->stream, m, n,        \
+                       rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
+                       carry_row, nw);                                                          \
   else                                                                                         \
-    hipLaunchKernelGGL((csr_group_kernel<false, L>), g8, block, 0, ctx->stream, m, n, rowptr,   \
-                       colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw);
+    hipLaunchKernelGGL((csr_group_kernel<false, L, PD>), g8, block, 0, ctx->stream, m, n,       \
+                       rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
+                       carry_row, nw);
+    // gathers in flight per wave: 2 at K = 32 (1.21 vs 1.35 ms on products),
+    // 1 below, where a gather costs a whole 128-B line and depth is no help
+    const int pd = pd_env > 0 ? pd_env : (n > 16 ? 2 : 1);
+#define SPMM_LAUNCH_GRP(L)                                                                     \
+  if (pd == 1) { SPMM_LAUNCH_GRP_PD(L, 1) }                                                    \
+  else if (pd == 4) { SPMM_LAUNCH_GRP_PD(L, 4) }                                               \
+  else { SPMM_LAUNCH_GRP_PD(L, 2) }
     // lanes per nnz: 4 columns each, so 2 / 4 / 8 lanes cover K <= 8 / 16 / 32
     if (n <= 8) {
       SPMM_LAUNCH_GRP(2)
@@ -609,6 +636,7 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
       SPMM_LAUNCH_GRP(8)
     }
 #undef SPMM_LAUNCH_GRP
+#undef SPMM_LAUNCH_GRP_PD
     timing_end(ctx, slot);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return from_hip(e);
