@@ -45,7 +45,7 @@ constexpr int kU = 8;            // nnz per pipeline group
 constexpr int kR = 4;            // colind/val registers per lane per chunk
 constexpr int kChunk = kWave * kR / kU;  // groups per chunk (32)
 constexpr int kMinItemsPerWave = 512;
-constexpr int kGroupMaxK = 32;  // K handled by csr_group_kernel (K = 48 / 64: main kernel faster)
+constexpr int kGroupMaxK = 64;  // K handled by csr_group_kernel
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -306,8 +306,8 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   }
 }
 
-// Small-K form (K <= 32, K % 4 == 0): the wave is cut into G = 64 / LPG lane
-// groups of LPG lanes (LPG = 2 / 4 / 8 for K <= 8 / 16 / 32; lane l: group
+// Small-K form (K <= 64, K % 4 == 0): the wave is cut into G = 64 / LPG lane
+// groups of LPG lanes (LPG = 2 / 4 / 8 / 16 for K <= 8 / 16 / 32 / 64; lane l: group
 // l / LPG, columns 4 (l % LPG) .. +3), each group a different nnz of the
 // wave's merge-path range per step. A step is one G-row gather with per-lane
 // colind / val loads instead of per-nnz v_readlane and scalar address
@@ -620,20 +620,24 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
     hipLaunchKernelGGL((csr_group_kernel<false, L, PD>), g8, block, 0, ctx->stream, m, n,       \
                        rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
                        carry_row, nw);
-    // gathers in flight per wave: 2 at K = 32 (1.21 vs 1.35 ms on products),
-    // 1 below, where a gather costs a whole 128-B line and depth is no help
-    const int pd = pd_env > 0 ? pd_env : (n > 16 ? 2 : 1);
+    // gathers in flight per wave: 1 at K <= 16, where a gather costs a whole
+    // 128-B line and depth is no help; 2 at K = 32 (1.21 vs 1.35 ms on
+    // products); 4 at K = 48 / 64 (2.19 / 2.27 ms vs 2.33 / 2.37 for the
+    // main kernel)
+    const int pd = pd_env > 0 ? pd_env : (n <= 16 ? 1 : (n <= 32 ? 2 : 4));
 #define SPMM_LAUNCH_GRP(L)                                                                     \
   if (pd == 1) { SPMM_LAUNCH_GRP_PD(L, 1) }                                                    \
   else if (pd == 4) { SPMM_LAUNCH_GRP_PD(L, 4) }                                               \
   else { SPMM_LAUNCH_GRP_PD(L, 2) }
-    // lanes per nnz: 4 columns each, so 2 / 4 / 8 lanes cover K <= 8 / 16 / 32
+    // lanes per nnz: 4 columns each, so 2 / 4 / 8 / 16 lanes cover K <= 8 / 16 / 32 / 64
     if (n <= 8) {
       SPMM_LAUNCH_GRP(2)
     } else if (n <= 16) {
       SPMM_LAUNCH_GRP(4)
-    } else {
+    } else if (n <= 32) {
       SPMM_LAUNCH_GRP(8)
+    } else {
+      SPMM_LAUNCH_GRP(16)
     }
 #undef SPMM_LAUNCH_GRP
 #undef SPMM_LAUNCH_GRP_PD
