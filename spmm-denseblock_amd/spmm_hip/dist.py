@@ -19,6 +19,11 @@ cut into ``nchunks`` pieces, and piece c's all-gather (RCCL on its own
 stream, ``async_op``) runs while piece c+1 is computed. The buffer is
 chunk-major, [nchunks, world, rows_per_chunk, K], so every piece's gather is
 one contiguous in-place all-gather.
+
+``stacked_block`` is the weak-scaling form (bench.py's default at N > 1):
+every rank owns a products-size row block of a world-times larger graph, B
+replicated, and C stays row-sharded where the kernel wrote it — no
+collective on the data path, per-GPU work fixed as N grows.
 """
 from __future__ import annotations
 
@@ -58,6 +63,28 @@ def make_shard(rowptr: np.ndarray, colind: np.ndarray, val: np.ndarray, rank: in
     j0, j1 = int(rowptr[r0]), int(rowptr[r1])
     lrp = (rowptr[r0:r1 + 1] - j0).astype(np.int32)
     return Shard(rank, world, bounds, r0, r1, lrp, colind[j0:j1], val[j0:j1])
+
+
+def stacked_block(n: int, nnz: int, max_deg: int, rank: int, world: int, seed: int = 1234,
+                  gamma: float = 2.3) -> tuple[np.ndarray, np.ndarray]:
+    """Row block `rank` of a (world*n)-node power-law graph for weak scaling:
+    each rank owns n rows and nnz nonzeros (the per-GPU work of the 1-GPU
+    workload), B is replicated with world*n rows, and no collective is on
+    the data path. Block r is the Chung-Lu stand-in with seed + r whose
+    column c is moved to c*world + ((off[c] + r) % world), off a seeded
+    per-column table: monotone in c (rows stay sorted), a hub's copies land
+    on different B rows in different blocks, and every block sees the same
+    popularity skew as the 1-GPU graph. world = 1 gives the 1-GPU graph
+    itself (block 0 = seed)."""
+    rp, ci = prep.powerlaw_csr(n, nnz, max_deg, gamma, seed + rank)
+    if world == 1:
+        return rp, ci
+    if world * n > np.iinfo(np.int32).max:
+        raise ValueError("stacked_block: world * n exceeds int32 column ids")
+    off = np.random.default_rng(seed ^ 0x5EED).integers(0, world, n, dtype=np.int64)
+    cj = ci.astype(np.int64)
+    cj = cj * world + (off[cj] + rank) % world
+    return rp, cj.astype(np.int32)
 
 
 def gather(local_out, shard: Shard, group=None, compact: bool = True):

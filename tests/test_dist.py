@@ -84,3 +84,37 @@ def test_row_partitioned_allgather_matches_single(world):
     nnzs = [z for *_, z in res]
     assert sum(nnzs) == 60000
     assert max(nnzs) - min(nnzs) <= 900 + 5000 // world  # balanced within a row + rows share
+
+
+def test_stacked_block_weak_scaling_graph():
+    """bench.py's weak-scaling input (spmm_hip.dist.stacked_block): world = 1
+    is the 1-GPU graph itself; at world > 1 block r keeps its generator's row
+    structure, its columns map back to the 1-GPU columns by // world, rows stay
+    sorted, ids span the world*n-row B, and blocks differ between ranks."""
+    sys.path.insert(0, os.path.join(ROOT, "spmm-denseblock_amd"))
+    from spmm_hip import dist as sdist
+    from spmm_hip import prep
+    n, nnz, md = 3000, 40000, 700
+    rp1, ci1 = prep.powerlaw_csr(n, nnz, md, 2.3, 1234)
+    rp, ci = sdist.stacked_block(n, nnz, md, 0, 1)
+    assert np.array_equal(rp, rp1) and np.array_equal(ci, ci1)
+    for world in (2, 8):
+        blocks = []
+        for r in range(world):
+            base_rp, base_ci = prep.powerlaw_csr(n, nnz, md, 2.3, 1234 + r)
+            rp, ci = sdist.stacked_block(n, nnz, md, r, world)
+            assert ci.dtype == np.int32 and rp.dtype == np.int32
+            assert np.array_equal(rp, base_rp) and ci.size == nnz
+            assert np.array_equal(ci // world, base_ci)
+            assert ci.min() >= 0 and ci.max() < world * n
+            d = np.diff(ci.astype(np.int64))
+            starts = np.zeros(nnz, bool)
+            starts[rp[:-1][np.diff(rp) > 0]] = True
+            assert np.all(d[~starts[1:]] >= 0), "rows must stay sorted"
+            blocks.append(ci)
+        # a column shared by two blocks lands on different B rows in each
+        for r in range(1, world):
+            m0 = dict(zip((blocks[0] // world).tolist(), blocks[0].tolist()))
+            shared = [(c, x) for c, x in zip((blocks[r] // world).tolist(), blocks[r].tolist())
+                      if c in m0]
+            assert shared and all(m0[c] != x for c, x in shared)
