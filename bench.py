@@ -425,10 +425,33 @@ def run_bsr(args, W, world, rank, dev, dist):
         h2.set_csr_options(args.csr_options)
     _, csr_ms = timed_loop(lambda: ops.csrmm(d_rp, d_ci, d_v, B32, m=n, n=K, k=mb * bs, ldb=K,
                                              C=C2, ldc=K, handle=h2), h2, 5, 2, 1, dist)
-    mfma_flops = 2.0 * nnzb * bs * bs * K
-    achieved = mfma_flops / (kms / 1e3) / 1e12
+    # Column-masked kernels (the row-major / ROW-block layout):
+    # a block's B rows are fetched only for its nonzero A columns, and bs = 32
+    # runs only the MFMA steps whose column pair holds a nonzero. The counts
+    # come from the CSR pattern (distinct (block row, column) and (block,
+    # column pair) keys, counted on the device).
+    cm = args.bsr_layout == "row"
+    d_r = torch.repeat_interleave(torch.arange(n, device=dev, dtype=torch.int64),
+                                  torch.from_numpy(np.diff(rp)).to(dev))
+    d_c = torch.from_numpy(ci).to(dev).to(torch.int64)
+    active_cols = int(torch.unique((d_r // bs) * n + d_c).numel())
+    active_pairs = int(torch.unique(((d_r // bs) * mb + d_c // bs) * (bs // 2) +
+                                    (d_c % bs) % (bs // 2)).numel())
+    del d_r, d_c
+    tile = 128 if bs == 32 else 256           # output columns per workgroup
+    ntiles = (K + tile - 1) // tile
+    dense_flops = 2.0 * nnzb * bs * bs * K    # SURVEY §8d "MFMA-executed" (dense blocks)
+    if cm and bs == 32:
+        mfma_flops = active_pairs * 2.0 * bs * 2 * K   # one 32x32x2 step per active pair
+    else:
+        mfma_flops = dense_flops
     peak = MFMA_PEAK_TFLOPS[dt]
     kbytes = bsr_bytes(mb, nnzb, bs, K, s)
+    # bytes the column-masked kernel must move: A values and block columns per
+    # column tile, the B rows of nonzero columns, the C write
+    cm_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + s * nnzb * bs * bs) + s * active_cols * K +
+                4 * mb * bs * K) if cm else kbytes
+    t = kms / 1e3
     rec = dict(
         value=2.0 * nnz * K * args.steps / elapsed / 1e9, ms_per_step=elapsed / args.steps * 1e3,
         dtype=dt,
@@ -437,26 +460,28 @@ def run_bsr(args, W, world, rank, dev, dist):
         config={"workload": f"{args.workload}: csr2bsr bs={bs} + bsrmm K={K} {dt}", "n": n,
                 "layout_BC": args.bsr_layout,
                 "nnz": nnz, "K": K, "bs": bs, "nnzb": nnzb,
-                "block_fill": round(nnz / (nnzb * bs * bs), 4), "parallelism": "single"},
-        roofline={"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-                  "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
-                  "kernel": f"bsr{bs}_lds_kernel<{'f32' if dt == 'fp32' else 'f16'}>",
-                  "kernel_ms": round(kms, 4), "mfma_flops_per_launch": mfma_flops,
-                  "algorithmic_bytes_per_launch": kbytes,
-                  "algorithmic_GBps": round(kbytes / (kms / 1e3) / 1e9, 1)},
+                "block_fill": round(nnz / (nnzb * bs * bs), 4),
+                "active_column_fraction": round(active_cols / (nnzb * bs), 4),
+                "active_pair_fraction": round(active_pairs / (nnzb * bs / 2), 4),
+                "parallelism": "single"},
+        roofline={"bound": "hbm", "achieved": round(cm_bytes / t / 1e9, 1),
+                  "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                  "frac": round(cm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                  "kernel": (f"bsr{bs}_{'f32_' if bs == 32 else ''}cm_kernel<"
+                             f"{'f32' if dt == 'fp32' else 'f16'}>" if cm else
+                             f"bsr{bs} register-fragment kernel (column-major operands)"),
+                  "kernel_ms": round(kms, 4),
+                  "bytes_per_launch": cm_bytes, "bytes_model": (
+                      "A values + block columns per column tile, B rows of nonzero A columns, "
+                      "C write" if cm else "SURVEY 8d full-panel model"),
+                  "mfma_executed_flops_per_launch": mfma_flops,
+                  "mfma_executed_TFLOPs": round(mfma_flops / t / 1e12, 2),
+                  "mfma_peak": peak, "mfma_frac": round(mfma_flops / t / 1e12 / peak, 4),
+                  "dense_block_equivalent_TFLOPs": round(dense_flops / t / 1e12, 2),
+                  "full_panel_model_bytes_per_launch": kbytes,
+                  "full_panel_model_GBps": round(kbytes / t / 1e9, 1)},
         csr_same_matrix_ms=round(csr_ms, 4), csr2bsr_host_seconds=round(t_conv, 2),
         gen_seconds=round(t_gen, 2))
-    # Per-block arithmetic intensity against the ridge point of the peak: the
-    # fp16 / bs=16 / K=512 case (15.5 flop/B vs a 312 flop/B ridge) is bound by
-    # bytes, so its roofline line is the HBM one (MFMA figures kept beside it).
-    # fp32 keeps the MFMA line north_star sets its target on.
-    ai = 2.0 * bs * bs * K / (s * (bs * bs + bs * K) + 4)
-    if ai < peak * 1e12 / (HBM_PEAK_GBPS * 1e9) / 4 and dt != "fp32":
-        rf = rec["roofline"]
-        rf.update({"bound": "hbm", "mfma_achieved_TFLOPs": rf["achieved"],
-                   "mfma_frac": rf["frac"], "achieved": rf["algorithmic_GBps"],
-                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                   "frac": round(rf["algorithmic_GBps"] / HBM_PEAK_GBPS, 4)})
     return rec, None
 
 

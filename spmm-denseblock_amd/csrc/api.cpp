@@ -310,7 +310,8 @@ extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
     const int mb = (m + blockDim - 1) / blockDim, kb = (k + blockDim - 1) / blockDim;
     spmm_status_t st = launch_bsrmm_f32(handle, SPMM_DIRECTION_ROW, mb, kb, n, nnzb, blockDim,
                                         alpha, bsrRowPtr, bsrColInd, bsrVal, B, ldb,
-                                        SPMM_ORDER_ROW, beta, C, ldc, SPMM_ORDER_ROW);
+                                        SPMM_ORDER_ROW, beta, C, ldc, SPMM_ORDER_ROW,
+                                        /*dense_blocks=*/true);
     if (st != SPMM_STATUS_SUCCESS) return st;
     csr_beta = 1.f;
   }

@@ -439,6 +439,191 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// bs = 32 fp32, column-masked ("CM"): the LDS kernel above, but a B-panel row
+// is fetched only when its column of the A block holds a nonzero, and an MFMA
+// step runs only when one of its two k columns does. Blocks that csr2bsr cuts
+// out of a sparse graph are mostly empty columns (19 % of panel rows used on
+// the reddit stand-in, 23 % on products at bs = 32), and the full-panel
+// kernel spends most of its HBM bytes and MFMA steps on them.
+//
+// The mask of a block needs its A values, so A runs ahead of B in its own
+// ring (DA = D + 3 stages): at iteration k the waves
+//   (a) OR the four per-wave partial masks of block k+D-1 (LDS, written at k-1),
+//   (b) copy B(k+D-1): each lane of a masked-off row reads a 512-B zero row
+//       instead (one L2-resident line set, same instruction count), so the
+//       stage row holds exact zeros — an explicit zero of A then multiplies 0,
+//       never stale data: explicit zeros inside a block act as structural
+//       zeros (the CSR semantics of the same matrix; with finite B this is
+//       the dense-block product exactly),
+//   (c) compute this wave's partial mask of block k+D (8 rows: its own DMA
+//       slot, one ds_read_b128, DPP OR inside 16-lane rows + 4 readlanes),
+//   (d) copy A(k+DA-1),
+//   (e) run block k's MFMAs, skipping quads / steps whose columns are empty.
+// Copies per iteration: 4 (B) + 1 (A); B(k) and A(k+D) are both complete
+// once at most 5 are outstanding, so one counted vmcnt(5) + lgkmcnt(0) and
+// the raw barrier order everything, as in the kernel above.
+// ---------------------------------------------------------------------------
+// 1 KB of zeros: the source of masked-off B-panel rows (one 256-column fp32 row)
+__device__ __attribute__((aligned(16))) float g_zero_row[256] = {0.f};
+
+__device__ __forceinline__ int or_wave(int x) {
+  // OR inside each 16-lane row (DPP row_ror 8 / 4 / 2 / 1), then across rows
+  x |= __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);
+  x |= __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false);
+  x |= __builtin_amdgcn_update_dpp(0, x, 0x122, 0xF, 0xF, false);
+  x |= __builtin_amdgcn_update_dpp(0, x, 0x121, 0xF, 0xF, false);
+  return __builtin_amdgcn_readlane(x, 0) | __builtin_amdgcn_readlane(x, 16) |
+         __builtin_amdgcn_readlane(x, 32) | __builtin_amdgcn_readlane(x, 48);
+}
+
+template <bool CROW, int XM, int D = 3, int DA = D + 3, bool NOMFMA = false>
+__global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  static_assert(D >= 2 && D <= 4 && DA >= D + 2, "ring depths");
+  // outstanding copies allowed at the top of iteration k with B(k) and A(k+D)
+  // complete: 1 + 5(D-2) were issued after B(k), 5(DA-D-2) after A(k+D)
+  constexpr int W = (1 + 5 * (D - 2)) < 5 * (DA - D - 2) ? 1 + 5 * (D - 2) : 5 * (DA - D - 2);
+  constexpr int kA = 1024, kB = 32 * 128;  // floats per A block / B panel stage
+  // one LDS array (A ring, B ring, partial masks [block & 3][wave])
+  __shared__ __attribute__((aligned(16))) float smem[DA * kA + D * kB + 16];
+  float* const sa = smem;
+  float* const sb = smem + DA * kA;
+  int* const part = reinterpret_cast<int*>(smem + DA * kA + D * kB);
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int br = xcd_block_row(blockIdx.x, mb, XM);
+  const int jt = blockIdx.y * 128;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  if (k0 >= k1) {
+    const int j = jt + 32 * wv + (lane & 31);
+    if (j < n)
+      for (int e = 0; e < 16; ++e) {
+        const size_t row = (size_t)br * 32 + 2 * e + (lane >> 5);
+        float* p = CROW ? C + row * ldc + j : C + (size_t)j * ldc + row;
+        *p = epi(0.f, alpha, beta, p);
+      }
+    return;
+  }
+
+  // A copy: lane l -> row 8w + l/8, LDS slot 4l holding logical chunk
+  // (l%8) ^ swz(row) (same layout as bsr32_f32_lds_kernel).
+  const int a_row = 8 * wv + (lane >> 3);
+  const int a_chunk = (lane & 7) ^ ((a_row >> 1) & 7);
+  const int a_src = a_row * 32 + 4 * a_chunk;
+  const int b_col = min(jt + 4 * (lane & 31), n - 4);
+  const int b_row = 8 * wv + (lane >> 5);
+  const float* zsrc = g_zero_row + 4 * (lane & 31);
+  auto wrapA = [](int s) { return s >= DA ? s - DA : s; };
+
+  auto issue_a = [&](int k, int slot) {
+    const int kk = min(k, k1 - 1);
+    __builtin_amdgcn_global_load_lds((gbl_void_t)(val + (size_t)kk * 1024 + a_src),
+                                     (lds_void_t)(sa + slot * kA + 256 * wv), 16, 0, 0);
+  };
+  auto issue_b = [&](int bc, unsigned mask, int slot) {
+    const float* bsrc = B + ((size_t)bc * 32 + b_row) * ldb + b_col;
+    float* dst = sb + slot * kB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float* src = ((mask >> (b_row + 2 * i)) & 1u) ? bsrc + (size_t)(2 * i) * ldb : zsrc;
+      __builtin_amdgcn_global_load_lds((gbl_void_t)src,
+                                       (lds_void_t)(dst + 128 * (8 * wv + 2 * i)), 16, 0, 0);
+    }
+  };
+  // This wave's 8 rows of the A block in ring slot `slot` -> their column mask.
+  auto partial = [&](int slot) -> int {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(sa + slot * kA + 256 * wv + 4 * lane);
+    const int nib = (x[0] != 0.f) | ((x[1] != 0.f) << 1) | ((x[2] != 0.f) << 2) |
+                    ((x[3] != 0.f) << 3);
+    return or_wave(nib << (4 * a_chunk));
+  };
+  // Read through inline asm: the compiler's waitcnt pass would otherwise put
+  // a vmcnt(0) on this LDS read (it cannot tell it from the DMA targets),
+  // draining the copy pipeline every iteration. The partials it reads were
+  // written with ds_write before the last barrier (lgkmcnt(0) there).
+  const unsigned part_lds = (unsigned)reinterpret_cast<uintptr_t>(part);
+  auto full = [&](int k) -> unsigned {
+    int4 p;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(p) : "v"(part_lds + 16u * (unsigned)(k & 3)) : "memory");
+    return (unsigned)__builtin_amdgcn_readfirstlane(p.x | p.y | p.z | p.w);
+  };
+
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  ColCursor cc(colind, k0, k1, lane);
+
+  // Prologue: A(k0 .. k0+DA-2), masks of k0 .. k0+D-1, B(k0 .. k0+D-2).
+#pragma unroll
+  for (int d = 0; d < DA - 1; ++d) issue_a(k0 + d, d);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int d = 0; d < D; ++d) part[4 * ((k0 + d) & 3) + wv] = partial(d);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
+  __builtin_amdgcn_s_barrier();
+  unsigned mr[D - 1];  // masks of blocks k .. k+D-2
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) {
+    mr[d] = full(k0 + d);
+    issue_b(cc.get(min(k0 + d, k1 - 1)), mr[d], d);
+  }
+  // B(k0) landed (4(D-2) copies follow it; the loop's W may exceed that)
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(W < 4 * (D - 2) ? W : 4 * (D - 2)));
+
+  int sA = 0, sB = 0;  // ring slots of block k
+  for (int k = k0; k < k1; ++k) {
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(W));
+    __builtin_amdgcn_s_barrier();
+    const unsigned mnew = full(k + D - 1);                                        // (a)
+    issue_b(cc.get(min(k + D - 1, k1 - 1)), mnew, sB == 0 ? D - 1 : sB - 1);     // (b)
+    part[4 * ((k + D) & 3) + wv] = partial(wrapA(sA + D));                       // (c)
+    issue_a(k + DA - 1, sA == 0 ? DA - 1 : sA - 1);                              // (d)
+    // (e) step s2 of half h uses column 16h + s2: pm bit s2 = either column set
+    const unsigned pm = NOMFMA ? 0u : (mr[0] | (mr[0] >> 16)) & 0xffffu;
+    const float* stA = sa + sA * kA;
+    const float* stB = sb + sB * kB + (16 * h) * 128 + 32 * wv + r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if ((pm >> (4 * q)) & 0xfu) {
+        const int pc = (4 * h + q) ^ ((r >> 1) & 7);
+        const f32x4 x = *reinterpret_cast<const f32x4*>(stA + r * 32 + 4 * pc);
+        float fb[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) fb[s] = stB[(4 * q + s) * 128];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if ((pm >> (4 * q + s)) & 1u)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s], fb[s], acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D - 2; ++d) mr[d] = mr[d + 1];
+    mr[D - 2] = mnew;
+    sA = wrapA(sA + 1);
+    sB = sB == D - 1 ? 0 : sB + 1;
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // drain the clamped tail copies
+
+  const int jcol = jt + 32 * wv + r;
+  if (jcol >= n) return;
+  const size_t row0 = (size_t)br * 32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = row0 + 8 * g + 4 * h + e;
+      float* p = CROW ? C + row * ldc + jcol : C + (size_t)jcol * ldc + row;
+      *p = epi(acc[4 * g + e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // bs = 16, LDS-staged (ROW blocks, row-major B), fp32 or fp16 A/B: the shipped
 // bs = 16 kernels where the layout allows it. Same scheme as the bs = 32
 // one: a workgroup (4 waves, 256 output columns, 64 per wave) copies each
@@ -565,6 +750,206 @@ __global__ __launch_bounds__(256) void bsr16_lds_kernel(
       }
     }
     st = st == D - 1 ? 0 : st + 1;
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int j = jt + 64 * wv + 16 * t + c16;
+    if (j >= n) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = (size_t)br * 16 + 4 * g + e;
+      float* p = CROW ? C + row * ldc + j : C + (size_t)j * ldc + row;
+      *p = epi(acc[t][e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 16, column-masked: the bs = 32 CM scheme on bsr16_lds_kernel's layout
+// (4 waves, 256 output columns, A block row-major in LDS, B panel rows
+// 16-B-chunk swizzled). Only B rows of nonzero A columns are fetched (41 % on
+// the products stand-in at bs = 16); the rest of the stage is zero-filled
+// from g_zero_row. The MFMAs are not skipped (see the loop). Copies per iteration:
+// P = 1 (A) + 2 (fp16) or 4 (fp32) (B).
+// ---------------------------------------------------------------------------
+template <typename T, bool CROW, int D = 2, int DA = D + 3>
+__global__ __launch_bounds__(256) void bsr16_cm_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const T* __restrict__ val, const T* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  constexpr int kEpc = 16 / sizeof(T);             // elements per 16-B chunk
+  constexpr int kA = 256 * sizeof(T);              // A block bytes
+  constexpr int kRowB = 256 * sizeof(T);           // B panel row bytes (256 columns)
+  constexpr int kStB = 16 * kRowB;                 // B stage bytes
+  constexpr int kRpi = 1024 / kRowB;               // B rows per copy instruction (1 or 2)
+  constexpr int kCpr = kRowB / 16;                 // chunks per B row (64 or 32)
+  constexpr int kNB = 4 / kRpi;                    // B copy instructions per wave and block
+  constexpr int P = 1 + kNB;
+  static_assert(D >= 2 && D <= 4 && DA >= D + 2, "ring depths");
+  constexpr int W = (1 + P * (D - 2)) < P * (DA - D - 2) ? 1 + P * (D - 2) : P * (DA - D - 2);
+  __shared__ __attribute__((aligned(16))) char smem[DA * kA + D * kStB + 64];
+  char* const sa = smem;
+  char* const sb = smem + DA * kA;
+  int* const part = reinterpret_cast<int*>(smem + DA * kA + D * kStB);
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int br = xcd_block_row(blockIdx.x, mb, 1);  // XCD-contiguous block rows
+  const int jt = blockIdx.y * 256;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  if (k0 >= k1) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = jt + 64 * wv + 16 * t + c16;
+      if (j >= n) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const size_t row = (size_t)br * 16 + 4 * g + e;
+        float* p = CROW ? C + row * ldc + j : C + (size_t)j * ldc + row;
+        *p = epi(0.f, alpha, beta, p);
+      }
+    }
+    return;
+  }
+
+  // A copy: lanes 0 .. kA/64 - 1 of wave w, 16 B each: rows 4w .. 4w+3.
+  const bool a_lane = lane < kA / 64;
+  const int a_src = (4 * wv) * 16 + lane * kEpc;
+  int b_src[kNB], b_rowi[kNB];
+#pragma unroll
+  for (int i = 0; i < kNB; ++i) {
+    const int row = 4 * wv + i * kRpi + lane / kCpr;
+    const int c = (lane % kCpr) ^ bsr16_swz<T>(row);
+    b_src[i] = row * ldb + min(jt + c * kEpc, n - kEpc);
+    b_rowi[i] = row;
+  }
+  const T* zsrc = reinterpret_cast<const T*>(g_zero_row) + (lane % kCpr) * kEpc;
+  auto wrapA = [](int s) { return s >= DA ? s - DA : s; };
+  auto issue_a = [&](int k, int slot) {
+    const int kk = min(k, k1 - 1);
+    if (a_lane)
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(val + (size_t)kk * 256 + a_src),
+                                       (lds_void_t)(sa + slot * kA + wv * (kA / 4)), 16, 0, 0);
+  };
+  auto issue_b = [&](int bc, unsigned mask, int slot) {
+    const T* bp = B + (size_t)bc * 16 * ldb;
+#pragma unroll
+    for (int i = 0; i < kNB; ++i) {
+      const T* src = ((mask >> b_rowi[i]) & 1u) ? bp + b_src[i] : zsrc;
+      __builtin_amdgcn_global_load_lds((gbl_void_t)src,
+                                       (lds_void_t)(sb + slot * kStB + (4 * wv + i * kRpi) * kRowB),
+                                       16, 0, 0);
+    }
+  };
+  // This wave's 4 rows of the A block in ring slot `slot` -> their column mask
+  // (lanes 0 .. 15 hold them: a DPP OR inside the first 16-lane row). A value
+  // counts as nonzero unless it is +-0 (NaN / inf count).
+  const unsigned sa_lds = (unsigned)reinterpret_cast<uintptr_t>(sa);
+  // No branch around the read (lanes past the slot re-read lane l % (kA/64)'s
+  // 16 B and are masked after): a divergent branch here made the compiler
+  // drain every copy in flight (vmcnt(0)) before the read.
+  auto partial = [&](int slot) -> int {
+    int nib = 0;
+    {
+      int4 x;  // inline asm for the same reason as full() below
+      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                   : "=v"(x)
+                   : "v"(sa_lds + (unsigned)(slot * kA + wv * (kA / 4) + 16 * (lane & (kA / 64 - 1))))
+                   : "memory");
+      const int xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if constexpr (sizeof(T) == 2) {
+          nib |= ((xs[e] & 0x7fff) != 0) << (2 * e);
+          nib |= ((xs[e] & 0x7fff0000) != 0) << (2 * e + 1);
+        } else {
+          nib |= ((xs[e] & 0x7fffffff) != 0) << e;
+        }
+      }
+      nib = a_lane ? nib << ((lane * kEpc) & 15) : 0;
+    }
+    nib |= __builtin_amdgcn_update_dpp(0, nib, 0x128, 0xF, 0xF, false);
+    nib |= __builtin_amdgcn_update_dpp(0, nib, 0x124, 0xF, 0xF, false);
+    nib |= __builtin_amdgcn_update_dpp(0, nib, 0x122, 0xF, 0xF, false);
+    nib |= __builtin_amdgcn_update_dpp(0, nib, 0x121, 0xF, 0xF, false);
+    return __builtin_amdgcn_readlane(nib, 0);
+  };
+  const unsigned part_lds = (unsigned)reinterpret_cast<uintptr_t>(part);
+  auto full = [&](int k) -> unsigned {  // inline asm: see bsr32_f32_cm_kernel
+    int4 p;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(p) : "v"(part_lds + 16u * (unsigned)(k & 3)) : "memory");
+    return (unsigned)__builtin_amdgcn_readfirstlane(p.x | p.y | p.z | p.w);
+  };
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  ColCursor cc(colind, k0, k1, lane);
+#pragma unroll
+  for (int d = 0; d < DA - 1; ++d) issue_a(k0 + d, d);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int d = 0; d < D; ++d) part[4 * ((k0 + d) & 3) + wv] = partial(d);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
+  __builtin_amdgcn_s_barrier();
+  unsigned mr[D - 1];
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) {
+    mr[d] = full(k0 + d);
+    issue_b(cc.get(min(k0 + d, k1 - 1)), mr[d], d);
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(W < kNB * (D - 2) ? W : kNB * (D - 2)));
+
+  int sA = 0, sB = 0;
+  for (int k = k0; k < k1; ++k) {
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(W));
+    __builtin_amdgcn_s_barrier();
+    const unsigned mnew = full(k + D - 1);
+    issue_b(cc.get(min(k + D - 1, k1 - 1)), mnew, sB == 0 ? D - 1 : sB - 1);
+    part[4 * ((k + D) & 3) + wv] = partial(wrapA(sA + D));
+    issue_a(k + DA - 1, sA == 0 ? DA - 1 : sA - 1);
+    const unsigned m = mr[0];
+    const char* stage = sa + sA * kA;
+    const char* bpan = sb + sB * kStB;
+    // MFMAs unconditional: at bs = 16 most blocks use every fp32 k step (each
+    // covers 4 columns) and fp16 takes the block in one step, and branching
+    // around them made the compiler move the accumulators through VGPRs.
+    (void)m;
+    if constexpr (sizeof(T) == 2) {
+      const f16x4 fa = *reinterpret_cast<const f16x4*>(stage + c16 * 32 + 8 * g);
+      const int q = (lane >> 2) & 3, p = lane & 3;
+      const int row = 4 * g + q;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int col = 64 * wv + 16 * t + 4 * p;
+        const int off = row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2;
+        const v4s raw = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(bpan + off));
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, __builtin_bit_cast(f16x4, raw),
+                                                       acc[t], 0, 0, 0);
+      }
+    } else {
+      const f32x4 fa = *reinterpret_cast<const f32x4*>(stage + c16 * 64 + 16 * g);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int row = 4 * g + s2;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int col = 64 * wv + 16 * t + c16;
+          const int off = row * kRowB + (((col >> 2) ^ bsr16_swz<T>(row)) << 4) + (col & 3) * 4;
+          const float fb = *reinterpret_cast<const float*>(bpan + off);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s2], fb, acc[t], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D - 2; ++d) mr[d] = mr[d + 1];
+    mr[D - 2] = mnew;
+    sA = wrapA(sA + 1);
+    sB = sB == D - 1 ? 0 : sB + 1;
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
 
@@ -994,14 +1379,21 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 
 constexpr int kBsr32Default = 40;
 // LDS-staged bs = 32 kernel: 4096 + D (+ 8: XCD-contiguous order; 4123-4125:
-// XCD order in chunks of 16 / 32 / 64 block rows).
-constexpr int kBsr32LdsDefault = 4124;
+// XCD order in chunks of 16 / 32 / 64 block rows). 42 D DA: column-masked,
+// B stages D, A stages DA; (2, 5) fits 3 workgroups per CU and is the
+// fastest measured (reddit stand-in 2.65 ms vs 4.57 for 4124; products bs = 32
+// 4.62 vs 8.51; (3, 6) 3.08 / 5.60; (4, 8) 4.87 / 9.09).
+constexpr int kBsr32LdsDefault = 4225;
+constexpr int kBsr32LdsDense = 4124;
 // LDS-staged bs = 16 kernels: 4096 + D (+ 8: XCD-contiguous block rows). fp16:
 // 6 waves/SIMD at D = 3 beat deeper rings, the XCD order 5 % more
 // (products_bsr16_f16 8.80 ms vs 10.38 for the register-fragment kernel);
 // fp32: D = 4, 18.4 vs 21.4.
-constexpr int kBsr16LdsDefault = 4100;
-constexpr int kBsr16F16LdsDefault = 4303;  // block-row pairs, D = 3 (4107: single rows)
+// 46 D DA: column-masked bs = 16 (bsr16_cm_kernel), B stages D, A stages DA.
+// products stand-in bs = 16 K = 512: fp16 (2, 5) 7.41 ms vs 8.81 for the
+// block-row pair kernel 4303, (3, 6) 9.40; fp32 (2, 5) 16.6 vs 18.5 for 4100.
+constexpr int kBsr16LdsDefault = 4625;
+constexpr int kBsr16F16LdsDefault = 4625;
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -1047,7 +1439,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                int nnzb, int bs, float alpha, const int* rowptr,
                                const int* colind, const float* val, const float* B, int ldb,
                                spmm_order_t orderB, float beta, float* C, int ldc,
-                               spmm_order_t orderC) {
+                               spmm_order_t orderC, bool dense_blocks) {
   (void)kb;
   (void)nnzb;
   if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
@@ -1060,7 +1452,13 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   if (bs == 32 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 && aligned(val, 16) &&
       aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 127) / 128);
-    const int lv = var < 0 ? kBsr32LdsDefault : var;
+    // 46xx select bs = 16 kernels: the bs = 32 default here. Blocks known to
+    // be dense (the hybrid's BSR part) take the full-panel kernel: with most
+    // columns set the mask buys nothing and its deeper B ring wins (reddit
+    // stand-in hybrid: 0.81 vs 0.96 ms).
+    const int lv = var < 0 || (var % 1000) / 100 == 6
+                       ? (dense_blocks ? kBsr32LdsDense : kBsr32LdsDefault)
+                       : var;
 #define L(D, X)                                                                                   \
   if (crow) hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, D, X>), grid, dim3(256), 0, ctx->stream,  \
                                mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, nullptr,  \
@@ -1077,13 +1475,25 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       case 4123: L(3, 16) break;  // 4123-4125: XCD order in chunks of 16 / 32 / 64
       case 4124: L(3, 32) break;
       case 4125: L(3, 64) break;
+      // column-masked (fetch only the B rows of nonzero A columns): 42DA:
+      // D = B stages, A = A stages (42 3 6 = D 3, DA 6); + 1000 = no MFMA (diagnostic)
+#define CM(V, ...)                                                                                     \
+  case V:                                                                                              \
+    if (crow) hipLaunchKernelGGL((bsr32_f32_cm_kernel<true, 32, __VA_ARGS__>), grid, dim3(256), 0,      \
+                                 ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
+    else hipLaunchKernelGGL((bsr32_f32_cm_kernel<false, 32, __VA_ARGS__>), grid, dim3(256), 0,          \
+                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);      \
+    break;
+      CM(4200, 3, 6) CM(4236, 3, 6) CM(4235, 3, 5) CM(4237, 3, 7) CM(4225, 2, 5) CM(4226, 2, 6)
+      CM(4247, 4, 7) CM(4248, 4, 8) CM(5236, 3, 6, true) CM(5225, 2, 5, true)
+#undef CM
       default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
     }
 #undef L
   } else if (bs == 32 && vec_ok) {
     const int waves = n <= 32 ? 1 : (n <= 64 ? 2 : 4);
     dim3 grid(mb, (n + 32 * waves - 1) / (32 * waves));
-    if (var >= 0 && rowd && brow && crow) {
+    if (var >= 0 && var < 4096 && rowd && brow && crow) {
       switch (var) {
 #define V(x) case x: hipLaunchKernelGGL((bsr32_f32_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
         V(40) V(44) V(42) V(50) V(58) V(66) V(41) V(49)
@@ -1097,7 +1507,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   } else if (bs == 16 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 &&
              aligned(val, 16) && aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
-    const int lv = var < 0 ? kBsr16LdsDefault : var;
+    // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
+    const int lv = var < 0 || (var % 1000) / 100 == 2 ? kBsr16LdsDefault : var;
 #define L(D)                                                                                     \
   if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<float, true, D>), grid, dim3(256), 0, ctx->stream, \
                                mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);         \
@@ -1107,6 +1518,15 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       case 4099: L(3) break;
       case 4100: L(4) break;
       case 4102: L(6) break;
+#define CM(V, ...)                                                                                  \
+  case V:                                                                                           \
+    if (crow) hipLaunchKernelGGL((bsr16_cm_kernel<float, true, __VA_ARGS__>), grid, dim3(256), 0,    \
+                                 ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
+    else hipLaunchKernelGGL((bsr16_cm_kernel<float, false, __VA_ARGS__>), grid, dim3(256), 0,        \
+                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);   \
+    break;
+      CM(4625, 2, 5) CM(4636, 3, 6) CM(4626, 2, 6) CM(4646, 4, 6)  // column-masked, 46 D DA
+#undef CM
       case 4108:  // + 8: XCD-contiguous block rows
         if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<float, true, 4, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
         else hipLaunchKernelGGL((bsr16_lds_kernel<float, false, 4, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
@@ -1117,7 +1537,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   } else if (bs == 16 && vec_ok) {
     const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
     dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
-    if (var >= 0 && rowd && brow && crow) {
+    if (var >= 0 && var < 4096 && rowd && brow && crow) {
       switch (var) {
 #define V(x) case x: hipLaunchKernelGGL((bsr16_f32_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
         V(8) V(9) V(10) V(12) V(13) V(14) V(40) V(66)
@@ -1180,7 +1600,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   if (bs == 16 && rowd && brow && n >= 8 && n % 8 == 0 && ldb % 8 == 0 && aligned(val, 16) &&
       aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
-    const int lv = var < 0 ? kBsr16F16LdsDefault : var;
+    const int lv = var < 0 || (var % 1000) / 100 == 2 ? kBsr16F16LdsDefault : var;
 #define L(D)                                                                                      \
   if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, true, D>), grid, dim3(256), 0,          \
                                ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
@@ -1194,6 +1614,15 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
         if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, true, 3, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
         else hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, false, 3, true>), grid, dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
         break;
+#define CM(V, ...)                                                                                  \
+  case V:                                                                                           \
+    if (crow) hipLaunchKernelGGL((bsr16_cm_kernel<_Float16, true, __VA_ARGS__>), grid, dim3(256), 0, \
+                                 ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
+    else hipLaunchKernelGGL((bsr16_cm_kernel<_Float16, false, __VA_ARGS__>), grid, dim3(256), 0,     \
+                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);   \
+    break;
+      CM(4625, 2, 5) CM(4636, 3, 6) CM(4626, 2, 6) CM(4646, 4, 6)  // column-masked, 46 D DA
+#undef CM
       case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4
         const dim3 gp((mb + 1) / 2, (n + 255) / 256);
         if (lv == 4303) {
@@ -1211,7 +1640,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   } else if (bs == 16 && vec_ok) {
     const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
     dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
-    if (var >= 0 && rowd && brow && crow) {
+    if (var >= 0 && var < 4096 && rowd && brow && crow) {
       switch (var) {
 #define V(x) case x: hipLaunchKernelGGL((bsr16_f16_mfma_kernel<true, true, true, x>), grid, dim3(64 * waves), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); break;
         V(8) V(9) V(10) V(12) V(13) V(14) V(40) V(66)

@@ -78,7 +78,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                int nnzb, int bs, float alpha, const int* rowptr,
                                const int* colind, const float* val, const float* B, int ldb,
                                spmm_order_t orderB, float beta, float* C, int ldc,
-                               spmm_order_t orderC);
+                               spmm_order_t orderC, bool dense_blocks = false);
 
 // Fused hybrid (bs = 32, row-major B and C): one launch, BSR MFMA part plus the
 // CSR remainder per block row (bsr_kernels.hip). C holds ceil(m/32)*32 rows.

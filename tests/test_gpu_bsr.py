@@ -297,3 +297,69 @@ def test_lds_staged_kernels(oracle, device, bs, dtype, n, oc):
     tol = TOL_F32 if dtype == "f32" else TOL_F16_ACC
     assert_normwise(got, alpha * ref + beta * C0, abs(alpha) * absd + abs(beta) * np.abs(C0), tol,
                     f"lds bs={bs} {dtype} n={n} oc={oc}")
+
+
+def _column_sparse_bsr(rng, mb, kb, bs, p):
+    """BSR whose blocks are mostly empty columns, like csr2bsr output of a
+    sparse graph: per block a random number of active columns (0 = an
+    explicit all-zero block, 1 = a single-column block, up to bs), each
+    active column holding a few nonzeros."""
+    rp, ci, _ = _rand_bsr(rng, mb, kb, bs, p, empty_rows=(3,))
+    nnzb = int(rp[-1])
+    v = np.zeros((nnzb, bs, bs), np.float32)
+    for b in range(nnzb):
+        kind = b % 5
+        ncols = {0: 0, 1: 1, 2: 2, 3: bs // 4, 4: bs}[kind]
+        cols = rng.choice(bs, ncols, replace=False)
+        for c in cols:
+            rows = rng.random(bs) < 0.3
+            rows[rng.integers(bs)] = True
+            v[b, rows, c] = rng.uniform(-1, 1, int(rows.sum()))
+    return rp, ci, v.reshape(-1)
+
+
+@pytest.mark.parametrize("bs,dtype", [(32, "f32"), (16, "f32"), (16, "f16")])
+@pytest.mark.parametrize("n", [64, 128, 264, 520])
+def test_column_sparse_blocks(oracle, device, bs, dtype, n):
+    """Blocks with empty columns (the column-masked kernels fetch only the B
+    rows of nonzero A columns and skip MFMA steps of empty ones): explicit
+    zero blocks, single-column blocks, quarter-full and full blocks, empty
+    block rows, long rows. Then the same with inf / NaN in B rows that only
+    empty A columns meet: those entries act as structural zeros (the CSR
+    semantics of the same matrix), so C stays finite and equal to the
+    product with those rows zeroed."""
+    rng = np.random.default_rng(n + bs)
+    mb, kb = 21, 80
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.3)
+    ldb = n
+    B = rng.uniform(-1, 1, (kb * bs, ldb)).astype(np.float32)
+    if dtype == "f16":
+        v, B = v.astype(np.float16), B.astype(np.float16)
+    fn = _ops().bsrmm if dtype == "f32" else _ops().bsrmm_f16
+    m = mb * bs
+    tol = TOL_F32 if dtype == "f32" else TOL_F16_ACC
+
+    def run(Bh):
+        drp, dci, dv, dB = _dev(rp, ci, v, Bh.reshape(-1))
+        dC = torch.full((m * n,), float("nan"), device=device)
+        fn(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=ldb, C=dC, ldc=n)
+        torch.cuda.synchronize()
+        return dC.cpu().numpy().reshape(m, n)
+
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, ldb, 0,
+                                 half=dtype == "f16")
+    assert_normwise(run(B), ref, absd, tol, f"column-sparse bs={bs} {dtype} n={n}")
+    # B rows that no nonzero of A meets
+    vb = v.reshape(-1, bs, bs).astype(np.float32)
+    used = np.zeros(kb * bs, bool)
+    for br in range(mb):
+        for k in range(rp[br], rp[br + 1]):
+            used[ci[k] * bs + np.nonzero(np.any(vb[k] != 0, axis=0))[0]] = True
+    unused = np.nonzero(~used)[0]
+    assert unused.size > 0
+    Bbad = B.copy()
+    Bbad[unused[0::2]] = np.inf
+    Bbad[unused[1::2]] = np.nan
+    got = run(Bbad)
+    assert np.isfinite(got).all(), "explicit zeros must not turn inf / NaN of B into NaN"
+    assert_normwise(got, ref, absd, tol, f"column-sparse bs={bs} {dtype} n={n}, non-finite B")
