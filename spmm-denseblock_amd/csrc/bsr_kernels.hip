@@ -774,8 +774,8 @@ __global__ __launch_bounds__(256) void bsr16_lds_kernel(
 // from g_zero_row. The MFMAs are not skipped (see the loop). Copies per iteration:
 // P = 1 (A) + 2 (fp16) or 4 (fp32) (B).
 // ---------------------------------------------------------------------------
-template <typename T, bool CROW, int D = 2, int DA = D + 3>
-__global__ __launch_bounds__(256) void bsr16_cm_kernel(
+template <typename T, bool CROW, int D = 2, int DA = D + 3, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void bsr16_cm_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const T* __restrict__ val, const T* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc) {
@@ -1392,8 +1392,10 @@ constexpr int kBsr32LdsDense = 4124;
 // 46 D DA: column-masked bs = 16 (bsr16_cm_kernel), B stages D, A stages DA.
 // products stand-in bs = 16 K = 512: fp16 (2, 5) 7.41 ms vs 8.81 for the
 // block-row pair kernel 4303, (3, 6) 9.40; fp32 (2, 5) 16.6 vs 18.5 for 4100.
+// 47 D DA: the same with amdgpu_waves_per_eu(8) (52 VGPRs, no AGPRs: 8 waves
+// per SIMD instead of 7): fp16 7.19 ms.
 constexpr int kBsr16LdsDefault = 4625;
-constexpr int kBsr16F16LdsDefault = 4625;
+constexpr int kBsr16F16LdsDefault = 4725;
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -1452,11 +1454,11 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   if (bs == 32 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 && aligned(val, 16) &&
       aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 127) / 128);
-    // 46xx select bs = 16 kernels: the bs = 32 default here. Blocks known to
+    // 46xx / 47xx select bs = 16 kernels: the bs = 32 default here. Blocks known to
     // be dense (the hybrid's BSR part) take the full-panel kernel: with most
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
-    const int lv = var < 0 || (var % 1000) / 100 == 6
+    const int lv = var < 0 || (var % 1000) / 100 >= 6
                        ? (dense_blocks ? kBsr32LdsDense : kBsr32LdsDefault)
                        : var;
 #define L(D, X)                                                                                   \
@@ -1622,6 +1624,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
                             ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);   \
     break;
       CM(4625, 2, 5) CM(4636, 3, 6) CM(4626, 2, 6) CM(4646, 4, 6)  // column-masked, 46 D DA
+      CM(4725, 2, 5, 8) CM(4724, 2, 4, 8)  // 47 D DA: + at least 8 waves per SIMD (<= 64 registers)
 #undef CM
       case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4
         const dim3 gp((mb + 1) / 2, (n + 255) / 256);
