@@ -774,14 +774,16 @@ __global__ __launch_bounds__(256) void bsr16_lds_kernel(
 // from g_zero_row. The MFMAs are not skipped (see the loop). Copies per iteration:
 // P = 1 (A) + 2 (fp16) or 4 (fp32) (B).
 // ---------------------------------------------------------------------------
-template <typename T, bool CROW, int D = 2, int DA = D + 3, int WPE = 1>
+template <typename T, bool CROW, int D = 2, int DA = D + 3, int WPE = 1, int COLS = 256>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void bsr16_cm_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const T* __restrict__ val, const T* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc) {
   constexpr int kEpc = 16 / sizeof(T);             // elements per 16-B chunk
   constexpr int kA = 256 * sizeof(T);              // A block bytes
-  constexpr int kRowB = 256 * sizeof(T);           // B panel row bytes (256 columns)
+  constexpr int kRowB = COLS * sizeof(T);          // B panel row bytes (COLS columns)
+  constexpr int kTpw = COLS / 64;                  // 16-column tiles per wave
+  static_assert(kRowB <= 1024, "one B row per copy instruction at most");
   constexpr int kStB = 16 * kRowB;                 // B stage bytes
   constexpr int kRpi = 1024 / kRowB;               // B rows per copy instruction (1 or 2)
   constexpr int kCpr = kRowB / 16;                 // chunks per B row (64 or 32)
@@ -796,13 +798,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int br = xcd_block_row(blockIdx.x, mb, 1);  // XCD-contiguous block rows
-  const int jt = blockIdx.y * 256;
+  const int jt = blockIdx.y * COLS;
+  const int wc = wv * (COLS / 4);  // first column of this wave inside the tile
   const int g = lane >> 4, c16 = lane & 15;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   if (k0 >= k1) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int j = jt + 64 * wv + 16 * t + c16;
+    for (int t = 0; t < kTpw; ++t) {
+      const int j = jt + wc + 16 * t + c16;
       if (j >= n) continue;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -884,9 +887,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     return (unsigned)__builtin_amdgcn_readfirstlane(p.x | p.y | p.z | p.w);
   };
 
-  f32x4 acc[4];
+  f32x4 acc[kTpw];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < kTpw; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   ColCursor cc(colind, k0, k1, lane);
 #pragma unroll
   for (int d = 0; d < DA - 1; ++d) issue_a(k0 + d, d);
@@ -924,8 +927,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const int q = (lane >> 2) & 3, p = lane & 3;
       const int row = 4 * g + q;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int col = 64 * wv + 16 * t + 4 * p;
+      for (int t = 0; t < kTpw; ++t) {
+        const int col = wc + 16 * t + 4 * p;
         const int off = row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2;
         const v4s raw = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(bpan + off));
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, __builtin_bit_cast(f16x4, raw),
@@ -937,8 +940,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       for (int s2 = 0; s2 < 4; ++s2) {
         const int row = 4 * g + s2;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int col = 64 * wv + 16 * t + c16;
+        for (int t = 0; t < kTpw; ++t) {
+          const int col = wc + 16 * t + c16;
           const int off = row * kRowB + (((col >> 2) ^ bsr16_swz<T>(row)) << 4) + (col & 3) * 4;
           const float fb = *reinterpret_cast<const float*>(bpan + off);
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s2], fb, acc[t], 0, 0, 0);
@@ -954,8 +957,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
 
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int j = jt + 64 * wv + 16 * t + c16;
+  for (int t = 0; t < kTpw; ++t) {
+    const int j = jt + wc + 16 * t + c16;
     if (j >= n) continue;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -1396,6 +1399,9 @@ constexpr int kBsr32LdsDense = 4124;
 // per SIMD instead of 7): fp16 7.19 ms.
 constexpr int kBsr16LdsDefault = 4625;
 constexpr int kBsr16F16LdsDefault = 4725;
+// 48 D DA: 512 output columns per workgroup (A once per 512 columns, 8 tiles
+// per wave): products stand-in K = 512 6.89 ms vs 7.08 for 4725.
+constexpr int kBsr16F16LdsWide = 4825;
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -1602,7 +1608,10 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   if (bs == 16 && rowd && brow && n >= 8 && n % 8 == 0 && ldb % 8 == 0 && aligned(val, 16) &&
       aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
-    const int lv = var < 0 || (var % 1000) / 100 == 2 ? kBsr16F16LdsDefault : var;
+    // K > 256: one workgroup per 512 columns (A read once per 512)
+    const int lv = var < 0 || (var % 1000) / 100 == 2
+                       ? (n > 256 ? kBsr16F16LdsWide : kBsr16F16LdsDefault)
+                       : var;
 #define L(D)                                                                                      \
   if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, true, D>), grid, dim3(256), 0,          \
                                ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
@@ -1625,6 +1634,18 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
     break;
       CM(4625, 2, 5) CM(4636, 3, 6) CM(4626, 2, 6) CM(4646, 4, 6)  // column-masked, 46 D DA
       CM(4725, 2, 5, 8) CM(4724, 2, 4, 8)  // 47 D DA: + at least 8 waves per SIMD (<= 64 registers)
+      // 48 D DA: 512 output columns per workgroup (8 tiles per wave; A once per 512 columns)
+#define CM512(V, ...)                                                                               \
+  case V: {                                                                                         \
+    const dim3 g5(mb, (n + 511) / 512);                                                             \
+    if (crow) hipLaunchKernelGGL((bsr16_cm_kernel<_Float16, true, __VA_ARGS__, 512>), g5, dim3(256), \
+                                 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
+    else hipLaunchKernelGGL((bsr16_cm_kernel<_Float16, false, __VA_ARGS__, 512>), g5, dim3(256), 0,  \
+                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);   \
+    break;                                                                                          \
+  }
+      CM512(4825, 2, 5, 1) CM512(4826, 2, 6, 1) CM512(4836, 3, 6, 1) CM512(4824, 2, 4, 1)
+#undef CM512
 #undef CM
       case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4
         const dim3 gp((mb + 1) / 2, (n + 255) / 256);
