@@ -438,7 +438,8 @@ def run_bsr(args, W, world, rank, dev, dist):
     active_pairs = int(torch.unique(((d_r // bs) * mb + d_c // bs) * (bs // 2) +
                                     (d_c % bs) % (bs // 2)).numel())
     del d_r, d_c
-    tile = 128 if bs == 32 else 256           # output columns per workgroup
+    # output columns per workgroup (bs 16 fp16 at K > 256: 512, kBsr16F16LdsWide)
+    tile = 128 if bs == 32 else (512 if dt == "fp16" and K > 256 else 256)
     ntiles = (K + tile - 1) // tile
     dense_flops = 2.0 * nnzb * bs * bs * K    # SURVEY §8d "MFMA-executed" (dense blocks)
     if cm and bs == 32:
