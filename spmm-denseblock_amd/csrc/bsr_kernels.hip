@@ -476,7 +476,7 @@ __device__ __forceinline__ int or_wave(int x) {
          __builtin_amdgcn_readlane(x, 32) | __builtin_amdgcn_readlane(x, 48);
 }
 
-template <bool CROW, int XM, int D = 3, int DA = D + 3, bool NOMFMA = false, int ORD = 0>
+template <bool CROW, int XM, int D = 3, int DA = D + 3, bool NOMFMA = false>
 __global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -581,7 +581,7 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
     __builtin_amdgcn_s_barrier();
     const unsigned mnew = full(k + D - 1);                                        // (a)
     issue_b(cc.get(min(k + D - 1, k1 - 1)), mnew, sB == 0 ? D - 1 : sB - 1);     // (b)
-    if constexpr (ORD == 0) part[4 * ((k + D) & 3) + wv] = partial(wrapA(sA + D));  // (c)
+    part[4 * ((k + D) & 3) + wv] = partial(wrapA(sA + D));                       // (c)
     issue_a(k + DA - 1, sA == 0 ? DA - 1 : sA - 1);                              // (d)
     // (e) step s2 of half h uses column 16h + s2: pm bit s2 = either column set
     const unsigned pm = NOMFMA ? 0u : (mr[0] | (mr[0] >> 16)) & 0xffffu;
@@ -601,9 +601,6 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s], fb[s], acc, 0, 0, 0);
       }
     }
-    // ORD 1: the next block's mask after the MFMAs (its LDS read and VALU no
-    // longer sit between the copies and the MFMA reads)
-    if constexpr (ORD == 1) part[4 * ((k + D) & 3) + wv] = partial(wrapA(sA + D));
 #pragma unroll
     for (int d = 0; d < D - 2; ++d) mr[d] = mr[d + 1];
     mr[D - 2] = mnew;
@@ -1497,7 +1494,6 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     break;
       CM(4200, 3, 6) CM(4236, 3, 6) CM(4235, 3, 5) CM(4237, 3, 7) CM(4225, 2, 5) CM(4226, 2, 6)
       CM(4247, 4, 7) CM(4248, 4, 8) CM(5236, 3, 6, true) CM(5225, 2, 5, true)
-      CM(4425, 2, 5, false, 1) CM(4424, 2, 4, false, 1)  // 44 D DA: mask after the MFMAs
 #undef CM
       default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
     }
@@ -1519,8 +1515,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   } else if (bs == 16 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 &&
              aligned(val, 16) && aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
-    // 42xx / 44xx / 52xx select bs = 32 kernels: the bs = 16 default here
-    const int lv = var < 0 || ((var % 1000) / 100 == 2 || (var % 1000) / 100 == 4) ? kBsr16LdsDefault : var;
+    // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
+    const int lv = var < 0 || (var % 1000) / 100 == 2 ? kBsr16LdsDefault : var;
 #define L(D)                                                                                     \
   if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<float, true, D>), grid, dim3(256), 0, ctx->stream, \
                                mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);         \
@@ -1613,7 +1609,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
     // K > 256: one workgroup per 512 columns (A read once per 512)
-    const int lv = var < 0 || ((var % 1000) / 100 == 2 || (var % 1000) / 100 == 4)
+    const int lv = var < 0 || (var % 1000) / 100 == 2
                        ? (n > 256 ? kBsr16F16LdsWide : kBsr16F16LdsDefault)
                        : var;
 #define L(D)                                                                                      \
