@@ -1,6 +1,7 @@
 // api.cpp — extern "C" SpMM entry points: argument checks (mirroring the
 // reference's status behaviour) and dispatch to the HIP launchers.
 #include <cstdint>
+#include <cstdlib>
 
 #include "context.hpp"
 
@@ -55,6 +56,37 @@ spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, f
   if (st != SPMM_STATUS_SUCCESS) return st;
   // C (m x n col-major, ldc) is an (n x m) row-major matrix with ld ldc.
   return launch_transpose(ctx, m, n, Ct, n, C, ldc, beta);
+}
+
+// Column-major B and / or C with ROW blocks at bs 32 / 16 (cusparseSbsrmm's
+// transB = N layout, run_bsrmm.cu:70-71) run on the column-masked LDS kernels
+// (DESIGN.md §4): B is transposed into a row-major workspace copy (the kernels
+// copy whole B-panel rows), C is written column-major by the kernels' own
+// LDS-transposed epilogue. The direct kernels for these layouts fetch B
+// fragment-wise and were 2.6x (bs 32) to 4.5x (bs 16 fp16) slower end to end.
+// Any other shape keeps the direct kernels.
+bool bsr_stage(spmm_direction_t dir, int bs, int n, int elem, spmm_order_t ob, spmm_order_t oc,
+               const void* val) {
+  const int vec = 16 / elem;  // elements per 16-byte copy
+  return dir == SPMM_DIRECTION_ROW && (bs == 16 || (bs == 32 && elem == 4)) &&
+         (ob == SPMM_ORDER_COL || oc == SPMM_ORDER_COL) && n >= vec && n % vec == 0 &&
+         reinterpret_cast<uintptr_t>(val) % 16 == 0;
+}
+
+template <typename T, typename Launch>
+spmm_status_t bsrmm_staged(spmm_context* ctx, int kb, int n, int bs, const T* B, int ldb,
+                           spmm_order_t ob, Launch&& launch) {
+  if (ob == SPMM_ORDER_ROW) return launch(B, ldb);
+  spmm_status_t st = ensure_workspace(ctx, (size_t)kb * bs * n * sizeof(T));
+  if (st != SPMM_STATUS_SUCCESS) return st;
+  // B (kb*bs x n col-major) is an (n x kb*bs) row-major matrix with ld ldb.
+  T* Bt = static_cast<T*>(ctx->ws);
+  if constexpr (sizeof(T) == 4)
+    st = launch_transpose(ctx, n, kb * bs, B, ldb, Bt, n, 0.f);
+  else
+    st = launch_transpose16(ctx, n, kb * bs, B, ldb, Bt, n);
+  if (st != SPMM_STATUS_SUCCESS) return st;
+  return launch(Bt, n);
 }
 
 }  // namespace
@@ -153,6 +185,14 @@ spmm_status_t spmm_bsrmm_ex_f32(spmm_handle_t handle, spmm_direction_t dir, int 
   spmm_status_t st = bsr_checks(mb, kb, n, nnzb, blockDim, bsrRowPtr, bsrColInd, bsrVal, B, ldb,
                                 orderB, C, ldc, orderC, &quick);
   if (st != SPMM_STATUS_SUCCESS || quick) return st;
+  if (bsr_stage(dir, blockDim, n, 4, orderB, orderC, bsrVal))
+    return bsrmm_staged<float>(handle, kb, n, blockDim, B, ldb, orderB,
+                               [&](const float* Bx, int ldbx) {
+                                 return launch_bsrmm_f32(handle, dir, mb, kb, n, nnzb, blockDim,
+                                                         alpha, bsrRowPtr, bsrColInd, bsrVal, Bx,
+                                                         ldbx, SPMM_ORDER_ROW, beta, C, ldc,
+                                                         orderC);
+                               });
   return launch_bsrmm_f32(handle, dir, mb, kb, n, nnzb, blockDim, alpha, bsrRowPtr, bsrColInd,
                           bsrVal, B, ldb, orderB, beta, C, ldc, orderC);
 }
@@ -168,6 +208,14 @@ spmm_status_t spmm_bsrmm_ex_f16(spmm_handle_t handle, spmm_direction_t dir, int 
   spmm_status_t st = bsr_checks(mb, kb, n, nnzb, blockDim, bsrRowPtr, bsrColInd, bsrVal, B, ldb,
                                 orderB, C, ldc, orderC, &quick);
   if (st != SPMM_STATUS_SUCCESS || quick) return st;
+  if (bsr_stage(dir, blockDim, n, 2, orderB, orderC, bsrVal))
+    return bsrmm_staged<uint16_t>(handle, kb, n, blockDim, B, ldb, orderB,
+                                  [&](const uint16_t* Bx, int ldbx) {
+                                    return launch_bsrmm_f16(handle, dir, mb, kb, n, nnzb,
+                                                            blockDim, alpha, bsrRowPtr, bsrColInd,
+                                                            bsrVal, Bx, ldbx, SPMM_ORDER_ROW, beta,
+                                                            C, ldc, orderC);
+                                  });
   return launch_bsrmm_f16(handle, dir, mb, kb, n, nnzb, blockDim, alpha, bsrRowPtr, bsrColInd,
                           bsrVal, B, ldb, orderB, beta, C, ldc, orderC);
 }

@@ -609,6 +609,29 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // drain the clamped tail copies
 
+  if constexpr (!CROW) {
+    // Column-major C (cusparse layouts): the 32 x 128 tile goes through LDS so
+    // each store instruction writes two whole 128-B column segments instead
+    // of 64 scattered words.
+    constexpr int kTs = 36;  // floats per tile column (32 rows, 16-B aligned)
+    float* tile = smem;
+    __syncthreads();  // every wave is past its last read of the rings
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(tile + (32 * wv + r) * kTs + 8 * g + 4 * h) =
+          f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+    __syncthreads();
+    const size_t row = (size_t)br * 32 + r;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int jl = 2 * (4 * it + wv) + h;  // local column
+      if (jt + jl < n) {
+        float* p = C + (size_t)(jt + jl) * ldc + row;
+        *p = epi(tile[jl * kTs + r], alpha, beta, p);
+      }
+    }
+    return;
+  }
   const int jcol = jt + 32 * wv + r;
   if (jcol >= n) return;
   const size_t row0 = (size_t)br * 32;
@@ -956,6 +979,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
 
+  if constexpr (!CROW) {
+    // Column-major C: the 16 x COLS tile through LDS, then 4 whole 64-B column
+    // segments per store instruction.
+    constexpr int kTs = 16;  // floats per tile column
+    static_assert(COLS * kTs * 4 <= DA * kA + D * kStB, "tile fits the rings");
+    float* tile = reinterpret_cast<float*>(smem);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kTpw; ++t)
+      *reinterpret_cast<f32x4*>(tile + (wc + 16 * t + c16) * kTs + 4 * g) = acc[t];
+    __syncthreads();
+    const size_t row = (size_t)br * 16 + c16;
+#pragma unroll 4
+    for (int it = 0; it < COLS / 16; ++it) {
+      const int jl = 4 * (4 * it + wv) + g;  // local column
+      if (jt + jl < n) {
+        float* p = C + (size_t)(jt + jl) * ldc + row;
+        *p = epi(tile[jl * kTs + c16], alpha, beta, p);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < kTpw; ++t) {
     const int j = jt + wc + 16 * t + c16;

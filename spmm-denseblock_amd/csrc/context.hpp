@@ -71,6 +71,8 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
                                     int ldc, float* carry_val, int* carry_row, int nnz_hint);
 size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n, int* nwaves_out);
 
+spmm_status_t launch_transpose16(spmm_context* ctx, int rows, int cols, const uint16_t* src,
+                                 int ld_src, uint16_t* dst, int ld_dst);
 spmm_status_t launch_transpose(spmm_context* ctx, int rows, int cols, const float* src,
                                int ld_src, float* dst, int ld_dst, float beta);
 

@@ -549,6 +549,28 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols,
   }
 }
 
+// 16-bit dst (cols x rows, ld_dst) = transpose(src (rows x cols, ld_src)):
+// the fp16 B operand of the column-major BSR forms, staged row-major.
+__global__ __launch_bounds__(256) void transpose16_kernel(int rows, int cols,
+                                                          const uint16_t* __restrict__ src,
+                                                          int ld_src, uint16_t* __restrict__ dst,
+                                                          int ld_dst) {
+  __shared__ uint16_t tile[32][34];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int r = r0 + ty + k, c = c0 + tx;
+    if (r < rows && c < cols) tile[ty + k][tx] = src[(size_t)r * ld_src + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int c = c0 + ty + k, r = r0 + tx;
+    if (r < rows && c < cols) dst[(size_t)c * ld_dst + r] = tile[tx][ty + k];
+  }
+}
+
 int pick_vec(int n, const float* B, int ldb, const float* C, int ldc) {
   auto aligned = [](const void* p, int bytes) {
     return (reinterpret_cast<uintptr_t>(p) % bytes) == 0;
@@ -685,6 +707,15 @@ spmm_status_t launch_transpose(spmm_context* ctx, int rows, int cols, const floa
   dim3 grid((cols + 31) / 32, (rows + 31) / 32);
   hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, ctx->stream, rows, cols, src, ld_src,
                      dst, ld_dst, beta);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_transpose16(spmm_context* ctx, int rows, int cols, const uint16_t* src,
+                                 int ld_src, uint16_t* dst, int ld_dst) {
+  if (rows == 0 || cols == 0) return SPMM_STATUS_SUCCESS;
+  dim3 grid((cols + 31) / 32, (rows + 31) / 32);
+  hipLaunchKernelGGL(transpose16_kernel, grid, dim3(256), 0, ctx->stream, rows, cols, src, ld_src,
+                     dst, ld_dst);
   return from_hip(hipGetLastError());
 }
 

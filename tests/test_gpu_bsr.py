@@ -320,14 +320,17 @@ def _column_sparse_bsr(rng, mb, kb, bs, p):
 
 @pytest.mark.parametrize("bs,dtype", [(32, "f32"), (16, "f32"), (16, "f16")])
 @pytest.mark.parametrize("n", [64, 128, 264, 520])
-def test_column_sparse_blocks(oracle, device, bs, dtype, n):
+@pytest.mark.parametrize("layout", ["row", "col"])
+def test_column_sparse_blocks(oracle, device, bs, dtype, n, layout):
     """Blocks with empty columns (the column-masked kernels fetch only the B
     rows of nonzero A columns and skip MFMA steps of empty ones): explicit
     zero blocks, single-column blocks, quarter-full and full blocks, empty
     block rows, long rows. Then the same with inf / NaN in B rows that only
     empty A columns meet: those entries act as structural zeros (the CSR
     semantics of the same matrix), so C stays finite and equal to the
-    product with those rows zeroed."""
+    product with those rows zeroed. layout "col" is cusparseSbsrmm's
+    transB = N form (column-major B and C, alpha / beta), which the library
+    stages through its workspace onto the same kernels."""
     rng = np.random.default_rng(n + bs)
     mb, kb = 21, 80
     rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.3)
@@ -339,16 +342,32 @@ def test_column_sparse_blocks(oracle, device, bs, dtype, n):
     m = mb * bs
     tol = TOL_F32 if dtype == "f32" else TOL_F16_ACC
 
+    ops = _ops()
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    alpha, beta = (1.0, 0.0) if layout == "row" else (0.5, -1.5)
+
     def run(Bh):
-        drp, dci, dv, dB = _dev(rp, ci, v, Bh.reshape(-1))
-        dC = torch.full((m * n,), float("nan"), device=device)
-        fn(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=ldb, C=dC, ldc=n)
+        if layout == "row":  # row-major B and C, beta = 0: C starts as NaN
+            drp, dci, dv, dB = _dev(rp, ci, v, Bh.reshape(-1))
+            dC = torch.full((m * n,), float("nan"), device=device)
+            fn(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=ldb, C=dC, ldc=n)
+            torch.cuda.synchronize()
+            return dC.cpu().numpy().reshape(m, n)
+        # cusparseSbsrmm transB = N: B and C column-major (staged through the workspace)
+        drp, dci, dv, dB, dC = _dev(rp, ci, v, np.ascontiguousarray(Bh.T).reshape(-1),
+                                    np.ascontiguousarray(C0.T).reshape(-1))
+        fn(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=kb * bs, order_b=ops.ORDER_COL, C=dC,
+           ldc=m, order_c=ops.ORDER_COL, alpha=alpha, beta=beta)
         torch.cuda.synchronize()
-        return dC.cpu().numpy().reshape(m, n)
+        return dC.cpu().numpy().reshape(n, m).T
 
     ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, ldb, 0,
                                  half=dtype == "f16")
-    assert_normwise(run(B), ref, absd, tol, f"column-sparse bs={bs} {dtype} n={n}")
+    c0 = 0.0 if layout == "row" else C0.astype(np.float64)
+    ref = alpha * ref + beta * c0
+    absd = abs(alpha) * absd + abs(beta) * np.abs(c0)
+    what = f"column-sparse bs={bs} {dtype} n={n} {layout}"
+    assert_normwise(run(B), ref, absd, tol, what)
     # B rows that no nonzero of A meets
     vb = v.reshape(-1, bs, bs).astype(np.float32)
     used = np.zeros(kb * bs, bool)
@@ -362,4 +381,4 @@ def test_column_sparse_blocks(oracle, device, bs, dtype, n):
     Bbad[unused[1::2]] = np.nan
     got = run(Bbad)
     assert np.isfinite(got).all(), "explicit zeros must not turn inf / NaN of B into NaN"
-    assert_normwise(got, ref, absd, tol, f"column-sparse bs={bs} {dtype} n={n}, non-finite B")
+    assert_normwise(got, ref, absd, tol, what + ", non-finite B")
