@@ -318,6 +318,16 @@ def run_csr(args, W, world, rank, dev, dist):
 
         def step():
             sdist.chunked_spmm(shard, out, compute_chunk, nch, compact=False)
+    elif args.csr_layout == "col":
+        if world > 1:
+            raise SystemExit("--csr-layout col is a 1-GPU form")
+        # cusparseScsrmm's layout (run_csrmm.cu:135-137): B and C column-major
+        Bc = B.t().contiguous()
+        Cc = torch.empty((K, n), device=dev)
+
+        def step():
+            ops.csrmm(d_rp, d_ci, d_v, Bc, m=n, n=K, k=n, ldb=n, order_b=ops.ORDER_COL, C=Cc,
+                      ldc=n, order_c=ops.ORDER_COL, handle=h)
     else:
         out = torch.empty((world * mr, K), device=dev)
         C_slot = out[rank * mr: rank * mr + shard.rows]
@@ -358,7 +368,7 @@ def run_csr(args, W, world, rank, dev, dist):
                 "parallelism": f"rows{world}" if world > 1 else "single",
                 "exchange_chunks": nch, "hip_graph": bool(GRAPH and world == 1),
                 "waves_per_cu": args.waves_per_cu or 16,
-                "csr_options": args.csr_options},
+                "csr_options": args.csr_options, "layout_BC": args.csr_layout},
         roofline={"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                   "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                   "traffic": traffic, "kernel": f"csr_mergepath_kernel<{vec}>",
@@ -587,6 +597,8 @@ def main() -> None:
                     help="override a BSR workload's value type")
     ap.add_argument("--bsr-layout", choices=["row", "col"], default="row",
                     help="B/C storage for BSR workloads (col = cusparse transB=N)")
+    ap.add_argument("--csr-layout", choices=["row", "col"], default="row",
+                    help="B/C storage for CSR workloads (col = cusparseScsrmm, run_csrmm.cu)")
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--csr-options", type=int, default=None, help="SPMM_CSR_* flags")
     ap.add_argument("--chunks", type=int, default=0,

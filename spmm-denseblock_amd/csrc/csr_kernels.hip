@@ -549,6 +549,55 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols,
   }
 }
 
+// The same with 16-byte accesses on both sides (64 x 64 tiles), for any shape:
+// loads go along src rows and stores along dst rows as 4-float vectors that
+// need only 4-byte alignment (odd leading dimensions such as the 2,449,029
+// rows of products), scalar at the matrix edges; the tile is read back down
+// its columns (stride 65: conflict-free).
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+__global__ __launch_bounds__(256) void transpose4_kernel(int rows, int cols,
+                                                         const float* __restrict__ src,
+                                                         int ld_src, float* __restrict__ dst,
+                                                         int ld_dst, float beta) {
+  __shared__ float tile[64][65];
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int q = t & 15, rb = t >> 4;  // 4-float group in a 64-wide row, first row
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = rb + 16 * i, c = 4 * q;
+    if (r0 + r >= rows) continue;
+    const float* p = src + (size_t)(r0 + r) * ld_src + c0 + c;
+    if (c0 + c + 3 < cols) {
+      const f32x4u x = *reinterpret_cast<const f32x4u*>(p);
+      tile[r][c] = x[0]; tile[r][c + 1] = x[1]; tile[r][c + 2] = x[2]; tile[r][c + 3] = x[3];
+    } else {
+      for (int e = 0; e < 4 && c0 + c + e < cols; ++e) tile[r][c + e] = p[e];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = rb + 16 * i, r = 4 * q;  // dst row c0 + c, dst columns r0 + r .. + 3
+    if (c0 + c >= cols || r0 + r >= rows) continue;
+    float* p = dst + (size_t)(c0 + c) * ld_dst + r0 + r;
+    if (r0 + r + 3 < rows) {
+      f32x4u x = {tile[r][c], tile[r + 1][c], tile[r + 2][c], tile[r + 3][c]};
+      if (beta != 0.f) {
+        const f32x4u o = *reinterpret_cast<const f32x4u*>(p);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = __builtin_fmaf(beta, o[e], x[e]);
+      }
+      *reinterpret_cast<f32x4u*>(p) = x;
+    } else {
+      for (int e = 0; e < 4 && r0 + r + e < rows; ++e) {
+        const float x = tile[r + e][c];
+        p[e] = (beta == 0.f) ? x : __builtin_fmaf(beta, p[e], x);
+      }
+    }
+  }
+}
+
 // 16-bit dst (cols x rows, ld_dst) = transpose(src (rows x cols, ld_src)):
 // the fp16 B operand of the column-major BSR forms, staged row-major.
 __global__ __launch_bounds__(256) void transpose16_kernel(int rows, int cols,
@@ -704,6 +753,12 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
 spmm_status_t launch_transpose(spmm_context* ctx, int rows, int cols, const float* src,
                                int ld_src, float* dst, int ld_dst, float beta) {
   if (rows == 0 || cols == 0) return SPMM_STATUS_SUCCESS;
+  if ((rows + 63) / 64 <= 65535) {
+    dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+    hipLaunchKernelGGL(transpose4_kernel, grid, dim3(256), 0, ctx->stream, rows, cols, src,
+                       ld_src, dst, ld_dst, beta);
+    return from_hip(hipGetLastError());
+  }
   dim3 grid((cols + 31) / 32, (rows + 31) / 32);
   hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, ctx->stream, rows, cols, src, ld_src,
                      dst, ld_dst, beta);
