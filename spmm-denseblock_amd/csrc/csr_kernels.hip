@@ -620,6 +620,43 @@ __global__ __launch_bounds__(256) void transpose16_kernel(int rows, int cols,
   }
 }
 
+// 16-bit, 64 x 64 tiles, 4 elements (8 B, 2-byte aligned) per access on both sides.
+typedef uint16_t u16x4u __attribute__((ext_vector_type(4), aligned(2)));
+__global__ __launch_bounds__(256) void transpose16x4_kernel(int rows, int cols,
+                                                            const uint16_t* __restrict__ src,
+                                                            int ld_src, uint16_t* __restrict__ dst,
+                                                            int ld_dst) {
+  __shared__ uint16_t tile[64][66];
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int q = t & 15, rb = t >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = rb + 16 * i, c = 4 * q;
+    if (r0 + r >= rows) continue;
+    const uint16_t* p = src + (size_t)(r0 + r) * ld_src + c0 + c;
+    if (c0 + c + 3 < cols) {
+      const u16x4u x = *reinterpret_cast<const u16x4u*>(p);
+      tile[r][c] = x[0]; tile[r][c + 1] = x[1]; tile[r][c + 2] = x[2]; tile[r][c + 3] = x[3];
+    } else {
+      for (int e = 0; e < 4 && c0 + c + e < cols; ++e) tile[r][c + e] = p[e];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = rb + 16 * i, r = 4 * q;
+    if (c0 + c >= cols || r0 + r >= rows) continue;
+    uint16_t* p = dst + (size_t)(c0 + c) * ld_dst + r0 + r;
+    if (r0 + r + 3 < rows) {
+      const u16x4u x = {tile[r][c], tile[r + 1][c], tile[r + 2][c], tile[r + 3][c]};
+      *reinterpret_cast<u16x4u*>(p) = x;
+    } else {
+      for (int e = 0; e < 4 && r0 + r + e < rows; ++e) p[e] = tile[r + e][c];
+    }
+  }
+}
+
 int pick_vec(int n, const float* B, int ldb, const float* C, int ldc) {
   auto aligned = [](const void* p, int bytes) {
     return (reinterpret_cast<uintptr_t>(p) % bytes) == 0;
@@ -768,6 +805,12 @@ spmm_status_t launch_transpose(spmm_context* ctx, int rows, int cols, const floa
 spmm_status_t launch_transpose16(spmm_context* ctx, int rows, int cols, const uint16_t* src,
                                  int ld_src, uint16_t* dst, int ld_dst) {
   if (rows == 0 || cols == 0) return SPMM_STATUS_SUCCESS;
+  if ((rows + 63) / 64 <= 65535 && reinterpret_cast<uintptr_t>(src) % 2 == 0) {
+    dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+    hipLaunchKernelGGL(transpose16x4_kernel, grid, dim3(256), 0, ctx->stream, rows, cols, src,
+                       ld_src, dst, ld_dst);
+    return from_hip(hipGetLastError());
+  }
   dim3 grid((cols + 31) / 32, (rows + 31) / 32);
   hipLaunchKernelGGL(transpose16_kernel, grid, dim3(256), 0, ctx->stream, rows, cols, src, ld_src,
                      dst, ld_dst);
