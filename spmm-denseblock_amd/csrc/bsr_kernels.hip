@@ -476,7 +476,9 @@ __device__ __forceinline__ int or_wave(int x) {
          __builtin_amdgcn_readlane(x, 32) | __builtin_amdgcn_readlane(x, 48);
 }
 
-template <bool CROW, int XM, int D = 3, int DA = D + 3, bool NOMFMA = false>
+// DIAG (diagnostic builds only, wrong results): bit 0 no MFMA, bit 1 no B
+// (every B row from the zero row), bit 2 every A copy from block k0.
+template <bool CROW, int XM, int D = 3, int DA = D + 3, int DIAG = 0>
 __global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
   auto wrapA = [](int s) { return s >= DA ? s - DA : s; };
 
   auto issue_a = [&](int k, int slot) {
-    const int kk = min(k, k1 - 1);
+    const int kk = (DIAG & 4) ? k0 : min(k, k1 - 1);
     __builtin_amdgcn_global_load_lds((gbl_void_t)(val + (size_t)kk * 1024 + a_src),
                                      (lds_void_t)(sa + slot * kA + 256 * wv), 16, 0, 0);
   };
@@ -527,7 +529,8 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
     float* dst = sb + slot * kB;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float* src = ((mask >> (b_row + 2 * i)) & 1u) ? bsrc + (size_t)(2 * i) * ldb : zsrc;
+      const bool on = !(DIAG & 2) && ((mask >> (b_row + 2 * i)) & 1u);
+      const float* src = on ? bsrc + (size_t)(2 * i) * ldb : zsrc;
       __builtin_amdgcn_global_load_lds((gbl_void_t)src,
                                        (lds_void_t)(dst + 128 * (8 * wv + 2 * i)), 16, 0, 0);
     }
@@ -584,7 +587,7 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
     part[4 * ((k + D) & 3) + wv] = partial(wrapA(sA + D));                       // (c)
     issue_a(k + DA - 1, sA == 0 ? DA - 1 : sA - 1);                              // (d)
     // (e) step s2 of half h uses column 16h + s2: pm bit s2 = either column set
-    const unsigned pm = NOMFMA ? 0u : (mr[0] | (mr[0] >> 16)) & 0xffffu;
+    const unsigned pm = (DIAG & 1) ? 0u : (mr[0] | (mr[0] >> 16)) & 0xffffu;
     const float* stA = sa + sA * kA;
     const float* stB = sb + sB * kB + (16 * h) * 128 + 32 * wv + r;
 #pragma unroll
@@ -1538,7 +1541,9 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                             ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);      \
     break;
       CM(4200, 3, 6) CM(4236, 3, 6) CM(4235, 3, 5) CM(4237, 3, 7) CM(4225, 2, 5) CM(4226, 2, 6)
-      CM(4247, 4, 7) CM(4248, 4, 8) CM(5236, 3, 6, true) CM(5225, 2, 5, true)
+      CM(4247, 4, 7) CM(4248, 4, 8) CM(5236, 3, 6, 1) CM(5225, 2, 5, 1)
+      // diagnostics: 602x = D 2, DA 5 with DIAG x (1 no MFMA, 2 no B, 4 A from k0)
+      CM(6022, 2, 5, 2) CM(6024, 2, 5, 4) CM(6026, 2, 5, 6) CM(6027, 2, 5, 7)
 #undef CM
       default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
     }
