@@ -1435,7 +1435,11 @@ constexpr int kBsr32Default = 40;
 // fastest measured (reddit stand-in 2.65 ms vs 4.57 for 4124; products bs = 32
 // 4.62 vs 8.51; (3, 6) 3.08 / 5.60; (4, 8) 4.87 / 9.09).
 constexpr int kBsr32LdsDefault = 4225;
-constexpr int kBsr32LdsDense = 4124;
+// Blocks known to be dense (the hybrid's BSR part, MFMA-pipe bound): the
+// full-panel kernel with D = 2 (40 KB, 4 workgroups per CU) and the chunked
+// XCD order. Products stand-in hybrid part 1.71 vs 1.87 ms for D = 3 (4124),
+// 1.90 for D = 4; reddit 0.85 vs 0.86.
+constexpr int kBsr32LdsDense = 4126;
 // LDS-staged bs = 16 kernels: 4096 + D (+ 8: XCD-contiguous block rows). fp16:
 // 6 waves/SIMD at D = 3 beat deeper rings, the XCD order 5 % more
 // (products_bsr16_f16 8.80 ms vs 10.38 for the register-fragment kernel);
@@ -1531,6 +1535,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       case 4123: L(3, 16) break;  // 4123-4125: XCD order in chunks of 16 / 32 / 64
       case 4124: L(3, 32) break;
       case 4125: L(3, 64) break;
+      case 4126: L(2, 32) break;  // D = 2 / 4 with the chunked XCD order
+      case 4127: L(4, 32) break;
       // column-masked (fetch only the B rows of nonzero A columns): 42DA:
       // D = B stages, A = A stages (42 3 6 = D 3, DA 6); + 1000 = no MFMA (diagnostic)
 #define CM(V, ...)                                                                                     \
