@@ -580,6 +580,15 @@ def run_hybrid(args, W, world, rank, dev, dist):
         plan=plan, reorder=reorder,
         part_kernel_ms=None if kt is None else [round(float(x), 4) for x in kt.mean(axis=0)])
     rec["roofline"]["frac"] = round(rec["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
+    if kt is not None and parts == 2 and bs == 32:
+        # The BSR part runs every MFMA step of its dense blocks and is bound by
+        # the MFMA pipe (DESIGN.md §4a PMC), not by HBM.
+        bsr_ms = float(kt.mean(axis=0)[0])
+        tf = 2.0 * bci.size * bs * bs * K / (bsr_ms / 1e3) / 1e12
+        rec["bsr_part"] = {"bound": "mfma", "kernel_ms": round(bsr_ms, 4),
+                           "mfma_executed_TFLOPs": round(tf, 1),
+                           "mfma_peak": MFMA_PEAK_TFLOPS["fp32"],
+                           "mfma_frac": round(tf / MFMA_PEAK_TFLOPS["fp32"], 4)}
     return rec, None
 
 
