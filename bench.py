@@ -549,11 +549,12 @@ def run_hybrid(args, W, world, rank, dev, dist):
     hopt = args.hybrid_options or 0
     if hopt:
         h.set_hybrid_options(hopt)
-    # SPMM_HYBRID_FUSED: both parts in one bs = 32 launch
-    fused = bs == 32 and bci.size > 0 and cci.size > 0 and K % 4 == 0 and bool(hopt & 1)
     elapsed, kt = timed_loop(step, h, args.steps, args.warmup, 1, dist, raw=True)
-    # launch order per step: the BSR kernel, then the CSR kernel (when both parts exist)
-    parts = 1 if fused else int(bci.size > 0) + int(cci.size > 0)
+    # Launches per step: one when the library fused both parts (bs = 32; by
+    # default when the remainder is short per block row), else
+    # the BSR kernel, then the CSR kernel (when both parts exist).
+    parts = len(kt) // args.steps if kt else 0
+    fused = parts == 1 and bci.size > 0 and cci.size > 0
     kt = np.array(kt[: parts * args.steps]).reshape(args.steps, parts) if parts else None
     h2 = ops.Handle()
     _, csr_ms = timed_loop(lambda: ops.csrmm(d[6], d[7], d[8], B, m=n, n=K, k=mb * bs, ldb=K,
@@ -622,7 +623,7 @@ def main() -> None:
     ap.add_argument("--no-exchange-probe", action="store_true",
                     help="weak scaling: skip timing the C all-gather after the step loop")
     ap.add_argument("--hybrid-options", type=int, default=None,
-                    help="SPMM_HYBRID_* flags (1 = fused single launch, bs = 32)")
+                    help="SPMM_HYBRID_* flags (0 = library default, 1 = force fused, 2 = force two launches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (DESIGN.md §7)")

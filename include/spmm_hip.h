@@ -315,12 +315,17 @@ spmm_status_t spmm_dbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_opera
 /* Hybrid dense-block + CSR-remainder SpMM (divide.cu:348-373)                */
 /* ------------------------------------------------------------------------ */
 
-/* Hybrid options (per handle): SPMM_HYBRID_FUSED computes both parts in one
- * bs = 32 launch (MFMA part, then each block row's CSR remainder in the same
- * workgroup) instead of two stream-ordered launches. Same result up to the
- * CSR kernel's split-row carries; measured no faster on bandwidth-bound
- * inputs, hence opt-in. */
+/* Hybrid options (per handle). At bs = 32 the hybrid runs either fused, in
+ * one launch (MFMA part, then each block row's CSR remainder in the same
+ * workgroup), or as two stream-ordered launches (BSR kernel, then the CSR
+ * kernel with beta = 1). Same result up to the CSR kernel's split-row carries.
+ * By default (flags 0) it is fused when the remainder averages at most 512
+ * entries per block row (csrNnz <= 512 * mb): the remainder then fits beside
+ * the MFMA work, while long per-block-row remainders leave a tail of single
+ * workgroups. SPMM_HYBRID_FUSED / SPMM_HYBRID_TWO_LAUNCH force
+ * one form. */
 #define SPMM_HYBRID_FUSED 1
+#define SPMM_HYBRID_TWO_LAUNCH 2
 spmm_status_t spmm_set_hybrid_options(spmm_handle_t handle, int flags);
 
 /* C(m x n) = alpha * (A_bsr + A_csr) * B(k x n) + beta * C, row-major B and C.

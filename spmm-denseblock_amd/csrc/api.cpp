@@ -333,6 +333,11 @@ spmm_status_t spmm_sbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_opera
 
 }  // extern "C"
 
+// Mean CSR-remainder entries per 32-row block row up to which the hybrid runs
+// fused by default (products stand-in 71: fused 2.41 vs 2.73 ms; reddit 222:
+// 1.01 vs 1.03; RCM-reordered reddit 2295: 2.37 vs 2.08, two launches win).
+constexpr int64_t kHybridFusedRemainderPerBlockRow = 512;
+
 extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
     spmm_handle_t handle, int m, int n, int k, float alpha, const int* csrRowPtr,
     const int* csrColInd, const float* csrVal, int csrNnz, int blockDim, const int* bsrRowPtr,
@@ -341,7 +346,8 @@ extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
   // divide.cu:348-373 runs csrmm2 and bsrmm back to back with alpha = beta = 1
   // onto a zeroed C. Here the BSR part applies the caller's beta and the CSR
   // remainder accumulates on top, both on the handle's stream; with
-  // SPMM_HYBRID_FUSED (bs = 32) one launch does both per block row (§4a).
+  // fused (bs = 32) one launch does both per block row (§4a): by default when
+  // the remainder averages <= 512 entries per block row, or forced by flags.
   if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
   if (m < 0 || n < 0 || k < 0 || csrNnz < 0 || nnzb < 0 || blockDim <= 0)
     return SPMM_STATUS_INVALID_VALUE;
@@ -349,7 +355,12 @@ extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
   if (!csrRowPtr || !C || ldb < n || ldc < n || (k > 0 && !B)) return SPMM_STATUS_INVALID_VALUE;
   if (nnzb > 0 && (!bsrRowPtr || !bsrColInd || !bsrVal)) return SPMM_STATUS_INVALID_VALUE;
   if (csrNnz > 0 && (!csrColInd || !csrVal)) return SPMM_STATUS_INVALID_VALUE;
-  if (blockDim == 32 && nnzb > 0 && csrNnz > 0 && (handle->hybrid_flags & SPMM_HYBRID_FUSED) &&
+  const int flags = handle->hybrid_flags;
+  const bool want_fused =
+      (flags & SPMM_HYBRID_FUSED) ||
+      (!(flags & SPMM_HYBRID_TWO_LAUNCH) &&
+       (int64_t)csrNnz <= kHybridFusedRemainderPerBlockRow * (int64_t)((m + 31) / 32));
+  if (blockDim == 32 && nnzb > 0 && csrNnz > 0 && want_fused &&
       hybrid32_fusable(n, ldb, ldc, bsrVal, B, C))
     return launch_hybrid32_fused(handle, m, n, alpha, csrRowPtr, csrColInd, csrVal, bsrRowPtr,
                                  bsrColInd, bsrVal, B, ldb, beta, C, ldc);

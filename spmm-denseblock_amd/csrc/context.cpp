@@ -13,7 +13,7 @@ spmm_status_t ensure_workspace(spmm_context* ctx, size_t bytes) {
   if (ctx->ws) {
     hipError_t e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return from_hip(e);
-    hipFree(ctx->ws);
+    (void)hipFree(ctx->ws);
     ctx->ws = nullptr;
     ctx->ws_bytes = 0;
   }
@@ -34,26 +34,26 @@ int timing_begin(spmm_context* ctx) {
     hipEvent_t a, b;
     if (hipEventCreate(&a) != hipSuccess) return -1;
     if (hipEventCreate(&b) != hipSuccess) {
-      hipEventDestroy(a);
+      (void)hipEventDestroy(a);
       return -1;
     }
     ctx->ev_start.push_back(a);
     ctx->ev_stop.push_back(b);
   }
-  hipEventRecord(ctx->ev_start[slot], ctx->stream);
+  (void)hipEventRecord(ctx->ev_start[slot], ctx->stream);
   ctx->ev_used = slot + 1;
   return (int)slot;
 }
 
 void timing_end(spmm_context* ctx, int slot) {
   if (slot < 0) return;
-  hipEventRecord(ctx->ev_stop[slot], ctx->stream);
+  (void)hipEventRecord(ctx->ev_stop[slot], ctx->stream);
 }
 
 static spmm_context* make_context() {
   spmm_context* ctx = new (std::nothrow) spmm_context();
   if (!ctx) return nullptr;
-  hipGetDevice(&ctx->device);
+  (void)hipGetDevice(&ctx->device);
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) ==
           hipSuccess &&
@@ -67,7 +67,7 @@ spmm_context* default_context() {
   static std::mutex mu;
   static spmm_context* ctxs[64] = {nullptr};
   int dev = 0;
-  hipGetDevice(&dev);
+  (void)hipGetDevice(&dev);
   if (dev < 0 || dev >= 64) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
   if (!ctxs[dev]) ctxs[dev] = make_context();
@@ -113,11 +113,11 @@ spmm_status_t spmm_create(spmm_handle_t* handle) {
 spmm_status_t spmm_destroy(spmm_handle_t h) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
   if (h->ws) {
-    hipStreamSynchronize(h->stream);
-    hipFree(h->ws);
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipFree(h->ws);
   }
-  for (auto e : h->ev_start) hipEventDestroy(e);
-  for (auto e : h->ev_stop) hipEventDestroy(e);
+  for (auto e : h->ev_start) (void)hipEventDestroy(e);
+  for (auto e : h->ev_stop) (void)hipEventDestroy(e);
   delete h;
   return SPMM_STATUS_SUCCESS;
 }
@@ -198,7 +198,9 @@ spmm_status_t spmm_set_csr_options(spmm_handle_t h, int flags) {
 
 spmm_status_t spmm_set_hybrid_options(spmm_handle_t h, int flags) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
-  if (flags & ~SPMM_HYBRID_FUSED) return SPMM_STATUS_INVALID_VALUE;
+  if ((flags & ~(SPMM_HYBRID_FUSED | SPMM_HYBRID_TWO_LAUNCH)) ||
+      (flags & SPMM_HYBRID_FUSED && flags & SPMM_HYBRID_TWO_LAUNCH))
+    return SPMM_STATUS_INVALID_VALUE;
   h->hybrid_flags = flags;
   return SPMM_STATUS_SUCCESS;
 }

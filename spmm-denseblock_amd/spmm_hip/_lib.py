@@ -32,6 +32,7 @@ INDEX_BASE_ZERO, INDEX_BASE_ONE = 0, 1
 CSR_NT_STREAMS = 1
 CSR_SEQUENTIAL_ROWS = 2
 HYBRID_FUSED = 1
+HYBRID_TWO_LAUNCH = 2
 
 
 class SpmmError(RuntimeError):

@@ -183,12 +183,13 @@ def test_hybrid_divide_spmm(oracle, device, bs, density, alpha, beta):
 @pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.5, 1.5)])
 def test_hybrid_fused_vs_two_launch(oracle, device, n, K, alpha, beta):
     """The fused bs = 32 hybrid (SPMM_HYBRID_FUSED: one launch, MFMA part +
-    per-block-row CSR remainder) against the oracle, and against the default
-    two-launch form: identical on every row the CSR kernel keeps in one wave.
+    per-block-row CSR remainder) against the oracle, and against the
+    two-launch form (SPMM_HYBRID_TWO_LAUNCH): identical on every row the CSR kernel keeps in one wave.
     Hub rows give remainders far longer than the 32-entry batch, sparse rows
     give block rows with no dense block at all."""
     from spmm_hip import prep
-    from spmm_hip._lib import CSR_NT_STREAMS, CSR_SEQUENTIAL_ROWS, HYBRID_FUSED
+    from spmm_hip._lib import (CSR_NT_STREAMS, CSR_SEQUENTIAL_ROWS, HYBRID_FUSED,
+                               HYBRID_TWO_LAUNCH)
     rp, ci = prep.community_csr(n, 30.0, 48, 160, 0.9, 7)
     rng = np.random.default_rng(8)
     rows = [ci[rp[i]:rp[i + 1]] for i in range(n)]
@@ -208,7 +209,7 @@ def test_hybrid_fused_vs_two_launch(oracle, device, n, K, alpha, beta):
     d = _dev(*parts, Bp)
     ops = _ops()
     outs = []
-    for flags in (HYBRID_FUSED, 0):
+    for flags in (HYBRID_FUSED, HYBRID_TWO_LAUNCH):
         h = ops.Handle()
         h.set_hybrid_options(flags)
         # the small-K lane-group CSR kernel folds partial sums: compare
