@@ -229,17 +229,16 @@ constexpr int waitcnt_vm_lgkm0(int n) { return (n & 15) | (7 << 4) | ((n >> 4) <
 // (a merge-path cut over the 33 row pointers, one ballot per wave). A wave
 // walks its rows with wave-uniform (scalar) colind/val loads, lanes across the
 // 128 columns (one float2 of each B row per lane, 512 B per wave-instruction),
-// 8 entries in flight per batch, one sequential FMA chain per element in CSR
+// HB (24) entries in flight per batch, one sequential FMA chain per element in CSR
 // order, and writes each row once:
 //   C = epi(tile, alpha, beta, C) + alpha * remainder
 // which is the two-launch result (BSR kernel, then the CSR kernel with
 // beta = 1) bit for bit on every row the CSR kernel keeps in one wave.
 // The remainder's HBM gathers of one workgroup overlap other workgroups' MFMA
 // phases on the same CU.
-constexpr int kHybBatch = 32;
 constexpr int kHybTs = 136;  // tile row stride (floats): the two half-waves' rows
                              // land 32 banks apart when the tile is written
-template <int D>
+template <int D, int kHybBatch>
 __device__ __forceinline__ void hyb_remainder(float* smem, const f32x16& acc, int br, int jt,
                                               int n, const int* __restrict__ rrp,
                                               const int* __restrict__ rci,
@@ -337,7 +336,8 @@ __device__ __forceinline__ int xcd_block_row(int b, int mb, int xm) {
   return b;
 }
 
-template <bool CROW, int D, int XM, bool HYB = false>
+// HB: remainder gathers in flight per wave in the fused hybrid (HYB).
+template <bool CROW, int D, int XM, bool HYB = false, int HB = 24>
 __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
   }
 
   if constexpr (HYB) {
-    hyb_remainder<D>(smem, acc, br, jt, n, rrp, rci, rv, m, B, ldb, alpha, beta, C, ldc);
+    hyb_remainder<D, HB>(smem, acc, br, jt, n, rrp, rci, rv, m, B, ldb, alpha, beta, C, ldc);
     return;
   }
   const int jcol = jt + 32 * wv + r;
@@ -1641,9 +1641,16 @@ spmm_status_t launch_hybrid32_fused(spmm_context* ctx, int m, int n, float alpha
   else if (var == 4124)
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 3, 32, true>), grid, dim3(256), 0, ctx->stream,
                        mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
-  else  // D = 2, 4 workgroups per CU (products stand-in 2.41 ms vs 2.81 for D = 3)
-    hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true>), grid, dim3(256), 0, ctx->stream,
-                       mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+  else if (var == 4126)  // 32 remainder gathers in flight: 113 VGPRs, 3 workgroups per CU
+    hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 32>), grid, dim3(256), 0,
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+  else if (var == 4128)
+    hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 16>), grid, dim3(256), 0,
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+  else  // D = 2 and 24 remainder gathers in flight (73 VGPRs): 4 workgroups per CU.
+        // Products stand-in 2.09 ms vs 2.42 with 32 in flight and 2.81 with D = 3.
+    hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 24>), grid, dim3(256), 0,
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
   timing_end(ctx, slot);
   return from_hip(hipGetLastError());
 }
