@@ -440,7 +440,11 @@ def run_bsr(args, W, world, rank, dev, dist):
     # runs only the MFMA steps whose column pair holds a nonzero. The counts
     # come from the CSR pattern (distinct (block row, column) and (block,
     # column pair) keys, counted on the device).
-    cm = args.bsr_layout == "row"
+    # The column-major layout (cusparse transB = N) runs the same kernels on a
+    # row-major staged copy of B, with C written column-major by their
+    # epilogue; the transposes are separate launches, outside
+    # kernel_ms.
+    cm = bs in (16, 32) and K % (4 if dt == "fp32" else 8) == 0
     d_r = torch.repeat_interleave(torch.arange(n, device=dev, dtype=torch.int64),
                                   torch.from_numpy(np.diff(rp)).to(dev))
     d_c = torch.from_numpy(ci).to(dev).to(torch.int64)
@@ -478,9 +482,11 @@ def run_bsr(args, W, world, rank, dev, dist):
         roofline={"bound": "hbm", "achieved": round(cm_bytes / t / 1e9, 1),
                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                   "frac": round(cm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-                  "kernel": (f"bsr{bs}_{'f32_' if bs == 32 else ''}cm_kernel<"
-                             f"{'f32' if dt == 'fp32' else 'f16'}>" if cm else
-                             f"bsr{bs} register-fragment kernel (column-major operands)"),
+                  "kernel": (("bsr32_f32_cm4_kernel" if bs == 32 else
+                              f"bsr16_cm_kernel<{'f32' if dt == 'fp32' else 'f16'}>")
+                             + (" (column-major C epilogue, B staged row-major)"
+                                if args.bsr_layout == "col" else "") if cm else
+                             f"bsr{bs} register-fragment kernel"),
                   "kernel_ms": round(kms, 4),
                   "bytes_per_launch": cm_bytes, "bytes_model": (
                       "A values + block columns per column tile, B rows of nonzero A columns, "

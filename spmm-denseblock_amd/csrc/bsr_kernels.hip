@@ -24,6 +24,8 @@
 // Fragments of block b+1 are loaded while block b's MFMAs issue.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "context.hpp"
 
 namespace {
@@ -644,6 +646,198 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm_kernel(
     for (int e = 0; e < 4; ++e) {
       const size_t row = row0 + 8 * g + 4 * h + e;
       float* p = CROW ? C + row * ldc + jcol : C + (size_t)jcol * ldc + row;
+      *p = epi(acc[4 * g + e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 32 fp32, column-masked, four workgroups per CU ("CM4"): the CM kernel
+// above in 40 960 B of LDS (2 A stages + 2 B stages), which is what a fourth
+// workgroup per CU needs; the CM kernel's A ring (5 stages) and mask words
+// hold it at three.
+//  * A goes through VGPRs: each wave loads its own 8 rows of a block (one
+//    dwordx4 per lane, the CM kernel's DMA layout) three blocks ahead and
+//    writes them into the A stage one block before their MFMAs.
+//  * No mask words: after a second barrier per block every wave reads the
+//    whole next A block from LDS (4 x ds_read_b128 per lane) and reduces its
+//    column mask itself.
+// Per block k: barrier (B(k) landed, MFMA(k-1) done) -> write A(k+1) ->
+// barrier -> mask(k+1) from LDS -> copy B(k+1) (zero row for empty columns)
+// -> load A(k+4) -> MFMA(k) (steps of empty column pairs skipped). Numerics
+// and semantics are the CM kernel's.
+// ---------------------------------------------------------------------------
+template <bool CROW, int XM>
+__global__ __launch_bounds__(256) void bsr32_f32_cm4_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  constexpr int kA = 1024, kB = 32 * 128;  // floats per A / B stage
+  __shared__ __attribute__((aligned(16))) float smem[2 * kA + 2 * kB];
+  float* const sa = smem;
+  float* const sb = smem + 2 * kA;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int br = xcd_block_row(blockIdx.x, mb, XM);
+  const int jt = blockIdx.y * 128;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  if (k0 >= k1) {
+    const int j = jt + 32 * wv + (lane & 31);
+    if (j < n)
+      for (int e = 0; e < 16; ++e) {
+        const size_t row = (size_t)br * 32 + 2 * e + (lane >> 5);
+        float* p = CROW ? C + row * ldc + j : C + (size_t)j * ldc + row;
+        *p = epi(0.f, alpha, beta, p);
+      }
+    return;
+  }
+
+  // A: lane l holds row 8w + l/8, logical chunk (l%8) ^ swz(row), and writes it
+  // to stage offset 256w + 4l (the CM kernel's swizzled layout).
+  const int a_row = 8 * wv + (lane >> 3);
+  const int a_src = a_row * 32 + 4 * ((lane & 7) ^ ((a_row >> 1) & 7));
+  const int a_dst = 256 * wv + 4 * lane;
+  const int b_col = min(jt + 4 * (lane & 31), n - 4);
+  const int b_row = 8 * wv + (lane >> 5);
+  const float* zsrc = g_zero_row + 4 * (lane & 31);
+  f32x4 ra[3];  // A of blocks j = k + 1 .. k + 3 (register set (j - k0) % 3)
+  auto load_a = [&](int j) -> f32x4 {
+    return *reinterpret_cast<const f32x4*>(val + (size_t)min(j, k1 - 1) * 1024 + a_src);
+  };
+  auto put_a = [&](const f32x4& x, int slot) {
+    *reinterpret_cast<f32x4*>(sa + slot * kA + a_dst) = x;
+  };
+  auto issue_b = [&](int bc, unsigned mask, int slot) {
+    const float* bsrc = B + ((size_t)bc * 32 + b_row) * ldb + b_col;
+    float* dst = sb + slot * kB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float* src = ((mask >> (b_row + 2 * i)) & 1u) ? bsrc + (size_t)(2 * i) * ldb : zsrc;
+      __builtin_amdgcn_global_load_lds((gbl_void_t)src,
+                                       (lds_void_t)(dst + 128 * (8 * wv + 2 * i)), 16, 0, 0);
+    }
+  };
+  // Column mask of the A block in `slot`, from the whole block: lane l reads
+  // stage positions l + 64 i (row l/8 + 8 i, physical chunk l % 8). Through
+  // inline asm: hipcc cannot tell the stage from the B copies' DMA targets
+  // and would put a vmcnt(0) on these reads.
+  const unsigned a_lds = (unsigned)reinterpret_cast<uintptr_t>(sa) + 16u * (unsigned)lane;
+  auto mask_of = [&](int slot) -> unsigned {
+    f32x4 x0, x1, x2, x3;
+    const unsigned addr = a_lds + 4096u * (unsigned)slot;
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %4 offset:1024\n\t"
+        "ds_read_b128 %2, %4 offset:2048\n\t"
+        "ds_read_b128 %3, %4 offset:3072\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)  // early clobber: the address
+        : "v"(addr)                                    // must outlive the first read
+        : "memory");
+    const f32x4 xs[4] = {x0, x1, x2, x3};
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lc = (lane & 7) ^ (((lane >> 4) + 4 * i) & 7);
+      const int nib = (xs[i][0] != 0.f) | ((xs[i][1] != 0.f) << 1) | ((xs[i][2] != 0.f) << 2) |
+                      ((xs[i][3] != 0.f) << 3);
+      m |= nib << (4 * lc);
+    }
+    return (unsigned)or_wave(m);
+  };
+
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  ColCursor cc(colind, k0, k1, lane);
+
+  // Prologue: A(k0 .. k0+2) into registers, A(k0) into stage 0, its mask,
+  // B(k0), then A(k0+3) into the registers A(k0) left.
+  ra[0] = load_a(k0);
+  ra[1] = load_a(k0 + 1);
+  ra[2] = load_a(k0 + 2);
+  put_a(ra[0], 0);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(63));
+  __builtin_amdgcn_s_barrier();
+  unsigned mk = mask_of(0);
+  issue_b(cc.get(k0), mk, 0);
+  ra[0] = load_a(k0 + 3);
+
+  // Block k uses A / B stage (k - k0) & 1; its A came from register set
+  // (k - k0) % 3. The loop runs in rounds of 3 blocks with no exit inside
+  // (an exit merging back into the loop head makes hipcc drain the register
+  // ring there); the remainder runs after it.
+  auto step = [&](auto U, int k) {
+    constexpr int u = decltype(U)::value;  // (k - k0) % 3
+    const int sl = (k - k0) & 1;
+    // B(k) landed (only A(k+3)'s load may be younger), MFMA(k-1) retired.
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(1));
+    __builtin_amdgcn_s_barrier();
+    put_a(ra[(u + 1) % 3], sl ^ 1);                       // A(k+1)
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(63));
+    __builtin_amdgcn_s_barrier();
+    const unsigned m1 = mask_of(sl ^ 1);
+    issue_b(cc.get(min(k + 1, k1 - 1)), m1, sl ^ 1);      // B(k+1)
+    ra[(u + 1) % 3] = load_a(k + 4);                      // A(k+4)
+    const unsigned pm = (mk | (mk >> 16)) & 0xffffu;
+    const float* stA = sa + sl * kA;
+    const float* stB = sb + sl * kB + (16 * h) * 128 + 32 * wv + r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if ((pm >> (4 * q)) & 0xfu) {
+        const int pc = (4 * h + q) ^ ((r >> 1) & 7);
+        const f32x4 x = *reinterpret_cast<const f32x4*>(stA + r * 32 + 4 * pc);
+        float fb[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) fb[s] = stB[(4 * q + s) * 128];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if ((pm >> (4 * q + s)) & 1u)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s], fb[s], acc, 0, 0, 0);
+      }
+    }
+    mk = m1;
+  };
+  const int kfull = k0 + (k1 - k0) / 3 * 3;
+  for (int kb = k0; kb < kfull; kb += 3) {
+    step(std::integral_constant<int, 0>{}, kb);
+    step(std::integral_constant<int, 1>{}, kb + 1);
+    step(std::integral_constant<int, 2>{}, kb + 2);
+  }
+  if (kfull < k1) step(std::integral_constant<int, 0>{}, kfull);
+  if (kfull + 1 < k1) step(std::integral_constant<int, 1>{}, kfull + 1);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // drain the clamped tail copies
+
+  if constexpr (!CROW) {
+    constexpr int kTs = 36;  // floats per tile column (32 rows, 16-B aligned)
+    float* tile = smem;
+    __syncthreads();  // every wave is past its last read of the stages
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(tile + (32 * wv + r) * kTs + 8 * g + 4 * h) =
+          f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+    __syncthreads();
+    const size_t row = (size_t)br * 32 + r;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int jl = 2 * (4 * it + wv) + h;  // local column
+      if (jt + jl < n) {
+        float* p = C + (size_t)(jt + jl) * ldc + row;
+        *p = epi(tile[jl * kTs + r], alpha, beta, p);
+      }
+    }
+    return;
+  }
+  const int jcol = jt + 32 * wv + r;
+  if (jcol >= n) return;
+  const size_t row0 = (size_t)br * 32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = row0 + 8 * g + 4 * h + e;
+      float* p = C + row * ldc + jcol;
       *p = epi(acc[4 * g + e], alpha, beta, p);
     }
   }
@@ -1434,7 +1628,8 @@ constexpr int kBsr32Default = 40;
 // B stages D, A stages DA; (2, 5) fits 3 workgroups per CU and is the
 // fastest measured (reddit stand-in 2.65 ms vs 4.57 for 4124; products bs = 32
 // 4.62 vs 8.51; (3, 6) 3.08 / 5.60; (4, 8) 4.87 / 9.09).
-constexpr int kBsr32LdsDefault = 4225;
+constexpr int kBsr32LdsDefault = 4402;  // CM4 (4 workgroups per CU): products
+                                         // 4.39 vs 4.58 ms for 4225, reddit equal
 // Blocks known to be dense (the hybrid's BSR part, MFMA-pipe bound): the
 // full-panel kernel with D = 2 (40 KB, 4 workgroups per CU) and the chunked
 // XCD order. Products stand-in hybrid part 1.71 vs 1.87 ms for D = 3 (4124),
@@ -1551,6 +1746,12 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       // diagnostics: 602x = D 2, DA 5 with DIAG x (1 no MFMA, 2 no B, 4 A from k0)
       CM(6022, 2, 5, 2) CM(6024, 2, 5, 4) CM(6026, 2, 5, 6) CM(6027, 2, 5, 7)
 #undef CM
+      case 4402:  // CM4: 4 workgroups per CU (bsr32_f32_cm4_kernel)
+        if (crow) hipLaunchKernelGGL((bsr32_f32_cm4_kernel<true, 32>), grid, dim3(256), 0, ctx->stream,
+                                     mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+        else hipLaunchKernelGGL((bsr32_f32_cm4_kernel<false, 32>), grid, dim3(256), 0, ctx->stream,
+                                mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+        break;
       default: timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE;
     }
 #undef L
@@ -1572,7 +1773,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
              aligned(val, 16) && aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
     // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
-    const int lv = var < 0 || (var % 1000) / 100 == 2 ? kBsr16LdsDefault : var;
+    const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 ? kBsr16LdsDefault : var;
 #define L(D)                                                                                     \
   if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<float, true, D>), grid, dim3(256), 0, ctx->stream, \
                                mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);         \
@@ -1675,7 +1876,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
     // K > 256: one workgroup per 512 columns (A read once per 512)
-    const int lv = var < 0 || (var % 1000) / 100 == 2
+    const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44
                        ? (n > 256 ? kBsr16F16LdsWide : kBsr16F16LdsDefault)
                        : var;
 #define L(D)                                                                                      \
