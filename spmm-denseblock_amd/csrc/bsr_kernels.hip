@@ -771,8 +771,14 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm4_kernel(
   auto step = [&](auto U, int k) {
     constexpr int u = decltype(U)::value;  // (k - k0) % 3
     const int sl = (k - k0) & 1;
-    // B(k) landed (only A(k+3)'s load may be younger), MFMA(k-1) retired.
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(1));
+    // B(k) landed, MFMA(k-1) retired. vmcnt(0), not vmcnt(1) for the one
+    // younger A(k+3) load: a VGPR load and the LDS-DMA copies issued before it
+    // do not retire in order. The A load can retire first, and vmcnt(1) then
+    // passes with one B row still in flight. Measured on the reddit stand-in:
+    // one or two rows per run lost a term a_rc * B[c] in the waves that read
+    // the stage early (tools/diag_bsr_race.py). A(k+3) was issued right after
+    // B(k), so this wait is about as long.
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
     __builtin_amdgcn_s_barrier();
     put_a(ra[(u + 1) % 3], sl ^ 1);                       // A(k+1)
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(63));
