@@ -629,7 +629,8 @@ def main() -> None:
     ap.add_argument("--no-exchange-probe", action="store_true",
                     help="weak scaling: skip timing the C all-gather after the step loop")
     ap.add_argument("--hybrid-options", type=int, default=None,
-                    help="SPMM_HYBRID_* flags (0 = library default, 1 = force fused, 2 = force two launches)")
+                    help="SPMM_HYBRID_* flags (0 = library default, 1 = force fused, 2 = force two launches, "
+                         "+4 = split-bf16 products in the dense-block part)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (DESIGN.md §7)")

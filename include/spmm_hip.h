@@ -326,6 +326,10 @@ spmm_status_t spmm_dbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_opera
  * one form. */
 #define SPMM_HYBRID_FUSED 1
 #define SPMM_HYBRID_TWO_LAUNCH 2
+/* Opt-in: the bs = 32 dense-block part computes each fp32 product as six
+ * bf16 MFMA products of an exact three-way bf16 split of A and B (dropped
+ * terms < 2^-21 |a||b| per product; accumulation in fp32). DESIGN.md §4a. */
+#define SPMM_HYBRID_SPLIT_BF16 4
 spmm_status_t spmm_set_hybrid_options(spmm_handle_t handle, int flags);
 
 /* C(m x n) = alpha * (A_bsr + A_csr) * B(k x n) + beta * C, row-major B and C.

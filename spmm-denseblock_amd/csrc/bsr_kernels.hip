@@ -338,8 +338,37 @@ __device__ __forceinline__ int xcd_block_row(int b, int mb, int xm) {
   return b;
 }
 
+// Split-bf16 products (SPLIT, opt-in: SPMM_HYBRID_SPLIT_BF16). Truncating an
+// fp32 x to its top 8 significant bits three times splits it exactly,
+// x = hi + mid + lo, each a bf16 (|mid| < 2^-7 |x|, |lo| < 2^-15 |x|). Of the
+// nine cross products the six above 2^-22 |a||b| run on
+// v_mfma_f32_32x32x16_bf16 (16x the fp32 MFMA rate per clock); the three
+// dropped ones are below 2^-21 |a||b| together. Per k = 16: 6 bf16 MFMAs of
+// 32 cycles in place of 8 fp32 ones of 64.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split3_bf16(const float* x, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+  u32x4 h, m, l;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const unsigned x0 = __float_as_uint(x[2 * p]), x1 = __float_as_uint(x[2 * p + 1]);
+    const float r0 = x[2 * p] - __uint_as_float(x0 & 0xffff0000u);
+    const float r1 = x[2 * p + 1] - __uint_as_float(x1 & 0xffff0000u);
+    const unsigned q0 = __float_as_uint(r0), q1 = __float_as_uint(r1);
+    const float l0 = r0 - __uint_as_float(q0 & 0xffff0000u);
+    const float l1 = r1 - __uint_as_float(q1 & 0xffff0000u);
+    // upper halves of (elem 2p, elem 2p+1) -> one packed bf16 pair, low k first
+    h[p] = __builtin_amdgcn_perm(x1, x0, 0x07060302u);
+    m[p] = __builtin_amdgcn_perm(q1, q0, 0x07060302u);
+    l[p] = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
+  }
+  hi = __builtin_bit_cast(bf16x8, h);
+  mid = __builtin_bit_cast(bf16x8, m);
+  lo = __builtin_bit_cast(bf16x8, l);
+}
+
 // HB: remainder gathers in flight per wave in the fused hybrid (HYB).
-template <bool CROW, int D, int XM, bool HYB = false, int HB = 24>
+template <bool CROW, int D, int XM, bool HYB = false, int HB = 24, bool SPLIT = false>
 __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -414,9 +443,25 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
     const float* bs_ = stage + 1024 + (16 * h) * 128 + 32 * wv + r;
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) fb[s2] = bs_[s2 * 128];
+    if constexpr (SPLIT) {
+      // lane (r, h) element i of MFMA j is k = 16h + 8j + i, for A and B alike
 #pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2], fb[s2], acc, 0, 0, 0);
+      for (int j = 0; j < 2; ++j) {
+        bf16x8 ah, am, al, bh, bm, bl;
+        split3_bf16(fa + 8 * j, ah, am, al);
+        split3_bf16(fb + 8 * j, bh, bm, bl);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s2], fb[s2], acc, 0, 0, 0);
+    }
     st = st == D - 1 ? 0 : st + 1;
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // drain the clamped tail copies
@@ -1717,9 +1762,9 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // be dense (the hybrid's BSR part) take the full-panel kernel: with most
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
-    const int lv = var < 0 || (var % 1000) / 100 >= 6
-                       ? (dense_blocks ? kBsr32LdsDense : kBsr32LdsDefault)
-                       : var;
+    int lv = var < 0 || (var % 1000) / 100 >= 6
+                 ? (dense_blocks ? kBsr32LdsDense : kBsr32LdsDefault)
+                 : var;
 #define L(D, X)                                                                                   \
   if (crow) hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, D, X>), grid, dim3(256), 0, ctx->stream,  \
                                mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, nullptr,  \
@@ -1727,7 +1772,16 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   else hipLaunchKernelGGL((bsr32_f32_lds_kernel<false, D, X>), grid, dim3(256), 0, ctx->stream,      \
                           mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, nullptr,       \
                           nullptr, nullptr, 0);
+    if (dense_blocks && var < 0 && (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16)) lv = 4926;
     switch (lv) {
+      case 4926:  // kBsr32LdsDense with split-bf16 products (SPMM_HYBRID_SPLIT_BF16)
+        if (crow) hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, false, 24, true>), grid,
+                                     dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,
+                                     alpha, beta, C, ldc, nullptr, nullptr, nullptr, 0);
+        else hipLaunchKernelGGL((bsr32_f32_lds_kernel<false, 2, 32, false, 24, true>), grid,
+                                dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,
+                                alpha, beta, C, ldc, nullptr, nullptr, nullptr, 0);
+        break;
       case 4098: L(2, 0) break;
       case 4099: L(3, 0) break;
       case 4100: L(4, 0) break;
@@ -1853,6 +1907,9 @@ spmm_status_t launch_hybrid32_fused(spmm_context* ctx, int m, int n, float alpha
                        ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
   else if (var == 4128)
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 16>), grid, dim3(256), 0,
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+  else if (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16)
+    hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 24, true>), grid, dim3(256), 0,
                        ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
   else  // D = 2 and 24 remainder gathers in flight (73 VGPRs): 4 workgroups per CU.
         // Products stand-in 2.09 ms vs 2.42 with 32 in flight and 2.81 with D = 3.

@@ -198,7 +198,7 @@ spmm_status_t spmm_set_csr_options(spmm_handle_t h, int flags) {
 
 spmm_status_t spmm_set_hybrid_options(spmm_handle_t h, int flags) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
-  if ((flags & ~(SPMM_HYBRID_FUSED | SPMM_HYBRID_TWO_LAUNCH)) ||
+  if ((flags & ~(SPMM_HYBRID_FUSED | SPMM_HYBRID_TWO_LAUNCH | SPMM_HYBRID_SPLIT_BF16)) ||
       (flags & SPMM_HYBRID_FUSED && flags & SPMM_HYBRID_TWO_LAUNCH))
     return SPMM_STATUS_INVALID_VALUE;
   h->hybrid_flags = flags;

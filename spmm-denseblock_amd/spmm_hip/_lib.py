@@ -33,6 +33,7 @@ CSR_NT_STREAMS = 1
 CSR_SEQUENTIAL_ROWS = 2
 HYBRID_FUSED = 1
 HYBRID_TWO_LAUNCH = 2
+HYBRID_SPLIT_BF16 = 4
 
 
 class SpmmError(RuntimeError):

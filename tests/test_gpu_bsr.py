@@ -231,6 +231,44 @@ def test_hybrid_fused_vs_two_launch(oracle, device, n, K, alpha, beta):
     np.testing.assert_allclose(fused[n:], two[n:], rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("form", ["fused", "two_launch"])
+@pytest.mark.parametrize("n,K", [(1000, 128), (963, 132)])
+def test_hybrid_split_bf16(oracle, device, form, n, K):
+    """SPMM_HYBRID_SPLIT_BF16: the dense-block part's fp32 products as six bf16
+    MFMA products of an exact three-way split. Held to the fp32 bar element by
+    element (|err| <= 1e-5 |A||B|) on values spread over six decades, and
+    within 2^-18 |A||B| of the fp32-MFMA form."""
+    from spmm_hip import prep
+    from spmm_hip._lib import HYBRID_FUSED, HYBRID_SPLIT_BF16, HYBRID_TWO_LAUNCH
+    rp, ci = prep.community_csr(n, 40.0, 48, 160, 0.95, 11)
+    rng = np.random.default_rng(12)
+    v = (rng.uniform(-1, 1, ci.size) * 10.0 ** rng.uniform(-3, 3, ci.size)).astype(np.float32)
+    parts = prep.divide(n, rp, ci, v, 32, 0.05)
+    assert parts[4].size > 0 and parts[1].size > 0
+    nb = (n + 31) // 32
+    Bp = np.zeros((nb * 32, K), np.float32)
+    Bp[:n] = rng.uniform(-1, 1, (n, K)) * 10.0 ** rng.uniform(-3, 3, (n, K))
+    d = _dev(*parts, Bp)
+    ops = _ops()
+    base = HYBRID_FUSED if form == "fused" else HYBRID_TWO_LAUNCH
+    outs = []
+    for flags in (base | HYBRID_SPLIT_BF16, base):
+        h = ops.Handle()
+        h.set_hybrid_options(flags)
+        C = torch.empty((nb * 32, K), device=device)
+        ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), d[6], m=n, n=K, k=n, bs=32, ldb=K, C=C,
+                         ldc=K, handle=h)
+        torch.cuda.synchronize()
+        outs.append(C.cpu().numpy()[:n].astype(np.float64))
+        h.close()
+    split, plain = outs
+    ref, absd = oracle_csrmm_f64(oracle, n, K, rp, ci, v, Bp, K, 0)
+    err = np.abs(split - ref)
+    assert np.all(err <= TOL_F32 * absd + 1e-30), \
+        f"split-bf16 {form}: max err / |A||B| {np.max(err / (absd + 1e-30)):.3g}"
+    assert np.all(np.abs(split - plain) <= 2.0 ** -18 * absd + 1e-30)
+
+
 def test_bsr_status_codes(device):
     """rocsparse_bsrmm.h:109-176 argument checks."""
     from spmm_hip._lib import (INVALID_VALUE, MATRIX_TYPE_NOT_SUPPORTED, NOT_INITIALIZED,
