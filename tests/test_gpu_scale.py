@@ -59,10 +59,16 @@ def test_reddit_scale_bsr32_and_hybrid_vs_csr(device):
     del brp, bci, bval
     parts = prep.divide(n, rp, ci, v, bs, prep.hybrid_plan(rp, ci, bs, K)["density"])
     d = _dev(*parts)
-    Ch = torch.empty((mb * bs, K), device=device)
-    ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=Ch, ldc=K)
-    torch.cuda.synchronize()
-    _within(Ch[:n], Cc, absd, 2 * TOL_F32, "reddit hybrid vs CSR")
+    from spmm_hip._lib import HYBRID_SPLIT_BF16
+    for flags in (0, HYBRID_SPLIT_BF16, 0, HYBRID_SPLIT_BF16):
+        h = ops.Handle()
+        h.set_hybrid_options(flags)
+        Ch = torch.empty((mb * bs, K), device=device)
+        ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=Ch,
+                         ldc=K, handle=h)
+        torch.cuda.synchronize()
+        _within(Ch[:n], Cc, absd, 2 * TOL_F32, f"reddit hybrid (flags {flags}) vs CSR")
+        h.close()
 
 
 def test_products_scale_bsr16_f16_vs_csr(device):
