@@ -1,0 +1,91 @@
+"""Run-to-run determinism of the shipped kernels at BASELINE sizes: every
+default path is written to be deterministic (no float atomics; fixed
+reduction orders), so repeated runs on the same inputs must agree bit for
+bit. A difference points at a copy/compute race like the one the CM4 kernel
+had. GPU box only; diagnostic, not a test.
+
+usage: python tools/determinism.py [reps]
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "spmm-denseblock_amd"))
+from spmm_hip import ops, prep  # noqa: E402
+
+
+def check(tag, run, reps):
+    first = run().clone()
+    torch.cuda.synchronize()
+    diffs = []
+    for _ in range(reps):
+        out = run()
+        torch.cuda.synchronize()
+        diffs.append(int((out != first).sum()))
+    print(f"{tag}: differing elements per rerun {diffs}", flush=True)
+    return sum(diffs)
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+    dev = torch.device("cuda:0")
+    bad = 0
+    # products stand-in (community order): CSR K=128, bs 32 CM4, bs 16 fp16
+    # K=512, hybrid fused (plain and split-bf16), device csr2bsr
+    n = 2449029
+    rp, ci = prep.community_csr(n, 27.0, 32, 512, 0.97, 1234)
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
+    drp, dci, dv = [torch.from_numpy(a).to(dev) for a in (rp, ci, v)]
+    torch.manual_seed(0)
+    for bs, K in ((32, 128), (16, 512)):
+        mb = (n + bs - 1) // bs
+        B = torch.rand((mb * bs, K), device=dev) * 2 - 1
+        if bs == 32:
+            Bn = B[:n].contiguous()
+            bad += check("csr K=128", lambda: ops.gespmm_csrmm(drp, dci, dv, Bn), reps)
+            del Bn
+        bad += check(f"csr2bsr bs={bs} (values)",
+                     lambda: ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)[2], 2)
+        brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
+        C = torch.empty((mb * bs, K), device=dev)
+        if bs == 32:
+            def run():
+                ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K)
+                return C
+            bad += check("bsr32 fp32 K=128 (CM4)", run, reps)
+        else:
+            bv16, B16 = bval.half(), B.half()
+            del bval, B
+
+            def run():
+                ops.bsrmm_f16(brp, bci, bv16, B16, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K)
+                return C
+            bad += check("bsr16 fp16 K=512 (CM)", run, reps)
+            del bv16, B16
+        del brp, bci, C
+        torch.cuda.empty_cache()
+    from spmm_hip._lib import HYBRID_SPLIT_BF16
+    K, bs = 128, 32
+    mb = (n + bs - 1) // bs
+    B = torch.rand((mb * bs, K), device=dev) * 2 - 1
+    parts = prep.divide(n, rp, ci, v, bs, prep.hybrid_plan(rp, ci, bs, K)["density"])
+    d = [torch.from_numpy(a).to(dev) for a in parts]
+    C = torch.empty((mb * bs, K), device=dev)
+    for flags in (0, HYBRID_SPLIT_BF16):
+        h = ops.Handle()
+        h.set_hybrid_options(flags)
+
+        def run():
+            ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=C,
+                             ldc=K, handle=h)
+            return C
+        bad += check(f"hybrid fused flags={flags}", run, reps)
+        h.close()
+    print(f"total differing elements: {bad}", flush=True)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
