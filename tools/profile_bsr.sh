@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd); export TMPDIR=/tmp
 WL=${WL:-reddit_bsr32}
-O=$R/gpurun_out/prof_$WL
+O=$R/gpurun_out/prof_$WL${TAG:-}
 mkdir -p $O
 (cd /tmp && timeout -k 10 120 rocprofv3 -L) > $O/counters_list.txt 2>&1 || true
 have() { grep -qw "$1" $O/counters_list.txt; }
