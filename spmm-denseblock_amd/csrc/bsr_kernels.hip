@@ -240,8 +240,9 @@ constexpr int waitcnt_vm_lgkm0(int n) { return (n & 15) | (7 << 4) | ((n >> 4) <
 // phases on the same CU.
 constexpr int kHybTs = 136;  // tile row stride (floats): the two half-waves' rows
                              // land 32 banks apart when the tile is written
-template <int D, int kHybBatch>
-__device__ __forceinline__ void hyb_remainder(float* smem, const f32x16& acc, int br, int jt,
+template <int D, int kHybBatch, bool PAIR = false>
+__device__ __forceinline__ void hyb_remainder(float* smem, const f32x16& acc, const f32x16& acc1,
+                                              int br, int jt,
                                               int n, const int* __restrict__ rrp,
                                               const int* __restrict__ rci,
                                               const float* __restrict__ rv, int m,
@@ -251,10 +252,32 @@ __device__ __forceinline__ void hyb_remainder(float* smem, const f32x16& acc, in
   const int wv = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
   __syncthreads();  // every wave is done with the stages (copies drained before)
+  if constexpr (!PAIR) {
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < 4; ++g)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) smem[(8 * g + 4 * h + e) * kHybTs + 32 * wv + r] = acc[4 * g + e];
+      for (int e = 0; e < 4; ++e) smem[(8 * g + 4 * h + e) * kHybTs + 32 * wv + r] = acc[4 * g + e];
+  } else {
+    // wave pair (2c, 2c+1) holds the two k halves of columns 64c .. 64c+63
+    const int kh = wv & 1, c0 = 64 * (wv >> 1) + r;
+    if (kh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          smem[(8 * g + 4 * h + e) * kHybTs + c0] = acc[4 * g + e];
+          smem[(8 * g + 4 * h + e) * kHybTs + c0 + 32] = acc1[4 * g + e];
+        }
+    __syncthreads();
+    if (!kh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          smem[(8 * g + 4 * h + e) * kHybTs + c0] += acc[4 * g + e];
+          smem[(8 * g + 4 * h + e) * kHybTs + c0 + 32] += acc1[4 * g + e];
+        }
+  }
   __syncthreads();
 
   const int R0 = br * 32;
@@ -368,7 +391,12 @@ __device__ __forceinline__ void split3_bf16(const float* x, bf16x8& hi, bf16x8& 
 }
 
 // HB: remainder gathers in flight per wave in the fused hybrid (HYB).
-template <bool CROW, int D, int XM, bool HYB = false, int HB = 24, bool SPLIT = false>
+// PAIR (with SPLIT, row-major C): split-K over wave pairs. Wave w takes k half
+// w & 1 of every block for 64 output columns (two tiles), so it splits 8 A
+// values per lane per block instead of 16; the pair's partial tiles are added
+// through LDS once per block row.
+template <bool CROW, int D, int XM, bool HYB = false, int HB = 24, bool SPLIT = false,
+          bool PAIR = false>
 __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -415,10 +443,11 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
                                        0, 0);
   };
 
+  static_assert(!PAIR || (SPLIT && CROW), "PAIR needs SPLIT and row-major C");
   const int r = lane & 31, h = lane >> 5;
-  f32x16 acc;
+  f32x16 acc, acc1;
 #pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  for (int e = 0; e < 16; ++e) acc[e] = acc1[e] = 0.f;
   // Block columns through the readlane cursor: no load per block (a scalar
   // load per block sat right before the copies it feeds), one refill per 64.
   if (!HYB || k0 < k1) {
@@ -432,6 +461,41 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
     __builtin_amdgcn_s_barrier();
     issue(k + D - 1, cc.get(min(k + D - 1, k1 - 1)), st == 0 ? D - 1 : st - 1);
     const float* stage = smem + st * kStage;
+    if constexpr (PAIR) {
+      // lane (r, h) element i: k = 16 kh + 8h + i; tiles t = 0, 1 at columns 64 ch + 32 t
+      const int kh = wv & 1, ch = wv >> 1;
+      float fa8[8], fb0[8], fb1[8];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int pc = (4 * kh + 2 * h + q) ^ ((r >> 1) & 7);
+        const f32x4 x = *reinterpret_cast<const f32x4*>(stage + r * 32 + 4 * pc);
+        fa8[4 * q] = x[0]; fa8[4 * q + 1] = x[1]; fa8[4 * q + 2] = x[2]; fa8[4 * q + 3] = x[3];
+      }
+      const float* bp = stage + 1024 + (16 * kh + 8 * h) * 128 + 64 * ch + r;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        fb0[i] = bp[i * 128];
+        fb1[i] = bp[i * 128 + 32];
+      }
+      bf16x8 ah, am, al, bh, bm, bl;
+      split3_bf16(fa8, ah, am, al);
+      split3_bf16(fb0, bh, bm, bl);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+      split3_bf16(fb1, bh, bm, bl);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc1, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc1, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc1, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc1, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc1, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc1, 0, 0, 0);
+      st = st == D - 1 ? 0 : st + 1;
+      continue;
+    }
     // A fragment: row r, logical chunks 4h .. 4h+3 (k = 16h + s).
     float fa[16], fb[16];
 #pragma unroll
@@ -468,7 +532,36 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
   }
 
   if constexpr (HYB) {
-    hyb_remainder<D, HB>(smem, acc, br, jt, n, rrp, rci, rv, m, B, ldb, alpha, beta, C, ldc);
+    hyb_remainder<D, HB, PAIR>(smem, acc, acc1, br, jt, n, rrp, rci, rv, m, B, ldb, alpha, beta,
+                               C, ldc);
+    return;
+  }
+  if constexpr (PAIR) {
+    const int kh = wv & 1, c0 = 64 * (wv >> 1) + r;
+    __syncthreads();  // every wave is done with the stages (copies drained above)
+    if (kh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          smem[(8 * g + 4 * h + e) * kHybTs + c0] = acc[4 * g + e];
+          smem[(8 * g + 4 * h + e) * kHybTs + c0 + 32] = acc1[4 * g + e];
+        }
+    __syncthreads();
+    if (kh) return;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int jc = jt + c0 + 32 * t;
+      if (jc >= n) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int lr = 8 * g + 4 * h + e;
+          float* p = C + ((size_t)br * 32 + lr) * ldc + jc;
+          *p = epi((t ? acc1 : acc)[4 * g + e] + smem[lr * kHybTs + c0 + 32 * t], alpha, beta, p);
+        }
+    }
     return;
   }
   const int jcol = jt + 32 * wv + r;
@@ -1762,7 +1855,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // be dense (the hybrid's BSR part) take the full-panel kernel: with most
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
-    int lv = var < 0 || (var % 1000) / 100 >= 6
+    int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8)
                  ? (dense_blocks ? kBsr32LdsDense : kBsr32LdsDefault)
                  : var;
 #define L(D, X)                                                                                   \
@@ -1772,7 +1865,10 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   else hipLaunchKernelGGL((bsr32_f32_lds_kernel<false, D, X>), grid, dim3(256), 0, ctx->stream,      \
                           mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, nullptr,       \
                           nullptr, nullptr, 0);
-    if (dense_blocks && var < 0 && (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16)) lv = 4926;
+    // split-bf16 (opt-in): wave-pair split-K form for row-major C (products
+    // hybrid 1.83 vs 1.87 ms fused, reddit 0.79 vs 0.82), else one k range per wave
+    if (dense_blocks && var < 0 && (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16))
+      lv = crow ? 4927 : 4926;
     switch (lv) {
       case 4926:  // kBsr32LdsDense with split-bf16 products (SPMM_HYBRID_SPLIT_BF16)
         if (crow) hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, false, 24, true>), grid,
@@ -1781,6 +1877,12 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
         else hipLaunchKernelGGL((bsr32_f32_lds_kernel<false, 2, 32, false, 24, true>), grid,
                                 dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,
                                 alpha, beta, C, ldc, nullptr, nullptr, nullptr, 0);
+        break;
+      case 4927:  // 4926 with split-K over wave pairs (PAIR)
+        if (!crow) { timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE; }
+        hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, false, 24, true, true>), grid,
+                           dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha,
+                           beta, C, ldc, nullptr, nullptr, nullptr, 0);
         break;
       case 4098: L(2, 0) break;
       case 4099: L(3, 0) break;
@@ -1908,8 +2010,11 @@ spmm_status_t launch_hybrid32_fused(spmm_context* ctx, int m, int n, float alpha
   else if (var == 4128)
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 16>), grid, dim3(256), 0,
                        ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
-  else if (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16)
+  else if (var == 4926)  // split-bf16, one k range per wave
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 24, true>), grid, dim3(256), 0,
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+  else if (var == 4927 || (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16))  // wave-pair split-K
+    hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 24, true, true>), grid, dim3(256), 0,
                        ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
   else  // D = 2 and 24 remainder gathers in flight (73 VGPRs): 4 workgroups per CU.
         // Products stand-in 2.09 ms vs 2.42 with 32 in flight and 2.81 with D = 3.
