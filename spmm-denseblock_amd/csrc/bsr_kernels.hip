@@ -839,8 +839,18 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm4_kernel(
   const int b_row = 8 * wv + (lane >> 5);
   const float* zsrc = g_zero_row + 4 * (lane & 31);
   f32x4 ra[3];  // A of blocks j = k + 1 .. k + 3 (register set (j - k0) % 3)
+  // The A load must be the one vector-memory operation younger than the B
+  // copies before it (the counted wait below keeps exactly one in flight).
+  // The empty asm on its address is ordered after those copies (both have
+  // side effects for the compiler), so the load cannot be hoisted above them;
+  // the keep-alive after the loop stops hipcc from deleting the tail steps'
+  // loads, whose values nothing reads (that deletion was the copy race, see
+  // the wait in step()).
+  typedef const __attribute__((address_space(1))) f32x4* gf32x4_ptr;  // a global load, not flat
   auto load_a = [&](int j) -> f32x4 {
-    return *reinterpret_cast<const f32x4*>(val + (size_t)min(j, k1 - 1) * 1024 + a_src);
+    gf32x4_ptr p = (gf32x4_ptr)(val + (size_t)min(j, k1 - 1) * 1024 + a_src);
+    asm volatile("" : "+v"(p));
+    return *p;
   };
   auto put_a = [&](const f32x4& x, int slot) {
     *reinterpret_cast<f32x4*>(sa + slot * kA + a_dst) = x;
@@ -909,14 +919,17 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm4_kernel(
   auto step = [&](auto U, int k) {
     constexpr int u = decltype(U)::value;  // (k - k0) % 3
     const int sl = (k - k0) & 1;
-    // B(k) landed, MFMA(k-1) retired. vmcnt(0), not vmcnt(1) for the one
-    // younger A(k+3) load: a VGPR load and the LDS-DMA copies issued before it
-    // do not retire in order. The A load can retire first, and vmcnt(1) then
-    // passes with one B row still in flight. Measured on the reddit stand-in:
-    // one or two rows per run lost a term a_rc * B[c] in the waves that read
-    // the stage early (tools/diag_bsr_race.py). A(k+3) was issued right after
-    // B(k), so this wait is about as long.
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
+    // B(k) landed, MFMA(k-1) retired: every operation but the youngest, the
+    // A(k+3) load issued right after the B(k) copies, is complete.
+    // History: this wait was vmcnt(1) from the start, but
+    // hipcc deleted the A loads of the two tail steps (their values are
+    // never read), so in the second tail step the one operation the wait left
+    // in flight was the last B copy of the row's last block, and the waves
+    // reading it early lost one term a_rc * B[c] (block rows with
+    // (k1 - k0) % 3 == 2). load_a pins the load in place and the keep-alive
+    // after the loop keeps it; tests/test_isa_waits.py checks the emitted
+    // window of every such wait.
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(1));
     __builtin_amdgcn_s_barrier();
     put_a(ra[(u + 1) % 3], sl ^ 1);                       // A(k+1)
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(63));
@@ -952,6 +965,7 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm4_kernel(
   if (kfull < k1) step(std::integral_constant<int, 0>{}, kfull);
   if (kfull + 1 < k1) step(std::integral_constant<int, 1>{}, kfull + 1);
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // drain the clamped tail copies
+  asm volatile("" ::"v"(ra[0]), "v"(ra[1]), "v"(ra[2]));  // keep every A load
 
   if constexpr (!CROW) {
     constexpr int kTs = 36;  // floats per tile column (32 rows, 16-B aligned)
@@ -1003,9 +1017,41 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm4_kernel(
 // B panel rows are 16-byte-chunk XOR-swizzled (source side and read side) so
 // the reads are bank-conflict-free.
 // ---------------------------------------------------------------------------
-typedef short v4s __attribute__((vector_size(8)));
-typedef __attribute__((address_space(3))) v4s lds_v4s;
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+// N x ds_read_b64_tr_b16 and their lgkmcnt(0) in one asm statement. The
+// builtin (__builtin_amdgcn_ds_read_tr16_b64_v4i16) carries no LDS alias
+// information, so hipcc's waitcnt pass put a vmcnt(0) before it whenever an
+// LDS-DMA copy was in flight: inside the copy loop that drained the copies of
+// the blocks ahead once per block (tools/isa_vmcnt.py, loop_drains). The
+// results exist for the compiler only after the wait, so nothing can use them
+// early. `a[i]` are LDS byte addresses.
+__device__ __forceinline__ void ds_read_tr16_x4(f16x4 (&r)[4], const unsigned (&a)[4]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %4\n\tds_read_b64_tr_b16 %1, %5\n\t"
+      "ds_read_b64_tr_b16 %2, %6\n\tds_read_b64_tr_b16 %3, %7\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void ds_read_tr16_n(f16x4 (&r)[N], const unsigned (&a)[N]) {
+  static_assert(N % 4 == 0, "groups of 4");
+#pragma unroll
+  for (int i = 0; i < N; i += 4) {
+    ds_read_tr16_x4(*reinterpret_cast<f16x4(*)[4]>(&r[i]), *reinterpret_cast<const unsigned(*)[4]>(&a[i]));
+  }
+}
+// One ds_read_b64 and its wait, for an LDS read hipcc would otherwise fence
+// with vmcnt(0) (same reason as above).
+__device__ __forceinline__ f16x4 ds_read_f16x4(unsigned a) {
+  f16x4 r;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)reinterpret_cast<uintptr_t>(p);
+}
 
 template <typename T>
 __device__ __forceinline__ int bsr16_swz(int row) {
@@ -1090,14 +1136,17 @@ __global__ __launch_bounds__(256) void bsr16_lds_kernel(
       const f16x4 fa = *reinterpret_cast<const f16x4*>(stage + c16 * 32 + 8 * g);
       const int q = (lane >> 2) & 3, p = lane & 3;
       const int row = 4 * g + q;
+      unsigned ad[4];
+      f16x4 fb[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int col = 64 * wv + 16 * t + 4 * p;
-        const int off = row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2;
-        const v4s raw = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(bpan + off));
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, __builtin_bit_cast(f16x4, raw),
-                                                       acc[t], 0, 0, 0);
+        ad[t] = lds_addr(bpan + row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2);
       }
+      ds_read_tr16_n(fb, ad);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[t], 0, 0, 0);
     } else {
       // A: row c16, k = 4g + s (s = 0..3) -> one 16-B read.
       const f32x4 fa = *reinterpret_cast<const f32x4*>(stage + c16 * 64 + 16 * g);
@@ -1290,14 +1339,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const f16x4 fa = *reinterpret_cast<const f16x4*>(stage + c16 * 32 + 8 * g);
       const int q = (lane >> 2) & 3, p = lane & 3;
       const int row = 4 * g + q;
+      unsigned ad[kTpw];
+      f16x4 fb[kTpw];
 #pragma unroll
       for (int t = 0; t < kTpw; ++t) {
         const int col = wc + 16 * t + 4 * p;
-        const int off = row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2;
-        const v4s raw = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(bpan + off));
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, __builtin_bit_cast(f16x4, raw),
-                                                       acc[t], 0, 0, 0);
+        ad[t] = lds_addr(bpan + row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2);
       }
+      ds_read_tr16_n(fb, ad);
+#pragma unroll
+      for (int t = 0; t < kTpw; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[t], 0, 0, 0);
     } else {
       const f32x4 fa = *reinterpret_cast<const f32x4*>(stage + c16 * 64 + 16 * g);
 #pragma unroll
@@ -1454,17 +1506,17 @@ __global__ __launch_bounds__(256) void bsr16_f16_pair_kernel(
       const int q4 = (lane >> 2) & 3, p4 = lane & 3;
       const int row = 4 * g + q4;
       f16x4 fb[4];
+      unsigned ad[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int col = 64 * wv + 16 * t + 4 * p4;
-        const int off = row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2;
-        fb[t] = __builtin_bit_cast(
-            f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(bpan + off)));
+        ad[t] = lds_addr(bpan + row * kRowB + (((col >> 3) ^ bsr16_swz<T>(row)) << 4) + (col & 7) * 2);
       }
+      ds_read_tr16_n(fb, ad);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if (!((mask >> q) & 1)) continue;
-        const f16x4 fa = *reinterpret_cast<const f16x4*>(stage + q * 1024 + c16 * 32 + 8 * g);
+        const f16x4 fa = ds_read_f16x4(lds_addr(stage + q * 1024 + c16 * 32 + 8 * g));
 #pragma unroll
         for (int t = 0; t < 4; ++t)
           acc[q][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[q][t], 0, 0, 0);

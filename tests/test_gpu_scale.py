@@ -48,19 +48,18 @@ def test_reddit_scale_bsr32_and_hybrid_vs_csr(device):
     absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B[:n].abs().contiguous())
     brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
     assert int(bci.numel()) > 1_000_000
-    # Repeated: a copy/compute race shows up in some runs only (the CM4
-    # kernel's counted vmcnt once lost one term a_rc * B[c] in ~1 run of 4).
-    for rep in range(8):
-        Cb = torch.empty((mb * bs, K), device=device)
-        ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=Cb, ldc=K)
-        torch.cuda.synchronize()
-        _within(Cb[:n], Cc, absd, 2 * TOL_F32, f"reddit bs32 BSR vs CSR (run {rep})")
-        assert not bool(Cb[n:].any()), "padding rows of C must be zero"
+    # One run: the counted waits of the copy rings are checked on the emitted
+    # code (tests/test_isa_waits.py), not by repetition.
+    Cb = torch.empty((mb * bs, K), device=device)
+    ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=Cb, ldc=K)
+    torch.cuda.synchronize()
+    _within(Cb[:n], Cc, absd, 2 * TOL_F32, "reddit bs32 BSR vs CSR")
+    assert not bool(Cb[n:].any()), "padding rows of C must be zero"
     del brp, bci, bval
     parts = prep.divide(n, rp, ci, v, bs, prep.hybrid_plan(rp, ci, bs, K)["density"])
     d = _dev(*parts)
     from spmm_hip._lib import HYBRID_SPLIT_BF16
-    for flags in (0, HYBRID_SPLIT_BF16, 0, HYBRID_SPLIT_BF16):
+    for flags in (0, HYBRID_SPLIT_BF16):
         h = ops.Handle()
         h.set_hybrid_options(flags)
         Ch = torch.empty((mb * bs, K), device=device)

@@ -1,0 +1,125 @@
+"""The counted vmcnt waits of the LDS-staged BSR kernels, checked on the device
+assembly the shipped object is assembled from ("Counted waits").
+
+A copy ring hands a stage to the other waves with `s_waitcnt vmcnt(N)` +
+`s_barrier`: N counts the vector-memory operations that may stay in flight,
+so it is right only for the instruction stream the compiler emitted. The bs 32
+CM4 kernel once lost B rows because hipcc deleted two dead A prefetches in the
+tail of a block row and the count then covered a B copy; a GPU rerun loop
+caught it about one run in four. These tests read the stream instead:
+
+* every stage hand-off wait keeps in flight only what its kernel plans for
+  (CM4: exactly the one A prefetch load; every other ring: LDS-DMA copies) and
+  retires an LDS-DMA copy as its youngest operation, on every path;
+* no copy loop holds a vmcnt(0) that drains the copies of the blocks ahead in
+  the middle of an iteration (hipcc put one before every fp16 B-fragment read
+  until those reads went through inline asm);
+* the checker flags the pre-fix CM4 tail (a synthetic excerpt of its shape).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "spmm-denseblock_amd")
+ASM = os.path.join(PKG, "build", "bsr_kernels-hip-amdgcn-amd-amdhsa-gfx950.s")
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import isa_vmcnt as iv  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def bsr_asm() -> str:
+    if not os.path.exists(ASM):
+        subprocess.run(["make", "-C", PKG, "lib"], check=True, capture_output=True)
+    with open(ASM) as f:
+        return f.read()
+
+
+def test_every_stage_handoff_wait(bsr_asm):
+    res = iv.audit(bsr_asm)
+    assert len(res) >= 40, f"expected the LDS-staged kernels, found {len(res)}"
+    bad = {k: v for k, v in res.items() if v}
+    assert not bad, "\n".join(f"{k}: {v}" for k, v in bad.items())
+
+
+def test_cm4_keeps_exactly_the_a_prefetch(bsr_asm):
+    funcs = iv.split_functions(bsr_asm)
+    cm4 = [k for k in funcs if "bsr32_f32_cm4_kernel" in k]
+    assert len(cm4) == 2  # row- and column-major C
+    for k in cm4:
+        waits = [r for r in iv.counted_waits(k, funcs[k]) if r["handoff"]]
+        # three unrolled steps + two tail steps
+        assert len(waits) >= 5, waits
+        for r in waits:
+            assert r["n"] == 1 and r["window"][0] == ["load"] and r["window"][1] == ["dma"], r
+
+
+def test_no_copy_loop_drains(bsr_asm):
+    drains = {}
+    for k, body in iv.split_functions(bsr_asm).items():
+        if iv.issues_dma(body) and (d := iv.loop_drains(body)):
+            drains[k] = d
+    assert not drains, drains
+
+
+_PRE_FIX_SHAPE = """\
+_Z10cm4_shapev:
+; %bb.0:
+\tglobal_load_lds_dwordx4 v[0:1], off
+\tglobal_load_lds_dwordx4 v[0:1], off
+\tglobal_load_dwordx4 v[2:5], v[6:7], off
+.LBB0_1:                                ; =>This Inner Loop Header: Depth=1
+\ts_waitcnt vmcnt(1) lgkmcnt(0)
+\ts_barrier
+\tglobal_load_lds_dwordx4 v[0:1], off
+\tglobal_load_lds_dwordx4 v[0:1], off
+\tglobal_load_dwordx4 v[2:5], v[6:7], off
+\ts_cbranch_scc1 .LBB0_1
+; %bb.2:
+\ts_waitcnt vmcnt(1) lgkmcnt(0)
+\ts_barrier
+\tglobal_load_lds_dwordx4 v[0:1], off
+\tglobal_load_lds_dwordx4 v[0:1], off
+{TAIL_LOAD}; %bb.3:
+\ts_waitcnt vmcnt(1) lgkmcnt(0)
+\ts_barrier
+\ts_waitcnt vmcnt(0)
+\ts_endpgm
+.Lfunc_end0:
+"""
+
+
+def test_checker_flags_the_pre_fix_tail():
+    """The loop steps load A after their B copies; the first tail step's A
+    load was deleted, so the second tail step's vmcnt(1) keeps a B copy."""
+    broken = _PRE_FIX_SHAPE.replace("{TAIL_LOAD}", "")
+    fixed = _PRE_FIX_SHAPE.replace("{TAIL_LOAD}", "\tglobal_load_dwordx4 v[2:5], v[6:7], off\n")
+    body = iv.split_functions(broken)["_Z10cm4_shapev"]
+    errs = iv.check_kernel("_Z10cm4_shapev", body, keep="load")
+    assert errs and "keeps [['dma']]" in errs[0], errs
+    body = iv.split_functions(fixed)["_Z10cm4_shapev"]
+    assert iv.check_kernel("_Z10cm4_shapev", body, keep="load") == []
+
+
+def test_checker_flags_a_mid_loop_drain():
+    text = """\
+_Z5drainv:
+.LBB1_1:                                ; =>This Inner Loop Header: Depth=1
+\ts_waitcnt vmcnt(2) lgkmcnt(0)
+\ts_barrier
+\tglobal_load_lds_dwordx4 v[0:1], off
+\tglobal_load_lds_dwordx4 v[0:1], off
+\ts_waitcnt vmcnt(0)
+\tds_read_b64_tr_b16 v[2:3], v4
+\ts_cbranch_scc1 .LBB1_1
+; %bb.2:
+\ts_endpgm
+.Lfunc_end1:
+"""
+    body = iv.split_functions(text)["_Z5drainv"]
+    assert len(iv.loop_drains(body)) == 1

@@ -1,0 +1,282 @@
+"""Counted-vmcnt audit of gfx950 kernel assembly ("counted waits").
+
+The LDS-staged BSR kernels wait for their LDS-DMA copies with a counted
+`s_waitcnt vmcnt(N)` (N > 0: the N youngest vector-memory operations may stay
+in flight) followed by `s_barrier`. The bs 32 CM4 kernel did that with one
+VGPR load (the next A block) younger than the B-panel copies and lost B rows
+on the GPU; with every vector-memory operation of the window an LDS-DMA copy
+the same kind of wait never failed. Its cause: hipcc deleted
+the A loads of the two tail steps of a block row (nothing reads their
+values), so in the second tail step the one operation the wait left in flight
+was a B copy of the row's last block. A counted wait is only as right as the
+instruction stream it counts, so this module checks the stream the compiler
+emitted (check_kernel: what a stage hand-off wait keeps in flight and what it
+retires; loop_drains: vmcnt(0) waits inside a copy loop that drain the
+prefetch). tools/vmcnt_order.hip measured the ordering rule itself on the
+GPU: a younger VGPR load never retired ahead of an older LDS-DMA copy, nor the
+reverse (profiles/r02_vmcnt_order.jsonl).
+
+The checks run per kernel as a forward
+dataflow over the control-flow graph. The state at a point is the sequence
+(youngest first) of the classes of vector-memory operations that may be in
+flight there; at a join the sequences are merged position by position (union
+of classes, longer length), which over-approximates every path. `s_waitcnt
+vmcnt(N)` truncates the state to its first N positions after the check.
+
+Classes: "dma" (global_load_lds_*, buffer_load_* ... lds), "load" (other
+global/buffer/scratch loads, returning atomics), "store" (stores, non-returning
+atomics), "flat" (flat_*).
+
+Usage: python tools/isa_vmcnt.py <kernel.s> [name-fragment ...]
+"""
+from __future__ import annotations
+
+import re
+import sys
+from dataclasses import dataclass, field
+
+_FUNC_START = re.compile(r"^(_Z\S+|[A-Za-z_][\w.$]*):\s*(;.*)?$")
+_LABEL = re.compile(r"^(\.LBB\d+_\d+):")
+_WAIT = re.compile(r"\bvmcnt\((\d+)\)")
+MAX_DEPTH = 64
+
+
+def classify(mn: str, ops: str) -> str | None:
+    """Vector-memory class of one instruction, or None."""
+    if mn.startswith("flat_"):
+        return "flat"
+    if mn.startswith("global_load_lds_") or (mn.startswith("buffer_load_") and re.search(r"\blds\b", ops)):
+        return "dma"
+    if mn.startswith(("global_load_", "buffer_load_", "scratch_load_")):
+        return "load"
+    if mn.startswith(("global_store_", "buffer_store_", "scratch_store_")):
+        return "store"
+    if mn.startswith(("global_atomic_", "buffer_atomic_")):
+        return "load" if re.search(r"\b(glc|sc0)\b", ops) else "store"
+    return None
+
+
+@dataclass
+class Block:
+    label: str
+    insts: list = field(default_factory=list)  # (line_no, mnemonic, operands)
+    succ: list = field(default_factory=list)
+    in_loop: bool = False  # the compiler's loop annotation ("in Loop" / "Loop Header")
+    header: str = ""       # innermost loop header ("BB12_34") of an in-loop block
+
+
+def split_functions(text: str) -> dict[str, list[tuple[int, str]]]:
+    """name -> [(line_no, line)] for every function body in the .s file."""
+    funcs: dict[str, list[tuple[int, str]]] = {}
+    cur = None
+    for no, line in enumerate(text.splitlines(), 1):
+        if cur is None:
+            m = _FUNC_START.match(line)
+            if m and not line.startswith(".") and "@function" not in line:
+                cur = m.group(1)
+                funcs[cur] = []
+            continue
+        if line.startswith(".Lfunc_end"):
+            cur = None
+            continue
+        funcs[cur].append((no, line))
+    return funcs
+
+
+def build_cfg(body: list[tuple[int, str]]) -> list[Block]:
+    blocks = [Block("<entry>")]
+    for no, raw in body:
+        if re.match(r"^; %bb\.\d+:", raw):  # fall-through block without a label
+            blocks.append(Block(raw.split(":")[0][2:]))
+        m = _LABEL.match(raw)
+        if m:
+            blocks.append(Block(m.group(1)))
+        if "in Loop:" in raw or "Loop Header" in raw:
+            blocks[-1].in_loop = True
+            h = re.search(r"Header=(BB\d+_\d+)", raw)
+            blocks[-1].header = h.group(1) if h else blocks[-1].label.lstrip(".L")
+        if m:
+            continue
+        line = raw.split(";")[0].rstrip()
+        if not line.strip():
+            continue
+        s = line.strip()
+        if s.startswith(".") or line[0] not in " \t":
+            continue
+        parts = s.split(None, 1)
+        blocks[-1].insts.append((no, parts[0], parts[1] if len(parts) > 1 else ""))
+    index = {b.label: i for i, b in enumerate(blocks)}
+    for i, b in enumerate(blocks):
+        last = b.insts[-1] if b.insts else None
+        fall = True
+        # terminators may sit before a trailing non-branch (e.g. s_nop); scan all
+        for _, mn, ops in b.insts:
+            if mn == "s_branch":
+                b.succ.append(index[ops.strip()])
+                fall = False
+            elif mn.startswith("s_cbranch_"):
+                b.succ.append(index[ops.strip().split()[0]])
+            elif mn in ("s_endpgm", "s_setpc_b64"):
+                fall = False
+        del last
+        if fall and i + 1 < len(blocks):
+            b.succ.append(i + 1)
+    return blocks
+
+
+def _merge(a: tuple, b: tuple) -> tuple:
+    """Position-wise union of two in-flight sequences (youngest first); a
+    position absent on one path holds the marker "none" (depth differs)."""
+    n = max(len(a), len(b))
+    none = frozenset(["none"])
+    return tuple((a[i] if i < len(a) else none) | (b[i] if i < len(b) else none) for i in range(n))
+
+
+def _handoff(block: Block, idx: int) -> bool:
+    """A wait that hands a stage over: an s_barrier follows it in the same
+    block before any other vector-memory instruction."""
+    for _, mn, ops in block.insts[idx + 1:]:
+        if mn == "s_barrier":
+            return True
+        if classify(mn, ops) is not None or mn == "s_waitcnt":
+            return False
+    return False
+
+
+def _transfer(block: Block, state: tuple, record: list | None, fname: str):
+    for i, (no, mn, ops) in enumerate(block.insts):
+        if mn == "s_waitcnt":
+            m = _WAIT.search(ops)
+            if m is None:
+                if re.fullmatch(r"\s*0\s*", ops):
+                    state = ()
+                continue
+            n = int(m.group(1))
+            if record is not None and n > 0:
+                record.append({"kernel": fname, "line": no, "n": n, "handoff": _handoff(block, i),
+                               "window": [sorted(x) for x in state[:n + 1]],
+                               "depth": len(state)})
+            state = state[:n]
+            continue
+        c = classify(mn, ops)
+        if c is not None:
+            state = ((frozenset([c]),) + state)[:MAX_DEPTH]
+    return state
+
+
+def counted_waits(fname: str, body: list[tuple[int, str]]) -> list[dict]:
+    """Every counted (N > 0) vmcnt wait of one function with the in-flight
+    window it sees: positions 0..N-1 stay in flight, position N is the
+    youngest operation it retires (merged over every path)."""
+    blocks = build_cfg(body)
+    ins: list = [None] * len(blocks)
+    ins[0] = ()
+    work = [0]
+    while work:
+        i = work.pop()
+        out = _transfer(blocks[i], ins[i], None, fname)
+        for s in blocks[i].succ:
+            new = out if ins[s] is None else _merge(ins[s], out)
+            if new != ins[s]:
+                ins[s] = new
+                work.append(s)
+    rec: list[dict] = []
+    for i, b in enumerate(blocks):
+        if ins[i] is not None:
+            _transfer(b, ins[i], rec, fname)
+    return sorted(rec, key=lambda r: r["line"])
+
+
+def issues_dma(body: list[tuple[int, str]]) -> bool:
+    for _, line in body:
+        t = line.strip().split(None, 1)
+        if t and classify(t[0], t[1] if len(t) > 1 else "") == "dma":
+            return True
+    return False
+
+
+def check_kernel(fname: str, body: list[tuple[int, str]], keep: str = "dma") -> list[str]:
+    """The stage hand-off rule for one LDS-DMA kernel, at every counted wait
+    vmcnt(N) followed by s_barrier (merged over every path; "none" marks a
+    position that is empty on some path, e.g. after a cursor refill drained
+    everything, which only makes the wait stronger):
+
+    keep == "load" (bs 32 CM4: A through VGPRs): the N operations left in
+        flight are exactly the A prefetch loads on every path, and the
+        youngest operation retired is an LDS-DMA copy on every path — so the
+        B copies of the stage handed over are all complete.
+    keep == "dma" (every other LDS-staged kernel): the N operations left in
+        flight and the youngest one retired are LDS-DMA copies (or nothing) on
+        every path — no VGPR load, store or flat access sits in the counted
+        window, whose count is planned in copies.
+    """
+    errs = []
+    for r in counted_waits(fname, body):
+        if not r["handoff"]:
+            continue
+        w, n = r["window"], r["n"]
+        kept = w[:n]
+        retired = w[n] if len(w) > n else ["none"]
+        if keep == "load":
+            if len(kept) < n or any(x != ["load"] for x in kept):
+                errs.append(f"line {r['line']}: vmcnt({n}) keeps {kept}, expected exactly {n} x load")
+            if retired != ["dma"]:
+                errs.append(f"line {r['line']}: vmcnt({n}) retires {retired} youngest, expected an LDS-DMA copy")
+        else:
+            if any(not set(x) <= {"dma", "none"} for x in kept):
+                errs.append(f"line {r['line']}: vmcnt({n}) keeps {kept} in flight, expected LDS-DMA copies only")
+            if not set(retired) <= {"dma", "none"}:
+                errs.append(f"line {r['line']}: vmcnt({n}) retires {retired} youngest, expected an LDS-DMA copy")
+    return errs
+
+
+def loop_drains(body: list[tuple[int, str]]) -> list[int]:
+    """Lines of vmcnt(0) waits inside a copy loop (one that issues LDS-DMA) that are
+    neither a stage hand-off (followed by s_barrier) nor the wait right after a
+    VGPR load of the same block (a column-cursor refill used at once). Such a
+    wait drains the copies of the blocks ahead in the middle of an iteration,
+    which is the prefetch the copy ring exists for."""
+    out = []
+    blocks = build_cfg(body)
+    copy_loops = {b.header for b in blocks
+                  if b.in_loop and any(classify(mn, ops) == "dma" for _, mn, ops in b.insts)}
+    for b in blocks:
+        if not b.in_loop or b.header not in copy_loops:
+            continue
+        last = None
+        for i, (no, mn, ops) in enumerate(b.insts):
+            c = classify(mn, ops)
+            if c is not None:
+                last = c
+            elif mn == "s_waitcnt" and (m := _WAIT.search(ops)) and int(m.group(1)) == 0:
+                if last != "load" and not _handoff(b, i):
+                    out.append(no)
+                last = None
+    return out
+
+
+def audit(text: str, fragments: list[str] | None = None, keep_load: tuple = ("bsr32_f32_cm4_kernel",)):
+    """-> {kernel: [errors]} over every LDS-DMA kernel whose name matches."""
+    out = {}
+    for name, body in split_functions(text).items():
+        if fragments and not any(f in name for f in fragments):
+            continue
+        if not issues_dma(body):
+            continue
+        keep = "load" if any(k in name for k in keep_load) else "dma"
+        out[name] = check_kernel(name, body, keep)
+    return out
+
+
+if __name__ == "__main__":
+    txt = open(sys.argv[1]).read()
+    res = audit(txt, sys.argv[2:] or None)
+    bad = 0
+    for k, errs in res.items():
+        waits = [r for r in counted_waits(k, split_functions(txt)[k]) if r["handoff"]]
+        print(f"{'FAIL' if errs else 'ok  '} {len(waits):3d} hand-off waits  {k[:100]}")
+        for e in errs:
+            print("      ", e)
+        bad += bool(errs)
+    print(f"{len(res)} LDS-DMA kernels, {bad} failing")
+    sys.exit(1 if bad else 0)
