@@ -14,13 +14,17 @@ Workloads (BASELINE.json configs; the default is the metric's own config):
   products_bsr16_f16 community-ordered products stand-in, bs=16, K=512, fp16 MFMA    (config 5)
 
 A step = one pass of the hot path over resident inputs. CSR: the merge-path
-kernel + carry fix-up on this rank's rows. At N > 1 the default is weak
-scaling (--scaling weak): each rank owns a products-size row block of a
-world-times larger graph, B replicated, C row-sharded, no collective in the
-step; the C all-gather is timed after the loop and reported as `exchange`.
---scaling strong is BASELINE config 4 as written: the one graph split
-nnz-balanced over the ranks plus the RCCL all-gather of C in every step.
-BSR: one bsrmm. Rank 0 prints ONE JSON line.
+kernel + carry fix-up on this rank's rows. With no --workload the N = 1 run is
+the metric's own workload (products_csr, K = 128) and an N > 1 launch runs
+BASELINE config 4 as written (products_csr_k256, --scaling strong): the one
+graph split nnz-balanced over the ranks, the chunked RCCL all-gather of C
+inside every step, per-GPU kernel ms and collective ms reported beside the
+step, and rank 0's 1-GPU time of the same product for the speed-up. GFLOP/s
+normalises K, so the N = 1 headline and the N > 1 config-4 lines form one
+series. --scaling weak keeps the weak-scaling form: each rank owns a
+products-size row block of a world-times larger graph, B replicated, C
+row-sharded, no collective in the step (the C all-gather is timed after the
+loop as `exchange`). BSR: one bsrmm. Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -106,6 +110,59 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _host_cpus() -> dict:
+    """Threads this process may run on (affinity / cgroup cpuset) and the
+    machine's physical cores (unique (package, core) pairs in /proc/cpuinfo)."""
+    phys, pkg = set(), None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    pkg = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    phys.add((pkg, line.split(":", 1)[1].strip()))
+    except OSError:
+        pass
+    return {"affinity_cpus": len(os.sched_getaffinity(0)),
+            "machine_physical_cores": len(phys) or None,
+            "machine_logical_cpus": os.cpu_count()}
+
+
+def cpu_baseline_config1(L, reps: int = 21) -> dict:
+    """BASELINE configs[0] / BASELINE.md §2 row 1 as stated: spmm.cc csr_spmm
+    (oracle_spmm_cc_csr: OpenMP rows, k-outer, double, unit values) on
+    randomCSRMatrix(16384, 16384, 2^-10) + randomDenseMatrix(16384, 32) from a
+    fresh mt19937_64(1234) (the reference generator's stream, bit-exact),
+    median of `reps` after one warm-up; coo_spmm (spmm.cc:27-43) beside it."""
+    from helpers import ptr
+    from spmm_hip import prep
+    m, K = 16384, 32
+    prep.rng_seed(1234)
+    rp, ci, _ = prep.random_csr(m, m, 2.0 ** -10)
+    B = prep.random_dense_matrix(m, K).astype(np.float64)
+    ip, ix = rp.astype(np.int64), ci.astype(np.int64)
+    row = np.repeat(np.arange(m, dtype=np.int64), np.diff(rp))
+    out = np.empty((m, K))
+    res = {}
+    for name, run in (("csr_spmm", lambda: L.oracle_spmm_cc_csr(m, K, ptr(ip), ptr(ix), ptr(B), K,
+                                                                ptr(out))),
+                      ("coo_spmm", lambda: L.oracle_spmm_cc_coo(m, K, ix.size, ptr(row), ptr(ix),
+                                                                ptr(B), K, ptr(out)))):
+        run()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            run()
+            ts.append(time.perf_counter() - t0)
+        med = float(np.median(ts))
+        res[name] = {"seconds": round(med, 6), "GFLOPs": round(2.0 * ci.size * K / med / 1e9, 3)}
+    return {"value": res["csr_spmm"]["GFLOPs"], "unit": "GFLOP/s", "kind": "port",
+            "cores": int(L.oracle_num_threads()),
+            "sample": (f"BASELINE config 1: spmm.cc csr_spmm restated on randomCSRMatrix(16384, "
+                       f"16384, 2^-10) ({ci.size} nnz, mt19937_64(1234)), K=32, double, unit "
+                       f"values, median of {reps} after a warm-up"), **res}
+
+
 def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0) -> dict:
     """spmm.cc csr_spmm restated (oracle_spmm_cc_csr: OpenMP rows, k-outer,
     double, unit values) on the SAME graph: a growing row prefix until about
@@ -144,6 +201,8 @@ def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0)
         "sample": (f"fp32 values, sequential FMA per element (oracle_csrmm_f32, OpenMP rows) on "
                    f"{'all' if rows == n else 'the first'} {rows} rows ({nnz_s} nnz), K={K}; "
                    f"median of {len(times)} runs ({med:.3f} s each)")}
+    res.update(_host_cpus())
+    res["config1"] = cpu_baseline_config1(L)
     return res
 
 
@@ -318,6 +377,12 @@ def run_csr(args, W, world, rank, dev, dist):
 
         def step():
             sdist.chunked_spmm(shard, out, compute_chunk, nch, compact=False)
+
+        def exchange_only():
+            works = [dist.all_gather_into_tensor(out[c].view(-1, K), out[c, rank], async_op=True)
+                     for c in range(nch)]
+            for w in works:
+                w.wait()
     elif args.csr_layout == "col":
         if world > 1:
             raise SystemExit("--csr-layout col is a 1-GPU form")
@@ -337,6 +402,9 @@ def run_csr(args, W, world, rank, dev, dist):
                       handle=h)
             if world > 1:
                 sdist.gather(out, shard, compact=False)
+
+        def exchange_only():
+            sdist.gather(out, shard, compact=False)
 
     elapsed, kt = timed_loop(step, h, args.steps, args.warmup, world, dist, raw=True)
     # kernel time per step (all chunks of a step; one launch when unchunked)
@@ -363,7 +431,8 @@ def run_csr(args, W, world, rank, dev, dist):
         data=("synthetic (Chung-Lu power-law digraph with the dataset's n / nnz / max degree, "
               "U(-1,1) values and B; OGB data not reachable offline)"),
         config={"workload": f"{args.workload}: csr_spmm K={K}" +
-                (" row-partitioned + RCCL all-gather" if world > 1 else ""),
+                (f" row-partitioned over {world} ranks (nnz-balanced) + chunked RCCL all-gather "
+                 f"of C in the step (BASELINE config 4), strong scaling" if world > 1 else ""),
                 "n": n, "nnz": nnz, "K": K, "max_deg": int(np.diff(rp).max()),
                 "parallelism": f"rows{world}" if world > 1 else "single",
                 "exchange_chunks": nch, "hip_graph": bool(GRAPH and world == 1),
@@ -376,11 +445,52 @@ def run_csr(args, W, world, rank, dev, dist):
                   "algorithmic_bytes_per_launch": kbytes},
         gen_seconds=round(t_gen, 2))
     if world > 1:
-        # compute and collective reported separately (the step
-        # minus the slowest rank's kernel time, i.e. the collective time not
-        # hidden behind compute; the fix-up kernel is ~4 us).
-        rec["collective_ms_est"] = round(rec["ms_per_step"] - kms_max, 4)
+        # compute and collective reported separately.
+        #  kernel_ms (roofline): this rank's kernels per step, max over ranks;
+        #  allgather_ms: the step's all-gathers alone (no compute), max over ranks;
+        #  collective_ms_exposed: step minus the slowest rank's kernel time, the
+        #    part of the collective the overlap did not hide.
+        for _ in range(2):
+            exchange_only()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            exchange_only()
+        torch.cuda.synchronize()
+        ag = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64,
+                          device=dev)
+        dist.all_reduce(ag, op=dist.ReduceOp.MAX)
+        recv = (world - 1) * (out.numel() // world) * 4
+        rec["allgather_ms"] = round(float(ag[0]), 4)
+        rec["allgather_bytes_received_per_rank"] = int(recv)
+        rec["allgather_GBps_per_rank"] = round(recv / (float(ag[0]) / 1e3) / 1e9, 1)
+        rec["collective_ms_exposed"] = round(rec["ms_per_step"] - kms_max, 4)
         rec["rows_per_rank"] = [int(b) for b in np.diff(shard.bounds)]
+        rec["nnz_per_rank"] = [int(rp[b1] - rp[b0]) for b0, b1 in
+                               zip(shard.bounds[:-1], shard.bounds[1:])]
+        # rank 0: the same product on one GPU (whole matrix, same kernel), for
+        # the speed-up of this strong-scaling run; outside the timed region
+        one = torch.zeros(1, dtype=torch.float64, device=dev)
+        if rank == 0:
+            del d_rp, d_ci, d_v
+            a_rp, a_ci, a_v = (torch.from_numpy(a).to(dev) for a in (rp, ci, val))
+            Cw = torch.empty((n, K), device=dev)
+            h1 = ops.Handle()
+            _, one_ms = timed_loop(lambda: ops.csrmm(a_rp, a_ci, a_v, B, n=K, k=n, ldb=K, C=Cw,
+                                                     ldc=K, handle=h1), h1, 5, 2, 1, dist)
+            t0 = time.perf_counter()
+            for _ in range(5):
+                ops.csrmm(a_rp, a_ci, a_v, B, n=K, k=n, ldb=K, C=Cw, ldc=K, handle=h1)
+            torch.cuda.synchronize()
+            one[0] = (time.perf_counter() - t0) / 5 * 1e3
+            rec["one_gpu"] = {"ms_per_step": round(float(one[0]), 4),
+                              "kernel_ms": round(one_ms, 4),
+                              "speedup": round(float(one[0]) / rec["ms_per_step"], 3),
+                              "note": "rank 0, whole matrix, same kernel, after the timed region"}
+            del a_rp, a_ci, a_v, Cw
+        dist.barrier()
     return rec, (rp, ci, K)
 
 
@@ -604,7 +714,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="products_csr", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: products_csr at N = 1 (the metric), products_csr_k256 "
+                         "(BASELINE config 4) at N > 1")
     ap.add_argument("--K", type=int, default=0, help="override the workload's K")
     ap.add_argument("--density", default=None,
                     help="hybrid workloads: divide threshold (a float, or 'auto' = spmm_hybrid_plan)")
@@ -621,11 +733,11 @@ def main() -> None:
                     help="row chunks per rank whose all-gathers overlap the next chunk's compute "
                          "(default 4 when N > 1; 1 = compute, then one all-gather; > 1 at N = 1 "
                          "needs a torch.distributed launcher)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="CSR at N > 1: weak = a products-size row block per rank, B "
-                         "replicated, no collective in the step (default); strong = BASELINE "
-                         "config 4 as stated: the one graph row-partitioned + RCCL all-gather "
-                         "of C in every step")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="CSR at N > 1: strong = BASELINE config 4 as stated: the one graph "
+                         "row-partitioned + RCCL all-gather of C in every step (default); weak = "
+                         "a products-size row block per rank, B replicated, no collective in "
+                         "the step")
     ap.add_argument("--no-exchange-probe", action="store_true",
                     help="weak scaling: skip timing the C all-gather after the step loop")
     ap.add_argument("--hybrid-options", type=int, default=None,
@@ -655,6 +767,8 @@ def main() -> None:
         # code path, its collectives and the max-over-ranks timing on one GPU)
         dist.init_process_group("nccl", device_id=dev)
 
+    if args.workload is None:
+        args.workload = "products_csr_k256" if world > 1 else "products_csr"
     W = WORKLOADS[args.workload]
     runner = {"csr": run_csr, "bsr": run_bsr, "hybrid": run_hybrid}[W["kind"]]
     weak = W["kind"] == "csr" and args.scaling == "weak"
@@ -671,7 +785,9 @@ def main() -> None:
                "value": round(rec.pop("value"), 2), "unit": "GFLOP/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(rec.pop("ms_per_step"), 4), "higher_is_better": True,
-               "scaling": "strong" if (W["kind"] == "csr" and not weak) else "weak",
+               # CSR: strong (the one graph, total work fixed) unless --scaling weak;
+               # the BSR / hybrid configs are single-GPU (BASELINE configs 3, 5)
+               "scaling": (("weak" if weak else "strong") if W["kind"] == "csr" else None),
                "vs_baseline": None}
         out.update(rec)
         rf = out.get("roofline") or {}

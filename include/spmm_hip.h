@@ -263,6 +263,13 @@ spmm_status_t spmm_sbsr2csr_dev(spmm_handle_t handle, spmm_direction_t dir, int 
                                 const spmm_mat_descr_t descrC, float* csrVal, int* csrRowPtr,
                                 int* csrColInd);
 
+/* cusparseXcoo2csr (csrmm.cu:148-149): csrRowPtr[m+1] of a COO whose row
+ * indices cooRowInd[nnz] are sorted ascending (device pointers, handle's
+ * stream). Row indices and the output are in idxBase, as in cuSPARSE:
+ * csrRowPtr[0] = idxBase, csrRowPtr[m] = nnz + idxBase. */
+spmm_status_t spmm_xcoo2csr(spmm_handle_t handle, const int* cooRowInd, int nnz, int m,
+                            int* csrRowPtr, spmm_index_base_t idxBase);
+
 /* Threshold planner for divide (the reference takes `density` from the user,
  * divide.cu:348): from the histogram of block fills it picks the count
  * threshold T minimising a bytes-over-bandwidth model of the hybrid SpMM,

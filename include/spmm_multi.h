@@ -1,0 +1,86 @@
+/*
+ * spmm_multi.h — single-process multi-GPU CSR x dense over RCCL
+ * (libspmm_hip.so; SURVEY.md §8b "spmm_csr_f32_multi", §8e; BASELINE.json
+ * configs[3]: row-partitioned ogbn-products K = 256 + RCCL all-gather).
+ *
+ * The reference has no multi-GPU code: this is the
+ * capability BASELINE config 4 names, behind the same plain-C conventions as
+ * spmm_hip.h. One host thread drives every GPU of the node: one RCCL
+ * communicator per device (ncclCommInitAll), one compute stream and one
+ * collective stream per device, one spmm handle per device.
+ *
+ * Partitioning (host, spmm_csr_partition_rows in spmm_hip.h): contiguous row
+ * ranges of A balanced on nnz + rows, part p = rows [bounds[p], bounds[p+1]).
+ * B is replicated (2.5 GB for products at K = 256 against 288 GB of HBM per
+ * GPU). Each device computes its rows into its slot of a padded output and
+ * the slots are exchanged with in-place ncclAllGather over xGMI, so every
+ * device ends up holding all of C.
+ *
+ * Output layout on every device: chunk-major [chunks][ngpu][slotRows][ldc]
+ * floats, slotRows = spmm_multi_slot_rows(...). Chunk c of part p holds the
+ * part's local rows [c*slotRows, min((c+1)*slotRows, rows_p)); rows past a
+ * part's end in its slot are left as they were (padding). chunks = 1 gives
+ * the plain [ngpu][maxRows][ldc] form. With chunks > 1 the all-gather of
+ * chunk c (collective stream) runs while chunk c+1 is computed.
+ *
+ * Numerics: each device runs the 1-GPU kernel on its rows, so with
+ * ngpu = 1 and chunks = 1 the result is bit-identical to spmm_csrmm_ex_f32 on
+ * the whole matrix; otherwise a row is bit-identical unless a merge-path
+ * wave boundary splits it (the carries' association depends on the shard).
+ */
+#ifndef SPMM_MULTI_H
+#define SPMM_MULTI_H
+
+#include <stdint.h>
+
+#include "spmm_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct spmm_multi* spmm_multi_t;
+
+/* devices: ngpu device ordinals (NULL = 0 .. ngpu-1). Restores the caller's
+ * current device before returning. RCCL failures map to
+ * SPMM_STATUS_EXECUTION_FAILED. */
+spmm_status_t spmm_multi_create(spmm_multi_t* ctx, int ngpu, const int* devices);
+spmm_status_t spmm_multi_destroy(spmm_multi_t ctx);
+int spmm_multi_size(spmm_multi_t ctx);
+/* The compute stream of part p (a hipStream_t; the call's results on device
+ * p are complete once this stream is). */
+spmm_status_t spmm_multi_get_stream(spmm_multi_t ctx, int part, void** stream);
+
+/* Rows per output slot for a partition: ceil(max_p rows_p / chunks). */
+int spmm_multi_slot_rows(int ngpu, const int* bounds, int chunks);
+
+/* C = A(m x k, csr) * B(k x n), A row-partitioned by `bounds` (host,
+ * ngpu + 1 entries, bounds[0] = 0, bounds[ngpu] = m).
+ *   rowPtr[p], colInd[p], val[p]: device pointers on device p to part p's
+ *     CSR: rowPtr[p] has rows_p + 1 entries and indexes colInd[p] / val[p]
+ *     directly (it need not start at 0, so a view into the whole matrix's
+ *     arrays uploaded to device p works);
+ *   partNnz[p]: host, rowPtr[p][rows_p] - rowPtr[p][0] (sizes the grid);
+ *   B[p]: device p's replica of B, row-major, ldb >= n;
+ *   C[p]: device p's output, layout above, ldc >= n.
+ * Asynchronous on the parts' streams; spmm_multi_synchronize waits. Status
+ * behaviour of spmm_csrmm_ex_f32 for bad sizes / pointers. */
+spmm_status_t spmm_csr_f32_multi(spmm_multi_t ctx, int m, int n, int k, const int* bounds,
+                                 const int* const* rowPtr, const int* const* colInd,
+                                 const float* const* val, const int* partNnz,
+                                 const float* const* B, int ldb, float* const* C, int ldc,
+                                 int chunks);
+spmm_status_t spmm_multi_synchronize(spmm_multi_t ctx);
+
+/* Per-part timing of the last spmm_csr_f32_multi call (events on the
+ * streams, recorded when enabled): compute_ms[p] = first kernel start to last
+ * kernel end on device p, total_ms[p] = first kernel start to the end of
+ * the last all-gather on device p. Synchronises. */
+spmm_status_t spmm_multi_set_timing(spmm_multi_t ctx, int enable);
+spmm_status_t spmm_multi_get_times(spmm_multi_t ctx, float* compute_ms, float* total_ms);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* SPMM_MULTI_H */

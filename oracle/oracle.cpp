@@ -151,6 +151,37 @@ void oracle_spmm_cc_csr(int64_t num_rows, int64_t num_cols_out, const int64_t* i
   }
 }
 
+// spmm.cc:27-43 coo_spmm, faithful: out zeroed (the memset at :32), OpenMP
+// over the nnz entries, each adding dense row `col` into out row `row` with
+// `omp atomic` (double, unit values). The order of the atomic adds is the
+// schedule's, so results can differ from the CSR form in the last bits.
+void oracle_spmm_cc_coo(int64_t num_rows, int64_t num_cols_out, int64_t nnz, const int64_t* row,
+                        const int64_t* col, const double* dense, int64_t dense_cols, double* out) {
+  std::memset(out, 0, sizeof(double) * (size_t)(num_rows * num_cols_out));
+#pragma omp parallel for
+  for (int64_t i = 0; i < nnz; ++i) {
+    const int64_t rid = row[i], cid = col[i];
+    double* out_off = out + rid * num_cols_out;
+    for (int64_t k = 0; k < num_cols_out; ++k) {
+#pragma omp atomic
+      out_off[k] += dense[cid * dense_cols + k];
+    }
+  }
+}
+
+// cusparseXcoo2csr semantics (csrmm.cu:148-149): row pointer of a row-sorted
+// COO, in the index base of its row indices (csr_rowptr[0] = base,
+// csr_rowptr[m] = nnz + base). Restated from the cuSPARSE documentation (the
+// library is closed source); pinned by the csrmm.cu KAT, whose rowptr the
+// conversion must produce.
+void oracle_coo2csr(const int* coo_row, int nnz, int m, int base, int* csr_rowptr) {
+  int i = 0;
+  for (int r = 0; r <= m; ++r) {
+    while (i < nnz && coo_row[i] - base < r) ++i;
+    csr_rowptr[r] = i + base;
+  }
+}
+
 int oracle_num_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

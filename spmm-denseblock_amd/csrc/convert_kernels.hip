@@ -173,9 +173,40 @@ __global__ __launch_bounds__(kWG) void bsr2csr_kernel(int mb, int bs,
   }
 }
 
+// coo2csr (cusparseXcoo2csr, csrmm.cu:148-149): row pointer of a row-sorted
+// COO. Thread r writes csr_rowptr[r] = (first entry with row >= r) + base by
+// a binary search over the sorted row indices; O(m log nnz), no atomics, so
+// it is exact and deterministic for any row distribution (empty rows,
+// power-law hubs).
+__global__ __launch_bounds__(256) void coo2csr_kernel(const int* __restrict__ coo_row, int nnz,
+                                                      int m, int base,
+                                                      int* __restrict__ csr_rowptr) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > m) return;
+  int lo = 0, hi = nnz;  // first index with coo_row[i] - base >= r
+  while (lo < hi) {
+    const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+    if (coo_row[mid] - base < r) lo = mid + 1;
+    else hi = mid;
+  }
+  csr_rowptr[r] = lo + base;
+}
+
 }  // namespace
 
 extern "C" {
+
+spmm_status_t spmm_xcoo2csr(spmm_handle_t handle, const int* cooRowInd, int nnz, int m,
+                            int* csrRowPtr, spmm_index_base_t idxBase) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (nnz < 0 || m < 0 || (idxBase != SPMM_INDEX_BASE_ZERO && idxBase != SPMM_INDEX_BASE_ONE))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (!csrRowPtr || (nnz > 0 && !cooRowInd)) return SPMM_STATUS_INVALID_VALUE;
+  spmm_context* ctx = handle;
+  hipLaunchKernelGGL(coo2csr_kernel, dim3((m + 1 + 255) / 256), dim3(256), 0, ctx->stream,
+                     cooRowInd, nnz, m, (int)idxBase, csrRowPtr);
+  return spmm::from_hip(hipGetLastError());
+}
 
 spmm_status_t spmm_xcsr2bsr_nnz_dev(spmm_handle_t handle, spmm_direction_t dir, int m, int n,
                                     const spmm_mat_descr_t descrA, const int* csrRowPtr,

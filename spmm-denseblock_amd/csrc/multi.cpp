@@ -1,0 +1,245 @@
+// multi.cpp — single-process multi-GPU row-partitioned CSR SpMM over RCCL
+// (include/spmm_multi.h).
+//
+// Per call and chunk c: every device p computes its chunk-c rows with the
+// 1-GPU merge-path kernel into its slot of the chunk-major output on its
+// compute stream, records an event, and its collective stream waits on that
+// event and runs the in-place ncclAllGather of chunk c (one ncclGroup over all
+// devices, so one host thread can drive every rank). Chunk c+1's kernel is
+// queued on the compute stream right away and overlaps chunk c's exchange.
+// At the end each compute stream waits for its collective stream, so a
+// caller that synchronises the compute stream sees all of C.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "context.hpp"
+#include "spmm_multi.h"
+
+struct spmm_multi {
+  int ngpu = 0;
+  std::vector<int> dev;
+  std::vector<ncclComm_t> comm;
+  std::vector<hipStream_t> compute, coll;
+  std::vector<spmm_handle_t> handle;
+  std::vector<std::vector<hipEvent_t>> chunk_done;  // [p][c]: chunk c's kernel finished
+  std::vector<hipEvent_t> t0, t_comp, t_end;         // timing, per part
+  std::vector<hipEvent_t> coll_done;                 // [p]: last all-gather finished
+  bool timing = false;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int saved = 0;
+  DeviceGuard() { (void)hipGetDevice(&saved); }
+  ~DeviceGuard() { (void)hipSetDevice(saved); }
+};
+
+spmm_status_t from_nccl(ncclResult_t r) {
+  return r == ncclSuccess ? SPMM_STATUS_SUCCESS : SPMM_STATUS_EXECUTION_FAILED;
+}
+
+#define SPMM_TRY_HIP(x)                                 \
+  do {                                                  \
+    hipError_t e_ = (x);                                \
+    if (e_ != hipSuccess) return spmm::from_hip(e_);    \
+  } while (0)
+
+void release(spmm_multi* c) {
+  for (int p = 0; p < c->ngpu; ++p) {
+    if (p < (int)c->dev.size()) (void)hipSetDevice(c->dev[p]);
+    if (p < (int)c->compute.size() && c->compute[p]) (void)hipStreamSynchronize(c->compute[p]);
+    if (p < (int)c->coll.size() && c->coll[p]) (void)hipStreamSynchronize(c->coll[p]);
+    if (p < (int)c->comm.size() && c->comm[p]) (void)ncclCommDestroy(c->comm[p]);
+    if (p < (int)c->handle.size() && c->handle[p]) (void)spmm_destroy(c->handle[p]);
+    if (p < (int)c->chunk_done.size())
+      for (auto e : c->chunk_done[p]) (void)hipEventDestroy(e);
+    for (auto* v : {&c->t0, &c->t_comp, &c->t_end, &c->coll_done})
+      if (p < (int)v->size() && (*v)[p]) (void)hipEventDestroy((*v)[p]);
+    if (p < (int)c->compute.size() && c->compute[p]) (void)hipStreamDestroy(c->compute[p]);
+    if (p < (int)c->coll.size() && c->coll[p]) (void)hipStreamDestroy(c->coll[p]);
+  }
+  delete c;
+}
+
+}  // namespace
+
+extern "C" {
+
+spmm_status_t spmm_multi_create(spmm_multi_t* out, int ngpu, const int* devices) {
+  if (!out) return SPMM_STATUS_INVALID_VALUE;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SPMM_STATUS_NOT_INITIALIZED;
+  if (ngpu < 1 || ngpu > ndev) return SPMM_STATUS_INVALID_VALUE;
+  std::vector<int> dev(ngpu);
+  for (int p = 0; p < ngpu; ++p) {
+    dev[p] = devices ? devices[p] : p;
+    if (dev[p] < 0 || dev[p] >= ndev) return SPMM_STATUS_INVALID_VALUE;
+    for (int q = 0; q < p; ++q)
+      if (dev[q] == dev[p]) return SPMM_STATUS_INVALID_VALUE;  // one rank per GPU
+  }
+  DeviceGuard guard;
+  spmm_multi* c = new (std::nothrow) spmm_multi();
+  if (!c) return SPMM_STATUS_ALLOC_FAILED;
+  c->ngpu = ngpu;
+  c->dev = dev;
+  c->comm.assign(ngpu, nullptr);
+  c->compute.assign(ngpu, nullptr);
+  c->coll.assign(ngpu, nullptr);
+  c->handle.assign(ngpu, nullptr);
+  c->chunk_done.assign(ngpu, {});
+  c->t0.assign(ngpu, nullptr);
+  c->t_comp.assign(ngpu, nullptr);
+  c->t_end.assign(ngpu, nullptr);
+  c->coll_done.assign(ngpu, nullptr);
+  spmm_status_t st = SPMM_STATUS_SUCCESS;
+  for (int p = 0; p < ngpu && st == SPMM_STATUS_SUCCESS; ++p) {
+    hipError_t e = hipSetDevice(dev[p]);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute[p], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->coll[p], hipStreamNonBlocking);
+    for (auto* v : {&c->t0, &c->t_comp, &c->t_end})
+      if (e == hipSuccess) e = hipEventCreate(&(*v)[p]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->coll_done[p], hipEventDisableTiming);
+    if (e != hipSuccess) {
+      st = spmm::from_hip(e);
+      break;
+    }
+    st = spmm_create(&c->handle[p]);
+    if (st == SPMM_STATUS_SUCCESS) st = spmm_set_stream(c->handle[p], c->compute[p]);
+  }
+  if (st == SPMM_STATUS_SUCCESS) st = from_nccl(ncclCommInitAll(c->comm.data(), ngpu, dev.data()));
+  if (st != SPMM_STATUS_SUCCESS) {
+    release(c);
+    return st;
+  }
+  *out = c;
+  return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t spmm_multi_destroy(spmm_multi_t c) {
+  if (!c) return SPMM_STATUS_NOT_INITIALIZED;
+  DeviceGuard guard;
+  release(c);
+  return SPMM_STATUS_SUCCESS;
+}
+
+int spmm_multi_size(spmm_multi_t c) { return c ? c->ngpu : 0; }
+
+spmm_status_t spmm_multi_get_stream(spmm_multi_t c, int part, void** stream) {
+  if (!c) return SPMM_STATUS_NOT_INITIALIZED;
+  if (!stream || part < 0 || part >= c->ngpu) return SPMM_STATUS_INVALID_VALUE;
+  *stream = reinterpret_cast<void*>(c->compute[part]);
+  return SPMM_STATUS_SUCCESS;
+}
+
+int spmm_multi_slot_rows(int ngpu, const int* bounds, int chunks) {
+  if (ngpu < 1 || !bounds || chunks < 1) return 0;
+  int mr = 0;
+  for (int p = 0; p < ngpu; ++p) mr = std::max(mr, bounds[p + 1] - bounds[p]);
+  return std::max(1, (mr + chunks - 1) / chunks);
+}
+
+spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int* bounds,
+                                 const int* const* rowPtr, const int* const* colInd,
+                                 const float* const* val, const int* partNnz,
+                                 const float* const* B, int ldb, float* const* C, int ldc,
+                                 int chunks) {
+  if (!c) return SPMM_STATUS_NOT_INITIALIZED;
+  const int P = c->ngpu;
+  if (m < 0 || n < 0 || k < 0 || chunks < 1 || !bounds || !partNnz) return SPMM_STATUS_INVALID_VALUE;
+  if (bounds[0] != 0 || bounds[P] != m) return SPMM_STATUS_INVALID_VALUE;
+  for (int p = 0; p < P; ++p)
+    if (bounds[p + 1] < bounds[p] || partNnz[p] < 0) return SPMM_STATUS_INVALID_VALUE;
+  if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  if (!rowPtr || !colInd || !val || !B || !C || ldb < n || ldc < n) return SPMM_STATUS_INVALID_VALUE;
+  for (int p = 0; p < P; ++p)
+    if (!rowPtr[p] || !C[p] || (k > 0 && !B[p]) || (partNnz[p] > 0 && (!colInd[p] || !val[p])))
+      return SPMM_STATUS_INVALID_VALUE;
+  const int cr = spmm_multi_slot_rows(P, bounds, chunks);
+  const size_t slot = (size_t)cr * ldc;  // floats per (chunk, part) slot
+  DeviceGuard guard;
+  for (int p = 0; p < P; ++p) {
+    auto& ev = c->chunk_done[p];
+    SPMM_TRY_HIP(hipSetDevice(c->dev[p]));
+    while ((int)ev.size() < chunks) {
+      hipEvent_t e;
+      SPMM_TRY_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ev.push_back(e);
+    }
+  }
+  for (int ch = 0; ch < chunks; ++ch) {
+    for (int p = 0; p < P; ++p) {
+      SPMM_TRY_HIP(hipSetDevice(c->dev[p]));
+      if (ch == 0 && c->timing) SPMM_TRY_HIP(hipEventRecord(c->t0[p], c->compute[p]));
+      const int rows = bounds[p + 1] - bounds[p];
+      const int r0 = std::min(ch * cr, rows), r1 = std::min(r0 + cr, rows);
+      if (r1 > r0) {
+        // nnz hint: the part's average share (grid sizing only)
+        const int nnz = (int)((long long)partNnz[p] * (r1 - r0) / std::max(rows, 1));
+        spmm_status_t st = spmm_csrmm_ex_f32(
+            c->handle[p], r1 - r0, n, k, nnz, 1.f, rowPtr[p] + r0, colInd[p], val[p],
+            SPMM_INDEX_BASE_ZERO, B[p], ldb, SPMM_ORDER_ROW, 0.f,
+            C[p] + ((size_t)ch * P + p) * slot, ldc, SPMM_ORDER_ROW);
+        if (st != SPMM_STATUS_SUCCESS) return st;
+      }
+      if (ch == chunks - 1 && c->timing) SPMM_TRY_HIP(hipEventRecord(c->t_comp[p], c->compute[p]));
+      SPMM_TRY_HIP(hipEventRecord(c->chunk_done[p][ch], c->compute[p]));
+      SPMM_TRY_HIP(hipStreamWaitEvent(c->coll[p], c->chunk_done[p][ch], 0));
+    }
+    if (P > 1) {
+      spmm_status_t st = from_nccl(ncclGroupStart());
+      for (int p = 0; p < P && st == SPMM_STATUS_SUCCESS; ++p) {
+        float* base = C[p] + (size_t)ch * P * slot;
+        st = from_nccl(ncclAllGather(base + (size_t)p * slot, base, slot, ncclFloat, c->comm[p],
+                                     c->coll[p]));
+      }
+      const spmm_status_t st2 = from_nccl(ncclGroupEnd());
+      if (st != SPMM_STATUS_SUCCESS) return st;
+      if (st2 != SPMM_STATUS_SUCCESS) return st2;
+    }
+  }
+  for (int p = 0; p < P; ++p) {
+    SPMM_TRY_HIP(hipSetDevice(c->dev[p]));
+    SPMM_TRY_HIP(hipEventRecord(c->coll_done[p], c->coll[p]));
+    SPMM_TRY_HIP(hipStreamWaitEvent(c->compute[p], c->coll_done[p], 0));
+    if (c->timing) SPMM_TRY_HIP(hipEventRecord(c->t_end[p], c->compute[p]));
+  }
+  return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t spmm_multi_synchronize(spmm_multi_t c) {
+  if (!c) return SPMM_STATUS_NOT_INITIALIZED;
+  DeviceGuard guard;
+  for (int p = 0; p < c->ngpu; ++p) {
+    SPMM_TRY_HIP(hipSetDevice(c->dev[p]));
+    SPMM_TRY_HIP(hipStreamSynchronize(c->compute[p]));
+    SPMM_TRY_HIP(hipStreamSynchronize(c->coll[p]));
+  }
+  return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t spmm_multi_set_timing(spmm_multi_t c, int enable) {
+  if (!c) return SPMM_STATUS_NOT_INITIALIZED;
+  c->timing = enable != 0;
+  return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t spmm_multi_get_times(spmm_multi_t c, float* compute_ms, float* total_ms) {
+  if (!c) return SPMM_STATUS_NOT_INITIALIZED;
+  if (!compute_ms || !total_ms) return SPMM_STATUS_INVALID_VALUE;
+  if (!c->timing) return SPMM_STATUS_INVALID_VALUE;
+  DeviceGuard guard;
+  for (int p = 0; p < c->ngpu; ++p) {
+    SPMM_TRY_HIP(hipSetDevice(c->dev[p]));
+    SPMM_TRY_HIP(hipEventSynchronize(c->t_end[p]));
+    SPMM_TRY_HIP(hipEventElapsedTime(&compute_ms[p], c->t0[p], c->t_comp[p]));
+    SPMM_TRY_HIP(hipEventElapsedTime(&total_ms[p], c->t0[p], c->t_end[p]));
+  }
+  return SPMM_STATUS_SUCCESS;
+}
+
+}  // extern "C"

@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <fstream>
 #include <string>
 #include <vector>
 
@@ -108,3 +109,17 @@ struct EventTimer {
     (void)hipEventDestroy(b);
   }
 };
+
+// SPMM_DRIVER_DUMP=<path>: write the result C (row-major rows x dim float32)
+// so a test can check it element by element against the oracle. Not in the
+// reference (whose drivers print timings only); off unless set.
+inline void dump_result(const std::vector<float>& z) {
+  const char* path = getenv("SPMM_DRIVER_DUMP");
+  if (!path || !*path) return;
+  std::ofstream f(path, std::ios::binary);
+  f.write(reinterpret_cast<const char*>(z.data()), (std::streamsize)(z.size() * sizeof(float)));
+  if (!f) {
+    printf("cannot write %s\n", path);
+    exit(-1);
+  }
+}

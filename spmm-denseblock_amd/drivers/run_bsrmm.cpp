@@ -74,6 +74,13 @@ int main(int argc, char* argv[]) {
   printf("bsrmm cost time:  %3.10f ms \n", t);
   printf("useful GFLOP/s (2*nnz*dim/t): %6.3f  MFMA-executed GFLOP/s (2*nnzb*bs^2*dim/t): %6.3f\n",
          2.0 * nnz * dim / (t * 1e6), 2.0 * nnzb * bs * (double)bs * dim / (t * 1e6));
+  {  // z is column-major (ldc = nb*bs): rows 0 .. n-1, row-major for the dump
+    std::vector<float> zc((size_t)nb * bs * dim), z((size_t)n * dim);
+    HANDLE_ERROR(hipMemcpy(zc.data(), d_z, zc.size() * sizeof(float), hipMemcpyDeviceToHost));
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < dim; ++c) z[(size_t)r * dim + c] = zc[(size_t)c * nb * bs + r];
+    dump_result(z);
+  }
   spmm_destroy_mat_descr(descr);
   spmm_destroy(handle);
   printf("end\n");

@@ -5,17 +5,35 @@
 // over rows, output column k OUTER and the row's nnz INNER, pattern only
 // (unit values), double dense/out, row-major. BASELINE configs[0]: N = 16384,
 // p = 2^-10 (randomCSRMatrix from the shared mt19937_64, ~256K nnz), K = 32.
-// Also runs spmm.cc's small test (spmm.cc:45-52; expected [[4,6,7],[8,17,3]]).
+// Also runs spmm.cc's small tests (spmm.cc:45-61; expected [[4,6,7],[8,17,3]])
+// and times coo_spmm (spmm.cc:27-43) on the same matrix, as spmm.cc's main does.
 #include <omp.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <string>
 #include <vector>
 
 #include "spmm_host.h"
+
+// spmm.cc:27-43 coo_spmm: out zeroed, OpenMP over the nnz entries, `omp atomic`
+// adds of the dense row into the output row.
+static void coo_spmm(int64_t rows, int64_t nnz, const int64_t* row, const int64_t* col,
+                     const double* dense, int64_t dcols, double* out) {
+  std::fill(out, out + rows * dcols, 0.0);
+#pragma omp parallel for
+  for (int64_t i = 0; i < nnz; ++i) {
+    double* o = out + row[i] * dcols;
+    const double* d = dense + col[i] * dcols;
+    for (int64_t k = 0; k < dcols; ++k) {
+#pragma omp atomic
+      o[k] += d[k];
+    }
+  }
+}
 
 static void csr_spmm(int64_t rows, const int64_t* indptr, const int64_t* indices,
                      const double* dense, int64_t dcols, double* out) {
@@ -42,6 +60,9 @@ int main(int argc, char** argv) {
     double o[6];
     csr_spmm(2, ip, ix, d, 3, o);
     printf("small csr_spmm: [[%g,%g,%g],[%g,%g,%g]]\n", o[0], o[1], o[2], o[3], o[4], o[5]);
+    const int64_t cr[] = {0, 1, 1};  // spmm.cc:56
+    coo_spmm(2, 3, cr, ix, d, 3, o);
+    printf("small coo_spmm: [[%g,%g,%g],[%g,%g,%g]]\n", o[0], o[1], o[2], o[3], o[4], o[5]);
   }
   std::vector<int> rp(N + 1);
   int* ci = nullptr;
@@ -66,5 +87,25 @@ int main(int argc, char** argv) {
   printf("N=%d nnz=%lld K=%d threads=%d\n", N, (long long)nnz, K, omp_get_max_threads());
   printf("csr_spmm time cost: %gs\n", med);
   printf("GFLOP/s (2*nnz*K/t): %.3f\n", 2.0 * nnz * K / med / 1e9);
+  {  // spmm.cc:27-43 / :75-85: the same product from COO
+    std::vector<int64_t> row(nnz);
+    for (int r = 0; r < N; ++r)
+      for (int64_t j = ip[r]; j < ip[r + 1]; ++j) row[j] = r;
+    std::vector<double> out2((size_t)N * K);
+    coo_spmm(N, nnz, row.data(), ix.data(), dense.data(), K, out2.data());  // warm-up
+    std::vector<double> tc;
+    for (int r = 0; r < reps; ++r) {
+      auto t0 = std::chrono::high_resolution_clock::now();
+      coo_spmm(N, nnz, row.data(), ix.data(), dense.data(), K, out2.data());
+      auto t1 = std::chrono::high_resolution_clock::now();
+      tc.push_back(std::chrono::duration<double>(t1 - t0).count());
+    }
+    std::sort(tc.begin(), tc.end());
+    double maxdiff = 0;
+    for (size_t i = 0; i < out.size(); ++i) maxdiff = std::max(maxdiff, std::fabs(out[i] - out2[i]));
+    printf("coo_spmm time cost: %gs\n", tc[tc.size() / 2]);
+    printf("coo GFLOP/s (2*nnz*K/t): %.3f  max |csr - coo| = %.3g\n",
+           2.0 * nnz * K / tc[tc.size() / 2] / 1e9, maxdiff);
+  }
   return 0;
 }

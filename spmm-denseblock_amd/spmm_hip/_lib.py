@@ -1,5 +1,5 @@
-"""ctypes binding of libspmm_hip.so (the C ABI declared in include/spmm_hip.h
-and include/spmm_host.h).
+"""ctypes binding of libspmm_hip.so (the C ABI declared in include/spmm_hip.h,
+include/spmm_host.h, include/spmm_reorder.h and include/spmm_multi.h).
 
 The library is built in-tree by ``make -C spmm-denseblock_amd lib`` (or
 ``__graft_entry__.build()``). There is no fallback: if the library is missing
@@ -104,6 +104,18 @@ _PROTOS = {
                                   _P]),
     "spmm_sbsr2csr_dev": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P,
                                   _P]),
+    "spmm_xcoo2csr": (c_int, [_P, _P, c_int, c_int, _P, c_int]),
+    # spmm_multi.h
+    "spmm_multi_create": (c_int, [POINTER(c_void_p), c_int, _P]),
+    "spmm_multi_destroy": (c_int, [_P]),
+    "spmm_multi_size": (c_int, [_P]),
+    "spmm_multi_get_stream": (c_int, [_P, c_int, POINTER(c_void_p)]),
+    "spmm_multi_slot_rows": (c_int, [c_int, _P, c_int]),
+    "spmm_csr_f32_multi": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P, _P, _P, _P, c_int, _P,
+                                   c_int, c_int]),
+    "spmm_multi_synchronize": (c_int, [_P]),
+    "spmm_multi_set_timing": (c_int, [_P, c_int]),
+    "spmm_multi_get_times": (c_int, [_P, POINTER(c_float), POINTER(c_float)]),
     "spmm_hybrid_plan": (c_int, [c_int, _P, _P, c_int, c_int, c_int, c_double, c_double,
                                  POINTER(c_float), POINTER(c_int64), POINTER(c_int64),
                                  POINTER(c_double)]),

@@ -266,5 +266,77 @@ def bsr2csr(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, *, mb
     return crp, cci, cv
 
 
-__all__ = ["csr2bsr", "bsr2csr", "Handle", "hybrid_csrmm", "default_handle", "gespmm_csrmm", "csrmm", "bsrmm", "bsrmm_f16",
+def coo2csr(coo_row: torch.Tensor, m: int, base: int = 0,
+            handle: Handle | None = None) -> torch.Tensor:
+    """cusparseXcoo2csr (csrmm.cu:148-149): int32[m+1] row pointer of a
+    row-sorted COO whose row indices are in `base`."""
+    _need(coo_row, torch.int32, "coo_row")
+    h = handle or default_handle()
+    rp = torch.empty(m + 1, dtype=torch.int32, device=coo_row.device)
+    check(lib().spmm_xcoo2csr(h.raw, _ptr(coo_row), coo_row.numel(), m, _ptr(rp), base),
+          "spmm_xcoo2csr")
+    return rp
+
+
+class MultiGPU:
+    """spmm_multi_t (include/spmm_multi.h): one host thread drives the row
+    shards of a CSR x dense product on several GPUs, RCCL communicators from
+    ncclCommInitAll, in-place all-gather of the padded output."""
+
+    def __init__(self, devices: list[int]):
+        self._c = c_void_p()
+        arr = (c_int * len(devices))(*devices)
+        check(lib().spmm_multi_create(byref(self._c), len(devices), arr), "spmm_multi_create")
+        self.devices = list(devices)
+
+    @staticmethod
+    def slot_rows(bounds, chunks: int = 1) -> int:
+        b = (c_int * len(bounds))(*[int(x) for x in bounds])
+        return lib().spmm_multi_slot_rows(len(bounds) - 1, b, chunks)
+
+    def csrmm(self, bounds, parts, part_nnz, Bs, Cs, *, m: int, n: int, k: int, ldb: int,
+              ldc: int, chunks: int = 1) -> None:
+        """parts[p] = (rowptr, colind, val) tensors on device p (rowptr of the
+        part's rows, indexing colind / val directly); Bs[p] B replicas; Cs[p]
+        the [chunks * world * slot_rows, ldc] outputs (include/spmm_multi.h)."""
+        P = len(self.devices)
+        for p in range(P):
+            rp, ci, v = parts[p]
+            for t, dt, nm in ((rp, torch.int32, "rowptr"), (ci, torch.int32, "colind"),
+                              (v, torch.float32, "val"), (Bs[p], torch.float32, "B"),
+                              (Cs[p], torch.float32, "C")):
+                _need(t, dt, nm)
+        vp = lambda ts: (c_void_p * P)(*[_ptr(t) for t in ts])  # noqa: E731
+        b = (c_int * (P + 1))(*[int(x) for x in bounds])
+        nz = (c_int * P)(*[int(x) for x in part_nnz])
+        check(lib().spmm_csr_f32_multi(self._c, m, n, k, b, vp([q[0] for q in parts]),
+                                       vp([q[1] for q in parts]), vp([q[2] for q in parts]), nz,
+                                       vp(Bs), ldb, vp(Cs), ldc, chunks), "spmm_csr_f32_multi")
+
+    def synchronize(self) -> None:
+        check(lib().spmm_multi_synchronize(self._c), "spmm_multi_synchronize")
+
+    def set_timing(self, enable: bool) -> None:
+        check(lib().spmm_multi_set_timing(self._c, int(enable)), "spmm_multi_set_timing")
+
+    def times(self) -> tuple[list[float], list[float]]:
+        """(compute_ms, total_ms) per part of the last call."""
+        P = len(self.devices)
+        a, t = (c_float * P)(), (c_float * P)()
+        check(lib().spmm_multi_get_times(self._c, a, t), "spmm_multi_get_times")
+        return list(a), list(t)
+
+    def close(self) -> None:
+        if getattr(self, "_c", None) is not None and self._c.value:
+            lib().spmm_multi_destroy(self._c)
+            self._c = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+__all__ = ["coo2csr", "MultiGPU", "csr2bsr", "bsr2csr", "Handle", "hybrid_csrmm", "default_handle", "gespmm_csrmm", "csrmm", "bsrmm", "bsrmm_f16",
            "SpmmError", "ORDER_ROW", "ORDER_COL"]

@@ -48,7 +48,8 @@ def kats() -> dict:
     y = np.array([10, 20, 30, 40, 50, 60, 70, 80], float).reshape(2, 4).T  # col-major 4x2
     z = A @ y
     rp = np.searchsorted(rows, np.arange(5)).tolist()
-    out["csrmm_cu"] = dict(src="csrmm.cu:47-99,148-149,183-185", m=4, k=4, n=2, rowptr=rp,
+    out["csrmm_cu"] = dict(src="csrmm.cu:47-99,148-149,183-185", m=4, k=4, n=2, coo_row=rows,
+                           rowptr=rp,
                            colind=cols, val=vals, B_colmajor=[10, 20, 30, 40, 50, 60, 70, 80],
                            ldb=4, ldc=4, C_colmajor=z.T.reshape(-1).tolist(),
                            survey=[190, 80, 510, 520, 430, 240, 1230, 1200])

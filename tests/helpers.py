@@ -45,6 +45,8 @@ def load_oracle() -> ctypes.CDLL:
         "oracle_bsrmm_d": (None, [I, I, I, I, P, P, P, P, I, I, ctypes.c_double,
                                   ctypes.c_double, P, I, I]),
         "oracle_spmm_cc_csr": (None, [I64, I64, P, P, P, I64, P]),
+        "oracle_spmm_cc_coo": (None, [I64, I64, I64, P, P, P, I64, P]),
+        "oracle_coo2csr": (None, [P, I, I, I, P]),
         "oracle_num_threads": (I, []),
         "oracle_reorder": (I, [I, I, P, P, P, P, P]),
         "oracle_bsrmm_f32": (None, [I, I, I, I, P, P, P, P, I, I, F, F, P, I, I]),

@@ -15,7 +15,7 @@ from conftest import ROOT
 
 def _declared() -> set[str]:
     names = set()
-    for h in ("spmm_hip.h", "spmm_host.h", "spmm_reorder.h"):
+    for h in ("spmm_hip.h", "spmm_host.h", "spmm_reorder.h", "spmm_multi.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(spmm_[a-z0-9_]+)\s*\(", src))
@@ -27,7 +27,8 @@ def test_headers_declare_the_boundary():
     for must in ("spmm_gespmm_csrmm_f32", "spmm_scsrmm", "spmm_scsrmm2", "spmm_sbsrmm",
                  "spmm_csrmm_ex_f32", "spmm_bsrmm_ex_f32", "spmm_bsrmm_ex_f16",
                  "spmm_xcsr2bsr_nnz", "spmm_scsr2bsr", "spmm_sbsr2csr", "spmm_calculate_nnzb",
-                 "spmm_csr_partition_rows"):
+                 "spmm_csr_partition_rows", "spmm_xcoo2csr", "spmm_csr_f32_multi",
+                 "spmm_multi_create"):
         assert must in d
 
 
@@ -67,6 +68,16 @@ def test_status_strings_and_host_side_checks():
                          None, 1, ctypes.byref(one), None, 1) == 1  # NOT_INITIALIZED
     assert L.spmm_csrmm_ex_f32(None, 1, 1, 1, 0, 1.0, None, None, None, 0, None, 1, 0, 0.0, None,
                                1, 0) == 1
+    # multi-GPU context: argument checks and the partition helper need no GPU
+    assert L.spmm_multi_destroy(None) == 1
+    assert L.spmm_multi_create(None, 1, None) == 3
+    assert L.spmm_csr_f32_multi(None, 4, 4, 4, None, None, None, None, None, None, 4, None, 4,
+                                1) == 1
+    b = (ctypes.c_int * 4)(0, 5, 9, 10)
+    assert L.spmm_multi_slot_rows(3, b, 1) == 5
+    assert L.spmm_multi_slot_rows(3, b, 2) == 3
+    assert L.spmm_multi_slot_rows(3, b, 0) == 0
+    assert L.spmm_xcoo2csr(None, None, 0, 0, None, 0) == 1
     d = ctypes.c_void_p()
     assert L.spmm_create_mat_descr(ctypes.byref(d)) == 0
     assert L.spmm_set_mat_index_base(d, 1) == 0

@@ -1,0 +1,181 @@
+"""BASELINE.json configs 1, 2 and 4 on the HIP path, each on its own inputs
+(SURVEY.md §8d table):
+
+* config 1: the graph spmm.cc's baseline is quoted on — randomCSRMatrix(16384,
+  16384, 2^-10) + randomDenseMatrix(16384, 32) from a fresh mt19937_64(1234),
+  whose digests tests/golden/ref_config1.json took from the reference's own
+  load_data.cc — run through the CSR kernel against the oracle, weighted and
+  pattern-only (spmm.cc's unit values);
+* config 2: the ogbn-arxiv stand-in (n = 169,343, nnz = 1,166,243), K = 128,
+  every element against the f64 oracle;
+* config 4: ogbn-products stand-in at K = 256, row-partitioned for 2 / 4 / 8
+  ranks on this one device (dist.make_shard, each shard into its slot of the
+  padded [world * max_rows, K] buffer the all-gather exchanges), reassembled
+  and compared with the whole-matrix run and sampled oracle rows; plus the
+  native single-process multi-GPU entry (spmm_csr_f32_multi over
+  ncclCommInitAll on this box's one GPU).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from helpers import TOL_F32, assert_normwise, oracle_csrmm_f64
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _dev(*arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+def _sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_config1_graph_on_the_gpu(oracle, device):
+    from spmm_hip import ops, prep
+    d = json.load(open(os.path.join(GOLDEN, "ref_config1.json")))
+    prep.rng_seed(1234)
+    rp, ci, v = prep.random_csr(d["m"], d["n"], d["p"])
+    B = prep.random_dense_matrix(d["m"], d["K"])
+    # the inputs are the reference's, bit for bit
+    assert ci.size == d["nnz"]
+    assert (_sha(rp), _sha(ci), _sha(v), _sha(B)) == (
+        d["rowptr_sha256"], d["colind_sha256"], d["val_sha256"], d["B_sha256"])
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    C = ops.gespmm_csrmm(drp, dci, dv, dB)
+    ones = torch.ones_like(dv)
+    Cp = ops.gespmm_csrmm(drp, dci, ones, dB)  # spmm.cc's pattern-only product
+    torch.cuda.synchronize()
+    ref, absd = oracle_csrmm_f64(oracle, d["m"], d["K"], rp, ci, v, B, d["K"], 0)
+    assert_normwise(C.cpu().numpy(), ref, absd, TOL_F32, "config 1 weighted")
+    # spmm.cc csr_spmm (double accumulation, unit values): the oracle restatement
+    ip64, ix64 = rp.astype(np.int64), ci.astype(np.int64)
+    Bd = B.astype(np.float64)
+    out = np.empty((d["m"], d["K"]))
+    from helpers import ptr
+    oracle.oracle_spmm_cc_csr(d["m"], d["K"], ptr(ip64), ptr(ix64), ptr(Bd), d["K"], ptr(out))
+    absp, _ = oracle_csrmm_f64(oracle, d["m"], d["K"], rp, ci, np.ones_like(v), np.abs(B),
+                               d["K"], 0)
+    assert_normwise(Cp.cpu().numpy(), out, absp, TOL_F32, "config 1 spmm.cc pattern-only")
+
+
+def test_config2_arxiv_size(oracle, device):
+    from spmm_hip import ops, prep
+    n, nnz, K = 169343, 1166243, 128
+    rp, ci = prep.powerlaw_csr(n, nnz, 13161, 2.3, 1234)
+    assert ci.size == nnz
+    rng = np.random.default_rng(5)
+    v = rng.uniform(-1, 1, nnz).astype(np.float32)
+    B = rng.uniform(-1, 1, (n, K)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    C = ops.gespmm_csrmm(drp, dci, dv, dB)
+    C2 = ops.gespmm_csrmm(drp, dci, dv, dB)
+    torch.cuda.synchronize()
+    assert torch.equal(C, C2), "not deterministic"
+    ref, absd = oracle_csrmm_f64(oracle, n, K, rp, ci, v, B, K, 0)
+    assert_normwise(C.cpu().numpy(), ref, absd, TOL_F32, "arxiv stand-in, every element")
+
+
+@pytest.fixture(scope="module")
+def products_k256():
+    from spmm_hip import prep
+    n, nnz, K = 2449029, 61859140, 256
+    rp, ci = prep.powerlaw_csr(n, nnz, 17481, 2.3, 1234)
+    v = np.random.default_rng(2).uniform(-1, 1, nnz).astype(np.float32)
+    return rp, ci, v, K
+
+
+def _sample_rows(rp, n, rng):
+    deg = np.diff(rp)
+    return np.unique(np.concatenate([rng.choice(n, 1500, replace=False), np.argsort(deg)[-20:]]))
+
+
+def _oracle_rows(oracle, rp, ci, v, Bh, rows, K):
+    deg = np.diff(rp)
+    sub_rp = np.concatenate([[0], np.cumsum(deg[rows])]).astype(np.int32)
+    sub_ci = np.concatenate([ci[rp[r]:rp[r + 1]] for r in rows]).astype(np.int32)
+    sub_v = np.concatenate([v[rp[r]:rp[r + 1]] for r in rows]).astype(np.float32)
+    return oracle_csrmm_f64(oracle, rows.size, K, sub_rp, sub_ci, sub_v, Bh, K, 0)
+
+
+def test_config4_products_k256_row_shards(oracle, device, products_k256):
+    from spmm_hip import dist as sdist
+    from spmm_hip import ops
+    rp, ci, v, K = products_k256
+    n = rp.size - 1
+    g = torch.Generator(device=device)
+    g.manual_seed(1234)
+    B = torch.rand((n, K), device=device, generator=g) * 2 - 1
+    drp, dci, dv = _dev(rp, ci, v)
+    Cw = torch.empty((n, K), device=device)
+    ops.csrmm(drp, dci, dv, B, n=K, k=n, ldb=K, C=Cw, ldc=K)
+    absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B.abs())
+    del drp, dci, dv
+    rng = np.random.default_rng(8)
+    rows = _sample_rows(rp, n, rng)
+    Bh = B.cpu().numpy()
+    ref, rabs = _oracle_rows(oracle, rp, ci, v, Bh, rows, K)
+    torch.cuda.synchronize()
+    assert_normwise(Cw.cpu().numpy()[rows], ref, rabs, TOL_F32, "products K=256 whole matrix")
+    for world in (2, 4, 8):
+        shards = [sdist.make_shard(rp, ci, v, r, world) for r in range(world)]
+        mr = shards[0].max_rows
+        # the padded buffer the in-place all-gather exchanges: rank r's rows
+        # in slot r, written there by the kernel
+        out = torch.full((world * mr, K), float("nan"), device=device)
+        for sh in shards:
+            srp, sci, sv = _dev(sh.rowptr, sh.colind, sh.val)
+            ops.csrmm(srp, sci, sv, B, m=sh.rows, n=K, k=n, ldb=K,
+                      C=out[sh.rank * mr: sh.rank * mr + sh.rows], ldc=K)
+        torch.cuda.synchronize()
+        C = torch.cat([out[r * mr: r * mr + shards[r].rows] for r in range(world)])
+        assert C.shape == Cw.shape
+        err = (C - Cw).abs()
+        assert bool((err <= 2 * TOL_F32 * absd + 1e-30).all()), f"world {world} vs whole matrix"
+        assert_normwise(C.cpu().numpy()[rows], ref, rabs, TOL_F32, f"world {world} sampled rows")
+        assert [sh.rows for sh in shards] == list(np.diff(shards[0].bounds))
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_config4_native_multi_entry(oracle, device, products_k256, chunks):
+    """spmm_csr_f32_multi (include/spmm_multi.h) over ncclCommInitAll on this
+    box's one GPU: one chunk is the same kernel on the same rows as the
+    whole-matrix call (bit-identical); four chunks overlap the exchange with
+    the compute and agree within the fp32 bar."""
+    from spmm_hip import ops, prep
+    rp, ci, v, K = products_k256
+    n = rp.size - 1
+    g = torch.Generator(device=device)
+    g.manual_seed(77)
+    B = torch.rand((n, K), device=device, generator=g) * 2 - 1
+    drp, dci, dv = _dev(rp, ci, v)
+    Cw = torch.empty((n, K), device=device)
+    ops.csrmm(drp, dci, dv, B, n=K, k=n, ldb=K, C=Cw, ldc=K)
+    mg = ops.MultiGPU([device.index or 0])
+    bounds = prep.partition_rows(rp, 1)
+    slot = ops.MultiGPU.slot_rows(bounds, chunks)
+    Cm = torch.empty((chunks * slot, K), device=device)
+    mg.set_timing(True)
+    mg.csrmm(bounds, [(drp, dci, dv)], [ci.size], [B], [Cm], m=n, n=K, k=n, ldb=K, ldc=K,
+             chunks=chunks)
+    mg.synchronize()
+    comp, tot = mg.times()
+    assert 0 < comp[0] <= tot[0]
+    torch.cuda.synchronize()
+    got = Cm[:n]
+    if chunks == 1:
+        assert torch.equal(got, Cw)
+    else:
+        absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B.abs())
+        assert bool(((got - Cw).abs() <= 2 * TOL_F32 * absd + 1e-30).all())
+    mg.close()

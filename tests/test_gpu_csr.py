@@ -74,6 +74,36 @@ def test_kat_csrmm_cu_via_scsrmm(oracle, golden, device):
     assert C.cpu().tolist() == k["C_colmajor"]
 
 
+def test_kat_csrmm_cu_coo_path(oracle, golden, device):
+    """csrmm.cu end to end: its COO rows through cusparseXcoo2csr
+    (csrmm.cu:148-149 -> spmm_xcoo2csr), then cusparseScsrmm; both index
+    bases; plus a larger row-sorted COO with empty rows against the oracle's
+    coo2csr."""
+    from helpers import ptr
+    k = golden["kats"]["csrmm_cu"]
+    ops = _ops()
+    for base in (0, 1):
+        rows = torch.tensor(np.array(k["coo_row"], np.int32) + base, device=device)
+        rp = ops.coo2csr(rows, k["m"], base=base)
+        torch.cuda.synchronize()
+        assert (rp.cpu().numpy() - base).tolist() == k["rowptr"]
+    rp = ops.coo2csr(torch.tensor(np.array(k["coo_row"], np.int32), device=device), k["m"])
+    ci, v = _dev(np.array(k["colind"], np.int32), np.array(k["val"], np.float32))
+    B = torch.tensor(k["B_colmajor"], dtype=torch.float32, device=device)
+    C = torch.zeros(8, dtype=torch.float32, device=device)
+    ops.csrmm(rp, ci, v, B, m=4, n=2, k=4, ldb=4, order_b=1, C=C, ldc=4, order_c=1)
+    assert C.cpu().tolist() == k["C_colmajor"]
+    rng = np.random.default_rng(4)
+    m = 100000
+    rows = np.sort(rng.integers(0, m, 700000)).astype(np.int32)
+    rows = rows[(rows % 7) != 3]  # every seventh row empty
+    want = np.zeros(m + 1, np.int32)
+    oracle.oracle_coo2csr(ptr(rows), rows.size, m, 0, ptr(want))
+    got = ops.coo2csr(torch.from_numpy(rows).to(device), m)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), want)
+
+
 def test_kat_try_cublas_dense_csr(golden, device):
     k = golden["kats"]["try_cublas_cu"]
     ops = _ops()

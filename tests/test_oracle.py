@@ -141,6 +141,51 @@ def test_kat_spmm_cc_small(oracle, golden):
     assert out.tolist() == k["out"]
 
 
+def test_kat_spmm_cc_small_coo(oracle, golden):
+    """spmm.cc:54-61 test_small_coo_spmm: the same product from COO rows
+    {0, 1, 1}, cols {1, 0, 2} (spmm.cc:56) through coo_spmm (:27-43)."""
+    k = golden["kats"]["spmm_cc_small"]
+    row = np.array([0, 1, 1], np.int64)
+    col = np.array([1, 0, 2], np.int64)
+    D = np.array(k["dense"], np.float64)
+    out = np.full(k["m"] * k["n"], np.nan)
+    oracle.oracle_spmm_cc_coo(k["m"], k["n"], 3, ptr(row), ptr(col), ptr(D), k["n"], ptr(out))
+    assert out.tolist() == k["out"]
+
+
+def test_coo_spmm_matches_csr_spmm(oracle):
+    """coo_spmm and csr_spmm of spmm.cc on one random pattern (double, unit
+    values; the atomic adds may reorder a sum, hence the 1e-12 bar)."""
+    from spmm_hip import prep
+    prep.rng_seed(1234)
+    rp, ci, _ = prep.random_csr(3000, 2500, 0.01)
+    m, K = 3000, 17
+    D = np.random.default_rng(3).uniform(-1, 1, (2500, K))
+    row = np.repeat(np.arange(m, dtype=np.int64), np.diff(rp))
+    col = ci.astype(np.int64)
+    a, b = np.empty((m, K)), np.empty((m, K))
+    ip = rp.astype(np.int64)
+    oracle.oracle_spmm_cc_csr(m, K, ptr(ip), ptr(col), ptr(D), K, ptr(a))
+    oracle.oracle_spmm_cc_coo(m, K, col.size, ptr(row), ptr(col), ptr(D), K, ptr(b))
+    assert np.abs(a - b).max() <= 1e-12
+
+
+def test_coo2csr_kat(oracle, golden):
+    """cusparseXcoo2csr on csrmm.cu's COO (csrmm.cu:47-99,148-149) gives the
+    KAT's row pointer, in both index bases; empty rows and trailing rows too."""
+    k = golden["kats"]["csrmm_cu"]
+    rows = np.array(k["coo_row"], np.int32)
+    for base in (0, 1):
+        out = np.zeros(k["m"] + 1, np.int32)
+        rb = rows + base
+        oracle.oracle_coo2csr(ptr(rb), rows.size, k["m"], base, ptr(out))
+        assert (out - base).tolist() == k["rowptr"]
+    rows = np.array([1, 1, 4, 4, 4], np.int32)  # rows 0, 2, 3, 5, 6 empty
+    out = np.zeros(8, np.int32)
+    oracle.oracle_coo2csr(ptr(rows), 5, 7, 0, ptr(out))
+    assert out.tolist() == [0, 0, 2, 2, 2, 5, 5, 5]
+
+
 def _divide_fixture(golden, g, bs, tag="all"):
     r = golden["ref"]
     return [r[f"{g}_bs{bs}_{tag}_{nm}"] for nm in ("csr_rp", "csr_ci", "bsr_rp", "bsr_ci",
