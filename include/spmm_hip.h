@@ -335,7 +335,14 @@ spmm_status_t spmm_dbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_opera
 #define SPMM_HYBRID_TWO_LAUNCH 2
 /* Opt-in: the bs = 32 dense-block part computes each fp32 product as six
  * bf16 MFMA products of an exact three-way bf16 split of A and B (dropped
- * terms < 2^-21 |a||b| per product; accumulation in fp32). DESIGN.md §4a. */
+ * terms < 2^-21 |a||b| per product; accumulation in fp32). DESIGN.md §4a.
+ * Inf and NaN inputs pass through the high part (the lower parts are zeroed),
+ * so non-finite values propagate as in the fp32 path. The flag takes effect
+ * only on the bs = 32 LDS-staged forms: the fused launch, and the two-launch
+ * BSR part when n % 4 == 0, ldb % 4 == 0 and B / bsrVal are 16-byte aligned;
+ * elsewhere (bs != 32, other layouts, a tuning SPMM_BSR_VARIANT override) the
+ * dense-block part runs the plain fp32 MFMA kernel, with the same result
+ * within the fp32 bar. */
 #define SPMM_HYBRID_SPLIT_BF16 4
 spmm_status_t spmm_set_hybrid_options(spmm_handle_t handle, int flags);
 

@@ -375,8 +375,12 @@ __device__ __forceinline__ void split3_bf16(const float* x, bf16x8& hi, bf16x8& 
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const unsigned x0 = __float_as_uint(x[2 * p]), x1 = __float_as_uint(x[2 * p + 1]);
-    const float r0 = x[2 * p] - __uint_as_float(x0 & 0xffff0000u);
-    const float r1 = x[2 * p + 1] - __uint_as_float(x1 & 0xffff0000u);
+    // Inf / NaN: hi carries the value (Inf - Inf would make mid and lo NaN)
+    const float r0 = (x0 & 0x7f800000u) == 0x7f800000u ? 0.f
+                                                        : x[2 * p] - __uint_as_float(x0 & 0xffff0000u);
+    const float r1 = (x1 & 0x7f800000u) == 0x7f800000u
+                         ? 0.f
+                         : x[2 * p + 1] - __uint_as_float(x1 & 0xffff0000u);
     const unsigned q0 = __float_as_uint(r0), q1 = __float_as_uint(r1);
     const float l0 = r0 - __uint_as_float(q0 & 0xffff0000u);
     const float l1 = r1 - __uint_as_float(q1 & 0xffff0000u);
@@ -1918,7 +1922,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                           mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, nullptr,       \
                           nullptr, nullptr, 0);
     // split-bf16 (opt-in): wave-pair split-K form for row-major C (products
-    // hybrid 1.83 vs 1.87 ms fused, reddit 0.79 vs 0.82), else one k range per wave
+    // hybrid 1.86-1.87 vs 1.89 ms fused, reddit 0.80 vs 0.83, profiles/r01_hybrid_split.jsonl), else one k range per wave
     if (dense_blocks && var < 0 && (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16))
       lv = crow ? 4927 : 4926;
     switch (lv) {

@@ -68,6 +68,51 @@ def test_kat_block_cublas(golden, device):
     assert C.cpu().tolist() == k["C_colmajor"]
 
 
+def test_reference_random_bsr_fixture(oracle, golden, device):
+    """randomBSRMatrix's own output (load_data.cc:81-113, compiled from the
+    reference into oracle/_ref: ref_host.npz bsr_12_10_4) through
+    cusparseSbsrmm's shapes, both B layouts, against the oracle."""
+    r = golden["ref"]
+    rp, ci, v = r["bsr_12_10_4_rowptr"], r["bsr_12_10_4_colind"], r["bsr_12_10_4_val"]
+    mb, kb, bs = 12, 10, 4
+    for n, ob in ((7, 0), (64, 1)):
+        B = np.random.default_rng(n).uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+        Bl = B if ob == 0 else np.ascontiguousarray(B.T)
+        drp, dci, dv, dB = _dev(rp, ci, v, Bl)
+        C = torch.zeros((n, mb * bs), dtype=torch.float32, device=device)  # col-major
+        _ops().bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n if ob == 0 else kb * bs,
+                     order_b=ob, C=C, ldc=mb * bs, order_c=1)
+        torch.cuda.synchronize()
+        ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
+        assert_normwise(C.cpu().numpy().T, ref, absd, TOL_F32, f"randomBSRMatrix n={n}")
+
+
+@pytest.mark.parametrize("bs,p,n", [(16, 0.05, 128), (32, 0.05, 128), (16, 0.1, 512)])
+def test_reference_generator_bsr_on_mfma(oracle, device, bs, p, n):
+    """randomBSRMatrix from the library's host generator (bit-exact with the
+    reference's, tests/test_prep.py) at the MFMA block sizes, row-major B and
+    C (the shipped kernels) and fp16 at bs 16."""
+    from spmm_hip import prep
+    mb = 4096 // bs
+    prep.rng_seed(1234)
+    rp, ci, v = prep.random_bsr(mb, mb, bs, p)
+    B = prep.random_dense_matrix(mb * bs, n)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    C = torch.empty((mb * bs, n), dtype=torch.float32, device=device)
+    _ops().bsrmm(drp, dci, dv, dB, mb=mb, kb=mb, n=n, bs=bs, ldb=n, C=C, ldc=n)
+    torch.cuda.synchronize()
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
+    assert_normwise(C.cpu().numpy(), ref, absd, TOL_F32, f"random_bsr bs={bs} fp32")
+    if bs == 16:
+        v16, B16 = v.astype(np.float16), B.astype(np.float16)
+        C16 = torch.empty((mb * bs, n), dtype=torch.float32, device=device)
+        _ops().bsrmm_f16(drp, dci, dv.half(), dB.half(), mb=mb, kb=mb, n=n, bs=bs, ldb=n, C=C16,
+                         ldc=n)
+        torch.cuda.synchronize()
+        ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v16, B16, n, 0, half=True)
+        assert_normwise(C16.cpu().numpy(), ref, absd, TOL_F16_ACC, "random_bsr bs=16 fp16")
+
+
 @pytest.mark.parametrize("bs", [2, 3, 4, 8, 16, 32, 64])
 @pytest.mark.parametrize("direction", [0, 1])
 @pytest.mark.parametrize("orders", [(0, 0), (1, 1), (0, 1)])
@@ -229,6 +274,64 @@ def test_hybrid_fused_vs_two_launch(oracle, device, n, K, alpha, beta):
     assert same > 0.9, f"only {same:.3f} of rows identical to the two-launch form"
     # padding rows (n .. nb*32): the BSR epilogue of an empty tail
     np.testing.assert_allclose(fused[n:], two[n:], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("form", ["fused", "two_launch"])
+def test_hybrid_split_bf16_alpha_beta_and_inf(oracle, device, form):
+    """The split-bf16 epilogues with alpha != 1 and beta != 0 (C read), both
+    launch forms; and an Inf in a dense block propagates as in fp32 (the
+    split keeps Inf in the high part instead of making Inf - Inf = NaN)."""
+    from spmm_hip import prep
+    from spmm_hip._lib import HYBRID_FUSED, HYBRID_SPLIT_BF16, HYBRID_TWO_LAUNCH
+    ops = _ops()
+    rng = np.random.default_rng(31)
+    n, K, bs = 1000, 128, 32
+    rp, ci, v = _rand_csr_blocky(rng, n, bs)
+    parts = prep.divide(n, rp, ci, v, bs, 0.25)
+    mb = (n + bs - 1) // bs
+    B = rng.uniform(-1, 1, (mb * bs, K)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (mb * bs, K)).astype(np.float32)
+    alpha, beta = 0.75, -1.25
+    flags = HYBRID_SPLIT_BF16 | (HYBRID_FUSED if form == "fused" else HYBRID_TWO_LAUNCH)
+    h = ops.Handle()
+    h.set_hybrid_options(flags)
+    d = _dev(*parts)
+    dB, dC = _dev(B, C0)
+    ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), dB, m=n, n=K, k=n, bs=bs, ldb=K, C=dC, ldc=K,
+                     alpha=alpha, beta=beta, handle=h)
+    torch.cuda.synchronize()
+    ref, absd = oracle_csrmm_f64(oracle, n, K, rp, ci, v, B[:n], K, 0)
+    want = alpha * ref + beta * C0[:n].astype(np.float64)
+    bound = abs(alpha) * absd + abs(beta) * np.abs(C0[:n])
+    assert_normwise(dC.cpu().numpy()[:n], want, bound, TOL_F32, f"split-bf16 {form} alpha/beta")
+    # Inf in one dense-block value: rows meeting it become +-Inf, none NaN
+    bval = parts[5].copy()
+    assert bval.size
+    bval[0] = np.inf
+    d2 = _dev(parts[0], parts[1], parts[2], parts[3], parts[4], bval)
+    dC2 = torch.empty((mb * bs, K), dtype=torch.float32, device=device)
+    ops.hybrid_csrmm(tuple(d2[0:3]), tuple(d2[3:6]), dB, m=n, n=K, k=n, bs=bs, ldb=K, C=dC2,
+                     ldc=K, handle=h)
+    torch.cuda.synchronize()
+    got = dC2.cpu().numpy()
+    r0 = 0  # block 0 of block row 0, entry (0, 0): row 0, column 32 * bci[0]
+    assert np.isinf(got[r0]).all() and not np.isnan(got[:n]).any()
+    h.close()
+
+
+def _rand_csr_blocky(rng, n, bs):
+    """A CSR with dense diagonal-ish blocks plus scattered entries (so divide
+    keeps a BSR part and a CSR remainder)."""
+    rows = []
+    for r in range(n):
+        b = r // bs
+        dense = b * bs + rng.choice(bs, 20, replace=False)
+        far = rng.choice(n, 3, replace=False)
+        rows.append(np.unique(np.concatenate([dense[dense < n], far])))
+    rp = np.concatenate([[0], np.cumsum([len(x) for x in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    v = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    return rp, ci, v
 
 
 @pytest.mark.parametrize("form", ["fused", "two_launch"])
