@@ -567,7 +567,9 @@ def run_bsr(args, W, world, rank, dev, dist):
     ntiles = (K + tile - 1) // tile
     dense_flops = 2.0 * nnzb * bs * bs * K    # SURVEY §8d "MFMA-executed" (dense blocks)
     if cm and bs == 32:
-        mfma_flops = active_pairs * 2.0 * bs * 2 * K   # one 32x32x2 step per active pair
+        # column stream: two v_mfma_f32_32x32x1_2b_f32 (32 rows x 64 columns,
+        # k = 1) per nonzero column of a block and 128 output columns
+        mfma_flops = active_cols * 2.0 * bs * K
     else:
         mfma_flops = dense_flops
     peak = MFMA_PEAK_TFLOPS[dt]
@@ -592,7 +594,7 @@ def run_bsr(args, W, world, rank, dev, dist):
         roofline={"bound": "hbm", "achieved": round(cm_bytes / t / 1e9, 1),
                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                   "frac": round(cm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-                  "kernel": (("bsr32_f32_cm4_kernel" if bs == 32 else
+                  "kernel": (("bsr32_f32_cs_kernel" if bs == 32 else
                               f"bsr16_cm_kernel<{'f32' if dt == 'fp32' else 'f16'}>")
                              + (" (column-major C epilogue, B staged row-major)"
                                 if args.bsr_layout == "col" else "") if cm else

@@ -370,28 +370,45 @@ __device__ __forceinline__ int xcd_block_row(int b, int mb, int xm) {
 // 32 cycles in place of 8 fp32 ones of 64.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void split3_bf16(const float* x, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
-  u32x4 h, m, l;
+__device__ __forceinline__ void split3_bf16(const float* x, bf16x8& hi, bf16x8& hif, bf16x8& mid,
+                                            bf16x8& lo) {
+  u32x4 h, hf, m, l;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const unsigned x0 = __float_as_uint(x[2 * p]), x1 = __float_as_uint(x[2 * p + 1]);
+    const bool f0 = (x0 & 0x7f800000u) != 0x7f800000u, f1 = (x1 & 0x7f800000u) != 0x7f800000u;
     // Inf / NaN: hi carries the value (Inf - Inf would make mid and lo NaN)
-    const float r0 = (x0 & 0x7f800000u) == 0x7f800000u ? 0.f
-                                                        : x[2 * p] - __uint_as_float(x0 & 0xffff0000u);
-    const float r1 = (x1 & 0x7f800000u) == 0x7f800000u
-                         ? 0.f
-                         : x[2 * p + 1] - __uint_as_float(x1 & 0xffff0000u);
+    const float r0 = f0 ? x[2 * p] - __uint_as_float(x0 & 0xffff0000u) : 0.f;
+    const float r1 = f1 ? x[2 * p + 1] - __uint_as_float(x1 & 0xffff0000u) : 0.f;
     const unsigned q0 = __float_as_uint(r0), q1 = __float_as_uint(r1);
     const float l0 = r0 - __uint_as_float(q0 & 0xffff0000u);
     const float l1 = r1 - __uint_as_float(q1 & 0xffff0000u);
     // upper halves of (elem 2p, elem 2p+1) -> one packed bf16 pair, low k first
     h[p] = __builtin_amdgcn_perm(x1, x0, 0x07060302u);
+    hf[p] = __builtin_amdgcn_perm(f1 ? x1 : 0u, f0 ? x0 : 0u, 0x07060302u);
     m[p] = __builtin_amdgcn_perm(q1, q0, 0x07060302u);
     l[p] = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
   }
   hi = __builtin_bit_cast(bf16x8, h);
+  hif = __builtin_bit_cast(bf16x8, hf);
   mid = __builtin_bit_cast(bf16x8, m);
   lo = __builtin_bit_cast(bf16x8, l);
+}
+
+// The six split products of one k range into acc. The high parts meet the
+// other operand's mid / lo parts in their finite-only form (hif: Inf / NaN
+// lanes zeroed), so a non-finite a meets b only through hi x hi, as an fp32
+// product would: Inf * (b_mid = 0) would otherwise add a NaN.
+__device__ __forceinline__ f32x16 split_mfma6(const bf16x8& ah, const bf16x8& ahf,
+                                              const bf16x8& am, const bf16x8& al,
+                                              const bf16x8& bh, const bf16x8& bhf,
+                                              const bf16x8& bm, const bf16x8& bl, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bhf, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahf, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bhf, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahf, bm, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
 
 // HB: remainder gathers in flight per wave in the fused hybrid (HYB).
@@ -481,22 +498,12 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
         fb0[i] = bp[i * 128];
         fb1[i] = bp[i * 128 + 32];
       }
-      bf16x8 ah, am, al, bh, bm, bl;
-      split3_bf16(fa8, ah, am, al);
-      split3_bf16(fb0, bh, bm, bl);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
-      split3_bf16(fb1, bh, bm, bl);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc1, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc1, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc1, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc1, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc1, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc1, 0, 0, 0);
+      bf16x8 ah, ahf, am, al, bh, bhf, bm, bl;
+      split3_bf16(fa8, ah, ahf, am, al);
+      split3_bf16(fb0, bh, bhf, bm, bl);
+      acc = split_mfma6(ah, ahf, am, al, bh, bhf, bm, bl, acc);
+      split3_bf16(fb1, bh, bhf, bm, bl);
+      acc1 = split_mfma6(ah, ahf, am, al, bh, bhf, bm, bl, acc1);
       st = st == D - 1 ? 0 : st + 1;
       continue;
     }
@@ -515,15 +522,10 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
       // lane (r, h) element i of MFMA j is k = 16h + 8j + i, for A and B alike
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        bf16x8 ah, am, al, bh, bm, bl;
-        split3_bf16(fa + 8 * j, ah, am, al);
-        split3_bf16(fb + 8 * j, bh, bm, bl);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+        bf16x8 ah, ahf, am, al, bh, bhf, bm, bl;
+        split3_bf16(fa + 8 * j, ah, ahf, am, al);
+        split3_bf16(fb + 8 * j, bh, bhf, bm, bl);
+        acc = split_mfma6(ah, ahf, am, al, bh, bhf, bm, bl, acc);
       }
     } else {
 #pragma unroll
@@ -1001,6 +1003,342 @@ __global__ __launch_bounds__(256) void bsr32_f32_cm4_kernel(
       const size_t row = row0 + 8 * g + 4 * h + e;
       float* p = C + row * ldc + jcol;
       *p = epi(acc[4 * g + e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 32, column stream (CS; ROW blocks, row-major B): one wave per (block
+// row, 128 output columns), no barriers. The block-level kernels above keep
+// four waves in step on one block at a time, so every block costs a barrier
+// chain and a B stage sized for 32 rows although 73-82 % of the blocks on
+// the stand-ins hold one nonzero column. Here a wave streams the block row as
+// a sequence of ITEMS, one per pair of nonzero columns (c0, c1) of a block
+// (a single column when the count is odd):
+//  * A ring (NA slots x 4 KB of LDS): block k + DA is copied by LDS-DMA (4 x
+//    global_load_lds_dwordx4, the XOR-swizzled layout of the kernels above)
+//    when the producer reaches block k. Its column mask comes from 8
+//    ds_read2st64_b32 (lane l reads column l % 32 of 16 rows, rows r and
+//    r + 16 share a swizzle), a masked OR of the 16 values and one ballot:
+//    no cross-lane reduction.
+//  * Item ring (P slots x 1 KB of LDS): an item's two B rows (512 B each,
+//    lanes 0-31 row c0, lanes 32-63 row c1) are one global_load_lds_dwordx4;
+//    its two A columns are read from the A slot into registers at issue time
+//    (a static ring of 2P VGPRs: the loop is unrolled P times), so the A slot
+//    is free as soon as the block's last item is issued.
+//  * The item issued P steps earlier is consumed: two ds_read_b64 and
+//    v_mfma_f32_32x32x1_2b_f32 per column and 64-column half. The 2-block
+//    form takes one k per MFMA, so a single column costs 2 MFMAs (128 cycles)
+//    and a pair 4 — the 32x32x2 step of a lone column is half zeros.
+// Waits: every vector-memory operation of the loop is an LDS-DMA copy (B rows,
+// A blocks) and they retire in issue order (MI355X_MICROARCH.md §vmcnt), so
+// the wave keeps a count of copies issued; each slot records the count at
+// its copy and the wait for it is vmcnt(q), q the largest ladder value not
+// above the number of younger copies (wait_vm_older). All LDS reads are inline
+// asm that end in lgkmcnt(0): their results exist when the compiler sees
+// them, and hipcc puts no conservative vmcnt(0) before them.
+// Tile columns: MFMA half u (0, 1) block b (lane / 32 of the B operand) holds
+// output column 4j + 2b + u of lane j, so a lane's B operands of one row are
+// one float2 and its four accumulators of one row are one float4 of C.
+// ---------------------------------------------------------------------------
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// s_waitcnt vmcnt(q), q = the largest value <= y of the ladder
+// 0 1 2 3 4 6 8 12 16 24 32 48: retires the operation that has y younger
+// vector-memory operations, over-waiting by at most a quarter of y (vmcnt is
+// 6 bits: y >= 63 needs no wait). A compare tree in one asm statement: as C,
+// hipcc's structurizer turned each leaf into a chain of exec-mask moves.
+__device__ __forceinline__ void wait_vm_older(int y) {
+  asm volatile(
+      "s_cmp_gt_i32 %0, 62\n\t"
+      "s_cbranch_scc1 20f\n\t"
+      "s_cmp_gt_i32 %0, 15\n\t"
+      "s_cbranch_scc1 16f\n\t"
+      "s_cmp_gt_i32 %0, 7\n\t"
+      "s_cbranch_scc1 8f\n\t"
+      "s_cmp_gt_i32 %0, 3\n\t"
+      "s_cbranch_scc1 4f\n\t"
+      "s_cmp_gt_i32 %0, 1\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_cmp_gt_i32 %0, 0\n\t"
+      "s_cbranch_scc1 1f\n\t"
+      "s_waitcnt vmcnt(0)\n\t"
+      "s_branch 20f\n"
+      "1:\n\t"
+      "s_waitcnt vmcnt(1)\n\t"
+      "s_branch 20f\n"
+      "2:\n\t"
+      "s_cmp_gt_i32 %0, 2\n\t"
+      "s_cbranch_scc1 3f\n\t"
+      "s_waitcnt vmcnt(2)\n\t"
+      "s_branch 20f\n"
+      "3:\n\t"
+      "s_waitcnt vmcnt(3)\n\t"
+      "s_branch 20f\n"
+      "4:\n\t"
+      "s_cmp_gt_i32 %0, 5\n\t"
+      "s_cbranch_scc1 6f\n\t"
+      "s_waitcnt vmcnt(4)\n\t"
+      "s_branch 20f\n"
+      "6:\n\t"
+      "s_waitcnt vmcnt(6)\n\t"
+      "s_branch 20f\n"
+      "8:\n\t"
+      "s_cmp_gt_i32 %0, 11\n\t"
+      "s_cbranch_scc1 12f\n\t"
+      "s_waitcnt vmcnt(8)\n\t"
+      "s_branch 20f\n"
+      "12:\n\t"
+      "s_waitcnt vmcnt(12)\n\t"
+      "s_branch 20f\n"
+      "16:\n\t"
+      "s_cmp_gt_i32 %0, 31\n\t"
+      "s_cbranch_scc1 32f\n\t"
+      "s_cmp_gt_i32 %0, 23\n\t"
+      "s_cbranch_scc1 24f\n\t"
+      "s_waitcnt vmcnt(16)\n\t"
+      "s_branch 20f\n"
+      "24:\n\t"
+      "s_waitcnt vmcnt(24)\n\t"
+      "s_branch 20f\n"
+      "32:\n\t"
+      "s_cmp_gt_i32 %0, 47\n\t"
+      "s_cbranch_scc1 48f\n\t"
+      "s_waitcnt vmcnt(32)\n\t"
+      "s_branch 20f\n"
+      "48:\n\t"
+      "s_waitcnt vmcnt(48)\n"
+      "20:"
+      :
+      : "s"(y)
+      : "scc", "memory");
+}
+
+template <bool CROW, int XM, int P, int NA>
+__global__ __launch_bounds__(64) void bsr32_f32_cs_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  static_assert(NA >= 2 && NA <= 4 && P >= 2 && P <= 16, "ring depths");
+  constexpr int DA = NA - 1;  // A blocks in flight ahead of the producer's block
+  constexpr int kRings = NA * 1024 + P * 256;  // floats
+  // (column-major C reuses the LDS for a 128 x 36-float tile)
+  __shared__ __attribute__((aligned(16))) float smem[CROW || kRings >= 128 * 36 ? kRings : 128 * 36];
+  const int lane = threadIdx.x;
+  const int j = lane & 31, h = lane >> 5;
+  const int br = xcd_block_row(blockIdx.x, mb, XM);
+  const int jt = blockIdx.y * 128;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  const unsigned lds_a = (unsigned)reinterpret_cast<uintptr_t>(smem);
+  const unsigned lds_b = lds_a + NA * 4096u;
+
+  // A copy q (0..3) of a block: lane l -> row 8q + l/8, logical chunk
+  // (l % 8) ^ ((row / 2) % 8); rows of copies q and q + 2 share the swizzle.
+  int a_src[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 8 * q + (lane >> 3);
+    a_src[q] = r * 32 + 4 * ((lane & 7) ^ ((r >> 1) & 7));
+  }
+  auto issue_a = [&](int kk, int slot) {
+    const float* src = val + (size_t)kk * 1024;
+    float* dst = smem + slot * 1024;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(src + a_src[q & 1] + 512 * (q >> 1)),
+                                       (lds_void_t)(dst + 256 * q), 16, 0, 0);
+  };
+  // Mask reads: rows 2i + h and 2i + h + 16 (i = 0..7), column j; row r holds
+  // column c at byte r*128 + 16*((c/4) ^ ((r/2) % 8)) + 4*(c % 4).
+  unsigned moff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    moff[i] = (unsigned)((2 * i + h) * 128 + 16 * ((j >> 2) ^ i) + 4 * (j & 3));
+  auto mask_of = [&](int slot) -> unsigned {
+    const unsigned base = lds_a + 4096u * (unsigned)slot;
+    f32x2 x[8];
+    asm volatile(
+        "ds_read2st64_b32 %0, %8 offset1:8\n\t"
+        "ds_read2st64_b32 %1, %9 offset1:8\n\t"
+        "ds_read2st64_b32 %2, %10 offset1:8\n\t"
+        "ds_read2st64_b32 %3, %11 offset1:8\n\t"
+        "ds_read2st64_b32 %4, %12 offset1:8\n\t"
+        "ds_read2st64_b32 %5, %13 offset1:8\n\t"
+        "ds_read2st64_b32 %6, %14 offset1:8\n\t"
+        "ds_read2st64_b32 %7, %15 offset1:8\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]),
+          "=&v"(x[6]), "=&v"(x[7])
+        : "v"(base + moff[0]), "v"(base + moff[1]), "v"(base + moff[2]), "v"(base + moff[3]),
+          "v"(base + moff[4]), "v"(base + moff[5]), "v"(base + moff[6]), "v"(base + moff[7])
+        : "memory");
+    unsigned t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      t |= (__float_as_uint(x[i][0]) | __float_as_uint(x[i][1])) & 0x7fffffffu;  // +-0 is zero
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(t != 0u);
+    return (unsigned)b | (unsigned)(b >> 32);
+  };
+  // A column c of the block in `slot`, lane (j, h): A[j][c]
+  const unsigned a_row = (unsigned)(j * 128);
+  const int a_sw = (j >> 1) & 7;
+  auto a_cols = [&](int slot, int c0, int c1, float& x0, float& x1) {
+    const unsigned base = lds_a + 4096u * (unsigned)slot + a_row;
+    const unsigned p0 = base + 16u * (unsigned)((c0 >> 2) ^ a_sw) + 4u * (unsigned)(c0 & 3);
+    const unsigned p1 = base + 16u * (unsigned)((c1 >> 2) ^ a_sw) + 4u * (unsigned)(c1 & 3);
+    asm volatile(
+        "ds_read_b32 %0, %2\n\t"
+        "ds_read_b32 %1, %3\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x0), "=&v"(x1)
+        : "v"(p0), "v"(p1)
+        : "memory");
+  };
+  const int bcol = min(jt + 4 * j, n - 4);
+  const unsigned b_rd = lds_b + 16u * (unsigned)j + 8u * (unsigned)h;
+
+  f32x32 u0, u1;  // MFMA halves u = 0, 1 (output columns 4j + 2b + u)
+#pragma unroll
+  for (int e = 0; e < 32; ++e) u0[e] = u1[e] = 0.f;
+
+  int nis = 0;  // copies issued by this wave
+  int ast[DA];  // copy count at each A block in flight (k+1 .. k+DA)
+  int aslot = NA - 1;
+  int k = k0 - 1;
+  unsigned m = 0;
+  bool more = true;
+  int bc = 0, bcn = k0 < k1 ? colind[k0] : 0;
+#pragma unroll
+  for (int d = 0; d < DA; ++d) {
+    if (k0 + d < k1) {
+      issue_a(k0 + d, d);
+      nis += 4;
+      ast[d] = nis;
+    } else {
+      ast[d] = -64;
+    }
+  }
+  int kind[P], stamp[P];
+  float ra0[P], ra1[P];
+#pragma unroll
+  for (int s = 0; s < P; ++s) {
+    kind[s] = 0;
+    stamp[s] = 0;
+    ra0[s] = ra1[s] = 0.f;
+  }
+
+  for (;;) {
+    const bool fin = !more;
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      // consume the item issued P steps ago
+      if (kind[s]) {
+        wait_vm_older(nis - stamp[s]);
+        f32x2 b0, b1;
+        asm volatile(
+            "ds_read_b64 %0, %2 offset:%3\n\t"
+            "ds_read_b64 %1, %2 offset:%4\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(b0), "=&v"(b1)
+            : "v"(b_rd), "n"(s * 1024), "n"(s * 1024 + 512)
+            : "memory");
+        u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(ra0[s], b0[0], u0, 0, 0, 0);
+        u1 = __builtin_amdgcn_mfma_f32_32x32x1f32(ra0[s], b0[1], u1, 0, 0, 0);
+        if (kind[s] == 2) {
+          u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(ra1[s], b1[0], u0, 0, 0, 0);
+          u1 = __builtin_amdgcn_mfma_f32_32x32x1f32(ra1[s], b1[1], u1, 0, 0, 0);
+        }
+      }
+      // produce the next item into slot s
+      kind[s] = 0;
+      if (more) {
+        while (m == 0u) {
+          if (k + 1 >= k1) {
+            more = false;
+            break;
+          }
+          ++k;
+          aslot = aslot + 1 == NA ? 0 : aslot + 1;
+          wait_vm_older(nis - ast[0]);  // A(k) landed
+#pragma unroll
+          for (int d = 0; d + 1 < DA; ++d) ast[d] = ast[d + 1];
+          bc = bcn;
+          bcn = colind[min(k + 1, k1 - 1)];
+          m = mask_of(aslot);
+          if (k + DA < k1) {
+            issue_a(k + DA, aslot + DA >= NA ? aslot + DA - NA : aslot + DA);
+            nis += 4;
+            ast[DA - 1] = nis;
+          } else {
+            ast[DA - 1] = -64;
+          }
+        }
+        if (m != 0u) {
+          const int c0 = __builtin_ctz(m);
+          m &= m - 1u;
+          int c1 = c0;
+          kind[s] = 1;
+          if (m != 0u) {
+            c1 = __builtin_ctz(m);
+            m &= m - 1u;
+            kind[s] = 2;
+          }
+          a_cols(aslot, c0, c1, ra0[s], ra1[s]);
+          const float* src = B + (size_t)(bc * 32 + (h ? c1 : c0)) * ldb + bcol;
+          __builtin_amdgcn_global_load_lds((gbl_void_t)src, (lds_void_t)(smem + NA * 1024 + s * 256),
+                                           16, 0, 0);
+          stamp[s] = ++nis;
+        }
+      }
+    }
+    // keeps the accumulators in AGPRs across the loop (else hipcc parks one
+    // in VGPRs at the loop head and copies it back before the first MFMA)
+    asm volatile("" : "+a"(u0), "+a"(u1));
+    if (fin) break;
+  }
+
+  // Epilogue. Lane (j, h), accumulator element e: row (e % 4) + 8 (e / 4) + 4h
+  // of the block row; u0 / u1 block 0 -> columns 4j, 4j + 1, block 1 ->
+  // 4j + 2, 4j + 3.
+  if constexpr (CROW) {
+    const int col = jt + 4 * j;
+    if (col >= n) return;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const size_t row = (size_t)br * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      f32x4* p = reinterpret_cast<f32x4*>(C + row * ldc + col);
+      f32x4 v = {u0[e], u1[e], u0[16 + e], u1[16 + e]};
+      if (beta == 0.f) {
+        v *= alpha;
+      } else {
+        const f32x4 c = *p;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
+      }
+      *p = v;
+    }
+  } else {
+    // column-major C: the tile goes through LDS as [column][row] (36-float
+    // columns), then each store writes two 128-B column segments
+    constexpr int kTs = 36;
+    float* tile = smem;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+      tile[(4 * j) * kTs + row] = u0[e];
+      tile[(4 * j + 1) * kTs + row] = u1[e];
+      tile[(4 * j + 2) * kTs + row] = u0[16 + e];
+      tile[(4 * j + 3) * kTs + row] = u1[16 + e];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const size_t row = (size_t)br * 32 + j;
+    for (int it = 0; it < 64; ++it) {
+      const int jl = 2 * it + h;
+      if (jt + jl < n) {
+        float* p = C + (size_t)(jt + jl) * ldc + row;
+        *p = epi(tile[jl * kTs + j], alpha, beta, p);
+      }
     }
   }
 }
@@ -1828,8 +2166,10 @@ constexpr int kBsr32Default = 40;
 // B stages D, A stages DA; (2, 5) fits 3 workgroups per CU and is the
 // fastest measured (reddit stand-in 2.65 ms vs 4.57 for 4124; products bs = 32
 // 4.62 vs 8.51; (3, 6) 3.08 / 5.60; (4, 8) 4.87 / 9.09).
-constexpr int kBsr32LdsDefault = 4402;  // CM4 (4 workgroups per CU): products
-                                         // 4.39 vs 4.58 ms for 4225, reddit equal
+// Column stream (bsr32_f32_cs_kernel, 8 item slots, 3 A slots): products
+// stand-in 3.18 vs 4.38 ms for CM4 (4402), reddit 2.13 vs 2.59
+// (profiles/r02_cs_sweep.jsonl).
+constexpr int kBsr32LdsDefault = 4583;
 // Blocks known to be dense (the hybrid's BSR part, MFMA-pipe bound): the
 // full-panel kernel with D = 2 (40 KB, 4 workgroups per CU) and the chunked
 // XCD order. Products stand-in hybrid part 1.71 vs 1.87 ms for D = 3 (4124),
@@ -1964,6 +2304,18 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       // diagnostics: 602x = D 2, DA 5 with DIAG x (1 no MFMA, 2 no B, 4 A from k0)
       CM(6022, 2, 5, 2) CM(6024, 2, 5, 4) CM(6026, 2, 5, 6) CM(6027, 2, 5, 7)
 #undef CM
+      // column stream (bsr32_f32_cs_kernel): 45PA = P item slots, NA A slots
+#define CS(V, P, A)                                                                              \
+  case V:                                                                                        \
+    if (crow) hipLaunchKernelGGL((bsr32_f32_cs_kernel<true, 32, P, A>), grid, dim3(64), 0,       \
+                                 ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, \
+                                 ldc);                                                           \
+    else hipLaunchKernelGGL((bsr32_f32_cs_kernel<false, 32, P, A>), grid, dim3(64), 0,           \
+                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
+    break;
+      CS(4583, 8, 3) CS(4584, 8, 4) CS(4582, 8, 2) CS(4563, 6, 3) CS(4543, 4, 3) CS(4542, 4, 2)
+      CS(4573, 7, 3) CS(4574, 7, 4)
+#undef CS
       case 4402:  // CM4: 4 workgroups per CU (bsr32_f32_cm4_kernel)
         if (crow) hipLaunchKernelGGL((bsr32_f32_cm4_kernel<true, 32>), grid, dim3(256), 0, ctx->stream,
                                      mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
@@ -1991,7 +2343,9 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
              aligned(val, 16) && aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
     // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
-    const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 ? kBsr16LdsDefault : var;
+    const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45
+                       ? kBsr16LdsDefault
+                       : var;
 #define L(D)                                                                                     \
   if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<float, true, D>), grid, dim3(256), 0, ctx->stream, \
                                mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);         \
@@ -2100,7 +2454,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
     // K > 256: one workgroup per 512 columns (A read once per 512)
-    const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44
+    const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45
                        ? (n > 256 ? kBsr16F16LdsWide : kBsr16F16LdsDefault)
                        : var;
 #define L(D)                                                                                      \

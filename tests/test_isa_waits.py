@@ -123,3 +123,33 @@ _Z5drainv:
 """
     body = iv.split_functions(text)["_Z5drainv"]
     assert len(iv.loop_drains(body)) == 1
+
+
+def test_column_stream_counts_only_its_copies(bsr_asm):
+    """bsr32_f32_cs_kernel waits with counts computed at run time from the
+    number of copies it issued (one per B item, four per A block). That is
+    exact only if every vector-memory operation of its loops is one of those
+    LDS-DMA copies and the compiler adds no waits of its own: no VGPR load,
+    store or spill (scratch) in a copy loop, and every vmcnt wait there is one
+    of the hand-placed ones (inline asm)."""
+    funcs = iv.split_functions(bsr_asm)
+    cs = [k for k in funcs if "bsr32_f32_cs_kernel" in k]
+    assert len(cs) >= 2, "column-stream instantiations"
+    for k in cs:
+        body = funcs[k]
+        assert not any(line.strip().startswith("scratch_") for _, line in body), f"{k}: spills"
+        blocks = iv.build_cfg(body)
+        loops = {b.header for b in blocks
+                 if b.in_loop and any(iv.classify(mn, ops) == "dma" for _, mn, ops in b.insts)}
+        assert loops, k
+        n_dma = 0
+        for b in blocks:
+            if not (b.in_loop and b.header in loops):
+                continue
+            for no, mn, ops in b.insts:
+                c = iv.classify(mn, ops)
+                assert c in (None, "dma"), f"{k} line {no}: {mn} {ops} in a copy loop"
+                n_dma += c == "dma"
+                if mn == "s_waitcnt" and "vmcnt" in ops:
+                    assert no in b.asm_lines, f"{k} line {no}: compiler-placed {mn} {ops}"
+        assert n_dma >= 8, (k, n_dma)

@@ -37,6 +37,7 @@ from dataclasses import dataclass, field
 
 _FUNC_START = re.compile(r"^(_Z\S+|[A-Za-z_][\w.$]*):\s*(;.*)?$")
 _LABEL = re.compile(r"^(\.LBB\d+_\d+):")
+_NUMLABEL = re.compile(r"^(\d+):\s*$")
 _WAIT = re.compile(r"\bvmcnt\((\d+)\)")
 MAX_DEPTH = 64
 
@@ -63,6 +64,7 @@ class Block:
     succ: list = field(default_factory=list)
     in_loop: bool = False  # the compiler's loop annotation ("in Loop" / "Loop Header")
     header: str = ""       # innermost loop header ("BB12_34") of an in-loop block
+    asm_lines: set = field(default_factory=set)  # line numbers inside inline asm
 
 
 def split_functions(text: str) -> dict[str, list[tuple[int, str]]]:
@@ -84,10 +86,22 @@ def split_functions(text: str) -> dict[str, list[tuple[int, str]]]:
 
 
 def build_cfg(body: list[tuple[int, str]]) -> list[Block]:
+    """Basic blocks and successors. Numeric local labels of inline asm ("20:",
+    targets "20f" / "20b", as in the column-stream kernel's wait ladder) become
+    blocks named "20@<n>" and resolve to the next / previous definition."""
     blocks = [Block("<entry>")]
+    in_asm = False
     for no, raw in body:
+        if "#ASMSTART" in raw:
+            in_asm = True
+        elif "#ASMEND" in raw:
+            in_asm = False
         if re.match(r"^; %bb\.\d+:", raw):  # fall-through block without a label
             blocks.append(Block(raw.split(":")[0][2:]))
+        num = _NUMLABEL.match(raw)
+        if num:
+            blocks.append(Block(f"{num.group(1)}@{len(blocks)}"))
+            continue
         m = _LABEL.match(raw)
         if m:
             blocks.append(Block(m.group(1)))
@@ -105,17 +119,29 @@ def build_cfg(body: list[tuple[int, str]]) -> list[Block]:
             continue
         parts = s.split(None, 1)
         blocks[-1].insts.append((no, parts[0], parts[1] if len(parts) > 1 else ""))
+        if in_asm:
+            blocks[-1].asm_lines.add(no)
     index = {b.label: i for i, b in enumerate(blocks)}
+
+    def target(i: int, op: str) -> int:
+        t = op.strip().split()[0]
+        lm = re.fullmatch(r"(\d+)([fb])", t)
+        if not lm:
+            return index[t]
+        cands = [k for k, b in enumerate(blocks) if b.label.split("@")[0] == lm.group(1)
+                 and "@" in b.label]
+        return min(k for k in cands if k > i) if lm.group(2) == "f" else max(k for k in cands if k <= i)
+
     for i, b in enumerate(blocks):
         last = b.insts[-1] if b.insts else None
         fall = True
         # terminators may sit before a trailing non-branch (e.g. s_nop); scan all
         for _, mn, ops in b.insts:
             if mn == "s_branch":
-                b.succ.append(index[ops.strip()])
+                b.succ.append(target(i, ops))
                 fall = False
             elif mn.startswith("s_cbranch_"):
-                b.succ.append(index[ops.strip().split()[0]])
+                b.succ.append(target(i, ops))
             elif mn in ("s_endpgm", "s_setpc_b64"):
                 fall = False
         del last
@@ -249,7 +275,9 @@ def loop_drains(body: list[tuple[int, str]]) -> list[int]:
             if c is not None:
                 last = c
             elif mn == "s_waitcnt" and (m := _WAIT.search(ops)) and int(m.group(1)) == 0:
-                if last != "load" and not _handoff(b, i):
+                # hand-placed waits in inline asm (the column-stream ladder's
+                # exact vmcnt(0) leaf) are not compiler drains
+                if last != "load" and not _handoff(b, i) and no not in b.asm_lines:
                     out.append(no)
                 last = None
     return out
