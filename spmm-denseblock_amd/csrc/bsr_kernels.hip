@@ -1049,70 +1049,69 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // vector-memory operations, over-waiting by at most a quarter of y (vmcnt is
 // 6 bits: y >= 63 needs no wait). A compare tree in one asm statement: as C,
 // hipcc's structurizer turned each leaf into a chain of exec-mask moves.
+#define SPMM_VM_LADDER(Y)                                                                     \
+  "s_cmp_gt_i32 " Y ", 62\n\t"                                                                \
+  "s_cbranch_scc1 20f\n\t"                                                                     \
+  "s_cmp_gt_i32 " Y ", 15\n\t"                                                                \
+  "s_cbranch_scc1 16f\n\t"                                                                     \
+  "s_cmp_gt_i32 " Y ", 7\n\t"                                                                 \
+  "s_cbranch_scc1 8f\n\t"                                                                      \
+  "s_cmp_gt_i32 " Y ", 3\n\t"                                                                 \
+  "s_cbranch_scc1 4f\n\t"                                                                      \
+  "s_cmp_gt_i32 " Y ", 1\n\t"                                                                 \
+  "s_cbranch_scc1 2f\n\t"                                                                      \
+  "s_cmp_gt_i32 " Y ", 0\n\t"                                                                 \
+  "s_cbranch_scc1 1f\n\t"                                                                      \
+  "s_waitcnt vmcnt(0)\n\t"                                                                     \
+  "s_branch 20f\n"                                                                              \
+  "1:\n\t"                                                                                     \
+  "s_waitcnt vmcnt(1)\n\t"                                                                     \
+  "s_branch 20f\n"                                                                              \
+  "2:\n\t"                                                                                     \
+  "s_cmp_gt_i32 " Y ", 2\n\t"                                                                 \
+  "s_cbranch_scc1 3f\n\t"                                                                      \
+  "s_waitcnt vmcnt(2)\n\t"                                                                     \
+  "s_branch 20f\n"                                                                              \
+  "3:\n\t"                                                                                     \
+  "s_waitcnt vmcnt(3)\n\t"                                                                     \
+  "s_branch 20f\n"                                                                              \
+  "4:\n\t"                                                                                     \
+  "s_cmp_gt_i32 " Y ", 5\n\t"                                                                 \
+  "s_cbranch_scc1 6f\n\t"                                                                      \
+  "s_waitcnt vmcnt(4)\n\t"                                                                     \
+  "s_branch 20f\n"                                                                              \
+  "6:\n\t"                                                                                     \
+  "s_waitcnt vmcnt(6)\n\t"                                                                     \
+  "s_branch 20f\n"                                                                              \
+  "8:\n\t"                                                                                     \
+  "s_cmp_gt_i32 " Y ", 11\n\t"                                                                \
+  "s_cbranch_scc1 12f\n\t"                                                                     \
+  "s_waitcnt vmcnt(8)\n\t"                                                                     \
+  "s_branch 20f\n"                                                                              \
+  "12:\n\t"                                                                                    \
+  "s_waitcnt vmcnt(12)\n\t"                                                                    \
+  "s_branch 20f\n"                                                                              \
+  "16:\n\t"                                                                                    \
+  "s_cmp_gt_i32 " Y ", 31\n\t"                                                                \
+  "s_cbranch_scc1 32f\n\t"                                                                     \
+  "s_cmp_gt_i32 " Y ", 23\n\t"                                                                \
+  "s_cbranch_scc1 24f\n\t"                                                                     \
+  "s_waitcnt vmcnt(16)\n\t"                                                                    \
+  "s_branch 20f\n"                                                                              \
+  "24:\n\t"                                                                                    \
+  "s_waitcnt vmcnt(24)\n\t"                                                                    \
+  "s_branch 20f\n"                                                                              \
+  "32:\n\t"                                                                                    \
+  "s_cmp_gt_i32 " Y ", 47\n\t"                                                                \
+  "s_cbranch_scc1 48f\n\t"                                                                     \
+  "s_waitcnt vmcnt(32)\n\t"                                                                    \
+  "s_branch 20f\n"                                                                              \
+  "48:\n\t"                                                                                    \
+  "s_waitcnt vmcnt(48)\n"                                                                       \
+  "20:\n\t"
+
 __device__ __forceinline__ void wait_vm_older(int y) {
-  asm volatile(
-      "s_cmp_gt_i32 %0, 62\n\t"
-      "s_cbranch_scc1 20f\n\t"
-      "s_cmp_gt_i32 %0, 15\n\t"
-      "s_cbranch_scc1 16f\n\t"
-      "s_cmp_gt_i32 %0, 7\n\t"
-      "s_cbranch_scc1 8f\n\t"
-      "s_cmp_gt_i32 %0, 3\n\t"
-      "s_cbranch_scc1 4f\n\t"
-      "s_cmp_gt_i32 %0, 1\n\t"
-      "s_cbranch_scc1 2f\n\t"
-      "s_cmp_gt_i32 %0, 0\n\t"
-      "s_cbranch_scc1 1f\n\t"
-      "s_waitcnt vmcnt(0)\n\t"
-      "s_branch 20f\n"
-      "1:\n\t"
-      "s_waitcnt vmcnt(1)\n\t"
-      "s_branch 20f\n"
-      "2:\n\t"
-      "s_cmp_gt_i32 %0, 2\n\t"
-      "s_cbranch_scc1 3f\n\t"
-      "s_waitcnt vmcnt(2)\n\t"
-      "s_branch 20f\n"
-      "3:\n\t"
-      "s_waitcnt vmcnt(3)\n\t"
-      "s_branch 20f\n"
-      "4:\n\t"
-      "s_cmp_gt_i32 %0, 5\n\t"
-      "s_cbranch_scc1 6f\n\t"
-      "s_waitcnt vmcnt(4)\n\t"
-      "s_branch 20f\n"
-      "6:\n\t"
-      "s_waitcnt vmcnt(6)\n\t"
-      "s_branch 20f\n"
-      "8:\n\t"
-      "s_cmp_gt_i32 %0, 11\n\t"
-      "s_cbranch_scc1 12f\n\t"
-      "s_waitcnt vmcnt(8)\n\t"
-      "s_branch 20f\n"
-      "12:\n\t"
-      "s_waitcnt vmcnt(12)\n\t"
-      "s_branch 20f\n"
-      "16:\n\t"
-      "s_cmp_gt_i32 %0, 31\n\t"
-      "s_cbranch_scc1 32f\n\t"
-      "s_cmp_gt_i32 %0, 23\n\t"
-      "s_cbranch_scc1 24f\n\t"
-      "s_waitcnt vmcnt(16)\n\t"
-      "s_branch 20f\n"
-      "24:\n\t"
-      "s_waitcnt vmcnt(24)\n\t"
-      "s_branch 20f\n"
-      "32:\n\t"
-      "s_cmp_gt_i32 %0, 47\n\t"
-      "s_cbranch_scc1 48f\n\t"
-      "s_waitcnt vmcnt(32)\n\t"
-      "s_branch 20f\n"
-      "48:\n\t"
-      "s_waitcnt vmcnt(48)\n"
-      "20:"
-      :
-      : "s"(y)
-      : "scc", "memory");
+  asm volatile(SPMM_VM_LADDER("%0") : : "s"(y) : "scc", "memory");
 }
 
 template <bool CROW, int XM, int P, int NA>
@@ -1321,6 +1320,277 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs_kernel(
   } else {
     // column-major C: the tile goes through LDS as [column][row] (36-float
     // columns), then each store writes two 128-B column segments
+    constexpr int kTs = 36;
+    float* tile = smem;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+      tile[(4 * j) * kTs + row] = u0[e];
+      tile[(4 * j + 1) * kTs + row] = u1[e];
+      tile[(4 * j + 2) * kTs + row] = u0[16 + e];
+      tile[(4 * j + 3) * kTs + row] = u1[16 + e];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const size_t row = (size_t)br * 32 + j;
+    for (int it = 0; it < 64; ++it) {
+      const int jl = 2 * it + h;
+      if (jt + jl < n) {
+        float* p = C + (size_t)(jt + jl) * ldc + row;
+        *p = epi(tile[jl * kTs + j], alpha, beta, p);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 32, column stream with register items (CS2). The CS kernel above
+// stages an item's two B rows in an LDS ring (8 KB of its 20 KB), which holds
+// it to eight waves per CU, and reads them back with one more LDS round trip
+// per item. Here the rows go straight into registers: per item one or two
+// global_load_dwordx2 (lane (j, h) columns 4j + 2h, 4j + 2h + 1 of a row:
+// the 64 lanes read the 512-B row whole), in a ring of P register slots
+// (the loop is unrolled P times). LDS holds only the A ring (12 KB at NA =
+// 3), so registers, not LDS, set the occupancy (3 waves per SIMD).
+//  * Every vector-memory operation of the loop is counted as before (A
+//    copies, B row loads, the block-column chunks), and every wait is the
+//    run-time ladder on that count.
+//  * The B row loads, the A column reads and the block-column chunk loads are
+//    inline asm that does NOT wait: hipcc does not know their registers are
+//    in flight. Their destination registers are therefore touched only by
+//    other inline asm: the consume step's asm waits (vmcnt ladder, then
+//    lgkmcnt(0)) and only then copies them into ordinary registers for the
+//    MFMAs. tests/test_isa_waits.py checks on the emitted code that no
+//    compiler-generated instruction reads or writes those registers.
+//  * Block columns come 64 at a time into one VGPR (lane l: colind[k0 +
+//    64c + l], read with v_readlane), the next chunk loaded ahead, so the
+//    loop has no scalar loads (an SMEM load in flight would make each
+//    lgkmcnt(0) of the LDS reads wait for it too).
+// ---------------------------------------------------------------------------
+// DIAG (diagnostic builds, wrong results, timing only): bit 0 no MFMA, bit 1
+// every B row from the L2-resident zero row, bit 2 every A copy from block k0.
+template <bool CROW, int XM, int P, int NA, int DIAG = 0>
+__global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  static_assert(NA >= 2 && NA <= 4 && P >= 2 && P <= 16, "ring depths");
+  constexpr int DA = NA - 1;  // A blocks in flight ahead of the producer's block
+  // (column-major C reuses the LDS for a 128 x 36-float tile)
+  __shared__ __attribute__((aligned(16)))
+  float smem[CROW || NA * 1024 >= 128 * 36 ? NA * 1024 : 128 * 36];
+  const int lane = threadIdx.x;
+  const int j = lane & 31, h = lane >> 5;
+  const int br = xcd_block_row(blockIdx.x, mb, XM);
+  const int jt = blockIdx.y * 128;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  const unsigned lds_a = (unsigned)reinterpret_cast<uintptr_t>(smem);
+
+  int a_src[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 8 * q + (lane >> 3);
+    a_src[q] = r * 32 + 4 * ((lane & 7) ^ ((r >> 1) & 7));
+  }
+  auto issue_a = [&](int kk, int slot) {
+    const float* src = val + (size_t)((DIAG & 4) ? k0 : kk) * 1024;
+    float* dst = smem + slot * 1024;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(src + a_src[q & 1] + 512 * (q >> 1)),
+                                       (lds_void_t)(dst + 256 * q), 16, 0, 0);
+  };
+  unsigned moff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    moff[i] = (unsigned)((2 * i + h) * 128 + 16 * ((j >> 2) ^ i) + 4 * (j & 3));
+  auto mask_of = [&](int slot) -> unsigned {
+    const unsigned base = lds_a + 4096u * (unsigned)slot;
+    f32x2 x[8];
+    asm volatile(
+        "ds_read2st64_b32 %0, %8 offset1:8\n\t"
+        "ds_read2st64_b32 %1, %9 offset1:8\n\t"
+        "ds_read2st64_b32 %2, %10 offset1:8\n\t"
+        "ds_read2st64_b32 %3, %11 offset1:8\n\t"
+        "ds_read2st64_b32 %4, %12 offset1:8\n\t"
+        "ds_read2st64_b32 %5, %13 offset1:8\n\t"
+        "ds_read2st64_b32 %6, %14 offset1:8\n\t"
+        "ds_read2st64_b32 %7, %15 offset1:8\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]),
+          "=&v"(x[6]), "=&v"(x[7])
+        : "v"(base + moff[0]), "v"(base + moff[1]), "v"(base + moff[2]), "v"(base + moff[3]),
+          "v"(base + moff[4]), "v"(base + moff[5]), "v"(base + moff[6]), "v"(base + moff[7])
+        : "memory");
+    unsigned t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      t |= (__float_as_uint(x[i][0]) | __float_as_uint(x[i][1])) & 0x7fffffffu;  // +-0 is zero
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(t != 0u);
+    return (unsigned)b | (unsigned)(b >> 32);
+  };
+  const unsigned a_row = (unsigned)(j * 128);
+  const int a_sw = (j >> 1) & 7;
+  const unsigned boff = 4u * (unsigned)min(jt + 4 * j + 2 * h, n - 2);  // byte offset in a row
+  const size_t ldb4 = (size_t)ldb * 4;
+
+  f32x32 u0, u1;  // MFMA halves u = 0, 1 (output columns 4j + 2b + u)
+#pragma unroll
+  for (int e = 0; e < 32; ++e) u0[e] = u1[e] = 0.f;
+
+  int nis = 0;  // vector-memory operations issued by this wave
+  int ast[DA];  // count at each A block in flight (k+1 .. k+DA)
+  int aslot = NA - 1;
+  int k = k0 - 1;
+  unsigned m = 0;
+  bool more = true;
+  const char* bblk = reinterpret_cast<const char*>(B);
+  int ccur = 0, cnext = 0, cstamp = 0;  // block-column chunks (cnext: in flight)
+  auto load_cols = [&](int kstart) {
+    const unsigned off = 4u * (unsigned)min(kstart + lane, k1 - 1);
+    asm volatile("global_load_dword %0, %1, %2" : "=&v"(cnext) : "v"(off), "s"(colind) : "memory");
+    cstamp = ++nis;
+  };
+  if (k0 < k1) load_cols(k0);
+#pragma unroll
+  for (int d = 0; d < DA; ++d) {
+    if (k0 + d < k1) {
+      issue_a(k0 + d, d);
+      nis += 4;
+      ast[d] = nis;
+    } else {
+      ast[d] = -64;
+    }
+  }
+  int kind[P], stamp[P];
+  float ra0[P], ra1[P];  // in flight: asm-only registers
+  f32x2 rb0[P], rb1[P];  // in flight: asm-only registers
+#pragma unroll
+  for (int s = 0; s < P; ++s) {
+    kind[s] = 0;
+    stamp[s] = -64;
+    ra0[s] = ra1[s] = 0.f;
+    rb0[s] = rb1[s] = f32x2{0.f, 0.f};
+  }
+
+  for (;;) {
+    const bool fin = !more;
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      // consume the item issued P steps ago. The asm runs for empty slots too
+      // (their count is old: no wait), so on every path the slot's registers
+      // are read by it before the produce step below writes them again.
+      {
+        f32x2 b0, b1;
+        float a0, a1;
+        asm volatile(SPMM_VM_LADDER("%4")
+                     "s_waitcnt lgkmcnt(0)\n\t"
+                     "v_mov_b64 %0, %5\n\t"
+                     "v_mov_b64 %1, %6\n\t"
+                     "v_mov_b32 %2, %7\n\t"
+                     "v_mov_b32 %3, %8"
+                     : "=&v"(b0), "=&v"(b1), "=&v"(a0), "=&v"(a1)
+                     : "s"(nis - stamp[s]), "v"(rb0[s]), "v"(rb1[s]), "v"(ra0[s]), "v"(ra1[s])
+                     : "scc", "memory");
+        if (!(DIAG & 1) && kind[s]) {
+          u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(a0, b0[0], u0, 0, 0, 0);
+          u1 = __builtin_amdgcn_mfma_f32_32x32x1f32(a0, b0[1], u1, 0, 0, 0);
+          if (kind[s] == 2) {
+            u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(a1, b1[0], u0, 0, 0, 0);
+            u1 = __builtin_amdgcn_mfma_f32_32x32x1f32(a1, b1[1], u1, 0, 0, 0);
+          }
+        }
+      }
+      // produce the next item into slot s
+      kind[s] = 0;
+      if (more) {
+        while (m == 0u) {
+          if (k + 1 >= k1) {
+            more = false;
+            break;
+          }
+          ++k;
+          aslot = aslot + 1 == NA ? 0 : aslot + 1;
+          const int kr = k - k0;
+          if ((kr & 63) == 0) {  // next block-column chunk
+            asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
+                         : "=&v"(ccur)
+                         : "s"(nis - cstamp), "v"(cnext)
+                         : "scc", "memory");
+            if (k + 64 < k1) load_cols(k + 64);
+          }
+          const int bc = __builtin_amdgcn_readlane(ccur, kr & 63);
+          bblk = (DIAG & 2) ? reinterpret_cast<const char*>(g_zero_row)
+                            : reinterpret_cast<const char*>(B) + (size_t)bc * 32 * ldb4;
+          wait_vm_older(nis - ast[0]);  // A(k) landed
+#pragma unroll
+          for (int d = 0; d + 1 < DA; ++d) ast[d] = ast[d + 1];
+          m = mask_of(aslot);
+          if (k + DA < k1) {
+            issue_a(k + DA, aslot + DA >= NA ? aslot + DA - NA : aslot + DA);
+            nis += 4;
+            ast[DA - 1] = nis;
+          } else {
+            ast[DA - 1] = -64;
+          }
+        }
+        if (m != 0u) {
+          const int c0 = __builtin_ctz(m);
+          m &= m - 1u;
+          int c1 = c0;
+          if (m != 0u) {
+            c1 = __builtin_ctz(m);
+            m &= m - 1u;
+          }
+          const unsigned base = lds_a + 4096u * (unsigned)aslot + a_row;
+          const unsigned p0 = base + 16u * (unsigned)((c0 >> 2) ^ a_sw) + 4u * (unsigned)(c0 & 3);
+          const unsigned p1 = base + 16u * (unsigned)((c1 >> 2) ^ a_sw) + 4u * (unsigned)(c1 & 3);
+          asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3"
+                       : "=&v"(ra0[s]), "=&v"(ra1[s])
+                       : "v"(p0), "v"(p1)
+                       : "memory");
+          asm volatile("global_load_dwordx2 %0, %1, %2"
+                       : "=&v"(rb0[s])
+                       : "v"(boff), "s"(bblk + ((DIAG & 2) ? 0 : (size_t)c0 * ldb4))
+                       : "memory");
+          ++nis;
+          kind[s] = 1;
+          if (c1 != c0) {
+            asm volatile("global_load_dwordx2 %0, %1, %2"
+                         : "=&v"(rb1[s])
+                         : "v"(boff), "s"(bblk + ((DIAG & 2) ? 0 : (size_t)c1 * ldb4))
+                         : "memory");
+            ++nis;
+            kind[s] = 2;
+          }
+          stamp[s] = nis;
+        }
+      }
+    }
+    asm volatile("" : "+a"(u0), "+a"(u1));
+    if (fin) break;
+  }
+  // nothing is in flight after the last round; the full wait makes that
+  // visible to the register check (tests/test_isa_waits.py)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : : "memory");
+
+  if constexpr (CROW) {
+    const int col = jt + 4 * j;
+    if (col >= n) return;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const size_t row = (size_t)br * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      f32x4* p = reinterpret_cast<f32x4*>(C + row * ldc + col);
+      f32x4 v = {u0[e], u1[e], u0[16 + e], u1[16 + e]};
+      if (beta == 0.f) {
+        v *= alpha;
+      } else {
+        const f32x4 c = *p;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
+      }
+      *p = v;
+    }
+  } else {
     constexpr int kTs = 36;
     float* tile = smem;
 #pragma unroll
@@ -2166,10 +2436,11 @@ constexpr int kBsr32Default = 40;
 // B stages D, A stages DA; (2, 5) fits 3 workgroups per CU and is the
 // fastest measured (reddit stand-in 2.65 ms vs 4.57 for 4124; products bs = 32
 // 4.62 vs 8.51; (3, 6) 3.08 / 5.60; (4, 8) 4.87 / 9.09).
-// Column stream (bsr32_f32_cs_kernel, 8 item slots, 3 A slots): products
-// stand-in 3.18 vs 4.38 ms for CM4 (4402), reddit 2.13 vs 2.59
-// (profiles/r02_cs_sweep.jsonl).
-constexpr int kBsr32LdsDefault = 4583;
+// Column stream with register items (bsr32_f32_cs2_kernel, 6 item slots, 3 A
+// slots): products stand-in 3.05 ms, reddit 2.01 (4583, the LDS item ring:
+// 3.21 / 2.16; CM4 4402: 4.38 / 2.59; profiles/r02_cs_sweep.jsonl,
+// r02_cs2_sweep.jsonl).
+constexpr int kBsr32LdsDefault = 4596;
 // Blocks known to be dense (the hybrid's BSR part, MFMA-pipe bound): the
 // full-panel kernel with D = 2 (40 KB, 4 workgroups per CU) and the chunked
 // XCD order. Products stand-in hybrid part 1.71 vs 1.87 ms for D = 3 (4124),
@@ -2316,6 +2587,23 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       CS(4583, 8, 3) CS(4584, 8, 4) CS(4582, 8, 2) CS(4563, 6, 3) CS(4543, 4, 3) CS(4542, 4, 2)
       CS(4573, 7, 3) CS(4574, 7, 4)
 #undef CS
+      // column stream with register items (bsr32_f32_cs2_kernel): 459x =
+      // (P, NA): 4593 (8, 3), 4594 (8, 4), 4592 (8, 2), 4596 (6, 3),
+      // 4597 (4, 3), 4598 (12, 3), 4599 (16, 3)
+#define CS2(V, P, A, ...)                                                                        \
+  case V:                                                                                        \
+    if (crow) hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, P, A, ##__VA_ARGS__>), grid,    \
+                                 dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,   \
+                                 alpha, beta, C, ldc);                                           \
+    else hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, P, A, ##__VA_ARGS__>), grid, dim3(64), 0, \
+                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
+    break;
+      CS2(4593, 8, 3) CS2(4594, 8, 4) CS2(4592, 8, 2) CS2(4596, 6, 3) CS2(4597, 4, 3)
+      CS2(4598, 12, 3) CS2(4599, 16, 3)
+      // diagnostics (wrong results): 960D = (6, 3) with DIAG D
+      CS2(9601, 6, 3, 1) CS2(9602, 6, 3, 2) CS2(9604, 6, 3, 4) CS2(9606, 6, 3, 6)
+      CS2(9607, 6, 3, 7)
+#undef CS2
       case 4402:  // CM4: 4 workgroups per CU (bsr32_f32_cm4_kernel)
         if (crow) hipLaunchKernelGGL((bsr32_f32_cm4_kernel<true, 32>), grid, dim3(256), 0, ctx->stream,
                                      mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
