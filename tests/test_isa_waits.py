@@ -175,7 +175,8 @@ def test_column_stream_registers_in_flight_are_asm_only(bsr_asm):
     flight; any compiler-generated instruction that reads or writes one of
     them (a copy, a spill, a reuse) fails the test."""
     funcs = iv.split_functions(bsr_asm)
-    cs2 = [k for k in funcs if "bsr32_f32_cs2_kernel" in k]
+    # shipped instantiations only (DIAG = 0; the diagnostic builds are timing tools)
+    cs2 = [k for k in funcs if "bsr32_f32_cs2_kernel" in k and "ELi0EEE" in k]
     assert len(cs2) >= 2, "column-stream (register items) instantiations"
     for k in cs2:
         body = funcs[k]
