@@ -12,6 +12,9 @@ Workloads (BASELINE.json configs; the default is the metric's own config):
   arxiv_csr          ogbn-arxiv stand-in (169,343 / 1,166,243), K=128   (config 2)
   reddit_bsr32       community-ordered reddit stand-in, csr2bsr bs=32, K=128, fp32 MFMA (config 3)
   products_bsr16_f16 community-ordered products stand-in, bs=16, K=512, fp16 MFMA    (config 5)
+  reddit_rcm_bsr32, products_rcm_bsr16_f16, products_rcm_bsr32
+                     the same with the reorder step in the loop: node ids scrambled,
+                     in-repo RCM (spmm_reorder_rcm), then csr2bsr
 
 A step = one pass of the hot path over resident inputs. CSR: the merge-path
 kernel + carry fix-up on this rank's rows. With no --workload the N = 1 run is
@@ -59,6 +62,16 @@ WORKLOADS = {
     # §8f rank 2 in the loop: scrambled ids -> in-repo RCM -> divide + hybrid
     "reddit_rcm_hybrid32": dict(kind="hybrid", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
                                 p_in=0.99, bs=32, K=128, density="auto", reorder="rcm"),
+    # configs 3 and 5 with the reorder step in the loop (reorder_graph.cc:26-49 ->
+    # run_bsrmm.cu): the same stand-ins with node ids scrambled, then the in-repo
+    # reorderer, then csr2bsr. The community-ordered workloads above are the
+    # upper bound a perfect reorderer reaches.
+    "reddit_rcm_bsr32": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
+                             p_in=0.99, bs=32, K=128, dtype="fp32", reorder="rcm"),
+    "products_rcm_bsr16_f16": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                                   p_in=0.97, bs=16, K=512, dtype="fp16", reorder="rcm"),
+    "products_rcm_bsr32": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                               p_in=0.97, bs=32, K=128, dtype="fp32", reorder="rcm"),
     # §8f next row: dense-block + CSR remainder (divide.cu) on the reddit stand-in
     "reddit_hybrid32": dict(kind="hybrid", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
                             p_in=0.99, bs=32, K=128, density="auto"),
@@ -75,6 +88,37 @@ def csr_bytes(n_rows: int, nnz: int, K: int) -> int:
 def bsr_bytes(mb: int, nnzb: int, bs: int, K: int, s: int) -> int:
     """SURVEY.md §8(d) BSR model, s = value size."""
     return 4 * (mb + 1) + 4 * nnzb + s * nnzb * bs * bs + s * nnzb * bs * K + 4 * mb * bs * K
+
+
+def community_graph(W, bs: int):
+    """The community stand-in of a BSR / hybrid workload. With W["reorder"] the
+    reorder-then-block pipeline of reorder_graph.cc:26-49 / run_bsrmm.cu runs on
+    it: node ids scrambled (the graph as downloaded), then the in-repo reorderer
+    (spmm_reorder_*). Returns rowptr, colind, the reorder record (None without
+    a reorder) and the `data` label."""
+    from spmm_hip import prep
+    rp, ci = prep.community_csr(W["n"], W["avg_deg"], W["cmin"], W["cmax"], W["p_in"], 1234)
+    if not W.get("reorder"):
+        return rp, ci, None, ("synthetic community-ordered graph (stand-in for the reordered "
+                              "dataset: rabbit_order / Gorder outputs are not reproducible "
+                              "offline; the upper bound a reorderer reaches), U(-1,1) values")
+    n = rp.size - 1
+    upper = prep.block_metrics(rp, ci, bs)
+    scr = np.random.default_rng(9).permutation(n).astype(np.int32)
+    rp, ci = prep.permute_csr(rp, ci, scr)
+    before = prep.block_metrics(rp, ci, bs)["nnzb"]
+    t_ro = time.perf_counter()
+    o2n = prep.reorder(rp, ci, W["reorder"])
+    rp, ci = prep.permute_csr(rp, ci, o2n)
+    t_ro = time.perf_counter() - t_ro
+    after = prep.block_metrics(rp, ci, bs)
+    rec = {"method": W["reorder"], "host_seconds": round(t_ro, 2),
+           "nnzb_scrambled": int(before), "nnzb_reordered": int(after["nnzb"]),
+           "block_fill_reordered": round(float(after["utilization"]), 4),
+           "community_order_upper_bound": {"nnzb": int(upper["nnzb"]),
+                                           "block_fill": round(float(upper["utilization"]), 4)}}
+    return rp, ci, rec, ("synthetic community graph, node ids scrambled, then reordered "
+                         f"in-repo ({W['reorder']}), U(-1,1) values")
 
 
 def _time_prefix(run, n: int, budget_s: float):
@@ -501,7 +545,7 @@ def run_bsr(args, W, world, rank, dev, dist):
         raise SystemExit("BSR workloads are single-GPU configs (BASELINE configs 3 and 5)")
     K, bs, dt = args.K or W["K"], W["bs"], args.dtype or W["dtype"]
     t_gen = time.perf_counter()
-    rp, ci = prep.community_csr(W["n"], W["avg_deg"], W["cmin"], W["cmax"], W["p_in"], 1234)
+    rp, ci, reorder, data = community_graph(W, bs)
     n, nnz = rp.size - 1, ci.size
     val = np.random.default_rng(2).uniform(-1, 1, nnz).astype(np.float32)
     t_gen = time.perf_counter() - t_gen
@@ -582,9 +626,10 @@ def run_bsr(args, W, world, rank, dev, dist):
     rec = dict(
         value=2.0 * nnz * K * args.steps / elapsed / 1e9, ms_per_step=elapsed / args.steps * 1e3,
         dtype=dt,
-        data=("synthetic community-ordered graph (stand-in for the reordered dataset: "
-              "rabbit_order / Gorder outputs are not reproducible offline), U(-1,1) values"),
-        config={"workload": f"{args.workload}: csr2bsr bs={bs} + bsrmm K={K} {dt}", "n": n,
+        data=data,
+        config={"workload": f"{args.workload}: " + (f"scrambled ids -> {reorder['method']} -> "
+                                                    if reorder else "") +
+                            f"csr2bsr bs={bs} + bsrmm K={K} {dt}", "n": n,
                 "layout_BC": args.bsr_layout,
                 "nnz": nnz, "K": K, "bs": bs, "nnzb": nnzb,
                 "block_fill": round(nnz / (nnzb * bs * bs), 4),
@@ -594,7 +639,7 @@ def run_bsr(args, W, world, rank, dev, dist):
         roofline={"bound": "hbm", "achieved": round(cm_bytes / t / 1e9, 1),
                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                   "frac": round(cm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-                  "kernel": (("bsr32_f32_cs_kernel" if bs == 32 else
+                  "kernel": (("bsr32_f32_cs2_kernel" if bs == 32 else
                               f"bsr16_cm_kernel<{'f32' if dt == 'fp32' else 'f16'}>")
                              + (" (column-major C epilogue, B staged row-major)"
                                 if args.bsr_layout == "col" else "") if cm else
@@ -610,7 +655,7 @@ def run_bsr(args, W, world, rank, dev, dist):
                   "full_panel_model_bytes_per_launch": kbytes,
                   "full_panel_model_GBps": round(kbytes / t / 1e9, 1)},
         csr_same_matrix_ms=round(csr_ms, 4), csr2bsr_host_seconds=round(t_conv, 2),
-        gen_seconds=round(t_gen, 2))
+        gen_seconds=round(t_gen, 2), reorder=reorder)
     return rec, None
 
 
@@ -623,23 +668,8 @@ def run_hybrid(args, W, world, rank, dev, dist):
     if world > 1:
         raise SystemExit("hybrid workloads are single-GPU")
     K, bs, dens = args.K or W["K"], args.bs or W["bs"], W["density"]
-    rp, ci = prep.community_csr(W["n"], W["avg_deg"], W["cmin"], W["cmax"], W["p_in"], 1234)
+    rp, ci, reorder, data = community_graph(W, bs)
     n, nnz = rp.size - 1, ci.size
-    reorder = None
-    if W.get("reorder"):
-        # The reorder-then-block pipeline of reorder_graph.cc / run_bsrmm.cu:
-        # node ids scrambled (the graph as downloaded), then the in-repo
-        # reorderer (spmm_reorder_*), then divide + hybrid SpMM.
-        scr = np.random.default_rng(9).permutation(n).astype(np.int32)
-        rp, ci = prep.permute_csr(rp, ci, scr)
-        before = prep.block_metrics(rp, ci, bs)["nnzb"]
-        t_ro = time.perf_counter()
-        o2n = prep.reorder(rp, ci, W["reorder"])
-        rp, ci = prep.permute_csr(rp, ci, o2n)
-        t_ro = time.perf_counter() - t_ro
-        reorder = {"method": W["reorder"], "host_seconds": round(t_ro, 2),
-                   "nnzb_scrambled": int(before),
-                   "nnzb_reordered": int(prep.block_metrics(rp, ci, bs)["nnzb"])}
     val = np.random.default_rng(2).uniform(-1, 1, nnz).astype(np.float32)
     plan = None
     if args.density is None and dens == "auto":
@@ -681,9 +711,7 @@ def run_hybrid(args, W, world, rank, dev, dist):
     useful = 2.0 * nnz * K
     rec = dict(
         value=useful * args.steps / elapsed / 1e9, ms_per_step=ms, dtype="fp32",
-        data=("synthetic community graph, node ids scrambled, then reordered in-repo (" +
-              W["reorder"] + ")" if W.get("reorder") else
-              "synthetic community-ordered graph (stand-in for a reordered dataset)"),
+        data=data,
         config={"workload": f"{args.workload}: divide(bs={bs}, density={dens}) + hybrid "
                             f"BSR-MFMA/CSR K={K}", "n": n, "nnz": nnz, "K": K, "bs": bs,
                 "nnzb": int(bci.size), "csr_remainder_nnz": int(cci.size),
