@@ -2020,6 +2020,306 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }
 
 // ---------------------------------------------------------------------------
+// bs = 16 fp16, column stream (CS16; ROW blocks, row-major B). bsr16_cm_kernel
+// keeps four waves in step on one block at a time: a barrier per block, and a
+// 16-row B stage per block although most of a block's columns are empty (59 %
+// on the products stand-in) and their rows come from the zero row. Here one
+// wave owns (block row, 256 output columns), no barriers, and streams the
+// block row's nonzero columns as ITEMS of 16 packed ACROSS blocks: the k index
+// of an item runs over 16 (block, column) pairs, so one
+// v_mfma_f32_16x16x16_f16 per 16 output columns takes 16 nonzero columns
+// whatever blocks they came from.
+// The per-column work runs on the vector unit and the LDS crossbar, not on
+// the scalar unit: a first form that picked columns one by one with
+// s_ff1 / address arithmetic issued ~590 SALU instructions per item, and the
+// one scalar unit per CU, shared by its four SIMDs, bounded it (products
+// stand-in 8.4 ms against 5.9 for bsr16_cm_kernel; PMC 2.57 G SALU
+// instructions against 1.21 G).
+//  * A ring (NA slots x 512 B, NA a power of two): blocks are copied by LDS-DMA
+//    two at a time (one global_load_lds_dwordx4, lanes 32-63 the second block),
+//    DA + 2 blocks ahead of the producer. A block's column mask: lane (g, r)
+//    reads column r of rows 4g .. 4g + 3 (four ds_read_u16), one ballot, two
+//    folds; +-0 is zero, anything else (NaN, inf) counts.
+//  * Pending list (lanes 0 .. 31 of two VGPRs: B row index, A LDS address):
+//    lane c < 16 of a block pushes its column to position npend + rank (one
+//    v_bcnt) with ds_permute_b32; at 16 entries an item is emitted and the
+//    rest moves down by 16 (ds_bpermute_b32).
+//  * Item stage (P slots x 8 KB), chunk-major: 16-B chunk c (8 columns) of
+//    item row r at c * 256 + 16 r. Copy j (global_load_lds_dwordx4) brings
+//    chunks 4j .. 4j + 3 of all 16 rows: lane L loads row L & 15, chunk
+//    4j + L / 16, so every lane pulls its row index once per item and each of
+//    the 8 copies costs one address add. The transposed reads
+//    (ds_read_b64_tr_b16, lane (g, q, p): row 4g + q, columns 16t + 4p ..)
+//    then sit at one base address plus immediate offsets.
+//  * The A fragment (lane (g, r): A[r][k = 4g .. 4g + 3]) is read from the A
+//    slots at item emission (four ds_bpermute_b32 of the pending A addresses,
+//    four ds_read_u16), so the A slots of every pending column must still be
+//    in the ring: a pending list that would span more than kSpan blocks is
+//    emitted early, padded. Padding: the zero B row and a zeroed A slot, so a
+//    padded k adds exactly 0.
+//  * The item issued P slots earlier is consumed: a counted wait on its last
+//    copy (the run-time vmcnt ladder of bsr32_f32_cs_kernel: every
+//    vector-memory operation of the loop is counted), 16 ds_read_b64_tr_b16
+//    and 16 MFMAs into 16 accumulator tiles.
+// ---------------------------------------------------------------------------
+template <bool CROW, int P, int NA>
+__global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
+    float beta, float* __restrict__ C, int ldc) {
+  static_assert((NA & (NA - 1)) == 0 && NA >= 16 && NA <= 32 && P >= 2 && P <= 5, "ring depths");
+  constexpr int DA = 4;                  // A blocks copied ahead of the producer (even)
+  constexpr int kSpan = NA - DA - 4;     // largest block distance inside one item
+  constexpr int kStage = 16 * 512;       // one item: 16 B rows x 256 fp16 columns
+  constexpr int kRing = (NA + 1) * 512;  // A ring + the zero slot
+  constexpr int kLds = kRing + P * kStage;
+  static_assert(kLds >= 256 * 16 * 4, "column-major C tile fits");
+  __shared__ __attribute__((aligned(16))) char smem[kLds];
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, r16 = lane & 15, h = lane >> 5;
+  const int br = xcd_block_row(blockIdx.x, mb, 32);
+  const int jt = blockIdx.y * 256;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  const unsigned lds0 = lds_addr(smem);
+  const unsigned zslot = lds0 + NA * 512u;
+  *reinterpret_cast<unsigned long long*>(smem + NA * 512 + 8 * lane) = 0ull;
+
+  // copy j: lane L loads chunk 4j + L / 16 of its row (columns jt + 8 (4j + L / 16) ..)
+  unsigned boff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) boff[j] = 2u * (unsigned)min(jt + 8 * (4 * j + g), n - 8);
+  const size_t ldb2 = (size_t)ldb * 2;
+  const char* const zrow = reinterpret_cast<const char*>(g_zero_row) - 2 * (size_t)jt;
+  // transposed B reads: lane (g, q = (lane >> 2) & 3, p = lane & 3) reads row 4g + q,
+  // columns 16t + 4p .. + 3: chunk 2t + p / 2 at byte 8 (p & 1); t by immediate offset
+  const unsigned tro = lds0 + kRing + 256u * ((lane & 3) >> 1) + 16u * (4 * g + ((lane >> 2) & 3)) +
+                       8u * (lane & 1);
+
+  int nis = 0;  // vector-memory operations issued by this wave
+  // block columns: 64 at a time in one VGPR (lane l: colind[k0 + 64c + l]), the next chunk in flight
+  int ccur = 0, cnext = 0, cstamp = 0;
+  auto load_cols = [&](int kstart) {
+    const unsigned off = 4u * (unsigned)min(kstart + lane, k1 - 1);
+    asm volatile("global_load_dword %0, %1, %2" : "=&v"(cnext) : "v"(off), "s"(colind) : "memory");
+    cstamp = ++nis;
+  };
+  auto issue_a = [&](int kr) {  // blocks k0 + kr, k0 + kr + 1 (kr even) -> slots kr, kr + 1
+    const int blk = min(k0 + kr + h, k1 - 1);
+    __builtin_amdgcn_global_load_lds((gbl_void_t)(val + (size_t)blk * 256 + 8 * (lane & 31)),
+                                     (lds_void_t)(smem + (kr & (NA - 1)) * 512), 16, 0, 0);
+    ++nis;
+  };
+  if (k0 < k1) load_cols(k0);
+  int ast[DA / 2 + 1];  // count at each A pair in flight
+#pragma unroll
+  for (int q = 0; q <= DA / 2; ++q) {
+    if (k0 + 2 * q < k1) {
+      issue_a(2 * q);
+      ast[q] = nis;
+    } else {
+      ast[q] = -64;
+    }
+  }
+
+  int kr = -1;  // producer block, relative to k0
+  const unsigned lowm = (1u << r16) - 1u;
+  int prow = 0;        // pending list: B row index (lanes 0 .. npend - 1)
+  unsigned pa = zslot;  // pending list: A LDS address of the column (row 0)
+  int npend = 0, kf = 0;  // entries, block of the oldest entry
+  bool blocks = true;     // blocks left to read
+  // next block: its A (pair) landed, its mask, its columns pushed to the list
+  auto advance = [&]() {
+    ++kr;
+    if ((kr & 63) == 0) {  // next block-column chunk
+      asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
+                   : "=&v"(ccur)
+                   : "s"(nis - cstamp), "v"(cnext)
+                   : "scc", "memory");
+      if (k0 + kr + 64 < k1) load_cols(k0 + kr + 64);
+    }
+    const int bc = __builtin_amdgcn_readlane(ccur, kr & 63);
+    if ((kr & 1) == 0) {
+      wait_vm_older(nis - ast[0]);  // pair kr / 2 landed
+#pragma unroll
+      for (int q = 0; q < DA / 2; ++q) ast[q] = ast[q + 1];
+      if (k0 + kr + DA + 2 < k1) {
+        issue_a(kr + DA + 2);
+        ast[DA / 2] = nis;
+      } else {
+        ast[DA / 2] = -64;
+      }
+    }
+    const unsigned aslot = lds0 + 512u * (unsigned)(kr & (NA - 1));
+    unsigned x0, x1, x2, x3;
+    asm volatile(
+        "ds_read_u16 %0, %4\n\t"
+        "ds_read_u16 %1, %4 offset:32\n\t"
+        "ds_read_u16 %2, %4 offset:64\n\t"
+        "ds_read_u16 %3, %4 offset:96\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+        : "v"(aslot + 128u * g + 2u * r16)
+        : "memory");
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(((x0 | x1 | x2 | x3) & 0x7fffu) != 0u);
+    const unsigned w = (unsigned)b | (unsigned)(b >> 32);
+    const unsigned m = (w | (w >> 16)) & 0xffffu;
+    if (m == 0u) return;
+    // lane c < 16 with bit c set -> position npend + popcount(m below c)
+    const bool act = lane < 16 && ((m >> r16) & 1u);
+    const int dest = act ? npend + __builtin_popcount(m & lowm) : 63;
+    const int nr = __builtin_amdgcn_ds_permute(4 * dest, bc * 16 + r16);
+    const int na = __builtin_amdgcn_ds_permute(4 * dest, (int)(aslot + 2u * r16));
+    const int cnt = __builtin_popcount(m);
+    const bool in = lane >= npend && lane < npend + cnt;
+    prow = in ? nr : prow;
+    pa = in ? (unsigned)na : pa;
+    if (npend == 0) kf = kr;
+    npend += cnt;
+  };
+
+  f32x4 acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int kind[P], stamp[P];
+  f16x4 fa[P];
+#pragma unroll
+  for (int s = 0; s < P; ++s) {
+    kind[s] = 0;
+    stamp[s] = -64;
+    fa[s] = f16x4{0, 0, 0, 0};
+  }
+
+  bool more = true;
+  for (;;) {
+    const bool fin = !more;
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      // consume the item issued P slots ago
+      if (kind[s]) {
+        wait_vm_older(nis - stamp[s]);
+#pragma unroll
+        for (int t0 = 0; t0 < 16; t0 += 8) {
+          f16x4 fb[8];
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %8 offset:%9\n\t"
+              "ds_read_b64_tr_b16 %1, %8 offset:%10\n\t"
+              "ds_read_b64_tr_b16 %2, %8 offset:%11\n\t"
+              "ds_read_b64_tr_b16 %3, %8 offset:%12\n\t"
+              "ds_read_b64_tr_b16 %4, %8 offset:%13\n\t"
+              "ds_read_b64_tr_b16 %5, %8 offset:%14\n\t"
+              "ds_read_b64_tr_b16 %6, %8 offset:%15\n\t"
+              "ds_read_b64_tr_b16 %7, %8 offset:%16\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
+              : "v"(tro), "n"(s * kStage + 512 * t0), "n"(s * kStage + 512 * (t0 + 1)),
+                "n"(s * kStage + 512 * (t0 + 2)), "n"(s * kStage + 512 * (t0 + 3)),
+                "n"(s * kStage + 512 * (t0 + 4)), "n"(s * kStage + 512 * (t0 + 5)),
+                "n"(s * kStage + 512 * (t0 + 6)), "n"(s * kStage + 512 * (t0 + 7))
+              : "memory");
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            acc[t0 + t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[t0 + t], 0, 0, 0);
+        }
+      }
+      // produce the next item into slot s: read blocks until 16 columns are
+      // pending, the blocks run out, or the list would outgrow the A ring
+      kind[s] = 0;
+      if (more) {
+        while (npend < 16 && blocks) {
+          if (k0 + kr + 1 >= k1) {
+            blocks = false;
+            break;
+          }
+          if (npend > 0 && kr + 1 - kf > kSpan) break;
+          advance();
+        }
+        if (npend == 0) {
+          more = false;
+        } else {
+          const int cnt = min(npend, 16);
+          // B rows: lane L -> item row L & 15 (the zero row past cnt)
+          const int r = __builtin_amdgcn_ds_bpermute(4 * r16, prow);
+          const char* base = r16 < cnt ? reinterpret_cast<const char*>(B) + (size_t)r * ldb2 : zrow;
+          char* const stage = smem + kRing + s * kStage;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            __builtin_amdgcn_global_load_lds((gbl_void_t)(base + boff[j]),
+                                             (lds_void_t)(stage + 1024 * j), 16, 0, 0);
+          nis += 8;
+          // A fragment: lane (g, r) <- A[r][entry 4g + i]
+          unsigned ad[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int e = 4 * g + i;
+            const unsigned a = (unsigned)__builtin_amdgcn_ds_bpermute(4 * e, (int)pa);
+            ad[i] = (e < cnt ? a : zslot) + 32u * r16;
+          }
+          unsigned y0, y1, y2, y3;
+          asm volatile(
+              "ds_read_u16 %0, %4\n\t"
+              "ds_read_u16 %1, %5\n\t"
+              "ds_read_u16 %2, %6\n\t"
+              "ds_read_u16 %3, %7\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3)
+              : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
+              : "memory");
+          const unsigned u[2] = {y0 | (y1 << 16), y2 | (y3 << 16)};
+          fa[s] = *reinterpret_cast<const f16x4*>(u);
+          kind[s] = 1;
+          stamp[s] = nis;
+          // the entries past 16 (all from block kr) move down
+          if (npend > 16) {
+            prow = __builtin_amdgcn_ds_bpermute(4 * ((lane + 16) & 63), prow);
+            pa = (unsigned)__builtin_amdgcn_ds_bpermute(4 * ((lane + 16) & 63), (int)pa);
+            npend -= 16;
+            kf = kr;
+          } else {
+            npend = 0;
+          }
+        }
+      }
+    }
+    if (fin) break;
+  }
+  // nothing is in flight after the last round (a block-column chunk may be);
+  // the full wait makes that visible to the register check (tests/test_isa_waits.py)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  if constexpr (!CROW) {
+    // column-major C: the 16 x 256 tile through LDS, then 4 whole 64-B column
+    // segments per store instruction
+    float* tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      *reinterpret_cast<f32x4*>(tile + (16 * t + r16) * 16 + 4 * g) = acc[t];
+    __builtin_amdgcn_s_waitcnt(0);
+    const size_t row = (size_t)br * 16 + r16;
+#pragma unroll 4
+    for (int it = 0; it < 64; ++it) {
+      const int jl = 4 * it + g;
+      if (jt + jl < n) {
+        float* p = C + (size_t)(jt + jl) * ldc + row;
+        *p = epi(tile[jl * 16 + r16], alpha, beta, p);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int j = jt + 16 * t + r16;
+    if (j >= n) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = (size_t)br * 16 + 4 * g + e;
+      float* p = C + row * ldc + j;
+      *p = epi(acc[t][e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // bs = 16 fp16, LDS-staged, TWO block rows per workgroup sharing B panels:
 // the workgroup walks the union of the two rows' block columns, copying each
 // B panel once (products stand-in: the union is 0.73 of the two rows' blocks).
@@ -2522,7 +2822,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // be dense (the hybrid's BSR part) take the full-panel kernel: with most
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
-    int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8)
+    int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8) || var / 100 == 50
                  ? (dense_blocks ? kBsr32LdsDense : kBsr32LdsDefault)
                  : var;
 #define L(D, X)                                                                                   \
@@ -2631,7 +2931,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
              aligned(val, 16) && aligned(B, 16) && (var < 0 || var >= 4096)) {
     dim3 grid(mb, (n + 255) / 256);
     // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
-    const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45
+    const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45 ||
+                           var / 100 == 50
                        ? kBsr16LdsDefault
                        : var;
 #define L(D)                                                                                     \
@@ -2779,6 +3080,17 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   }
       CM512(4825, 2, 5, 1) CM512(4826, 2, 6, 1) CM512(4836, 3, 6, 1) CM512(4824, 2, 4, 1)
 #undef CM512
+      // column stream (bsr16_f16_cs_kernel): 50PN = P item stages, NA = 16 (N = 1) / 32 (N = 2)
+#define CS16(V, P, A)                                                                             \
+  case V:                                                                                         \
+    if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A>), grid, dim3(64), 0, ctx->stream, \
+                                 mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);        \
+    else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A>), grid, dim3(64), 0, ctx->stream,     \
+                            mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);             \
+    break;
+      CS16(5021, 2, 16) CS16(5031, 3, 16) CS16(5041, 4, 16) CS16(5051, 5, 16) CS16(5032, 3, 32)
+      CS16(5042, 4, 32)
+#undef CS16
 #undef CM
       case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4
         const dim3 gp((mb + 1) / 2, (n + 255) / 256);

@@ -165,10 +165,12 @@ def _vregs(ops: str) -> set:
     return out
 
 
-def test_column_stream_registers_in_flight_are_asm_only(bsr_asm):
+@pytest.mark.parametrize("kernel,tag", [("bsr32_f32_cs2_kernel", "ELi0EEE"),
+                                        ("bsr16_f16_cs_kernel", "")])
+def test_column_stream_registers_in_flight_are_asm_only(bsr_asm, kernel, tag):
     """bsr32_f32_cs2_kernel loads B rows, block-column chunks and A columns
-    with inline asm that does not wait, so hipcc believes their registers hold
-    data at once. They are safe only if nothing but inline asm touches them
+    (bsr16_f16_cs_kernel: block-column chunks) with inline asm that does not
+    wait, so hipcc believes their registers hold data at once. They are safe only if nothing but inline asm touches them
     while the load is in flight: the consume step's asm waits (vmcnt ladder,
     lgkmcnt(0)) and then copies them out with v_mov. A forward dataflow over
     the kernel's control-flow graph (union at joins) tracks the registers in
@@ -176,8 +178,8 @@ def test_column_stream_registers_in_flight_are_asm_only(bsr_asm):
     them (a copy, a spill, a reuse) fails the test."""
     funcs = iv.split_functions(bsr_asm)
     # shipped instantiations only (DIAG = 0; the diagnostic builds are timing tools)
-    cs2 = [k for k in funcs if "bsr32_f32_cs2_kernel" in k and "ELi0EEE" in k]
-    assert len(cs2) >= 2, "column-stream (register items) instantiations"
+    cs2 = [k for k in funcs if kernel in k and tag in k]
+    assert len(cs2) >= 2, f"{kernel} instantiations"
     for k in cs2:
         body = funcs[k]
         stmt_wait, cur, waits = {}, None, False   # asm line -> its statement waits?
