@@ -606,13 +606,20 @@ def run_bsr(args, W, world, rank, dev, dist):
     active_pairs = int(torch.unique(((d_r // bs) * mb + d_c // bs) * (bs // 2) +
                                     (d_c % bs) % (bs // 2)).numel())
     del d_r, d_c
-    # output columns per workgroup (bs 16 fp16 at K > 256: 512, kBsr16F16LdsWide)
-    tile = 128 if bs == 32 else (512 if dt == "fp16" and K > 256 else 256)
+    # output columns per workgroup (bs 32: 128; bs 16: 256)
+    tile = 128 if bs == 32 else 256
     ntiles = (K + tile - 1) // tile
     dense_flops = 2.0 * nnzb * bs * bs * K    # SURVEY §8d "MFMA-executed" (dense blocks)
+    cs16 = cm and bs == 16 and dt == "fp16" and K >= 128
     if cm and bs == 32:
         # column stream: two v_mfma_f32_32x32x1_2b_f32 (32 rows x 64 columns,
         # k = 1) per nonzero column of a block and 128 output columns
+        mfma_flops = active_cols * 2.0 * bs * K
+    elif cs16:
+        # column stream: items of 16 nonzero columns packed across blocks, one
+        # v_mfma_f32_16x16x16_f16 per item and 16 output columns (the last
+        # item of a block row padded: counted as executed work below only
+        # for the columns it holds)
         mfma_flops = active_cols * 2.0 * bs * K
     else:
         mfma_flops = dense_flops
@@ -640,6 +647,7 @@ def run_bsr(args, W, world, rank, dev, dist):
                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                   "frac": round(cm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
                   "kernel": (("bsr32_f32_cs2_kernel" if bs == 32 else
+                              "bsr16_f16_cs_kernel" if cs16 else
                               f"bsr16_cm_kernel<{'f32' if dt == 'fp32' else 'f16'}>")
                              + (" (column-major C epilogue, B staged row-major)"
                                 if args.bsr_layout == "col" else "") if cm else

@@ -2034,45 +2034,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // s_ff1 / address arithmetic issued ~590 SALU instructions per item, and the
 // one scalar unit per CU, shared by its four SIMDs, bounded it (products
 // stand-in 8.4 ms against 5.9 for bsr16_cm_kernel; PMC 2.57 G SALU
-// instructions against 1.21 G).
-//  * A ring (NA slots x 512 B, NA a power of two): blocks are copied by LDS-DMA
-//    two at a time (one global_load_lds_dwordx4, lanes 32-63 the second block),
-//    DA + 2 blocks ahead of the producer. A block's column mask: lane (g, r)
-//    reads column r of rows 4g .. 4g + 3 (four ds_read_u16), one ballot, two
-//    folds; +-0 is zero, anything else (NaN, inf) counts.
-//  * Pending list (lanes 0 .. 31 of two VGPRs: B row index, A LDS address):
-//    lane c < 16 of a block pushes its column to position npend + rank (one
-//    v_bcnt) with ds_permute_b32; at 16 entries an item is emitted and the
-//    rest moves down by 16 (ds_bpermute_b32).
+// instructions against 1.21 G, profiles/r02_cs16_pmc/).
+//  * A ring (NA slots x 512 B): blocks are copied by LDS-DMA two at a time
+//    (one global_load_lds_dwordx4, lanes 32-63 the second block), DA + 2
+//    blocks ahead of the producer. Reading a block: lane (g, c) reads column
+//    c of rows 4g .. 4g + 3 (four ds_read_u16); one ballot and two folds give
+//    the column mask (+-0 is zero, anything else, NaN and inf too, counts).
+//    The slot is dead after that read.
+//  * Pending list, 32 circular entries: lane c < 16 of a block pushes its B
+//    row index to entry (ebase + npend + rank) with ds_permute_b32 (rank = one
+//    v_bcnt), and every lane (g, c) writes its four A values to the entry's
+//    column of the A-fragment buffer (16 rows x 32 entries of fp16 in 72-B
+//    rows: the four row groups' writes land in different banks). At 16
+//    entries an item is emitted and ebase moves on by 16.
 //  * Item stage (P slots x 8 KB), chunk-major: 16-B chunk c (8 columns) of
 //    item row r at c * 256 + 16 r. Copy j (global_load_lds_dwordx4) brings
 //    chunks 4j .. 4j + 3 of all 16 rows: lane L loads row L & 15, chunk
-//    4j + L / 16, so every lane pulls its row index once per item and each of
-//    the 8 copies costs one address add. The transposed reads
-//    (ds_read_b64_tr_b16, lane (g, q, p): row 4g + q, columns 16t + 4p ..)
-//    then sit at one base address plus immediate offsets.
-//  * The A fragment (lane (g, r): A[r][k = 4g .. 4g + 3]) is read from the A
-//    slots at item emission (four ds_bpermute_b32 of the pending A addresses,
-//    four ds_read_u16), so the A slots of every pending column must still be
-//    in the ring: a pending list that would span more than kSpan blocks is
-//    emitted early, padded. Padding: the zero B row and a zeroed A slot, so a
-//    padded k adds exactly 0.
+//    4j + L / 16, so every lane pulls its row index once per item (one
+//    ds_bpermute_b32) and each of the 8 copies costs one address add. The
+//    transposed reads (ds_read_b64_tr_b16, lane (g, q, p): row 4g + q,
+//    columns 16t + 4p ..) are one address plus immediate offsets.
+//  * The A fragment (lane (g, r): A[r][k = 4g .. 4g + 3]) is one ds_read_b64
+//    of the buffer at emission. Padding (the block row's last item): the zero
+//    B row and A values masked to zero in registers, so a padded k adds 0.
 //  * The item issued P slots earlier is consumed: a counted wait on its last
 //    copy (the run-time vmcnt ladder of bsr32_f32_cs_kernel: every
 //    vector-memory operation of the loop is counted), 16 ds_read_b64_tr_b16
-//    and 16 MFMAs into 16 accumulator tiles.
+//    under one lgkmcnt wait, 16 MFMAs into 16 accumulator tiles.
 // ---------------------------------------------------------------------------
-template <bool CROW, int P, int NA>
+template <bool CROW, int P, int NA, int DA>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
     float beta, float* __restrict__ C, int ldc) {
-  static_assert((NA & (NA - 1)) == 0 && NA >= 16 && NA <= 32 && P >= 2 && P <= 5, "ring depths");
-  constexpr int DA = 4;                  // A blocks copied ahead of the producer (even)
-  constexpr int kSpan = NA - DA - 4;     // largest block distance inside one item
-  constexpr int kStage = 16 * 512;       // one item: 16 B rows x 256 fp16 columns
-  constexpr int kRing = (NA + 1) * 512;  // A ring + the zero slot
-  constexpr int kLds = kRing + P * kStage;
+  // the pair copied at block kr (blocks kr + DA + 2, + 3) overwrites blocks
+  // kr + DA + 2 - NA, + 3 - NA, which must be read already (< kr)
+  static_assert((NA & (NA - 1)) == 0 && DA % 2 == 0 && NA >= DA + 4 && P >= 2 && P <= 4,
+                "ring depths");
+  constexpr int kStage = 16 * 512;  // one item: 16 B rows x 256 fp16 columns
+  constexpr int kAbRow = 72;        // A-fragment buffer row: 32 entries + a dummy entry + pad
+  constexpr int kAbuf = NA * 512;   // offset of the A-fragment buffer
+  constexpr int kStg = kAbuf + 16 * kAbRow;  // offset of the item stages
+  constexpr int kLds = kStg + P * kStage;
   static_assert(kLds >= 256 * 16 * 4, "column-major C tile fits");
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int lane = threadIdx.x;
@@ -2081,8 +2084,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   const int jt = blockIdx.y * 256;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const unsigned lds0 = lds_addr(smem);
-  const unsigned zslot = lds0 + NA * 512u;
-  *reinterpret_cast<unsigned long long*>(smem + NA * 512 + 8 * lane) = 0ull;
+  const unsigned abuf = lds0 + kAbuf;
 
   // copy j: lane L loads chunk 4j + L / 16 of its row (columns jt + 8 (4j + L / 16) ..)
   unsigned boff[8];
@@ -2092,7 +2094,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   const char* const zrow = reinterpret_cast<const char*>(g_zero_row) - 2 * (size_t)jt;
   // transposed B reads: lane (g, q = (lane >> 2) & 3, p = lane & 3) reads row 4g + q,
   // columns 16t + 4p .. + 3: chunk 2t + p / 2 at byte 8 (p & 1); t by immediate offset
-  const unsigned tro = lds0 + kRing + 256u * ((lane & 3) >> 1) + 16u * (4 * g + ((lane >> 2) & 3)) +
+  const unsigned tro = lds0 + kStg + 256u * ((lane & 3) >> 1) + 16u * (4 * g + ((lane >> 2) & 3)) +
                        8u * (lane & 1);
 
   int nis = 0;  // vector-memory operations issued by this wave
@@ -2123,10 +2125,8 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
 
   int kr = -1;  // producer block, relative to k0
   const unsigned lowm = (1u << r16) - 1u;
-  int prow = 0;        // pending list: B row index (lanes 0 .. npend - 1)
-  unsigned pa = zslot;  // pending list: A LDS address of the column (row 0)
-  int npend = 0, kf = 0;  // entries, block of the oldest entry
-  bool blocks = true;     // blocks left to read
+  int prow = 0;  // pending B row indices (lane e < 32: entry e)
+  int npend = 0, ebase = 0;
   // next block: its A (pair) landed, its mask, its columns pushed to the list
   auto advance = [&]() {
     ++kr;
@@ -2149,7 +2149,6 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
         ast[DA / 2] = -64;
       }
     }
-    const unsigned aslot = lds0 + 512u * (unsigned)(kr & (NA - 1));
     unsigned x0, x1, x2, x3;
     asm volatile(
         "ds_read_u16 %0, %4\n\t"
@@ -2158,22 +2157,28 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
         "ds_read_u16 %3, %4 offset:96\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
-        : "v"(aslot + 128u * g + 2u * r16)
+        : "v"(lds0 + 512u * (unsigned)(kr & (NA - 1)) + 128u * g + 2u * r16)
         : "memory");
     const unsigned long long b = __builtin_amdgcn_ballot_w64(((x0 | x1 | x2 | x3) & 0x7fffu) != 0u);
     const unsigned w = (unsigned)b | (unsigned)(b >> 32);
     const unsigned m = (w | (w >> 16)) & 0xffffu;
     if (m == 0u) return;
-    // lane c < 16 with bit c set -> position npend + popcount(m below c)
-    const bool act = lane < 16 && ((m >> r16) & 1u);
-    const int dest = act ? npend + __builtin_popcount(m & lowm) : 63;
-    const int nr = __builtin_amdgcn_ds_permute(4 * dest, bc * 16 + r16);
-    const int na = __builtin_amdgcn_ds_permute(4 * dest, (int)(aslot + 2u * r16));
+    const bool bit = (m >> r16) & 1u;
+    const int pos = (ebase + npend + __builtin_popcount(m & lowm)) & 31;
+    const int nr = __builtin_amdgcn_ds_permute(4 * (lane < 16 && bit ? pos : 63), bc * 16 + r16);
+    // (entry 32 of each row takes the writes of empty columns)
+    const unsigned wa = abuf + 2u * (unsigned)(bit ? pos : 32) + kAbRow * 4u * g;
+    asm volatile(
+        "ds_write_b16 %0, %1\n\t"
+        "ds_write_b16 %0, %2 offset:%5\n\t"
+        "ds_write_b16 %0, %3 offset:%6\n\t"
+        "ds_write_b16 %0, %4 offset:%7"
+        :
+        : "v"(wa), "v"(x0), "v"(x1), "v"(x2), "v"(x3), "n"(kAbRow), "n"(2 * kAbRow),
+          "n"(3 * kAbRow)
+        : "memory");
     const int cnt = __builtin_popcount(m);
-    const bool in = lane >= npend && lane < npend + cnt;
-    prow = in ? nr : prow;
-    pa = in ? (unsigned)na : pa;
-    if (npend == 0) kf = kr;
+    prow = lane < 32 && ((lane - ebase - npend) & 31) < cnt ? nr : prow;
     npend += cnt;
   };
 
@@ -2189,7 +2194,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     fa[s] = f16x4{0, 0, 0, 0};
   }
 
-  bool more = true;
+  bool more = true, blocks = true;
   for (;;) {
     const bool fin = !more;
 #pragma unroll
@@ -2197,33 +2202,37 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       // consume the item issued P slots ago
       if (kind[s]) {
         wait_vm_older(nis - stamp[s]);
+        f16x4 fb[16];
+        asm volatile(
+            "ds_read_b64_tr_b16 %0, %16\n\t"
+            "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
+            "ds_read_b64_tr_b16 %2, %16 offset:1024\n\t"
+            "ds_read_b64_tr_b16 %3, %16 offset:1536\n\t"
+            "ds_read_b64_tr_b16 %4, %16 offset:2048\n\t"
+            "ds_read_b64_tr_b16 %5, %16 offset:2560\n\t"
+            "ds_read_b64_tr_b16 %6, %16 offset:3072\n\t"
+            "ds_read_b64_tr_b16 %7, %16 offset:3584\n\t"
+            "ds_read_b64_tr_b16 %8, %16 offset:4096\n\t"
+            "ds_read_b64_tr_b16 %9, %16 offset:4608\n\t"
+            "ds_read_b64_tr_b16 %10, %16 offset:5120\n\t"
+            "ds_read_b64_tr_b16 %11, %16 offset:5632\n\t"
+            "ds_read_b64_tr_b16 %12, %16 offset:6144\n\t"
+            "ds_read_b64_tr_b16 %13, %16 offset:6656\n\t"
+            "ds_read_b64_tr_b16 %14, %16 offset:7168\n\t"
+            "ds_read_b64_tr_b16 %15, %16 offset:7680\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+              "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7]), "=&v"(fb[8]), "=&v"(fb[9]),
+              "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]), "=&v"(fb[13]), "=&v"(fb[14]),
+              "=&v"(fb[15])
+            : "v"(tro + (unsigned)(s * kStage))
+            : "memory");
 #pragma unroll
-        for (int t0 = 0; t0 < 16; t0 += 8) {
-          f16x4 fb[8];
-          asm volatile(
-              "ds_read_b64_tr_b16 %0, %8 offset:%9\n\t"
-              "ds_read_b64_tr_b16 %1, %8 offset:%10\n\t"
-              "ds_read_b64_tr_b16 %2, %8 offset:%11\n\t"
-              "ds_read_b64_tr_b16 %3, %8 offset:%12\n\t"
-              "ds_read_b64_tr_b16 %4, %8 offset:%13\n\t"
-              "ds_read_b64_tr_b16 %5, %8 offset:%14\n\t"
-              "ds_read_b64_tr_b16 %6, %8 offset:%15\n\t"
-              "ds_read_b64_tr_b16 %7, %8 offset:%16\n\t"
-              "s_waitcnt lgkmcnt(0)"
-              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
-                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
-              : "v"(tro), "n"(s * kStage + 512 * t0), "n"(s * kStage + 512 * (t0 + 1)),
-                "n"(s * kStage + 512 * (t0 + 2)), "n"(s * kStage + 512 * (t0 + 3)),
-                "n"(s * kStage + 512 * (t0 + 4)), "n"(s * kStage + 512 * (t0 + 5)),
-                "n"(s * kStage + 512 * (t0 + 6)), "n"(s * kStage + 512 * (t0 + 7))
-              : "memory");
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            acc[t0 + t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[t0 + t], 0, 0, 0);
-        }
+        for (int t = 0; t < 16; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[t], 0, 0, 0);
       }
       // produce the next item into slot s: read blocks until 16 columns are
-      // pending, the blocks run out, or the list would outgrow the A ring
+      // pending or the blocks run out
       kind[s] = 0;
       if (more) {
         while (npend < 16 && blocks) {
@@ -2231,7 +2240,6 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
             blocks = false;
             break;
           }
-          if (npend > 0 && kr + 1 - kf > kSpan) break;
           advance();
         }
         if (npend == 0) {
@@ -2239,45 +2247,33 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
         } else {
           const int cnt = min(npend, 16);
           // B rows: lane L -> item row L & 15 (the zero row past cnt)
-          const int r = __builtin_amdgcn_ds_bpermute(4 * r16, prow);
+          const int r = __builtin_amdgcn_ds_bpermute(4 * ((ebase + r16) & 31), prow);
           const char* base = r16 < cnt ? reinterpret_cast<const char*>(B) + (size_t)r * ldb2 : zrow;
-          char* const stage = smem + kRing + s * kStage;
+          char* const stage = smem + kStg + s * kStage;
 #pragma unroll
           for (int j = 0; j < 8; ++j)
             __builtin_amdgcn_global_load_lds((gbl_void_t)(base + boff[j]),
                                              (lds_void_t)(stage + 1024 * j), 16, 0, 0);
           nis += 8;
-          // A fragment: lane (g, r) <- A[r][entry 4g + i]
-          unsigned ad[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int e = 4 * g + i;
-            const unsigned a = (unsigned)__builtin_amdgcn_ds_bpermute(4 * e, (int)pa);
-            ad[i] = (e < cnt ? a : zslot) + 32u * r16;
+          // A fragment: lane (g, r) <- A[r][entries 4g .. 4g + 3]
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          u32x2 y;
+          asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                       : "=&v"(y)
+                       : "v"(abuf + kAbRow * (unsigned)r16 + 2u * (unsigned)((ebase + 4 * g) & 31))
+                       : "memory");
+          unsigned y0 = y[0], y1 = y[1];
+          if (cnt < 16) {  // padded entries: stale values (NaN / inf) must not meet the zero rows
+            const int e = 4 * g;
+            y0 &= (e < cnt ? 0xffffu : 0u) | (e + 1 < cnt ? 0xffff0000u : 0u);
+            y1 &= (e + 2 < cnt ? 0xffffu : 0u) | (e + 3 < cnt ? 0xffff0000u : 0u);
           }
-          unsigned y0, y1, y2, y3;
-          asm volatile(
-              "ds_read_u16 %0, %4\n\t"
-              "ds_read_u16 %1, %5\n\t"
-              "ds_read_u16 %2, %6\n\t"
-              "ds_read_u16 %3, %7\n\t"
-              "s_waitcnt lgkmcnt(0)"
-              : "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3)
-              : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
-              : "memory");
-          const unsigned u[2] = {y0 | (y1 << 16), y2 | (y3 << 16)};
+          const unsigned u[2] = {y0, y1};
           fa[s] = *reinterpret_cast<const f16x4*>(u);
           kind[s] = 1;
           stamp[s] = nis;
-          // the entries past 16 (all from block kr) move down
-          if (npend > 16) {
-            prow = __builtin_amdgcn_ds_bpermute(4 * ((lane + 16) & 63), prow);
-            pa = (unsigned)__builtin_amdgcn_ds_bpermute(4 * ((lane + 16) & 63), (int)pa);
-            npend -= 16;
-            kf = kr;
-          } else {
-            npend = 0;
-          }
+          ebase ^= 16;
+          npend = npend > 16 ? npend - 16 : 0;
         }
       }
     }
@@ -2760,6 +2756,9 @@ constexpr int kBsr16F16LdsDefault = 4725;
 // 48 D DA: 512 output columns per workgroup (A once per 512 columns, 8 tiles
 // per wave): products stand-in K = 512 6.89 ms vs 7.08 for 4725.
 constexpr int kBsr16F16LdsWide = 4825;
+// Column stream (bsr16_f16_cs_kernel, 2 item stages, NA = 8, DA = 4): products
+// stand-in K = 512 4.57 ms vs 5.94 for 4825 (profiles/r02_cs16_v3_sweep.jsonl).
+constexpr int kBsr16F16Cs = 5021;
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -3044,7 +3043,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
     dim3 grid(mb, (n + 255) / 256);
     // K > 256: one workgroup per 512 columns (A read once per 512)
     const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45
-                       ? (n > 256 ? kBsr16F16LdsWide : kBsr16F16LdsDefault)
+                       ? (n >= 128 ? kBsr16F16Cs : kBsr16F16LdsDefault)
                        : var;
 #define L(D)                                                                                      \
   if (crow) hipLaunchKernelGGL((bsr16_lds_kernel<_Float16, true, D>), grid, dim3(256), 0,          \
@@ -3080,16 +3079,17 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   }
       CM512(4825, 2, 5, 1) CM512(4826, 2, 6, 1) CM512(4836, 3, 6, 1) CM512(4824, 2, 4, 1)
 #undef CM512
-      // column stream (bsr16_f16_cs_kernel): 50PN = P item stages, NA = 16 (N = 1) / 32 (N = 2)
-#define CS16(V, P, A)                                                                             \
+      // column stream (bsr16_f16_cs_kernel): 50PN = P item stages, (NA, DA) = (8, 4) (N = 1),
+      // (16, 8) (N = 2), (8, 2) (N = 0)
+#define CS16(V, P, A, D)                                                                          \
   case V:                                                                                         \
-    if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A>), grid, dim3(64), 0, ctx->stream, \
+    if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A, D>), grid, dim3(64), 0, ctx->stream, \
                                  mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);        \
-    else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A>), grid, dim3(64), 0, ctx->stream,     \
+    else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A, D>), grid, dim3(64), 0, ctx->stream,  \
                             mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);             \
     break;
-      CS16(5021, 2, 16) CS16(5031, 3, 16) CS16(5041, 4, 16) CS16(5051, 5, 16) CS16(5032, 3, 32)
-      CS16(5042, 4, 32)
+      CS16(5021, 2, 8, 4) CS16(5031, 3, 8, 4) CS16(5041, 4, 8, 4) CS16(5022, 2, 16, 8)
+      CS16(5032, 3, 16, 8) CS16(5020, 2, 8, 2)
 #undef CS16
 #undef CM
       case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4

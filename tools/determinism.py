@@ -54,7 +54,7 @@ def main():
             def run():
                 ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K)
                 return C
-            bad += check("bsr32 fp32 K=128 (CM4)", run, reps)
+            bad += check("bsr32 fp32 K=128 (column stream, CS2)", run, reps)
         else:
             bv16, B16 = bval.half(), B.half()
             del bval, B
@@ -62,7 +62,7 @@ def main():
             def run():
                 ops.bsrmm_f16(brp, bci, bv16, B16, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K)
                 return C
-            bad += check("bsr16 fp16 K=512 (CM)", run, reps)
+            bad += check("bsr16 fp16 K=512 (column stream, CS16)", run, reps)
             del bv16, B16
         del brp, bci, C
         torch.cuda.empty_cache()
