@@ -422,12 +422,12 @@ __global__ __launch_bounds__(256) void bsr32_f32_lds_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc, const int* __restrict__ rrp, const int* __restrict__ rci,
-    const float* __restrict__ rv, int m) {
+    const float* __restrict__ rv, int m, const int* __restrict__ order) {
   constexpr int kStage = 1024 + 32 * 128;  // floats: A block + B panel (20 KB)
   __shared__ __attribute__((aligned(16))) float smem[D * kStage];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int br = xcd_block_row(blockIdx.x, mb, XM);
+  const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, XM);
   const int jt = blockIdx.y * 128;  // first output column of the workgroup
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   if (!HYB && k0 >= k1) {  // empty block row: C = beta * C (alpha * 0)
@@ -1114,6 +1114,47 @@ __device__ __forceinline__ void wait_vm_older(int y) {
   asm volatile(SPMM_VM_LADDER("%0") : : "s"(y) : "scc", "memory");
 }
 
+// Longest-first block-row order for the one-wave-per-block-row kernels (the
+// column streams). Their waves run as long as their block rows; when the grid
+// is only a few waves per slot deep, dispatching in block-row order leaves a
+// tail of long rows started last (reddit stand-in, bs 32: a list-scheduling
+// model puts the makespan 55 % above the mean load, 18 % with the longest
+// rows first). A counting sort by blocks per row, descending, in one
+// workgroup: histogram of min(nnzb_row, 1023) in LDS, a scan, a scatter. The
+// order inside a bucket is whatever the atomics give: it only schedules, every
+// block row's result is the same in any order.
+// With a CSR remainder (crp, the fused hybrid: m rows, 32 per block row) the
+// key is (32 x blocks + remainder entries) / 8: a dense block's MFMA work
+// weighs about as much as 32 remainder gathers.
+__device__ __forceinline__ int block_row_key(int i, const int* __restrict__ rowptr,
+                                             const int* __restrict__ crp, int m) {
+  const int nb = rowptr[i + 1] - rowptr[i];
+  if (!crp) return min(nb, 1023);
+  const int rem = crp[min(32 * i + 32, m)] - crp[32 * i];
+  return min((32 * nb + rem) >> 3, 1023);
+}
+__global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int* __restrict__ rowptr,
+                                                               const int* __restrict__ crp, int m,
+                                                               int* __restrict__ order) {
+  __shared__ int cnt[1024];
+  const int t = threadIdx.x;
+  cnt[t] = 0;
+  __syncthreads();
+  for (int i = t; i < mb; i += 1024) atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m)], 1);
+  __syncthreads();
+  const int own = cnt[t];
+  for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan
+    const int u = t >= off ? cnt[t - off] : 0;
+    __syncthreads();
+    cnt[t] += u;
+    __syncthreads();
+  }
+  cnt[t] -= own;  // exclusive
+  __syncthreads();
+  for (int i = t; i < mb; i += 1024)
+    order[atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m)], 1)] = i;
+}
+
 template <bool CROW, int XM, int P, int NA>
 __global__ __launch_bounds__(64) void bsr32_f32_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
@@ -1368,11 +1409,15 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs_kernel(
 // ---------------------------------------------------------------------------
 // DIAG (diagnostic builds, wrong results, timing only): bit 0 no MFMA, bit 1
 // every B row from the L2-resident zero row, bit 2 every A copy from block k0.
-template <bool CROW, int XM, int P, int NA, int DIAG = 0>
+// O32: the B-row loads take the block's panel base in SGPRs and the row
+// offset c * ldb * 4 + column offset in the 32-bit VGPR offset (one s_mul and
+// one v_add per load instead of a 64-bit address on the scalar unit); needs
+// 32 * ldb * 4 < 2^31 (checked by the launcher).
+template <bool CROW, int XM, int P, int NA, int DIAG = 0, bool O32 = false>
 __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
-    float* __restrict__ C, int ldc) {
+    float* __restrict__ C, int ldc, const int* __restrict__ order) {
   static_assert(NA >= 2 && NA <= 4 && P >= 2 && P <= 16, "ring depths");
   constexpr int DA = NA - 1;  // A blocks in flight ahead of the producer's block
   // (column-major C reuses the LDS for a 128 x 36-float tile)
@@ -1380,7 +1425,7 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   float smem[CROW || NA * 1024 >= 128 * 36 ? NA * 1024 : 128 * 36];
   const int lane = threadIdx.x;
   const int j = lane & 31, h = lane >> 5;
-  const int br = xcd_block_row(blockIdx.x, mb, XM);
+  const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, XM);
   const int jt = blockIdx.y * 128;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const unsigned lds_a = (unsigned)reinterpret_cast<uintptr_t>(smem);
@@ -1432,6 +1477,7 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   const int a_sw = (j >> 1) & 7;
   const unsigned boff = 4u * (unsigned)min(jt + 4 * j + 2 * h, n - 2);  // byte offset in a row
   const size_t ldb4 = (size_t)ldb * 4;
+  const unsigned ldb4u = (unsigned)ldb * 4u;
 
   f32x32 u0, u1;  // MFMA halves u = 0, 1 (output columns 4j + 2b + u)
 #pragma unroll
@@ -1548,17 +1594,29 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
                        : "=&v"(ra0[s]), "=&v"(ra1[s])
                        : "v"(p0), "v"(p1)
                        : "memory");
-          asm volatile("global_load_dwordx2 %0, %1, %2"
-                       : "=&v"(rb0[s])
-                       : "v"(boff), "s"(bblk + ((DIAG & 2) ? 0 : (size_t)c0 * ldb4))
-                       : "memory");
+          if constexpr (O32)
+            asm volatile("global_load_dwordx2 %0, %1, %2"
+                         : "=&v"(rb0[s])
+                         : "v"(boff + (unsigned)c0 * ldb4u), "s"(bblk)
+                         : "memory");
+          else
+            asm volatile("global_load_dwordx2 %0, %1, %2"
+                         : "=&v"(rb0[s])
+                         : "v"(boff), "s"(bblk + ((DIAG & 2) ? 0 : (size_t)c0 * ldb4))
+                         : "memory");
           ++nis;
           kind[s] = 1;
           if (c1 != c0) {
-            asm volatile("global_load_dwordx2 %0, %1, %2"
-                         : "=&v"(rb1[s])
-                         : "v"(boff), "s"(bblk + ((DIAG & 2) ? 0 : (size_t)c1 * ldb4))
-                         : "memory");
+            if constexpr (O32)
+              asm volatile("global_load_dwordx2 %0, %1, %2"
+                           : "=&v"(rb1[s])
+                           : "v"(boff + (unsigned)c1 * ldb4u), "s"(bblk)
+                           : "memory");
+            else
+              asm volatile("global_load_dwordx2 %0, %1, %2"
+                           : "=&v"(rb1[s])
+                           : "v"(boff), "s"(bblk + ((DIAG & 2) ? 0 : (size_t)c1 * ldb4))
+                           : "memory");
             ++nis;
             kind[s] = 2;
           }
@@ -2066,7 +2124,7 @@ template <bool CROW, int P, int NA, int DA>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
-    float beta, float* __restrict__ C, int ldc) {
+    float beta, float* __restrict__ C, int ldc, const int* __restrict__ order) {
   // the pair copied at block kr (blocks kr + DA + 2, + 3) overwrites blocks
   // kr + DA + 2 - NA, + 3 - NA, which must be read already (< kr)
   static_assert((NA & (NA - 1)) == 0 && DA % 2 == 0 && NA >= DA + 4 && P >= 2 && P <= 4,
@@ -2080,7 +2138,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int lane = threadIdx.x;
   const int g = lane >> 4, r16 = lane & 15, h = lane >> 5;
-  const int br = xcd_block_row(blockIdx.x, mb, 32);
+  const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
   const int jt = blockIdx.y * 256;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const unsigned lds0 = lds_addr(smem);
@@ -2735,8 +2793,11 @@ constexpr int kBsr32Default = 40;
 // Column stream with register items (bsr32_f32_cs2_kernel, 6 item slots, 3 A
 // slots): products stand-in 3.05 ms, reddit 2.01 (4583, the LDS item ring:
 // 3.21 / 2.16; CM4 4402: 4.38 / 2.59; profiles/r02_cs_sweep.jsonl,
-// r02_cs2_sweep.jsonl).
-constexpr int kBsr32LdsDefault = 4596;
+// r02_cs2_sweep.jsonl). With 32-bit row offsets in the B loads (4556, O32):
+// products 3.02 vs 3.11, reddit 2.04 vs 2.05 (profiles/r02_bsr_order_sweep.jsonl);
+// 4596 where 32 * ldb * 4 does not fit 31 bits.
+constexpr int kBsr32LdsDefault = 4556;
+constexpr int kBsr32LdsDefaultWideLdb = 4596;
 // Blocks known to be dense (the hybrid's BSR part, MFMA-pipe bound): the
 // full-panel kernel with D = 2 (40 KB, 4 workgroups per CU) and the chunked
 // XCD order. Products stand-in hybrid part 1.71 vs 1.87 ms for D = 3 (4124),
@@ -2772,6 +2833,30 @@ int variant_override() {
   return var;
 }
 #define SPMM_COMMA ,
+
+// Block-row order for the column-stream kernels: longest first when the grid
+// is at most kLptRounds waves per resident slot deep (a few long rows would
+// otherwise start last and run alone), else nullptr (the kernels' XCD-chunked
+// order, which keeps neighbouring block rows in one L2). SPMM_BSR_ORDER=1
+// forces longest first, 2 the XCD order (tuning). One launch of
+// block_row_order_kernel into the handle's order buffer, in stream order.
+constexpr int kLptRounds = 8;
+spmm_status_t block_row_order(spmm_context* ctx, int mb, int ntiles, const int* rowptr,
+                              const int** order, long slots_per_cu = 12, const int* crp = nullptr,
+                              int m = 0) {
+  static const int force = [] {
+    const char* e = getenv("SPMM_BSR_ORDER");
+    return e ? atoi(e) : 0;
+  }();
+  *order = nullptr;
+  const long waves = (long)mb * ntiles, slots = slots_per_cu * ctx->num_cus;
+  if (force == 2 || (force != 1 && waves > kLptRounds * slots)) return SPMM_STATUS_SUCCESS;
+  if (spmm_status_t st = spmm::ensure_order_buffer(ctx, mb)) return st;
+  hipLaunchKernelGGL(block_row_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, mb, rowptr,
+                     crp, m, ctx->order);
+  *order = ctx->order;
+  return SPMM_STATUS_SUCCESS;
+}
 
 #define SPMM_BSR_DISPATCH(KERNEL, TA, GRID, BLOCK, STREAM, ROWD, BR, CR, ...)                 \
   do {                                                                                    \
@@ -2822,15 +2907,19 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
     int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8) || var / 100 == 50
-                 ? (dense_blocks ? kBsr32LdsDense : kBsr32LdsDefault)
+                 ? (dense_blocks ? kBsr32LdsDense
+                                 : ((size_t)ldb * 128 < (1u << 31) ? kBsr32LdsDefault
+                                                                     : kBsr32LdsDefaultWideLdb))
                  : var;
+    if ((lv == 4556 || lv == 4558 || lv == 4554) && (size_t)ldb * 128 >= (1u << 31))
+      lv = kBsr32LdsDefaultWideLdb;  // O32 needs 32-row panels addressable in 31 bits
 #define L(D, X)                                                                                   \
   if (crow) hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, D, X>), grid, dim3(256), 0, ctx->stream,  \
                                mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, nullptr,  \
-                               nullptr, nullptr, 0);                                              \
+                               nullptr, nullptr, 0, nullptr);                                        \
   else hipLaunchKernelGGL((bsr32_f32_lds_kernel<false, D, X>), grid, dim3(256), 0, ctx->stream,      \
                           mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, nullptr,       \
-                          nullptr, nullptr, 0);
+                          nullptr, nullptr, 0, nullptr);
     // split-bf16 (opt-in): wave-pair split-K form for row-major C (products
     // hybrid 1.86-1.87 vs 1.89 ms fused, reddit 0.80 vs 0.83, profiles/r01_hybrid_split.jsonl), else one k range per wave
     if (dense_blocks && var < 0 && (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16))
@@ -2839,16 +2928,16 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       case 4926:  // kBsr32LdsDense with split-bf16 products (SPMM_HYBRID_SPLIT_BF16)
         if (crow) hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, false, 24, true>), grid,
                                      dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,
-                                     alpha, beta, C, ldc, nullptr, nullptr, nullptr, 0);
+                                     alpha, beta, C, ldc, nullptr, nullptr, nullptr, 0, nullptr);
         else hipLaunchKernelGGL((bsr32_f32_lds_kernel<false, 2, 32, false, 24, true>), grid,
                                 dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,
-                                alpha, beta, C, ldc, nullptr, nullptr, nullptr, 0);
+                                alpha, beta, C, ldc, nullptr, nullptr, nullptr, 0, nullptr);
         break;
       case 4927:  // 4926 with split-K over wave pairs (PAIR)
         if (!crow) { timing_end(ctx, slot); return SPMM_STATUS_INVALID_VALUE; }
         hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, false, 24, true, true>), grid,
                            dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha,
-                           beta, C, ldc, nullptr, nullptr, nullptr, 0);
+                           beta, C, ldc, nullptr, nullptr, nullptr, 0, nullptr);
         break;
       case 4098: L(2, 0) break;
       case 4099: L(3, 0) break;
@@ -2890,15 +2979,24 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       // (P, NA): 4593 (8, 3), 4594 (8, 4), 4592 (8, 2), 4596 (6, 3),
       // 4597 (4, 3), 4598 (12, 3), 4599 (16, 3)
 #define CS2(V, P, A, ...)                                                                        \
-  case V:                                                                                        \
+  case V: {                                                                                      \
+    const int* ord = nullptr;                                                                    \
+    if (const spmm_status_t st = block_row_order(ctx, mb, (n + 127) / 128, rowptr, &ord)) {      \
+      timing_end(ctx, slot);                                                                     \
+      return st;                                                                                 \
+    }                                                                                            \
     if (crow) hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, P, A, ##__VA_ARGS__>), grid,    \
                                  dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,   \
-                                 alpha, beta, C, ldc);                                           \
+                                 alpha, beta, C, ldc, ord);                                      \
     else hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, P, A, ##__VA_ARGS__>), grid, dim3(64), 0, \
-                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc); \
-    break;
+                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, \
+                            ord);                                                                \
+    break;                                                                                       \
+  }
       CS2(4593, 8, 3) CS2(4594, 8, 4) CS2(4592, 8, 2) CS2(4596, 6, 3) CS2(4597, 4, 3)
       CS2(4598, 12, 3) CS2(4599, 16, 3)
+      // 455P: 32-bit row offsets in the load's VGPR offset (O32), P item slots, NA = 3
+      CS2(4556, 6, 3, 0, true) CS2(4558, 8, 3, 0, true) CS2(4554, 4, 3, 0, true)
       // diagnostics (wrong results): 960D = (6, 3) with DIAG D
       CS2(9601, 6, 3, 1) CS2(9602, 6, 3, 2) CS2(9604, 6, 3, 4) CS2(9606, 6, 3, 6)
       CS2(9607, 6, 3, 7)
@@ -2996,28 +3094,35 @@ spmm_status_t launch_hybrid32_fused(spmm_context* ctx, int m, int n, float alpha
   const int slot = timing_begin(ctx);
   const dim3 grid(mb, (n + 127) / 128);
   const int var = variant_override();
+  // longest first (blocks and remainder entries) when the grid is a few
+  // workgroups per slot deep (4 workgroups per CU)
+  const int* ord = nullptr;
+  if (const spmm_status_t st = block_row_order(ctx, mb, grid.y, brp, &ord, 4, crp, m)) {
+    timing_end(ctx, slot);
+    return st;
+  }
   if (var == 4107)
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 3, 1, true>), grid, dim3(256), 0, ctx->stream,
-                       mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+                       mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m, ord);
   else if (var == 4124)
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 3, 32, true>), grid, dim3(256), 0, ctx->stream,
-                       mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+                       mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m, ord);
   else if (var == 4126)  // 32 remainder gathers in flight: 113 VGPRs, 3 workgroups per CU
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 32>), grid, dim3(256), 0,
-                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m, ord);
   else if (var == 4128)
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 16>), grid, dim3(256), 0,
-                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m, ord);
   else if (var == 4926)  // split-bf16, one k range per wave
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 24, true>), grid, dim3(256), 0,
-                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m, ord);
   else if (var == 4927 || (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16))  // wave-pair split-K
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 24, true, true>), grid, dim3(256), 0,
-                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m, ord);
   else  // D = 2 and 24 remainder gathers in flight (73 VGPRs): 4 workgroups per CU.
         // Products stand-in 2.09 ms vs 2.42 with 32 in flight and 2.81 with D = 3.
     hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, true, 24>), grid, dim3(256), 0,
-                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m);
+                       ctx->stream, mb, n, brp, bci, bval, B, ldb, alpha, beta, C, ldc, crp, cci, cv, m, ord);
   timing_end(ctx, slot);
   return from_hip(hipGetLastError());
 }
@@ -3082,12 +3187,18 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       // column stream (bsr16_f16_cs_kernel): 50PN = P item stages, (NA, DA) = (8, 4) (N = 1),
       // (16, 8) (N = 2), (8, 2) (N = 0)
 #define CS16(V, P, A, D)                                                                          \
-  case V:                                                                                         \
+  case V: {                                                                                       \
+    const int* ord = nullptr;                                                                     \
+    if (const spmm_status_t st = block_row_order(ctx, mb, (n + 255) / 256, rowptr, &ord)) {       \
+      timing_end(ctx, slot);                                                                      \
+      return st;                                                                                  \
+    }                                                                                             \
     if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A, D>), grid, dim3(64), 0, ctx->stream, \
-                                 mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);        \
+                                 mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, ord);   \
     else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A, D>), grid, dim3(64), 0, ctx->stream,  \
-                            mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);             \
-    break;
+                            mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, ord);        \
+    break;                                                                                        \
+  }
       CS16(5021, 2, 8, 4) CS16(5031, 3, 8, 4) CS16(5041, 4, 8, 4) CS16(5022, 2, 16, 8)
       CS16(5032, 3, 16, 8) CS16(5020, 2, 8, 2)
 #undef CS16

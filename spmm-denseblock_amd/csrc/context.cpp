@@ -27,6 +27,27 @@ spmm_status_t ensure_workspace(spmm_context* ctx, size_t bytes) {
   return SPMM_STATUS_SUCCESS;
 }
 
+spmm_status_t ensure_order_buffer(spmm_context* ctx, size_t n) {
+  if (n <= ctx->order_cap) return SPMM_STATUS_SUCCESS;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (n <= ctx->order_cap) return SPMM_STATUS_SUCCESS;
+  if (ctx->order) {
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return from_hip(e);
+    (void)hipFree(ctx->order);
+    ctx->order = nullptr;
+    ctx->order_cap = 0;
+  }
+  const size_t want = n + n / 4 + 1024;
+  hipError_t e = hipMalloc(&ctx->order, want * sizeof(int));
+  if (e != hipSuccess) {
+    ctx->order = nullptr;
+    return from_hip(e);
+  }
+  ctx->order_cap = want;
+  return SPMM_STATUS_SUCCESS;
+}
+
 int timing_begin(spmm_context* ctx) {
   if (!ctx->timing) return -1;
   const size_t slot = ctx->ev_used;
@@ -112,10 +133,9 @@ spmm_status_t spmm_create(spmm_handle_t* handle) {
 
 spmm_status_t spmm_destroy(spmm_handle_t h) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
-  if (h->ws) {
-    (void)hipStreamSynchronize(h->stream);
-    (void)hipFree(h->ws);
-  }
+  if (h->ws || h->order) (void)hipStreamSynchronize(h->stream);
+  if (h->ws) (void)hipFree(h->ws);
+  if (h->order) (void)hipFree(h->order);
   for (auto e : h->ev_start) (void)hipEventDestroy(e);
   for (auto e : h->ev_stop) (void)hipEventDestroy(e);
   delete h;

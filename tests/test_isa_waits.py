@@ -165,7 +165,7 @@ def _vregs(ops: str) -> set:
     return out
 
 
-@pytest.mark.parametrize("kernel,tag", [("bsr32_f32_cs2_kernel", "ELi0EEE"),
+@pytest.mark.parametrize("kernel,tag", [("bsr32_f32_cs2_kernel", "ELi0ELb"),
                                         ("bsr16_f16_cs_kernel", "")])
 def test_column_stream_registers_in_flight_are_asm_only(bsr_asm, kernel, tag):
     """bsr32_f32_cs2_kernel loads B rows, block-column chunks and A columns
