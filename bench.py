@@ -79,6 +79,25 @@ WORKLOADS = {
 METRIC = "SpMM GFLOP/s (2*nnz*K/t) + achieved HBM GB/s, ogbn-products K=128"
 
 
+BSR_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_bytes", "bytes.jsonl")
+
+
+def bsr_traffic(workload: str, kernel: str):
+    """PMC HBM bytes per launch of a BSR workload's kernel (tools/pmc_bytes.sh:
+    FETCH_SIZE x calibration + WRITE_SIZE, MI355X_MICROARCH.md §HBM), the last
+    matching record of profiles/r02_pmc_bytes/bytes.jsonl, or None."""
+    rec = None
+    try:
+        with open(BSR_TRAFFIC) as f:
+            for line in f:
+                r = json.loads(line)
+                if r.get("workload") == workload and r.get("kernel") == kernel:
+                    rec = r
+    except (OSError, ValueError):
+        return None
+    return rec and rec.get("counter_bytes_per_launch")
+
+
 def csr_bytes(n_rows: int, nnz: int, K: int) -> int:
     """SURVEY.md §8(d) CSR gather model: rowptr + (colind, val) + one B row per
     nnz + the C write."""
@@ -645,7 +664,10 @@ def run_bsr(args, W, world, rank, dev, dist):
                 "parallelism": "single"},
         roofline={"bound": "hbm", "achieved": round(cm_bytes / t / 1e9, 1),
                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                  "frac": round(cm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                  "frac": round(cm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4),
+                  "traffic": None if args.bsr_layout != "row" else bsr_traffic(
+                      args.workload, "bsr32_f32_cs2_kernel" if bs == 32 else
+                      "bsr16_f16_cs_kernel" if cs16 else "bsr16_cm_kernel"),
                   "kernel": (("bsr32_f32_cs2_kernel" if bs == 32 else
                               "bsr16_f16_cs_kernel" if cs16 else
                               f"bsr16_cm_kernel<{'f32' if dt == 'fp32' else 'f16'}>")
@@ -664,6 +686,12 @@ def run_bsr(args, W, world, rank, dev, dist):
                   "full_panel_model_GBps": round(kbytes / t / 1e9, 1)},
         csr_same_matrix_ms=round(csr_ms, 4), csr2bsr_host_seconds=round(t_conv, 2),
         gen_seconds=round(t_gen, 2), reorder=reorder)
+    tr = rec["roofline"]["traffic"]
+    if tr:
+        # the PMC bytes (profiled launch) over this run's kernel time: the HBM
+        # rate the kernel actually drives, beside the byte-model rate above
+        rec["roofline"]["traffic_GBps"] = round(tr / t / 1e9, 1)
+        rec["roofline"]["traffic_frac"] = round(tr / t / 1e9 / HBM_PEAK_GBPS, 4)
     return rec, None
 
 

@@ -2130,7 +2130,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   static_assert((NA & (NA - 1)) == 0 && DA % 2 == 0 && NA >= DA + 4 && P >= 2 && P <= 4,
                 "ring depths");
   constexpr int kStage = 16 * 512;  // one item: 16 B rows x 256 fp16 columns
-  constexpr int kAbRow = 72;        // A-fragment buffer row: 32 entries + a dummy entry + pad
+  constexpr int kAbRow = 136;       // A-fragment buffer row: 64 entries + a dummy entry + pad
   constexpr int kAbuf = NA * 512;   // offset of the A-fragment buffer
   constexpr int kStg = kAbuf + 16 * kAbRow;  // offset of the item stages
   constexpr int kLds = kStg + P * kStage;
@@ -2181,13 +2181,13 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     }
   }
 
-  int kr = -1;  // producer block, relative to k0
+  int kr = 0;  // next block to read, relative to k0 (even)
   const unsigned lowm = (1u << r16) - 1u;
-  int prow = 0;  // pending B row indices (lane e < 32: entry e)
+  int prow = 0;  // pending B row indices (lane e: entry e, circular over 64)
   int npend = 0, ebase = 0;
-  // next block: its A (pair) landed, its mask, its columns pushed to the list
-  auto advance = [&]() {
-    ++kr;
+  // the next two blocks (one A pair): their masks, their columns pushed to the
+  // list. One LDS round trip reads both blocks' values, one more pushes both.
+  auto advance2 = [&]() {
     if ((kr & 63) == 0) {  // next block-column chunk
       asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
                    : "=&v"(ccur)
@@ -2195,49 +2195,79 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
                    : "scc", "memory");
       if (k0 + kr + 64 < k1) load_cols(k0 + kr + 64);
     }
-    const int bc = __builtin_amdgcn_readlane(ccur, kr & 63);
-    if ((kr & 1) == 0) {
-      wait_vm_older(nis - ast[0]);  // pair kr / 2 landed
+    const bool two = k0 + kr + 1 < k1;
+    const int bc0 = __builtin_amdgcn_readlane(ccur, kr & 63);
+    const int bc1 = __builtin_amdgcn_readlane(ccur, (kr + 1) & 63);
+    wait_vm_older(nis - ast[0]);  // pair kr / 2 landed
 #pragma unroll
-      for (int q = 0; q < DA / 2; ++q) ast[q] = ast[q + 1];
-      if (k0 + kr + DA + 2 < k1) {
-        issue_a(kr + DA + 2);
-        ast[DA / 2] = nis;
-      } else {
-        ast[DA / 2] = -64;
-      }
+    for (int q = 0; q < DA / 2; ++q) ast[q] = ast[q + 1];
+    if (k0 + kr + DA + 2 < k1) {
+      issue_a(kr + DA + 2);
+      ast[DA / 2] = nis;
+    } else {
+      ast[DA / 2] = -64;
     }
-    unsigned x0, x1, x2, x3;
+    unsigned x[8];
     asm volatile(
-        "ds_read_u16 %0, %4\n\t"
-        "ds_read_u16 %1, %4 offset:32\n\t"
-        "ds_read_u16 %2, %4 offset:64\n\t"
-        "ds_read_u16 %3, %4 offset:96\n\t"
+        "ds_read_u16 %0, %8\n\t"
+        "ds_read_u16 %1, %8 offset:32\n\t"
+        "ds_read_u16 %2, %8 offset:64\n\t"
+        "ds_read_u16 %3, %8 offset:96\n\t"
+        "ds_read_u16 %4, %8 offset:512\n\t"
+        "ds_read_u16 %5, %8 offset:544\n\t"
+        "ds_read_u16 %6, %8 offset:576\n\t"
+        "ds_read_u16 %7, %8 offset:608\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+        : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]),
+          "=&v"(x[6]), "=&v"(x[7])
         : "v"(lds0 + 512u * (unsigned)(kr & (NA - 1)) + 128u * g + 2u * r16)
         : "memory");
-    const unsigned long long b = __builtin_amdgcn_ballot_w64(((x0 | x1 | x2 | x3) & 0x7fffu) != 0u);
-    const unsigned w = (unsigned)b | (unsigned)(b >> 32);
-    const unsigned m = (w | (w >> 16)) & 0xffffu;
-    if (m == 0u) return;
-    const bool bit = (m >> r16) & 1u;
-    const int pos = (ebase + npend + __builtin_popcount(m & lowm)) & 31;
-    const int nr = __builtin_amdgcn_ds_permute(4 * (lane < 16 && bit ? pos : 63), bc * 16 + r16);
-    // (entry 32 of each row takes the writes of empty columns)
-    const unsigned wa = abuf + 2u * (unsigned)(bit ? pos : 32) + kAbRow * 4u * g;
+    kr += 2;
+    unsigned m[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const unsigned long long b =
+          __builtin_amdgcn_ballot_w64(((x[4 * u] | x[4 * u + 1] | x[4 * u + 2] | x[4 * u + 3]) & 0x7fffu) != 0u);
+      const unsigned w = (unsigned)b | (unsigned)(b >> 32);
+      m[u] = (w | (w >> 16)) & 0xffffu;
+    }
+    if (!two) m[1] = 0u;  // the pair's second copy repeated the last block
+    const int cnt0 = __builtin_popcount(m[0]), cnt1 = __builtin_popcount(m[1]);
+    if (cnt0 + cnt1 == 0) return;
+    // lane c < 16 with bit c set -> entry ebase + npend (+ cnt0) + popcount(mask below c);
+    // other lanes -> the entry just before the range (not taken by the merge)
+    const int s0 = ebase + npend, s1 = s0 + cnt0;
+    int d[2], wa[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool bit = (m[u] >> r16) & 1u;
+      const int st = u ? s1 : s0;
+      d[u] = 4 * ((lane < 16 && bit ? st + __builtin_popcount(m[u] & lowm) : st + 63) & 63);
+      // A values of column r16, rows 4g .. 4g + 3 -> buffer column (entry 64 for empty columns)
+      wa[u] = (int)(abuf + 2u * (unsigned)(bit ? ((st + __builtin_popcount(m[u] & lowm)) & 63) : 64) +
+                    kAbRow * 4u * g);
+    }
+    int nr0, nr1;
     asm volatile(
-        "ds_write_b16 %0, %1\n\t"
-        "ds_write_b16 %0, %2 offset:%5\n\t"
-        "ds_write_b16 %0, %3 offset:%6\n\t"
-        "ds_write_b16 %0, %4 offset:%7"
-        :
-        : "v"(wa), "v"(x0), "v"(x1), "v"(x2), "v"(x3), "n"(kAbRow), "n"(2 * kAbRow),
-          "n"(3 * kAbRow)
+        "ds_write_b16 %2, %4\n\t"
+        "ds_write_b16 %2, %5 offset:%12\n\t"
+        "ds_write_b16 %2, %6 offset:%13\n\t"
+        "ds_write_b16 %2, %7 offset:%14\n\t"
+        "ds_write_b16 %3, %8\n\t"
+        "ds_write_b16 %3, %9 offset:%12\n\t"
+        "ds_write_b16 %3, %10 offset:%13\n\t"
+        "ds_write_b16 %3, %11 offset:%14\n\t"
+        "ds_permute_b32 %0, %15, %17\n\t"
+        "ds_permute_b32 %1, %16, %18\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(nr0), "=&v"(nr1)
+        : "v"(wa[0]), "v"(wa[1]), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]),
+          "v"(x[5]), "v"(x[6]), "v"(x[7]), "n"(kAbRow), "n"(2 * kAbRow), "n"(3 * kAbRow),
+          "v"(d[0]), "v"(d[1]), "v"(bc0 * 16 + r16), "v"(bc1 * 16 + r16)
         : "memory");
-    const int cnt = __builtin_popcount(m);
-    prow = lane < 32 && ((lane - ebase - npend) & 31) < cnt ? nr : prow;
-    npend += cnt;
+    const int rel = (lane - s0) & 63;
+    prow = rel < cnt0 ? nr0 : (rel < cnt0 + cnt1 ? nr1 : prow);
+    npend += cnt0 + cnt1;
   };
 
   f32x4 acc[16];
@@ -2294,18 +2324,28 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       kind[s] = 0;
       if (more) {
         while (npend < 16 && blocks) {
-          if (k0 + kr + 1 >= k1) {
+          if (k0 + kr >= k1) {
             blocks = false;
             break;
           }
-          advance();
+          advance2();
         }
         if (npend == 0) {
           more = false;
         } else {
           const int cnt = min(npend, 16);
-          // B rows: lane L -> item row L & 15 (the zero row past cnt)
-          const int r = __builtin_amdgcn_ds_bpermute(4 * ((ebase + r16) & 31), prow);
+          // B rows: lane L -> item row L & 15 (the zero row past cnt); A fragment:
+          // lane (g, r) <- A[r][entries 4g .. 4g + 3]; one round trip for both
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          u32x2 y;
+          int r;
+          asm volatile("ds_bpermute_b32 %0, %2, %3\n\t"
+                       "ds_read_b64 %1, %4\n\t"
+                       "s_waitcnt lgkmcnt(0)"
+                       : "=&v"(r), "=&v"(y)
+                       : "v"(4 * ((ebase + r16) & 63)), "v"(prow),
+                         "v"(abuf + kAbRow * (unsigned)r16 + 2u * (unsigned)((ebase + 4 * g) & 63))
+                       : "memory");
           const char* base = r16 < cnt ? reinterpret_cast<const char*>(B) + (size_t)r * ldb2 : zrow;
           char* const stage = smem + kStg + s * kStage;
 #pragma unroll
@@ -2313,13 +2353,6 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
             __builtin_amdgcn_global_load_lds((gbl_void_t)(base + boff[j]),
                                              (lds_void_t)(stage + 1024 * j), 16, 0, 0);
           nis += 8;
-          // A fragment: lane (g, r) <- A[r][entries 4g .. 4g + 3]
-          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-          u32x2 y;
-          asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                       : "=&v"(y)
-                       : "v"(abuf + kAbRow * (unsigned)r16 + 2u * (unsigned)((ebase + 4 * g) & 31))
-                       : "memory");
           unsigned y0 = y[0], y1 = y[1];
           if (cnt < 16) {  // padded entries: stale values (NaN / inf) must not meet the zero rows
             const int e = 4 * g;
@@ -2330,7 +2363,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
           fa[s] = *reinterpret_cast<const f16x4*>(u);
           kind[s] = 1;
           stamp[s] = nis;
-          ebase ^= 16;
+          ebase = (ebase + 16) & 63;
           npend = npend > 16 ? npend - 16 : 0;
         }
       }
