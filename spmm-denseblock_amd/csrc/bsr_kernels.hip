@@ -1413,7 +1413,13 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs_kernel(
 // offset c * ldb * 4 + column offset in the 32-bit VGPR offset (one s_mul and
 // one v_add per load instead of a 64-bit address on the scalar unit); needs
 // 32 * ldb * 4 < 2^31 (checked by the launcher).
-template <bool CROW, int XM, int P, int NA, int DIAG = 0, bool O32 = false>
+// PK: an item whose block has no second column left takes the first column
+// of the next block (its A column from that block's slot, its B row from that
+// block's panel), so single-column blocks no longer make half-empty items.
+// The first column's A read is complete before the next block's A copy can
+// reuse its slot: advancing reads the new block's mask with lgkmcnt(0) before
+// it issues that copy (NA = 3: the copy of block k + 3 lands in block k's slot).
+template <bool CROW, int XM, int P, int NA, int DIAG = 0, bool O32 = false, bool PK = false>
 __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -1518,6 +1524,53 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     rb0[s] = rb1[s] = f32x2{0.f, 0.f};
   }
 
+  // next block: its column chunk, A landed, its mask, the copy of block k + DA
+  auto advance = [&]() {
+    ++k;
+    aslot = aslot + 1 == NA ? 0 : aslot + 1;
+    const int kr = k - k0;
+    if ((kr & 63) == 0) {  // next block-column chunk
+      asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
+                   : "=&v"(ccur)
+                   : "s"(nis - cstamp), "v"(cnext)
+                   : "scc", "memory");
+      if (k + 64 < k1) load_cols(k + 64);
+    }
+    const int bc = __builtin_amdgcn_readlane(ccur, kr & 63);
+    bblk = (DIAG & 2) ? reinterpret_cast<const char*>(g_zero_row)
+                      : reinterpret_cast<const char*>(B) + (size_t)bc * 32 * ldb4;
+    wait_vm_older(nis - ast[0]);  // A(k) landed
+#pragma unroll
+    for (int d = 0; d + 1 < DA; ++d) ast[d] = ast[d + 1];
+    m = mask_of(aslot);
+    if (k + DA < k1) {
+      issue_a(k + DA, aslot + DA >= NA ? aslot + DA - NA : aslot + DA);
+      nis += 4;
+      ast[DA - 1] = nis;
+    } else {
+      ast[DA - 1] = -64;
+    }
+  };
+  // LDS address of this lane's A value of column c of the current block
+  auto acol = [&](int c) -> unsigned {
+    return lds_a + 4096u * (unsigned)aslot + a_row + 16u * (unsigned)((c >> 2) ^ a_sw) +
+           4u * (unsigned)(c & 3);
+  };
+  // B row c of the current block's panel into r (in flight: asm-only register)
+  auto load_row = [&](f32x2& r, int c) {
+    if constexpr (O32)
+      asm volatile("global_load_dwordx2 %0, %1, %2"
+                   : "=&v"(r)
+                   : "v"(boff + (unsigned)c * ldb4u), "s"(bblk)
+                   : "memory");
+    else
+      asm volatile("global_load_dwordx2 %0, %1, %2"
+                   : "=&v"(r)
+                   : "v"(boff), "s"(bblk + ((DIAG & 2) ? 0 : (size_t)c * ldb4))
+                   : "memory");
+    ++nis;
+  };
+
   for (;;) {
     const bool fin = !more;
 #pragma unroll
@@ -1554,71 +1607,40 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
             more = false;
             break;
           }
-          ++k;
-          aslot = aslot + 1 == NA ? 0 : aslot + 1;
-          const int kr = k - k0;
-          if ((kr & 63) == 0) {  // next block-column chunk
-            asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
-                         : "=&v"(ccur)
-                         : "s"(nis - cstamp), "v"(cnext)
-                         : "scc", "memory");
-            if (k + 64 < k1) load_cols(k + 64);
-          }
-          const int bc = __builtin_amdgcn_readlane(ccur, kr & 63);
-          bblk = (DIAG & 2) ? reinterpret_cast<const char*>(g_zero_row)
-                            : reinterpret_cast<const char*>(B) + (size_t)bc * 32 * ldb4;
-          wait_vm_older(nis - ast[0]);  // A(k) landed
-#pragma unroll
-          for (int d = 0; d + 1 < DA; ++d) ast[d] = ast[d + 1];
-          m = mask_of(aslot);
-          if (k + DA < k1) {
-            issue_a(k + DA, aslot + DA >= NA ? aslot + DA - NA : aslot + DA);
-            nis += 4;
-            ast[DA - 1] = nis;
-          } else {
-            ast[DA - 1] = -64;
-          }
+          advance();
         }
         if (m != 0u) {
           const int c0 = __builtin_ctz(m);
           m &= m - 1u;
-          int c1 = c0;
-          if (m != 0u) {
-            c1 = __builtin_ctz(m);
-            m &= m - 1u;
-          }
-          const unsigned base = lds_a + 4096u * (unsigned)aslot + a_row;
-          const unsigned p0 = base + 16u * (unsigned)((c0 >> 2) ^ a_sw) + 4u * (unsigned)(c0 & 3);
-          const unsigned p1 = base + 16u * (unsigned)((c1 >> 2) ^ a_sw) + 4u * (unsigned)(c1 & 3);
-          asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3"
-                       : "=&v"(ra0[s]), "=&v"(ra1[s])
-                       : "v"(p0), "v"(p1)
-                       : "memory");
-          if constexpr (O32)
-            asm volatile("global_load_dwordx2 %0, %1, %2"
-                         : "=&v"(rb0[s])
-                         : "v"(boff + (unsigned)c0 * ldb4u), "s"(bblk)
+          if constexpr (PK) {
+            // first column: A read and B load now, from this block
+            asm volatile("ds_read_b32 %0, %1" : "=&v"(ra0[s]) : "v"(acol(c0)) : "memory");
+            load_row(rb0[s], c0);
+            kind[s] = 1;
+            while (m == 0u && k + 1 < k1) advance();  // pair with the next block's first column
+            if (m != 0u) {
+              const int c1 = __builtin_ctz(m);
+              m &= m - 1u;
+              asm volatile("ds_read_b32 %0, %1" : "=&v"(ra1[s]) : "v"(acol(c1)) : "memory");
+              load_row(rb1[s], c1);
+              kind[s] = 2;
+            }
+          } else {
+            int c1 = c0;
+            if (m != 0u) {
+              c1 = __builtin_ctz(m);
+              m &= m - 1u;
+            }
+            asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3"
+                         : "=&v"(ra0[s]), "=&v"(ra1[s])
+                         : "v"(acol(c0)), "v"(acol(c1))
                          : "memory");
-          else
-            asm volatile("global_load_dwordx2 %0, %1, %2"
-                         : "=&v"(rb0[s])
-                         : "v"(boff), "s"(bblk + ((DIAG & 2) ? 0 : (size_t)c0 * ldb4))
-                         : "memory");
-          ++nis;
-          kind[s] = 1;
-          if (c1 != c0) {
-            if constexpr (O32)
-              asm volatile("global_load_dwordx2 %0, %1, %2"
-                           : "=&v"(rb1[s])
-                           : "v"(boff + (unsigned)c1 * ldb4u), "s"(bblk)
-                           : "memory");
-            else
-              asm volatile("global_load_dwordx2 %0, %1, %2"
-                           : "=&v"(rb1[s])
-                           : "v"(boff), "s"(bblk + ((DIAG & 2) ? 0 : (size_t)c1 * ldb4))
-                           : "memory");
-            ++nis;
-            kind[s] = 2;
+            load_row(rb0[s], c0);
+            kind[s] = 1;
+            if (c1 != c0) {
+              load_row(rb1[s], c1);
+              kind[s] = 2;
+            }
           }
           stamp[s] = nis;
         }
@@ -2828,8 +2850,10 @@ constexpr int kBsr32Default = 40;
 // 3.21 / 2.16; CM4 4402: 4.38 / 2.59; profiles/r02_cs_sweep.jsonl,
 // r02_cs2_sweep.jsonl). With 32-bit row offsets in the B loads (4556, O32):
 // products 3.02 vs 3.11, reddit 2.04 vs 2.05 (profiles/r02_bsr_order_sweep.jsonl);
-// 4596 where 32 * ldb * 4 does not fit 31 bits.
-constexpr int kBsr32LdsDefault = 4556;
+// 4596 where 32 * ldb * 4 does not fit 31 bits. With cross-block pairs (4516,
+// PK): reddit 2.01-2.02 vs 2.04-2.05, products 3.31 vs 3.30 (same box,
+// profiles/r02_cs2_pk_sweep.jsonl).
+constexpr int kBsr32LdsDefault = 4516;
 constexpr int kBsr32LdsDefaultWideLdb = 4596;
 // Blocks known to be dense (the hybrid's BSR part, MFMA-pipe bound): the
 // full-panel kernel with D = 2 (40 KB, 4 workgroups per CU) and the chunked
@@ -2944,7 +2968,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                  : ((size_t)ldb * 128 < (1u << 31) ? kBsr32LdsDefault
                                                                      : kBsr32LdsDefaultWideLdb))
                  : var;
-    if ((lv == 4556 || lv == 4558 || lv == 4554) && (size_t)ldb * 128 >= (1u << 31))
+    if ((lv == 4556 || lv == 4558 || lv == 4554 || lv == 4516 || lv == 4518) &&
+        (size_t)ldb * 128 >= (1u << 31))
       lv = kBsr32LdsDefaultWideLdb;  // O32 needs 32-row panels addressable in 31 bits
 #define L(D, X)                                                                                   \
   if (crow) hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, D, X>), grid, dim3(256), 0, ctx->stream,  \
@@ -3030,6 +3055,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       CS2(4598, 12, 3) CS2(4599, 16, 3)
       // 455P: 32-bit row offsets in the load's VGPR offset (O32), P item slots, NA = 3
       CS2(4556, 6, 3, 0, true) CS2(4558, 8, 3, 0, true) CS2(4554, 4, 3, 0, true)
+      // 457P... taken by CS; 4516 / 4518: O32 + cross-block pairs (PK), P = 6 / 8
+      CS2(4516, 6, 3, 0, true, true) CS2(4518, 8, 3, 0, true, true)
       // diagnostics (wrong results): 960D = (6, 3) with DIAG D
       CS2(9601, 6, 3, 1) CS2(9602, 6, 3, 2) CS2(9604, 6, 3, 4) CS2(9606, 6, 3, 6)
       CS2(9607, 6, 3, 7)
