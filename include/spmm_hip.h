@@ -326,10 +326,9 @@ spmm_status_t spmm_dbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_opera
  * one launch (MFMA part, then each block row's CSR remainder in the same
  * workgroup), or as two stream-ordered launches (BSR kernel, then the CSR
  * kernel with beta = 1). Same result up to the CSR kernel's split-row carries.
- * By default (flags 0) it is fused when the remainder averages at most 512
- * entries per block row (csrNnz <= 512 * mb): the remainder then fits beside
- * the MFMA work, while long per-block-row remainders leave a tail of single
- * workgroups. SPMM_HYBRID_FUSED / SPMM_HYBRID_TWO_LAUNCH force
+ * By default (flags 0) it is fused when the remainder averages at most 4096
+ * entries per block row (csrNnz <= 4096 * mb); longer per-block-row
+ * remainders keep the merge-path CSR kernel's balance. SPMM_HYBRID_FUSED / SPMM_HYBRID_TWO_LAUNCH force
  * one form. */
 #define SPMM_HYBRID_FUSED 1
 #define SPMM_HYBRID_TWO_LAUNCH 2

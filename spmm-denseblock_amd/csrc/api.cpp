@@ -334,9 +334,12 @@ spmm_status_t spmm_sbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_opera
 }  // extern "C"
 
 // Mean CSR-remainder entries per 32-row block row up to which the hybrid runs
-// fused by default (products stand-in 71: fused 2.41 vs 2.73 ms; reddit 222:
-// 1.01 vs 1.03; RCM-reordered reddit 2295: 2.37 vs 2.08, two launches win).
-constexpr int64_t kHybridFusedRemainderPerBlockRow = 512;
+// fused by default (products stand-in 71: fused 2.02 vs 2.68 ms; reddit 222:
+// 0.90 vs 0.96; RCM-reordered reddit 2295: 1.94 vs 2.02 since the fused kernel
+// starts the longest block rows first, 2.04 vs 2.03 before;
+// profiles/r02_hybrid_order_sweep.jsonl). Past it the merge-path CSR kernel's
+// balance is kept.
+constexpr int64_t kHybridFusedRemainderPerBlockRow = 4096;
 
 extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
     spmm_handle_t handle, int m, int n, int k, float alpha, const int* csrRowPtr,
@@ -347,7 +350,7 @@ extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
   // onto a zeroed C. Here the BSR part applies the caller's beta and the CSR
   // remainder accumulates on top, both on the handle's stream; with
   // fused (bs = 32) one launch does both per block row (§4a): by default when
-  // the remainder averages <= 512 entries per block row, or forced by flags.
+  // the remainder averages <= 4096 entries per block row, or forced by flags.
   if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
   if (m < 0 || n < 0 || k < 0 || csrNnz < 0 || nnzb < 0 || blockDim <= 0)
     return SPMM_STATUS_INVALID_VALUE;

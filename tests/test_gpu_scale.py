@@ -134,3 +134,13 @@ def test_reordered_reddit_scale_bsr_vs_csr(device, bs):
     torch.cuda.synchronize()
     _within(Cb[:n], Cc, absd, tol, f"RCM-reordered reddit bs{bs} BSR vs CSR")
     assert not bool(Cb[n:].any()), "padding rows of C must be zero"
+    if bs == 32:
+        # the hybrid on the same matrix: its remainder averages ~2,300 entries per
+        # block row with heavy rows of ~17 k, the fused launch's longest-first order
+        del brp, bci, bval, Cb
+        parts = prep.divide(n, rp, ci, v, bs, prep.hybrid_plan(rp, ci, bs, K)["density"])
+        d = _dev(*parts)
+        Ch = torch.empty((mb * bs, K), device=device)
+        ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=Ch, ldc=K)
+        torch.cuda.synchronize()
+        _within(Ch[:n], Cc, absd, 2 * TOL_F32, "RCM-reordered reddit hybrid vs CSR")
