@@ -2142,34 +2142,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 //    vector-memory operation of the loop is counted), 16 ds_read_b64_tr_b16
 //    under one lgkmcnt wait, 16 MFMAs into 16 accumulator tiles.
 // ---------------------------------------------------------------------------
-template <bool CROW, int P, int NA, int DA>
+template <bool CROW, int P, int NA, int DA, int COLS = 256>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
     float beta, float* __restrict__ C, int ldc, const int* __restrict__ order) {
   // the pair copied at block kr (blocks kr + DA + 2, + 3) overwrites blocks
   // kr + DA + 2 - NA, + 3 - NA, which must be read already (< kr)
-  static_assert((NA & (NA - 1)) == 0 && DA % 2 == 0 && NA >= DA + 4 && P >= 2 && P <= 4,
+  static_assert((NA & (NA - 1)) == 0 && DA % 2 == 0 && NA >= DA + 4 && P >= 2 && P <= 6,
                 "ring depths");
-  constexpr int kStage = 16 * 512;  // one item: 16 B rows x 256 fp16 columns
+  static_assert(COLS == 128 || COLS == 256, "column tile");
+  constexpr int kT = COLS / 16;           // 16-column MFMA tiles per wave
+  constexpr int kCopies = COLS / 32;      // copies per item (16 rows x 4 chunks each)
+  constexpr int kStage = 16 * COLS * 2;   // one item: 16 B rows x COLS fp16 columns
   constexpr int kAbRow = 136;       // A-fragment buffer row: 64 entries + a dummy entry + pad
   constexpr int kAbuf = NA * 512;   // offset of the A-fragment buffer
   constexpr int kStg = kAbuf + 16 * kAbRow;  // offset of the item stages
   constexpr int kLds = kStg + P * kStage;
-  static_assert(kLds >= 256 * 16 * 4, "column-major C tile fits");
+  static_assert(kLds >= COLS * 16 * 4, "column-major C tile fits");
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int lane = threadIdx.x;
   const int g = lane >> 4, r16 = lane & 15, h = lane >> 5;
   const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
-  const int jt = blockIdx.y * 256;
+  const int jt = blockIdx.y * COLS;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const unsigned lds0 = lds_addr(smem);
   const unsigned abuf = lds0 + kAbuf;
 
   // copy j: lane L loads chunk 4j + L / 16 of its row (columns jt + 8 (4j + L / 16) ..)
-  unsigned boff[8];
+  unsigned boff[kCopies];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) boff[j] = 2u * (unsigned)min(jt + 8 * (4 * j + g), n - 8);
+  for (int j = 0; j < kCopies; ++j) boff[j] = 2u * (unsigned)min(jt + 8 * (4 * j + g), n - 8);
   const size_t ldb2 = (size_t)ldb * 2;
   const char* const zrow = reinterpret_cast<const char*>(g_zero_row) - 2 * (size_t)jt;
   // transposed B reads: lane (g, q = (lane >> 2) & 3, p = lane & 3) reads row 4g + q,
@@ -2292,9 +2295,9 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     npend += cnt0 + cnt1;
   };
 
-  f32x4 acc[16];
+  f32x4 acc[kT];
 #pragma unroll
-  for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < kT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   int kind[P], stamp[P];
   f16x4 fa[P];
 #pragma unroll
@@ -2312,33 +2315,50 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       // consume the item issued P slots ago
       if (kind[s]) {
         wait_vm_older(nis - stamp[s]);
-        f16x4 fb[16];
-        asm volatile(
-            "ds_read_b64_tr_b16 %0, %16\n\t"
-            "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
-            "ds_read_b64_tr_b16 %2, %16 offset:1024\n\t"
-            "ds_read_b64_tr_b16 %3, %16 offset:1536\n\t"
-            "ds_read_b64_tr_b16 %4, %16 offset:2048\n\t"
-            "ds_read_b64_tr_b16 %5, %16 offset:2560\n\t"
-            "ds_read_b64_tr_b16 %6, %16 offset:3072\n\t"
-            "ds_read_b64_tr_b16 %7, %16 offset:3584\n\t"
-            "ds_read_b64_tr_b16 %8, %16 offset:4096\n\t"
-            "ds_read_b64_tr_b16 %9, %16 offset:4608\n\t"
-            "ds_read_b64_tr_b16 %10, %16 offset:5120\n\t"
-            "ds_read_b64_tr_b16 %11, %16 offset:5632\n\t"
-            "ds_read_b64_tr_b16 %12, %16 offset:6144\n\t"
-            "ds_read_b64_tr_b16 %13, %16 offset:6656\n\t"
-            "ds_read_b64_tr_b16 %14, %16 offset:7168\n\t"
-            "ds_read_b64_tr_b16 %15, %16 offset:7680\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
-              "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7]), "=&v"(fb[8]), "=&v"(fb[9]),
-              "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]), "=&v"(fb[13]), "=&v"(fb[14]),
-              "=&v"(fb[15])
-            : "v"(tro + (unsigned)(s * kStage))
-            : "memory");
+        f16x4 fb[kT];
+        if constexpr (COLS == 256) {
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %16\n\t"
+              "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
+              "ds_read_b64_tr_b16 %2, %16 offset:1024\n\t"
+              "ds_read_b64_tr_b16 %3, %16 offset:1536\n\t"
+              "ds_read_b64_tr_b16 %4, %16 offset:2048\n\t"
+              "ds_read_b64_tr_b16 %5, %16 offset:2560\n\t"
+              "ds_read_b64_tr_b16 %6, %16 offset:3072\n\t"
+              "ds_read_b64_tr_b16 %7, %16 offset:3584\n\t"
+              "ds_read_b64_tr_b16 %8, %16 offset:4096\n\t"
+              "ds_read_b64_tr_b16 %9, %16 offset:4608\n\t"
+              "ds_read_b64_tr_b16 %10, %16 offset:5120\n\t"
+              "ds_read_b64_tr_b16 %11, %16 offset:5632\n\t"
+              "ds_read_b64_tr_b16 %12, %16 offset:6144\n\t"
+              "ds_read_b64_tr_b16 %13, %16 offset:6656\n\t"
+              "ds_read_b64_tr_b16 %14, %16 offset:7168\n\t"
+              "ds_read_b64_tr_b16 %15, %16 offset:7680\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7]), "=&v"(fb[8]), "=&v"(fb[9]),
+                "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]), "=&v"(fb[13]), "=&v"(fb[14]),
+                "=&v"(fb[15])
+              : "v"(tro + (unsigned)(s * kStage))
+              : "memory");
+        } else {
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %8\n\t"
+              "ds_read_b64_tr_b16 %1, %8 offset:512\n\t"
+              "ds_read_b64_tr_b16 %2, %8 offset:1024\n\t"
+              "ds_read_b64_tr_b16 %3, %8 offset:1536\n\t"
+              "ds_read_b64_tr_b16 %4, %8 offset:2048\n\t"
+              "ds_read_b64_tr_b16 %5, %8 offset:2560\n\t"
+              "ds_read_b64_tr_b16 %6, %8 offset:3072\n\t"
+              "ds_read_b64_tr_b16 %7, %8 offset:3584\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
+              : "v"(tro + (unsigned)(s * kStage))
+              : "memory");
+        }
 #pragma unroll
-        for (int t = 0; t < 16; ++t)
+        for (int t = 0; t < kT; ++t)
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[t], 0, 0, 0);
       }
       // produce the next item into slot s: read blocks until 16 columns are
@@ -2371,10 +2391,10 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
           const char* base = r16 < cnt ? reinterpret_cast<const char*>(B) + (size_t)r * ldb2 : zrow;
           char* const stage = smem + kStg + s * kStage;
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
+          for (int j = 0; j < kCopies; ++j)
             __builtin_amdgcn_global_load_lds((gbl_void_t)(base + boff[j]),
                                              (lds_void_t)(stage + 1024 * j), 16, 0, 0);
-          nis += 8;
+          nis += kCopies;
           unsigned y0 = y[0], y1 = y[1];
           if (cnt < 16) {  // padded entries: stale values (NaN / inf) must not meet the zero rows
             const int e = 4 * g;
@@ -2397,16 +2417,16 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
   if constexpr (!CROW) {
-    // column-major C: the 16 x 256 tile through LDS, then 4 whole 64-B column
+    // column-major C: the 16 x COLS tile through LDS, then 4 whole 64-B column
     // segments per store instruction
     float* tile = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int t = 0; t < 16; ++t)
+    for (int t = 0; t < kT; ++t)
       *reinterpret_cast<f32x4*>(tile + (16 * t + r16) * 16 + 4 * g) = acc[t];
     __builtin_amdgcn_s_waitcnt(0);
     const size_t row = (size_t)br * 16 + r16;
 #pragma unroll 4
-    for (int it = 0; it < 64; ++it) {
+    for (int it = 0; it < COLS / 4; ++it) {
       const int jl = 4 * it + g;
       if (jt + jl < n) {
         float* p = C + (size_t)(jt + jl) * ldc + row;
@@ -2416,7 +2436,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     return;
   }
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
+  for (int t = 0; t < kT; ++t) {
     const int j = jt + 16 * t + r16;
     if (j >= n) continue;
 #pragma unroll
@@ -2963,7 +2983,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // be dense (the hybrid's BSR part) take the full-panel kernel: with most
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
-    int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8) || var / 100 == 50
+    int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8) || var / 100 == 50 ||
+                     var / 100 == 51
                  ? (dense_blocks ? kBsr32LdsDense
                                  : ((size_t)ldb * 128 < (1u << 31) ? kBsr32LdsDefault
                                                                      : kBsr32LdsDefaultWideLdb))
@@ -3089,7 +3110,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     dim3 grid(mb, (n + 255) / 256);
     // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
     const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45 ||
-                           var / 100 == 50
+                           var / 100 == 50 || var / 100 == 51
                        ? kBsr16LdsDefault
                        : var;
 #define L(D)                                                                                     \
@@ -3246,21 +3267,27 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
 #undef CM512
       // column stream (bsr16_f16_cs_kernel): 50PN = P item stages, (NA, DA) = (8, 4) (N = 1),
       // (16, 8) (N = 2), (8, 2) (N = 0)
-#define CS16(V, P, A, D)                                                                          \
+#define CS16(V, P, A, D, COLS)                                                                    \
   case V: {                                                                                       \
     const int* ord = nullptr;                                                                     \
-    if (const spmm_status_t st = block_row_order(ctx, mb, (n + 255) / 256, rowptr, &ord)) {       \
+    const dim3 gc(mb, (n + COLS - 1) / COLS);                                                     \
+    if (const spmm_status_t st = block_row_order(ctx, mb, gc.y, rowptr, &ord)) {                  \
       timing_end(ctx, slot);                                                                      \
       return st;                                                                                  \
     }                                                                                             \
-    if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A, D>), grid, dim3(64), 0, ctx->stream, \
-                                 mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, ord);   \
-    else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A, D>), grid, dim3(64), 0, ctx->stream,  \
-                            mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, ord);        \
+    if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A, D, COLS>), gc, dim3(64), 0,      \
+                                 ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, \
+                                 ldc, ord);                                                       \
+    else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A, D, COLS>), gc, dim3(64), 0,          \
+                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, \
+                            ord);                                                                 \
     break;                                                                                        \
   }
-      CS16(5021, 2, 8, 4) CS16(5031, 3, 8, 4) CS16(5041, 4, 8, 4) CS16(5022, 2, 16, 8)
-      CS16(5032, 3, 16, 8) CS16(5020, 2, 8, 2)
+      CS16(5021, 2, 8, 4, 256) CS16(5031, 3, 8, 4, 256) CS16(5041, 4, 8, 4, 256)
+      CS16(5022, 2, 16, 8, 256) CS16(5032, 3, 16, 8, 256) CS16(5020, 2, 8, 2, 256)
+      // 51PN: 128 output columns per wave (4-KB item stages)
+      CS16(5121, 2, 8, 4, 128) CS16(5131, 3, 8, 4, 128) CS16(5141, 4, 8, 4, 128)
+      CS16(5151, 5, 8, 4, 128)
 #undef CS16
 #undef CM
       case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4
