@@ -1114,6 +1114,145 @@ __device__ __forceinline__ void wait_vm_older(int y) {
   asm volatile(SPMM_VM_LADDER("%0") : : "s"(y) : "scc", "memory");
 }
 
+// Segments of long block rows for the bs = 32 column stream (row-major C). A
+// wave runs as long as its block row; after a longest-first order the longest
+// rows still set the makespan when one of them is a large share of the mean
+// load per wave slot (RCM-reordered reddit stand-in: 2,257 blocks in its
+// longest row against ~1,100 per slot). Rows longer than L blocks are cut into
+// ceil(nb / L) segments of equal length; each segment's wave writes its raw
+// 32 x 128 tile to a partial buffer, and seg_fixup_kernel sums a row's
+// partials in segment order (deterministic) and applies alpha / beta. One
+// workgroup builds everything:
+//  * pass 1 (rows in contiguous per-thread chunks, a scan): segment, split-row
+//    and partial counts per row in row order, so part bases are fixed by the
+//    matrix, not by scheduling;
+//  * pass 2: split rows -> splits[] {row, part base, segments}; segments ->
+//    segs[] {row, k begin, k end, part or -1} in longest-first order (a
+//    counting sort on min(length, 1023) as in block_row_order_kernel; the order
+//    inside a bucket only schedules);
+//  * entries past the counts are marked empty (row -1): the grids are sized by
+//    host bounds (segments <= mb + nnzb / L, split rows <= nnzb / L).
+__global__ __launch_bounds__(1024) void seg_build_kernel(int mb, const int* __restrict__ rowptr,
+                                                         int L, int split_if, int seg_cap,
+                                                         int split_cap, int part_cap,
+                                                         int4* __restrict__ segs,
+                                                         int4* __restrict__ splits) {
+  __shared__ int cnt[1024];
+  __shared__ int sseg[1024], ssplit[1024], spart[1024];
+  __shared__ int over, maxnb;
+  const int t = threadIdx.x;
+  const int chunk = (mb + 1023) / 1024;
+  const int r0 = min(t * chunk, mb), r1 = min(r0 + chunk, mb);
+  if (t == 0) maxnb = 0;
+  __syncthreads();
+  for (int pass = 0; pass < 2; ++pass) {
+  int nseg = 0, nsplit = 0, npart = 0, mx = 0;
+  for (int i = r0; i < r1; ++i) {
+    const int nb = rowptr[i + 1] - rowptr[i];
+    const int k = nb > L ? (nb + L - 1) / L : 1;
+    nseg += k;
+    nsplit += k > 1;
+    npart += k > 1 ? k : 0;
+    mx = max(mx, nb);
+  }
+  if (pass == 0) atomicMax(&maxnb, mx);
+  sseg[t] = nseg;
+  ssplit[t] = nsplit;
+  spart[t] = npart;
+  cnt[t] = 0;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // inclusive scans
+    const int a = t >= off ? sseg[t - off] : 0, b = t >= off ? ssplit[t - off] : 0,
+              c = t >= off ? spart[t - off] : 0;
+    __syncthreads();
+    sseg[t] += a;
+    ssplit[t] += b;
+    spart[t] += c;
+    __syncthreads();
+  }
+  const int total_seg = sseg[1023], total_split = ssplit[1023];
+  // the host sized the lists from the nnzb argument: if the row pointer holds
+  // more blocks than that, do not split at all (every row one segment, mb <=
+  // seg_cap) rather than write past the lists
+  // and split only when the longest row is an outlier: more than split_if
+  // blocks (twice the mean load per wave slot); splitting ordinary rows costs
+  // more than it balances (reddit stand-in: 2.32 vs 2.02 ms)
+  if (t == 0)
+    over = total_seg > seg_cap || total_split > split_cap || spart[1023] > part_cap ||
+           maxnb <= split_if;
+  __syncthreads();
+  if (over && pass == 0) {
+    L = 0x7fffffff;
+    __syncthreads();
+    continue;
+  }
+  int split_at = ssplit[t] - nsplit, part_at = spart[t] - npart;
+  // histogram of segment lengths (descending buckets)
+  for (int i = r0; i < r1; ++i) {
+    const int nb = rowptr[i + 1] - rowptr[i];
+    const int k = nb > L ? (nb + L - 1) / L : 1;
+    const int len = (nb + k - 1) / k;
+    atomicAdd(&cnt[1023 - min(len, 1023)], k);
+  }
+  __syncthreads();
+  const int own = cnt[t];
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int u = t >= off ? cnt[t - off] : 0;
+    __syncthreads();
+    cnt[t] += u;
+    __syncthreads();
+  }
+  cnt[t] -= own;
+  __syncthreads();
+  for (int i = r0; i < r1; ++i) {
+    const int kb0 = rowptr[i], nb = rowptr[i + 1] - kb0;
+    const int k = nb > L ? (nb + L - 1) / L : 1;
+    const int len = (nb + k - 1) / k;
+    const int b = 1023 - min(len, 1023);
+    if (k > 1) splits[split_at++] = make_int4(i, part_at, k, 0);
+    for (int j = 0; j < k; ++j) {
+      const int pos = atomicAdd(&cnt[b], 1);
+      segs[pos] = make_int4(i, kb0 + min(j * len, nb), kb0 + min((j + 1) * len, nb),
+                            k > 1 ? part_at + j : -1);
+    }
+    if (k > 1) part_at += k;
+  }
+  for (int i = total_seg + t; i < seg_cap; i += 1024) segs[i] = make_int4(-1, 0, 0, -1);
+  for (int i = total_split + t; i < split_cap; i += 1024) splits[i] = make_int4(-1, 0, 0, 0);
+  break;
+  }
+}
+
+// C tile of a split block row = epi(sum of its segments' partial tiles, in
+// segment order). Partial tile layout: [part][column tile][32 rows][128].
+__global__ __launch_bounds__(256) void seg_fixup_kernel(int n, const int4* __restrict__ splits,
+                                                        const float* __restrict__ part, float alpha,
+                                                        float beta, float* __restrict__ C, int ldc) {
+  const int4 sp = splits[blockIdx.x];
+  if (sp.x < 0) return;
+  const int tile = blockIdx.y, ntiles = gridDim.y;
+  const int c4 = threadIdx.x & 31, r8 = threadIdx.x >> 5;  // 4 columns, rows r8 + 8i
+  const int col = tile * 128 + 4 * c4;
+  if (col >= n) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r8 + 8 * i;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < sp.z; ++j)
+      acc += *reinterpret_cast<const f32x4*>(
+          part + (((size_t)(sp.y + j) * ntiles + tile) * 32 + r) * 128 + 4 * c4);
+    f32x4* p = reinterpret_cast<f32x4*>(C + ((size_t)sp.x * 32 + r) * ldc + col);
+    if (beta == 0.f) {
+      acc *= alpha;
+    } else {
+      const f32x4 c = *p;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(beta, c[e], alpha * acc[e]);
+    }
+    *p = acc;
+  }
+}
+
 // Longest-first block-row order for the one-wave-per-block-row kernels (the
 // column streams). Their waves run as long as their block rows; when the grid
 // is only a few waves per slot deep, dispatching in block-row order leaves a
@@ -1423,7 +1562,8 @@ template <bool CROW, int XM, int P, int NA, int DIAG = 0, bool O32 = false, bool
 __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
-    float* __restrict__ C, int ldc, const int* __restrict__ order) {
+    float* __restrict__ C, int ldc, const int* __restrict__ order,
+    const int4* __restrict__ segs = nullptr, float* __restrict__ part = nullptr) {
   static_assert(NA >= 2 && NA <= 4 && P >= 2 && P <= 16, "ring depths");
   constexpr int DA = NA - 1;  // A blocks in flight ahead of the producer's block
   // (column-major C reuses the LDS for a 128 x 36-float tile)
@@ -1431,9 +1571,21 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   float smem[CROW || NA * 1024 >= 128 * 36 ? NA * 1024 : 128 * 36];
   const int lane = threadIdx.x;
   const int j = lane & 31, h = lane >> 5;
-  const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, XM);
+  // a segment of a block row (seg_build_kernel; row-major C only) or a whole row
+  int br, k0, k1, pidx = -1;
+  if (segs) {
+    const int4 sg = segs[blockIdx.x];
+    if (sg.x < 0) return;
+    br = sg.x;
+    k0 = sg.y;
+    k1 = sg.z;
+    pidx = sg.w;
+  } else {
+    br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, XM);
+    k0 = rowptr[br];
+    k1 = rowptr[br + 1];
+  }
   const int jt = blockIdx.y * 128;
-  const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const unsigned lds_a = (unsigned)reinterpret_cast<uintptr_t>(smem);
 
   int a_src[2];
@@ -1656,6 +1808,15 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   if constexpr (CROW) {
     const int col = jt + 4 * j;
     if (col >= n) return;
+    if (pidx >= 0) {  // a segment of a split row: the raw tile to its partial
+      float* pt = part + ((size_t)pidx * gridDim.y + blockIdx.y) * 32 * 128;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+        *reinterpret_cast<f32x4*>(pt + row * 128 + 4 * j) = f32x4{u0[e], u1[e], u0[16 + e], u1[16 + e]};
+      }
+      return;
+    }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const size_t row = (size_t)br * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
@@ -2918,6 +3079,46 @@ int variant_override() {
 // forces longest first, 2 the XCD order (tuning). One launch of
 // block_row_order_kernel into the handle's order buffer, in stream order.
 constexpr int kLptRounds = 8;
+
+// Segments for the bs = 32 column stream with row-major C (seg_build_kernel):
+// on a shallow grid (the block_row_order rule), when the longest row holds
+// more than twice the mean load per wave slot (2 nnzb / slots blocks), rows
+// longer than L = max(64, nnzb / (2 * slots)) blocks are split. Fills the segment and
+// split-row lists (order buffer) and the partial tiles (workspace); *segs stays
+// nullptr on a deep grid or with SPMM_BSR_ORDER=2 / 3 (3: longest first, no
+// splitting).
+spmm_status_t cs2_segments(spmm_context* ctx, int mb, int nnzb, int ntiles, const int* rowptr,
+                           const int4** segs, const int4** splits, float** part, int* nseg,
+                           int* nsplit) {
+  static const int force = [] {
+    const char* e = getenv("SPMM_BSR_ORDER");
+    return e ? atoi(e) : 0;
+  }();
+  *segs = nullptr;
+  *splits = nullptr;
+  *part = nullptr;
+  const long slots = 12L * ctx->num_cus;
+  if (force == 2 || force == 3 || (force != 1 && (long)mb * ntiles > kLptRounds * slots) || nnzb <= 0)
+    return SPMM_STATUS_SUCCESS;
+  const int L = (int)std::max<long>(64, ((long)nnzb + 2 * slots - 1) / (2 * slots));
+  const int split_cap = nnzb / L + 1;
+  const int seg_cap = mb + split_cap;
+  const size_t parts_cap = 2 * (size_t)split_cap;
+  if (spmm_status_t st = spmm::ensure_order_buffer(ctx, 4 * ((size_t)seg_cap + split_cap))) return st;
+  if (spmm_status_t st = spmm::ensure_workspace(ctx, parts_cap * ntiles * 32 * 128 * sizeof(float)))
+    return st;
+  int4* sg = reinterpret_cast<int4*>(ctx->order);
+  int4* sp = sg + seg_cap;
+  const int split_if = (int)std::min<long>(0x7fffffff, 2 * ((long)nnzb + slots - 1) / slots);
+  hipLaunchKernelGGL(seg_build_kernel, dim3(1), dim3(1024), 0, ctx->stream, mb, rowptr, L, split_if,
+                     seg_cap, split_cap, (int)parts_cap, sg, sp);
+  *segs = sg;
+  *splits = sp;
+  *part = reinterpret_cast<float*>(ctx->ws);
+  *nseg = seg_cap;
+  *nsplit = split_cap;
+  return SPMM_STATUS_SUCCESS;
+}
 spmm_status_t block_row_order(spmm_context* ctx, int mb, int ntiles, const int* rowptr,
                               const int** order, long slots_per_cu = 12, const int* crp = nullptr,
                               int m = 0) {
@@ -2927,7 +3128,8 @@ spmm_status_t block_row_order(spmm_context* ctx, int mb, int ntiles, const int* 
   }();
   *order = nullptr;
   const long waves = (long)mb * ntiles, slots = slots_per_cu * ctx->num_cus;
-  if (force == 2 || (force != 1 && waves > kLptRounds * slots)) return SPMM_STATUS_SUCCESS;
+  if (force == 2 || (force != 1 && force != 3 && waves > kLptRounds * slots))
+    return SPMM_STATUS_SUCCESS;
   if (spmm_status_t st = spmm::ensure_order_buffer(ctx, mb)) return st;
   hipLaunchKernelGGL(block_row_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, mb, rowptr,
                      crp, m, ctx->order);
@@ -2968,7 +3170,6 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                spmm_order_t orderB, float beta, float* C, int ldc,
                                spmm_order_t orderC, bool dense_blocks) {
   (void)kb;
-  (void)nnzb;
   if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   const bool rowd = dir == SPMM_DIRECTION_ROW;
   const bool brow = orderB == SPMM_ORDER_ROW;
@@ -3060,16 +3261,28 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
 #define CS2(V, P, A, ...)                                                                        \
   case V: {                                                                                      \
     const int* ord = nullptr;                                                                    \
-    if (const spmm_status_t st = block_row_order(ctx, mb, (n + 127) / 128, rowptr, &ord)) {      \
+    const int4 *sg = nullptr, *spl = nullptr;                                                    \
+    float* pt = nullptr;                                                                         \
+    int nsg = 0, nspl = 0;                                                                       \
+    spmm_status_t st = SPMM_STATUS_SUCCESS;                                                      \
+    if (crow) st = cs2_segments(ctx, mb, nnzb, grid.y, rowptr, &sg, &spl, &pt, &nsg, &nspl);     \
+    if (st == SPMM_STATUS_SUCCESS && !sg) st = block_row_order(ctx, mb, grid.y, rowptr, &ord);   \
+    if (st != SPMM_STATUS_SUCCESS) {                                                             \
       timing_end(ctx, slot);                                                                     \
       return st;                                                                                 \
     }                                                                                            \
-    if (crow) hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, P, A, ##__VA_ARGS__>), grid,    \
-                                 dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,   \
-                                 alpha, beta, C, ldc, ord);                                      \
-    else hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, P, A, ##__VA_ARGS__>), grid, dim3(64), 0, \
-                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, \
-                            ord);                                                                \
+    if (crow) {                                                                                  \
+      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, P, A, ##__VA_ARGS__>),                  \
+                         dim3(sg ? nsg : mb, grid.y), dim3(64), 0, ctx->stream, mb, n, rowptr,    \
+                         colind, val, B, ldb, alpha, beta, C, ldc, ord, sg, pt);                 \
+      if (spl)                                                                                   \
+        hipLaunchKernelGGL(seg_fixup_kernel, dim3(nspl, grid.y), dim3(256), 0, ctx->stream, n,   \
+                           spl, pt, alpha, beta, C, ldc);                                        \
+    } else {                                                                                     \
+      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, P, A, ##__VA_ARGS__>), grid, dim3(64), \
+                         0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, \
+                         ord, nullptr, nullptr);                                                 \
+    }                                                                                            \
     break;                                                                                       \
   }
       CS2(4593, 8, 3) CS2(4594, 8, 4) CS2(4592, 8, 2) CS2(4596, 6, 3) CS2(4597, 4, 3)
