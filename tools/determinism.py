@@ -83,6 +83,33 @@ def main():
             return C
         bad += check(f"hybrid fused flags={flags}", run, reps)
         h.close()
+    del d, C, B
+    torch.cuda.empty_cache()
+    # RCM-reordered reddit stand-in, bs 32: the longest-first order with
+    # segments of the outlier rows (partial tiles + fix-up) and the fused
+    # hybrid on the same matrix (longest-first order)
+    n = 232965
+    rp, ci = prep.community_csr(n, 670.0, 512, 2048, 0.99, 1234)
+    rp, ci = prep.permute_csr(rp, ci, np.random.default_rng(9).permutation(n).astype(np.int32))
+    rp, ci = prep.permute_csr(rp, ci, prep.reorder(rp, ci, "rcm"))
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
+    drp, dci, dv = [torch.from_numpy(a).to(dev) for a in (rp, ci, v)]
+    mb = (n + bs - 1) // bs
+    B = torch.rand((mb * bs, K), device=dev) * 2 - 1
+    brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
+    C = torch.empty((mb * bs, K), device=dev)
+
+    def run():
+        ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K)
+        return C
+    bad += check("RCM reddit bsr32 (segments)", run, reps)
+    parts = prep.divide(n, rp, ci, v, bs, prep.hybrid_plan(rp, ci, bs, K)["density"])
+    d = [torch.from_numpy(a).to(dev) for a in parts]
+
+    def run():
+        ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=C, ldc=K)
+        return C
+    bad += check("RCM reddit hybrid (fused, longest first)", run, reps)
     print(f"total differing elements: {bad}", flush=True)
     sys.exit(1 if bad else 0)
 
