@@ -17,4 +17,6 @@ for w in reddit_bsr32 products_bsr32 products_bsr16_f16 reddit_rcm_bsr32 product
   grep '^{' gpurun_out/bw.log >> gpurun_out/workloads.jsonl
   grep '^{' gpurun_out/bw.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); print('$w', r['ms_per_step'], r['roofline'].get('kernel_ms'), r.get('csr_same_matrix_ms'))"
 done
-WLS="reddit_bsr32 products_bsr32 products_bsr16_f16" bash tools/pmc_bytes.sh
+timeout -k 10 900 python tools/determinism.py 3 > gpurun_out/determinism.log 2>&1 || { tail -5 gpurun_out/determinism.log; exit 1; }
+tail -12 gpurun_out/determinism.log
+WLS="${PMC_WLS:-reddit_bsr32 products_bsr32 products_bsr16_f16}" bash tools/pmc_bytes.sh
