@@ -2303,7 +2303,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 //    vector-memory operation of the loop is counted), 16 ds_read_b64_tr_b16
 //    under one lgkmcnt wait, 16 MFMAs into 16 accumulator tiles.
 // ---------------------------------------------------------------------------
-template <bool CROW, int P, int NA, int DA, int COLS = 256>
+template <bool CROW, int P, int NA, int DA, int COLS = 256, int CAP = 64>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
@@ -2313,10 +2313,15 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   static_assert((NA & (NA - 1)) == 0 && DA % 2 == 0 && NA >= DA + 4 && P >= 2 && P <= 6,
                 "ring depths");
   static_assert(COLS == 128 || COLS == 256, "column tile");
+  // pending-list capacity: 64 entries, or 48 (a smaller A-fragment buffer: 8 waves per CU
+  // with NA = 4); a pair of blocks adds at most 32 to at most 15 pending
+  static_assert(CAP == 64 || CAP == 48, "pending capacity");
   constexpr int kT = COLS / 16;           // 16-column MFMA tiles per wave
   constexpr int kCopies = COLS / 32;      // copies per item (16 rows x 4 chunks each)
   constexpr int kStage = 16 * COLS * 2;   // one item: 16 B rows x COLS fp16 columns
-  constexpr int kAbRow = 136;       // A-fragment buffer row: 64 entries + a dummy entry + pad
+  // A-fragment buffer row: CAP entries + a dummy entry (index CAP) + pad; 136 / 104 B rows put
+  // the four row groups' writes in different banks
+  constexpr int kAbRow = CAP == 64 ? 136 : 104;
   constexpr int kAbuf = NA * 512;   // offset of the A-fragment buffer
   constexpr int kStg = kAbuf + 16 * kAbRow;  // offset of the item stages
   constexpr int kLds = kStg + P * kStage;
@@ -2369,7 +2374,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
 
   int kr = 0;  // next block to read, relative to k0 (even)
   const unsigned lowm = (1u << r16) - 1u;
-  int prow = 0;  // pending B row indices (lane e: entry e, circular over 64)
+  int prow = 0;  // pending B row indices (lane e: entry e, circular over CAP)
   int npend = 0, ebase = 0;
   // the next two blocks (one A pair): their masks, their columns pushed to the
   // list. One LDS round trip reads both blocks' values, one more pushes both.
@@ -2428,10 +2433,12 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     for (int u = 0; u < 2; ++u) {
       const bool bit = (m[u] >> r16) & 1u;
       const int st = u ? s1 : s0;
-      d[u] = 4 * ((lane < 16 && bit ? st + __builtin_popcount(m[u] & lowm) : st + 63) & 63);
-      // A values of column r16, rows 4g .. 4g + 3 -> buffer column (entry 64 for empty columns)
-      wa[u] = (int)(abuf + 2u * (unsigned)(bit ? ((st + __builtin_popcount(m[u] & lowm)) & 63) : 64) +
-                    kAbRow * 4u * g);
+      const int e = (st + __builtin_popcount(m[u] & lowm)) % CAP;
+      // inactive lanes: an entry the merge below does not take (CAP = 64: the one before
+      // the range; CAP = 48: lane 63, which holds no entry)
+      d[u] = 4 * (lane < 16 && bit ? e : (CAP == 64 ? (st + 63) & 63 : 63));
+      // A values of column r16, rows 4g .. 4g + 3 -> buffer column (entry CAP for empty columns)
+      wa[u] = (int)(abuf + 2u * (unsigned)(bit ? e : CAP) + kAbRow * 4u * g);
     }
     int nr0, nr1;
     asm volatile(
@@ -2451,8 +2458,8 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
           "v"(x[5]), "v"(x[6]), "v"(x[7]), "n"(kAbRow), "n"(2 * kAbRow), "n"(3 * kAbRow),
           "v"(d[0]), "v"(d[1]), "v"(bc0 * 16 + r16), "v"(bc1 * 16 + r16)
         : "memory");
-    const int rel = (lane - s0) & 63;
-    prow = rel < cnt0 ? nr0 : (rel < cnt0 + cnt1 ? nr1 : prow);
+    const int rel = (lane - s0 + 2 * CAP) % CAP;
+    if (lane < CAP) prow = rel < cnt0 ? nr0 : (rel < cnt0 + cnt1 ? nr1 : prow);
     npend += cnt0 + cnt1;
   };
 
@@ -2546,8 +2553,8 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
                        "ds_read_b64 %1, %4\n\t"
                        "s_waitcnt lgkmcnt(0)"
                        : "=&v"(r), "=&v"(y)
-                       : "v"(4 * ((ebase + r16) & 63)), "v"(prow),
-                         "v"(abuf + kAbRow * (unsigned)r16 + 2u * (unsigned)((ebase + 4 * g) & 63))
+                       : "v"(4 * ((ebase + r16) % CAP)), "v"(prow),
+                         "v"(abuf + kAbRow * (unsigned)r16 + 2u * (unsigned)((ebase + 4 * g) % CAP))
                        : "memory");
           const char* base = r16 < cnt ? reinterpret_cast<const char*>(B) + (size_t)r * ldb2 : zrow;
           char* const stage = smem + kStg + s * kStage;
@@ -2566,7 +2573,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
           fa[s] = *reinterpret_cast<const f16x4*>(u);
           kind[s] = 1;
           stamp[s] = nis;
-          ebase = (ebase + 16) & 63;
+          ebase = (ebase + 16) % CAP;
           npend = npend > 16 ? npend - 16 : 0;
         }
       }
@@ -3185,7 +3192,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
     int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8) || var / 100 == 50 ||
-                     var / 100 == 51
+                     var / 100 == 51 || var / 100 == 53
                  ? (dense_blocks ? kBsr32LdsDense
                                  : ((size_t)ldb * 128 < (1u << 31) ? kBsr32LdsDefault
                                                                      : kBsr32LdsDefaultWideLdb))
@@ -3323,7 +3330,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     dim3 grid(mb, (n + 255) / 256);
     // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
     const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45 ||
-                           var / 100 == 50 || var / 100 == 51
+                           var / 100 == 50 || var / 100 == 51 || var / 100 == 53
                        ? kBsr16LdsDefault
                        : var;
 #define L(D)                                                                                     \
@@ -3480,7 +3487,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
 #undef CM512
       // column stream (bsr16_f16_cs_kernel): 50PN = P item stages, (NA, DA) = (8, 4) (N = 1),
       // (16, 8) (N = 2), (8, 2) (N = 0)
-#define CS16(V, P, A, D, COLS)                                                                    \
+#define CS16(V, P, A, D, COLS, ...)                                                               \
   case V: {                                                                                       \
     const int* ord = nullptr;                                                                     \
     const dim3 gc(mb, (n + COLS - 1) / COLS);                                                     \
@@ -3488,10 +3495,10 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       timing_end(ctx, slot);                                                                      \
       return st;                                                                                  \
     }                                                                                             \
-    if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A, D, COLS>), gc, dim3(64), 0,      \
+    if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A, D, COLS, ##__VA_ARGS__>), gc, dim3(64), 0, \
                                  ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, \
                                  ldc, ord);                                                       \
-    else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A, D, COLS>), gc, dim3(64), 0,          \
+    else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A, D, COLS, ##__VA_ARGS__>), gc, dim3(64), 0, \
                             ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, \
                             ord);                                                                 \
     break;                                                                                        \
@@ -3501,6 +3508,9 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       // 51PN: 128 output columns per wave (4-KB item stages)
       CS16(5121, 2, 8, 4, 128) CS16(5131, 3, 8, 4, 128) CS16(5141, 4, 8, 4, 128)
       CS16(5151, 5, 8, 4, 128)
+      // 53xx: pending capacity 48: 5304 = P 2, NA 4, DA 0 (19.7 KB: 8 waves per CU);
+      // 5308 = P 2, NA 8, DA 4; 5334 = P 3, NA 4, DA 0
+      CS16(5304, 2, 4, 0, 256, 48) CS16(5308, 2, 8, 4, 256, 48) CS16(5334, 3, 4, 0, 256, 48)
 #undef CS16
 #undef CM
       case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4
