@@ -2303,7 +2303,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 //    vector-memory operation of the loop is counted), 16 ds_read_b64_tr_b16
 //    under one lgkmcnt wait, 16 MFMAs into 16 accumulator tiles.
 // ---------------------------------------------------------------------------
-template <bool CROW, int P, int NA, int DA, int COLS = 256, int CAP = 64>
+// DIAG (diagnostic builds, wrong results, timing only): bit 0 no MFMA, bit 1 every B row
+// from the L2-resident zero row, bit 2 every A copy from the row's first block, bit 3 no
+// item copies at all (the stage is read stale).
+template <bool CROW, int P, int NA, int DA, int COLS = 256, int CAP = 64, int DIAG = 0>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
@@ -2355,7 +2358,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     cstamp = ++nis;
   };
   auto issue_a = [&](int kr) {  // blocks k0 + kr, k0 + kr + 1 (kr even) -> slots kr, kr + 1
-    const int blk = min(k0 + kr + h, k1 - 1);
+    const int blk = (DIAG & 4) ? k0 : min(k0 + kr + h, k1 - 1);
     __builtin_amdgcn_global_load_lds((gbl_void_t)(val + (size_t)blk * 256 + 8 * (lane & 31)),
                                      (lds_void_t)(smem + (kr & (NA - 1)) * 512), 16, 0, 0);
     ++nis;
@@ -2527,7 +2530,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
         }
 #pragma unroll
         for (int t = 0; t < kT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[t], 0, 0, 0);
+          if (!(DIAG & 1)) acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[t], 0, 0, 0);
       }
       // produce the next item into slot s: read blocks until 16 columns are
       // pending or the blocks run out
@@ -2556,13 +2559,15 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
                        : "v"(4 * ((ebase + r16) % CAP)), "v"(prow),
                          "v"(abuf + kAbRow * (unsigned)r16 + 2u * (unsigned)((ebase + 4 * g) % CAP))
                        : "memory");
-          const char* base = r16 < cnt ? reinterpret_cast<const char*>(B) + (size_t)r * ldb2 : zrow;
+          const char* base = r16 < cnt && !(DIAG & 2) ? reinterpret_cast<const char*>(B) + (size_t)r * ldb2 : zrow;
           char* const stage = smem + kStg + s * kStage;
+          if constexpr (!(DIAG & 8)) {
 #pragma unroll
-          for (int j = 0; j < kCopies; ++j)
-            __builtin_amdgcn_global_load_lds((gbl_void_t)(base + boff[j]),
-                                             (lds_void_t)(stage + 1024 * j), 16, 0, 0);
-          nis += kCopies;
+            for (int j = 0; j < kCopies; ++j)
+              __builtin_amdgcn_global_load_lds((gbl_void_t)(base + boff[j]),
+                                               (lds_void_t)(stage + 1024 * j), 16, 0, 0);
+            nis += kCopies;
+          }
           unsigned y0 = y[0], y1 = y[1];
           if (cnt < 16) {  // padded entries: stale values (NaN / inf) must not meet the zero rows
             const int e = 4 * g;
@@ -3192,7 +3197,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
     int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8) || var / 100 == 50 ||
-                     var / 100 == 51 || var / 100 == 53
+                     var / 100 == 51 || var / 100 == 53 || var / 100 == 97
                  ? (dense_blocks ? kBsr32LdsDense
                                  : ((size_t)ldb * 128 < (1u << 31) ? kBsr32LdsDefault
                                                                      : kBsr32LdsDefaultWideLdb))
@@ -3330,7 +3335,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     dim3 grid(mb, (n + 255) / 256);
     // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
     const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45 ||
-                           var / 100 == 50 || var / 100 == 51 || var / 100 == 53
+                           var / 100 == 50 || var / 100 == 51 || var / 100 == 53 ||
+                           var / 100 == 97
                        ? kBsr16LdsDefault
                        : var;
 #define L(D)                                                                                     \
@@ -3511,6 +3517,9 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       // 53xx: pending capacity 48: 5304 = P 2, NA 4, DA 0 (19.7 KB: 8 waves per CU);
       // 5308 = P 2, NA 8, DA 4; 5334 = P 3, NA 4, DA 0
       CS16(5304, 2, 4, 0, 256, 48) CS16(5308, 2, 8, 4, 256, 48) CS16(5334, 3, 4, 0, 256, 48)
+      // diagnostics (wrong results): 970D = 5021 with DIAG D
+      CS16(9701, 2, 8, 4, 256, 64, 1) CS16(9702, 2, 8, 4, 256, 64, 2) CS16(9704, 2, 8, 4, 256, 64, 4)
+      CS16(9708, 2, 8, 4, 256, 64, 8) CS16(9706, 2, 8, 4, 256, 64, 6) CS16(9715, 2, 8, 4, 256, 64, 15)
 #undef CS16
 #undef CM
       case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4
