@@ -1546,6 +1546,7 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs_kernel(
 //    loop has no scalar loads (an SMEM load in flight would make each
 //    lgkmcnt(0) of the LDS reads wait for it too).
 // ---------------------------------------------------------------------------
+constexpr int kIsRec = 576;  // item record: 16 B-row indices + the 16 x 16 fp16 A fragment
 // DIAG (diagnostic builds, wrong results, timing only): bit 0 no MFMA, bit 1
 // every B row from the L2-resident zero row, bit 2 every A copy from block k0.
 // O32: the B-row loads take the block's panel base in SGPRs and the row
@@ -2306,11 +2307,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // DIAG (diagnostic builds, wrong results, timing only): bit 0 no MFMA, bit 1 every B row
 // from the L2-resident zero row, bit 2 every A copy from the row's first block, bit 3 no
 // item copies at all (the stage is read stale).
-template <bool CROW, int P, int NA, int DA, int COLS = 256, int CAP = 64, int DIAG = 0>
+// BUILD (the item-stream builder, bsr16_f16_is_kernel's first launch): the same walk over
+// the block row, once for all columns; each emitted item is stored as a 576-B record
+// (kIsRec) instead of being copied and multiplied, and nitems[br] gets the item count.
+// FLC (full-line copies): the item's B rows are copied one 256-B half row per LDS-DMA
+// (global_load_lds_dword, 32 per item) into rows of 528 B, so every copy reads two whole
+// 128-B lines (the 16-B form reads 16 half lines per copy, the other halves one copy
+// later) and the transposed reads (16 rows at a 528-B pitch) stay conflict-free.
+template <bool CROW, int P, int NA, int DA, int COLS = 256, int CAP = 64, int DIAG = 0,
+          bool BUILD = false, bool FLC = false>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
-    float beta, float* __restrict__ C, int ldc, const int* __restrict__ order) {
+    float beta, float* __restrict__ C, int ldc, const int* __restrict__ order,
+    char* __restrict__ items, int* __restrict__ nitems) {
   // the pair copied at block kr (blocks kr + DA + 2, + 3) overwrites blocks
   // kr + DA + 2 - NA, + 3 - NA, which must be read already (< kr)
   static_assert((NA & (NA - 1)) == 0 && DA % 2 == 0 && NA >= DA + 4 && P >= 2 && P <= 6,
@@ -2321,18 +2331,21 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   static_assert(CAP == 64 || CAP == 48, "pending capacity");
   constexpr int kT = COLS / 16;           // 16-column MFMA tiles per wave
   constexpr int kCopies = COLS / 32;      // copies per item (16 rows x 4 chunks each)
-  constexpr int kStage = 16 * COLS * 2;   // one item: 16 B rows x COLS fp16 columns
+  static_assert(!FLC || COLS == 256, "full-line copies: 256 columns");
+  constexpr int kRowP = 528;              // FLC row pitch
+  constexpr int kStage = FLC ? 16 * kRowP : 16 * COLS * 2;  // one item: 16 B rows x COLS fp16
   // A-fragment buffer row: CAP entries + a dummy entry (index CAP) + pad; 136 / 104 B rows put
   // the four row groups' writes in different banks
   constexpr int kAbRow = CAP == 64 ? 136 : 104;
   constexpr int kAbuf = NA * 512;   // offset of the A-fragment buffer
   constexpr int kStg = kAbuf + 16 * kAbRow;  // offset of the item stages
-  constexpr int kLds = kStg + P * kStage;
-  static_assert(kLds >= COLS * 16 * 4, "column-major C tile fits");
+  constexpr int kLds = BUILD ? kStg : kStg + P * kStage;
+  static_assert(BUILD || kLds >= COLS * 16 * 4, "column-major C tile fits");
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int lane = threadIdx.x;
   const int g = lane >> 4, r16 = lane & 15, h = lane >> 5;
   const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
+  int nit = 0;  // BUILD: items stored
   const int jt = blockIdx.y * COLS;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const unsigned lds0 = lds_addr(smem);
@@ -2346,8 +2359,13 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   const char* const zrow = reinterpret_cast<const char*>(g_zero_row) - 2 * (size_t)jt;
   // transposed B reads: lane (g, q = (lane >> 2) & 3, p = lane & 3) reads row 4g + q,
   // columns 16t + 4p .. + 3: chunk 2t + p / 2 at byte 8 (p & 1); t by immediate offset
-  const unsigned tro = lds0 + kStg + 256u * ((lane & 3) >> 1) + 16u * (4 * g + ((lane >> 2) & 3)) +
-                       8u * (lane & 1);
+  const unsigned tro =
+      FLC ? lds0 + kStg + (unsigned)kRowP * (4 * g + ((lane >> 2) & 3)) + 8u * (lane & 3)
+          : lds0 + kStg + 256u * ((lane & 3) >> 1) + 16u * (4 * g + ((lane >> 2) & 3)) +
+                8u * (lane & 1);
+  // FLC: 4 B (2 columns) per lane and copy, the row's two halves
+  const unsigned boffl = 2u * (unsigned)min(jt + 2 * lane, n - 2);
+  const unsigned boffh = 2u * (unsigned)min(jt + 128 + 2 * lane, n - 2);
 
   int nis = 0;  // vector-memory operations issued by this wave
   // block columns: 64 at a time in one VGPR (lane l: colind[k0 + 64c + l]), the next chunk in flight
@@ -2487,7 +2505,32 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       if (kind[s]) {
         wait_vm_older(nis - stamp[s]);
         f16x4 fb[kT];
-        if constexpr (COLS == 256) {
+        if constexpr (FLC) {
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %16\n\t"
+              "ds_read_b64_tr_b16 %1, %16 offset:32\n\t"
+              "ds_read_b64_tr_b16 %2, %16 offset:64\n\t"
+              "ds_read_b64_tr_b16 %3, %16 offset:96\n\t"
+              "ds_read_b64_tr_b16 %4, %16 offset:128\n\t"
+              "ds_read_b64_tr_b16 %5, %16 offset:160\n\t"
+              "ds_read_b64_tr_b16 %6, %16 offset:192\n\t"
+              "ds_read_b64_tr_b16 %7, %16 offset:224\n\t"
+              "ds_read_b64_tr_b16 %8, %16 offset:256\n\t"
+              "ds_read_b64_tr_b16 %9, %16 offset:288\n\t"
+              "ds_read_b64_tr_b16 %10, %16 offset:320\n\t"
+              "ds_read_b64_tr_b16 %11, %16 offset:352\n\t"
+              "ds_read_b64_tr_b16 %12, %16 offset:384\n\t"
+              "ds_read_b64_tr_b16 %13, %16 offset:416\n\t"
+              "ds_read_b64_tr_b16 %14, %16 offset:448\n\t"
+              "ds_read_b64_tr_b16 %15, %16 offset:480\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7]), "=&v"(fb[8]), "=&v"(fb[9]),
+                "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]), "=&v"(fb[13]), "=&v"(fb[14]),
+                "=&v"(fb[15])
+              : "v"(tro + (unsigned)(s * kStage))
+              : "memory");
+        } else if constexpr (COLS == 256) {
           asm volatile(
               "ds_read_b64_tr_b16 %0, %16\n\t"
               "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
@@ -2561,7 +2604,36 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
                        : "memory");
           const char* base = r16 < cnt && !(DIAG & 2) ? reinterpret_cast<const char*>(B) + (size_t)r * ldb2 : zrow;
           char* const stage = smem + kStg + s * kStage;
-          if constexpr (!(DIAG & 8)) {
+          if constexpr (BUILD) {
+            // record: 16 B-row indices (-1: padding), then the A fragment of lane L at 64 + 8 L
+            char* const rec = items + (size_t)(k0 + nit) * kIsRec;
+            // every lane stores (lanes 16-63 repeat lanes 0-15: no divergent branch)
+            *reinterpret_cast<int*>(rec + 4 * r16) = r16 < cnt ? r : -1;
+            unsigned ym0 = y[0], ym1 = y[1];
+            if (cnt < 16) {
+              const int e = 4 * g;
+              ym0 &= (e < cnt ? 0xffffu : 0u) | (e + 1 < cnt ? 0xffff0000u : 0u);
+              ym1 &= (e + 2 < cnt ? 0xffffu : 0u) | (e + 3 < cnt ? 0xffff0000u : 0u);
+            }
+            *reinterpret_cast<u32x2*>(rec + 64 + 8 * lane) = u32x2{ym0, ym1};
+            nis += 2;
+            ++nit;
+            ebase = (ebase + 16) % CAP;
+            npend = npend > 16 ? npend - 16 : 0;
+            continue;
+          }
+          if constexpr (FLC) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int re = __builtin_amdgcn_readlane(r, e);
+              const char* be = e < cnt ? reinterpret_cast<const char*>(B) + (size_t)re * ldb2 : zrow;
+              __builtin_amdgcn_global_load_lds((gbl_void_t)(be + boffl),
+                                               (lds_void_t)(stage + kRowP * e), 4, 0, 0);
+              __builtin_amdgcn_global_load_lds((gbl_void_t)(be + boffh),
+                                               (lds_void_t)(stage + kRowP * e + 256), 4, 0, 0);
+            }
+            nis += 32;
+          } else if constexpr (!(DIAG & 8)) {
 #pragma unroll
             for (int j = 0; j < kCopies; ++j)
               __builtin_amdgcn_global_load_lds((gbl_void_t)(base + boff[j]),
@@ -2588,10 +2660,430 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   // nothing is in flight after the last round (a block-column chunk may be);
   // the full wait makes that visible to the register check (tests/test_isa_waits.py)
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (BUILD) {
+    if (lane == 0) nitems[br] = nit;
+    return;
+  }
 
   if constexpr (!CROW) {
     // column-major C: the 16 x COLS tile through LDS, then 4 whole 64-B column
     // segments per store instruction
+    float* tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int t = 0; t < kT; ++t)
+      *reinterpret_cast<f32x4*>(tile + (16 * t + r16) * 16 + 4 * g) = acc[t];
+    __builtin_amdgcn_s_waitcnt(0);
+    const size_t row = (size_t)br * 16 + r16;
+#pragma unroll 4
+    for (int it = 0; it < COLS / 4; ++it) {
+      const int jl = 4 * it + g;
+      if (jt + jl < n) {
+        float* p = C + (size_t)(jt + jl) * ldc + row;
+        *p = epi(tile[jl * 16 + r16], alpha, beta, p);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < kT; ++t) {
+    const int j = jt + 16 * t + r16;
+    if (j >= n) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = (size_t)br * 16 + 4 * g + e;
+      float* p = C + row * ldc + j;
+      *p = epi(acc[t][e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 16 fp16, item stream (IS16; ROW blocks, row-major B): two launches.
+// The column stream above walks each block row once per 256-column tile, and
+// its chain A copy -> column mask -> push -> B-row copies runs at 7 waves per CU
+// (22 KB of LDS each). Diagnostic builds of it (profiles/r02_cs16_diag.jsonl)
+// put ~2.3 ms of its 4.5 in that walk: with no MFMA, no B rows and no item
+// copies it still takes 2.27 ms. Here the walk runs ONCE per block row, as
+// bsr16_f16_cs_kernel<BUILD> at ~24 waves per CU (6 KB of LDS: no item stage),
+// and stores each item as a 576-B record: 16 B-row indices (-1: a padding
+// entry, read from the zero row) and the MFMA A fragment of lane L at 64 + 8 L.
+// Item records of block row br start at record rowptr[br] (a block row emits at
+// most one item per block: a block adds at most 16 entries), nitems[br] counts them.
+// This kernel then streams the records: one wave per (block row, COLS output
+// columns), no dependence on A, so record r + R is in flight while item r's
+// B rows are copied and item r - P + 1 is multiplied:
+//  * record ring (R slots x 1 KB): one global_load_lds_dwordx4 per record
+//    (lanes 36-63 repeat lane 35's 16 B: no divergent branch), issued R items ahead;
+//  * item stage (P slots x 16 rows x COLS fp16): the copies of
+//    bsr16_f16_cs_kernel (one ds_read_b32 of the record gives lane L the row of
+//    entry L & 15), consumed P - 1 items later by 16 ds_read_b64_tr_b16 and 16
+//    MFMAs, in the same item order and with the same fragments as the column
+//    stream: the result is bit-identical to bsr16_f16_cs_kernel's.
+// Every vector-memory operation of the loop is an LDS-DMA copy, counted in nis;
+// waits are the run-time ladder (wait_vm_older), LDS reads inline asm ending in
+// lgkmcnt(0), as in the column stream.
+// ---------------------------------------------------------------------------
+template <bool CROW, int P, int R, int COLS = 256>
+__global__ __launch_bounds__(64) void bsr16_f16_is_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const char* __restrict__ items,
+    const int* __restrict__ nitems, const _Float16* __restrict__ B, int ldb, float alpha,
+    float beta, float* __restrict__ C, int ldc, const int* __restrict__ order) {
+  static_assert(P >= 2 && P <= 4 && R % P == 0 && R <= 8, "ring depths");
+  static_assert(COLS == 128 || COLS == 256, "column tile");
+  constexpr int kT = COLS / 16;
+  constexpr int kCopies = COLS / 32;
+  constexpr int kStage = 16 * COLS * 2;
+  constexpr int kRecs = P * kStage;  // record ring after the item stages
+  constexpr int kRecSlot = 1024;     // one record copy: 64 lanes x 16 B (lanes 36-63 repeat 35)
+  constexpr int kLds = kRecs + R * kRecSlot;
+  static_assert(kLds >= COLS * 16 * 4, "column-major C tile fits");
+  __shared__ __attribute__((aligned(16))) char smem[kLds];
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
+  const int jt = blockIdx.y * COLS;
+  const int k0 = rowptr[br], ni = nitems[br];
+  const unsigned lds0 = lds_addr(smem);
+  unsigned boff[kCopies];
+#pragma unroll
+  for (int j = 0; j < kCopies; ++j) boff[j] = 2u * (unsigned)min(jt + 8 * (4 * j + g), n - 8);
+  const size_t ldb2 = (size_t)ldb * 2;
+  const char* const zrow = reinterpret_cast<const char*>(g_zero_row) - 2 * (size_t)jt;
+  const unsigned tro = lds0 + 256u * ((lane & 3) >> 1) + 16u * (4 * g + ((lane >> 2) & 3)) +
+                       8u * (lane & 1);
+  const char* const rec0 = items + (size_t)k0 * kIsRec + 16 * min(lane, 35);
+
+  int nis = 0;
+  int rstamp[R], stamp[P];
+  f16x4 fa[P];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    rstamp[q] = -64;
+    if (q < ni) {
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(rec0 + (size_t)q * kIsRec),
+                                       (lds_void_t)(smem + kRecs + q * kRecSlot), 16, 0, 0);
+      rstamp[q] = ++nis;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < P; ++s) {
+    stamp[s] = -64;
+    fa[s] = f16x4{0, 0, 0, 0};
+  }
+  f32x4 acc[kT];
+#pragma unroll
+  for (int t = 0; t < kT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int i0 = 0; i0 < ni + P - 1; i0 += R) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int i = i0 + u;
+      if (i < ni) {
+        const int s = u % P;
+        wait_vm_older(nis - rstamp[u]);  // record i landed
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 y;
+        int r;
+        asm volatile("ds_read_b32 %0, %2\n\t"
+                     "ds_read_b64 %1, %3\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(r), "=&v"(y)
+                     : "v"(lds0 + kRecs + u * kRecSlot + 4u * r16),
+                       "v"(lds0 + kRecs + u * kRecSlot + 64u + 8u * lane)
+                     : "memory");
+        const char* base = r >= 0 ? reinterpret_cast<const char*>(B) + (size_t)r * ldb2 : zrow;
+        char* const stage = smem + s * kStage;
+#pragma unroll
+        for (int j = 0; j < kCopies; ++j)
+          __builtin_amdgcn_global_load_lds((gbl_void_t)(base + boff[j]),
+                                           (lds_void_t)(stage + 1024 * j), 16, 0, 0);
+        nis += kCopies;
+        stamp[s] = nis;
+        const unsigned uy[2] = {y[0], y[1]};
+        fa[s] = *reinterpret_cast<const f16x4*>(uy);
+        // the slot just read takes record i + R
+        if (i + R < ni) {
+          __builtin_amdgcn_global_load_lds((gbl_void_t)(rec0 + (size_t)(i + R) * kIsRec),
+                                           (lds_void_t)(smem + kRecs + u * kRecSlot), 16, 0, 0);
+          rstamp[u] = ++nis;
+        }
+      }
+      const int j = i - P + 1;
+      if (j >= 0 && j < ni) {
+        const int s = (u + 1) % P;  // j % P (i0 is a multiple of R, R of P)
+        wait_vm_older(nis - stamp[s]);
+        f16x4 fb[kT];
+        if constexpr (COLS == 256) {
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %16\n\t"
+              "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
+              "ds_read_b64_tr_b16 %2, %16 offset:1024\n\t"
+              "ds_read_b64_tr_b16 %3, %16 offset:1536\n\t"
+              "ds_read_b64_tr_b16 %4, %16 offset:2048\n\t"
+              "ds_read_b64_tr_b16 %5, %16 offset:2560\n\t"
+              "ds_read_b64_tr_b16 %6, %16 offset:3072\n\t"
+              "ds_read_b64_tr_b16 %7, %16 offset:3584\n\t"
+              "ds_read_b64_tr_b16 %8, %16 offset:4096\n\t"
+              "ds_read_b64_tr_b16 %9, %16 offset:4608\n\t"
+              "ds_read_b64_tr_b16 %10, %16 offset:5120\n\t"
+              "ds_read_b64_tr_b16 %11, %16 offset:5632\n\t"
+              "ds_read_b64_tr_b16 %12, %16 offset:6144\n\t"
+              "ds_read_b64_tr_b16 %13, %16 offset:6656\n\t"
+              "ds_read_b64_tr_b16 %14, %16 offset:7168\n\t"
+              "ds_read_b64_tr_b16 %15, %16 offset:7680\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7]), "=&v"(fb[8]), "=&v"(fb[9]),
+                "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]), "=&v"(fb[13]), "=&v"(fb[14]),
+                "=&v"(fb[15])
+              : "v"(tro + (unsigned)(s * kStage))
+              : "memory");
+        } else {
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %8\n\t"
+              "ds_read_b64_tr_b16 %1, %8 offset:512\n\t"
+              "ds_read_b64_tr_b16 %2, %8 offset:1024\n\t"
+              "ds_read_b64_tr_b16 %3, %8 offset:1536\n\t"
+              "ds_read_b64_tr_b16 %4, %8 offset:2048\n\t"
+              "ds_read_b64_tr_b16 %5, %8 offset:2560\n\t"
+              "ds_read_b64_tr_b16 %6, %8 offset:3072\n\t"
+              "ds_read_b64_tr_b16 %7, %8 offset:3584\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
+              : "v"(tro + (unsigned)(s * kStage))
+              : "memory");
+        }
+#pragma unroll
+        for (int t = 0; t < kT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[t], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  if constexpr (!CROW) {
+    float* tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int t = 0; t < kT; ++t)
+      *reinterpret_cast<f32x4*>(tile + (16 * t + r16) * 16 + 4 * g) = acc[t];
+    __builtin_amdgcn_s_waitcnt(0);
+    const size_t row = (size_t)br * 16 + r16;
+#pragma unroll 4
+    for (int it = 0; it < COLS / 4; ++it) {
+      const int jl = 4 * it + g;
+      if (jt + jl < n) {
+        float* p = C + (size_t)(jt + jl) * ldc + row;
+        *p = epi(tile[jl * 16 + r16], alpha, beta, p);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < kT; ++t) {
+    const int j = jt + 16 * t + r16;
+    if (j >= n) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = (size_t)br * 16 + 4 * g + e;
+      float* p = C + row * ldc + j;
+      *p = epi(acc[t][e], alpha, beta, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 16 fp16, item stream with register-staged B rows (IS16R; the second
+// launch after the same builder). The kernel trace of bsr16_f16_is_kernel shows
+// the walk is not what bounds the column stream: without it the streaming
+// kernel alone takes 4.43 ms against 4.51 for the whole column stream, and the
+// builder 0.76 ms (profiles/r02_is16_kt). What bounds both is the B bytes in
+// flight: the LDS item stages hold them, and 5-8 waves per CU with 1-2 stages
+// in flight each keep ~80 KB per CU outstanding. Here the B rows of the next D
+// items travel in VGPRs (32 per item and lane: lane L holds, for copy j, row
+// L & 15, 16-B chunk 4j + L / 16, the LDS-DMA layout of the column stream) and
+// only the item being multiplied passes through LDS (8 ds_write_b128 into the
+// same chunk-major stage, then the same 16 ds_read_b64_tr_b16): D x 8 KB per
+// wave in flight at one 8-KB stage of LDS. Records and B rows are plain loads
+// (the compiler's own vmcnt waits); the stage's writes and reads are one
+// wave's, in LDS order. Same items, same order, same fragments: bit-identical
+// to bsr16_f16_cs_kernel.
+// ---------------------------------------------------------------------------
+template <bool CROW, int D, int COLS = 256, bool FL = false>
+__global__ __launch_bounds__(64) void bsr16_f16_isr_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const char* __restrict__ items,
+    const int* __restrict__ nitems, const _Float16* __restrict__ B, int ldb, float alpha,
+    float beta, float* __restrict__ C, int ldc, const int* __restrict__ order) {
+  static_assert(D >= 1 && D <= 4, "items in flight");
+  static_assert(COLS == 128 || COLS == 256, "column tile");
+  static_assert(!FL || COLS == 256, "full-line loads: 256 columns");
+  constexpr int DR = 2 * D;  // records in flight (the next D items' rows are needed D early)
+  constexpr int kT = COLS / 16;
+  constexpr int kCopies = COLS / 32;
+  // FL: chunk stride 272 B (16 rows x 16 B + 16): row j of chunk c at bank slot c + j, so the
+  // 8-B writes of one row (chunks 0-31) and the transposed reads (16 rows of one chunk) are
+  // conflict-free, and chunk 2t + 1 stays an immediate offset (544 t) from chunk 2t
+  constexpr int kCs = FL ? 272 : 256;
+  constexpr int kStage = FL ? 32 * kCs : 16 * COLS * 2;
+  constexpr int kLds = CROW ? kStage : (kStage > COLS * 64 ? kStage : COLS * 64);
+  constexpr int kLoads = FL ? 16 : kCopies;  // B loads per item and lane
+  __shared__ __attribute__((aligned(16))) char smem[kLds];
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
+  const int jt = blockIdx.y * COLS;
+  const int k0 = rowptr[br], ni = nitems[br];
+  const unsigned lds0 = lds_addr(smem);
+  unsigned boff[kCopies];
+#pragma unroll
+  for (int j = 0; j < kCopies; ++j) boff[j] = 2u * (unsigned)min(jt + 8 * (4 * j + g), n - 8);
+  const size_t ldb2 = (size_t)ldb * 2;
+  const char* const zrow = reinterpret_cast<const char*>(g_zero_row) - 2 * (size_t)jt;
+  const unsigned tro = lds0 + (unsigned)kCs * ((lane & 3) >> 1) + 16u * (4 * g + ((lane >> 2) & 3)) +
+                       8u * (lane & 1);
+  // FL: lane L loads 8 B (columns 4L .. 4L + 3) of one B row per load, 16 loads per item
+  const unsigned boffl = 2u * (unsigned)min(jt + 4 * lane, n - 4);
+  char* const wfl = smem + kCs * (lane >> 1) + 8 * (lane & 1);
+  const char* const recs = items + (size_t)k0 * kIsRec;
+
+  f32x4 acc[kT];
+#pragma unroll
+  for (int t = 0; t < kT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int rrow[DR];
+  u32x2 ra[DR];
+  typedef typename std::conditional<FL, u32x2, u32x4>::type bvec;
+  bvec bq[D][kLoads];
+  // Every load is issued whatever the item count (records clamped to the last
+  // one, B rows of items past the end from the zero row): with loads under
+  // branches hipcc's waits merge pessimistically and wait for every
+  // outstanding load before each item (vmcnt(0)); straight-line issue keeps
+  // its counts exact, so item i waits only for its own rows.
+  auto load_rec = [&](int q, int i) {
+    const char* rec = recs + (size_t)min(i, ni - 1) * kIsRec;
+    rrow[q] = *reinterpret_cast<const int*>(rec + 4 * r16);
+    ra[q] = *reinterpret_cast<const u32x2*>(rec + 64 + 8 * lane);
+  };
+  auto load_b = [&](int d, int q, bool live) {
+    if constexpr (FL) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int rj = __builtin_amdgcn_readlane(rrow[q], j);
+        const char* base = live && rj >= 0 ? reinterpret_cast<const char*>(B) + (size_t)rj * ldb2 : zrow;
+        bq[d][j] = *reinterpret_cast<const bvec*>(base + boffl);
+      }
+    } else {
+      const char* base = live && rrow[q] >= 0 ? reinterpret_cast<const char*>(B) + (size_t)rrow[q] * ldb2 : zrow;
+#pragma unroll
+      for (int j = 0; j < kCopies; ++j) bq[d][j] = *reinterpret_cast<const bvec*>(base + boff[j]);
+    }
+  };
+  if (ni > 0) {
+#pragma unroll
+    for (int q = 0; q < DR; ++q) load_rec(q, q);
+#pragma unroll
+    for (int d = 0; d < D; ++d) load_b(d, d, d < ni);
+  }
+
+  for (int i0 = 0; i0 < ni; i0 += DR) {
+#pragma unroll
+    for (int u = 0; u < DR; ++u) {
+      const int i = i0 + u;
+      if (i < ni) {
+        const int d = u % D;  // i % D (i0 is a multiple of DR, DR of D)
+        // item i: its rows to the stage, transposed reads, MFMAs
+        if constexpr (FL) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) *reinterpret_cast<bvec*>(wfl + 16 * j) = bq[d][j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < kCopies; ++j)
+            *reinterpret_cast<bvec*>(smem + 1024 * j + 16 * lane) = bq[d][j];
+        }
+        f16x4 fb[kT];
+        if constexpr (FL) {
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %16\n\t"
+              "ds_read_b64_tr_b16 %1, %16 offset:544\n\t"
+              "ds_read_b64_tr_b16 %2, %16 offset:1088\n\t"
+              "ds_read_b64_tr_b16 %3, %16 offset:1632\n\t"
+              "ds_read_b64_tr_b16 %4, %16 offset:2176\n\t"
+              "ds_read_b64_tr_b16 %5, %16 offset:2720\n\t"
+              "ds_read_b64_tr_b16 %6, %16 offset:3264\n\t"
+              "ds_read_b64_tr_b16 %7, %16 offset:3808\n\t"
+              "ds_read_b64_tr_b16 %8, %16 offset:4352\n\t"
+              "ds_read_b64_tr_b16 %9, %16 offset:4896\n\t"
+              "ds_read_b64_tr_b16 %10, %16 offset:5440\n\t"
+              "ds_read_b64_tr_b16 %11, %16 offset:5984\n\t"
+              "ds_read_b64_tr_b16 %12, %16 offset:6528\n\t"
+              "ds_read_b64_tr_b16 %13, %16 offset:7072\n\t"
+              "ds_read_b64_tr_b16 %14, %16 offset:7616\n\t"
+              "ds_read_b64_tr_b16 %15, %16 offset:8160\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7]), "=&v"(fb[8]), "=&v"(fb[9]),
+                "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]), "=&v"(fb[13]), "=&v"(fb[14]),
+                "=&v"(fb[15])
+              : "v"(tro)
+              : "memory");
+        } else if constexpr (COLS == 256) {
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %16\n\t"
+              "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
+              "ds_read_b64_tr_b16 %2, %16 offset:1024\n\t"
+              "ds_read_b64_tr_b16 %3, %16 offset:1536\n\t"
+              "ds_read_b64_tr_b16 %4, %16 offset:2048\n\t"
+              "ds_read_b64_tr_b16 %5, %16 offset:2560\n\t"
+              "ds_read_b64_tr_b16 %6, %16 offset:3072\n\t"
+              "ds_read_b64_tr_b16 %7, %16 offset:3584\n\t"
+              "ds_read_b64_tr_b16 %8, %16 offset:4096\n\t"
+              "ds_read_b64_tr_b16 %9, %16 offset:4608\n\t"
+              "ds_read_b64_tr_b16 %10, %16 offset:5120\n\t"
+              "ds_read_b64_tr_b16 %11, %16 offset:5632\n\t"
+              "ds_read_b64_tr_b16 %12, %16 offset:6144\n\t"
+              "ds_read_b64_tr_b16 %13, %16 offset:6656\n\t"
+              "ds_read_b64_tr_b16 %14, %16 offset:7168\n\t"
+              "ds_read_b64_tr_b16 %15, %16 offset:7680\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7]), "=&v"(fb[8]), "=&v"(fb[9]),
+                "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]), "=&v"(fb[13]), "=&v"(fb[14]),
+                "=&v"(fb[15])
+              : "v"(tro)
+              : "memory");
+        } else {
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %8\n\t"
+              "ds_read_b64_tr_b16 %1, %8 offset:512\n\t"
+              "ds_read_b64_tr_b16 %2, %8 offset:1024\n\t"
+              "ds_read_b64_tr_b16 %3, %8 offset:1536\n\t"
+              "ds_read_b64_tr_b16 %4, %8 offset:2048\n\t"
+              "ds_read_b64_tr_b16 %5, %8 offset:2560\n\t"
+              "ds_read_b64_tr_b16 %6, %8 offset:3072\n\t"
+              "ds_read_b64_tr_b16 %7, %8 offset:3584\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
+              : "v"(tro)
+              : "memory");
+        }
+        const u32x2 a2 = ra[u];
+        const unsigned uy[2] = {a2[0], a2[1]};
+        const f16x4 fa = *reinterpret_cast<const f16x4*>(uy);
+#pragma unroll
+        for (int t = 0; t < kT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[t], 0, 0, 0);
+      }
+      // item i + D's rows into the registers just freed (its record is q = (u + D) % DR),
+      // then record i + DR into record slot u
+      load_b(u % D, (u + D) % DR, i + D < ni);
+      load_rec(u, i + DR);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight at the epilogue
+
+  if constexpr (!CROW) {
     float* tile = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int t = 0; t < kT; ++t)
@@ -3117,7 +3609,7 @@ spmm_status_t cs2_segments(spmm_context* ctx, int mb, int nnzb, int ntiles, cons
   const int seg_cap = mb + split_cap;
   const size_t parts_cap = 2 * (size_t)split_cap;
   if (spmm_status_t st = spmm::ensure_order_buffer(ctx, 4 * ((size_t)seg_cap + split_cap))) return st;
-  if (spmm_status_t st = spmm::ensure_workspace(ctx, parts_cap * ntiles * 32 * 128 * sizeof(float)))
+  if (spmm_status_t st = spmm::ensure_scratch(ctx, parts_cap * ntiles * 32 * 128 * sizeof(float)))
     return st;
   int4* sg = reinterpret_cast<int4*>(ctx->order);
   int4* sp = sg + seg_cap;
@@ -3126,7 +3618,7 @@ spmm_status_t cs2_segments(spmm_context* ctx, int mb, int nnzb, int ntiles, cons
                      seg_cap, split_cap, (int)parts_cap, sg, sp);
   *segs = sg;
   *splits = sp;
-  *part = reinterpret_cast<float*>(ctx->ws);
+  *part = reinterpret_cast<float*>(ctx->scratch);
   *nseg = seg_cap;
   *nsplit = split_cap;
   return SPMM_STATUS_SUCCESS;
@@ -3197,7 +3689,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
     int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8) || var / 100 == 50 ||
-                     var / 100 == 51 || var / 100 == 53 || var / 100 == 97
+                     var / 100 == 51 || var / 100 == 53 || var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 60)
                  ? (dense_blocks ? kBsr32LdsDense
                                  : ((size_t)ldb * 128 < (1u << 31) ? kBsr32LdsDefault
                                                                      : kBsr32LdsDefaultWideLdb))
@@ -3336,7 +3828,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
     const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45 ||
                            var / 100 == 50 || var / 100 == 51 || var / 100 == 53 ||
-                           var / 100 == 97
+                           var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 60)
                        ? kBsr16LdsDefault
                        : var;
 #define L(D)                                                                                     \
@@ -3440,7 +3932,6 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                int ldb, spmm_order_t orderB, float beta, float* C, int ldc,
                                spmm_order_t orderC) {
   (void)kb;
-  (void)nnzb;
   if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   const _Float16* val = reinterpret_cast<const _Float16*>(val16);
   const _Float16* B = reinterpret_cast<const _Float16*>(B16);
@@ -3503,10 +3994,10 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
     }                                                                                             \
     if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A, D, COLS, ##__VA_ARGS__>), gc, dim3(64), 0, \
                                  ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, \
-                                 ldc, ord);                                                       \
+                                 ldc, ord, nullptr, nullptr);                                     \
     else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A, D, COLS, ##__VA_ARGS__>), gc, dim3(64), 0, \
                             ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, \
-                            ord);                                                                 \
+                            ord, nullptr, nullptr);                                               \
     break;                                                                                        \
   }
       CS16(5021, 2, 8, 4, 256) CS16(5031, 3, 8, 4, 256) CS16(5041, 4, 8, 4, 256)
@@ -3520,7 +4011,68 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       // diagnostics (wrong results): 970D = 5021 with DIAG D
       CS16(9701, 2, 8, 4, 256, 64, 1) CS16(9702, 2, 8, 4, 256, 64, 2) CS16(9704, 2, 8, 4, 256, 64, 4)
       CS16(9708, 2, 8, 4, 256, 64, 8) CS16(9706, 2, 8, 4, 256, 64, 6) CS16(9715, 2, 8, 4, 256, 64, 15)
+      // 60PN: 50PN with full-line copies (FLC)
+      CS16(6021, 2, 8, 4, 256, 64, 0, false, true)
 #undef CS16
+      // item stream (bsr16_f16_is_kernel): 55PR = P item stages, R records ahead, 256
+      // columns; 56PR: 128 columns. First launch: the builder (the column stream's walk,
+      // NA = 8, DA = 4) into the workspace.
+#define IS16(V, P, R, COLS)                                                                       \
+  case V: {                                                                                       \
+    const int* ord = nullptr;                                                                     \
+    const dim3 gc(mb, (n + COLS - 1) / COLS);                                                     \
+    const size_t rec_bytes = (size_t)nnzb * kIsRec;                                               \
+    spmm_status_t st = spmm::ensure_scratch(ctx, rec_bytes + 4 * (size_t)mb);                     \
+    if (st == SPMM_STATUS_SUCCESS) st = block_row_order(ctx, mb, gc.y, rowptr, &ord);             \
+    if (st != SPMM_STATUS_SUCCESS) {                                                              \
+      timing_end(ctx, slot);                                                                      \
+      return st;                                                                                  \
+    }                                                                                             \
+    char* const recs = reinterpret_cast<char*>(ctx->scratch);                                     \
+    int* const nit = reinterpret_cast<int*>(recs + rec_bytes);                                    \
+    hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, 2, 8, 4, 256, 64, 0, true>), dim3(mb), dim3(64), \
+                       0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
+                       nullptr, recs, nit);                                                       \
+    if (crow) hipLaunchKernelGGL((bsr16_f16_is_kernel<true, P, R, COLS>), gc, dim3(64), 0,        \
+                                 ctx->stream, mb, n, rowptr, recs, nit, B, ldb, alpha, beta, C,   \
+                                 ldc, ord);                                                       \
+    else hipLaunchKernelGGL((bsr16_f16_is_kernel<false, P, R, COLS>), gc, dim3(64), 0,            \
+                            ctx->stream, mb, n, rowptr, recs, nit, B, ldb, alpha, beta, C, ldc,   \
+                            ord);                                                                 \
+    break;                                                                                        \
+  }
+      IS16(5522, 2, 2, 256) IS16(5533, 3, 3, 256) IS16(5644, 4, 4, 128)
+#undef IS16
+      // 57D0 / 58D0: register-staged item stream (bsr16_f16_isr_kernel), D items in flight,
+      // 256 / 128 columns
+#define IS16R(V, D, COLS, ...)                                                                    \
+  case V: {                                                                                       \
+    const int* ord = nullptr;                                                                     \
+    const dim3 gc(mb, (n + COLS - 1) / COLS);                                                     \
+    const size_t rec_bytes = (size_t)nnzb * kIsRec;                                               \
+    spmm_status_t st = spmm::ensure_scratch(ctx, rec_bytes + 4 * (size_t)mb);                     \
+    if (st == SPMM_STATUS_SUCCESS) st = block_row_order(ctx, mb, gc.y, rowptr, &ord);             \
+    if (st != SPMM_STATUS_SUCCESS) {                                                              \
+      timing_end(ctx, slot);                                                                      \
+      return st;                                                                                  \
+    }                                                                                             \
+    char* const recs = reinterpret_cast<char*>(ctx->scratch);                                     \
+    int* const nit = reinterpret_cast<int*>(recs + rec_bytes);                                    \
+    hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, 2, 8, 4, 256, 64, 0, true>), dim3(mb), dim3(64), \
+                       0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
+                       nullptr, recs, nit);                                                       \
+    if (crow) hipLaunchKernelGGL((bsr16_f16_isr_kernel<true, D, COLS, ##__VA_ARGS__>), gc, dim3(64), 0, \
+                                 ctx->stream, mb, n, rowptr, recs, nit, B, ldb, alpha, beta, C,   \
+                                 ldc, ord);                                                       \
+    else hipLaunchKernelGGL((bsr16_f16_isr_kernel<false, D, COLS, ##__VA_ARGS__>), gc, dim3(64), 0, \
+                            ctx->stream, mb, n, rowptr, recs, nit, B, ldb, alpha, beta, C, ldc,   \
+                            ord);                                                                 \
+    break;                                                                                        \
+  }
+      IS16R(5710, 1, 256) IS16R(5720, 2, 256) IS16R(5840, 4, 128)
+      // 59D0: the same with full-line B loads (one 512-B row per load instruction)
+      IS16R(5910, 1, 256, true) IS16R(5920, 2, 256, true)
+#undef IS16R
 #undef CM
       case 4303: case 4304: {  // block-row pairs sharing B panels, D = 3 / 4
         const dim3 gp((mb + 1) / 2, (n + 255) / 256);

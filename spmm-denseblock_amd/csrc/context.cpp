@@ -5,26 +5,34 @@
 
 namespace spmm {
 
-spmm_status_t ensure_workspace(spmm_context* ctx, size_t bytes) {
-  if (bytes <= ctx->ws_bytes) return SPMM_STATUS_SUCCESS;
+static spmm_status_t grow_buffer(spmm_context* ctx, void*& buf, size_t& cap, size_t bytes) {
+  if (bytes <= cap) return SPMM_STATUS_SUCCESS;
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (bytes <= ctx->ws_bytes) return SPMM_STATUS_SUCCESS;
+  if (bytes <= cap) return SPMM_STATUS_SUCCESS;
   // The old buffer may still be in use by queued work on this stream.
-  if (ctx->ws) {
+  if (buf) {
     hipError_t e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return from_hip(e);
-    (void)hipFree(ctx->ws);
-    ctx->ws = nullptr;
-    ctx->ws_bytes = 0;
+    (void)hipFree(buf);
+    buf = nullptr;
+    cap = 0;
   }
   size_t want = bytes + bytes / 4;  // grow with slack
-  hipError_t e = hipMalloc(&ctx->ws, want);
+  hipError_t e = hipMalloc(&buf, want);
   if (e != hipSuccess) {
-    ctx->ws = nullptr;
+    buf = nullptr;
     return from_hip(e);
   }
-  ctx->ws_bytes = want;
+  cap = want;
   return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t ensure_workspace(spmm_context* ctx, size_t bytes) {
+  return grow_buffer(ctx, ctx->ws, ctx->ws_bytes, bytes);
+}
+
+spmm_status_t ensure_scratch(spmm_context* ctx, size_t bytes) {
+  return grow_buffer(ctx, ctx->scratch, ctx->scratch_bytes, bytes);
 }
 
 spmm_status_t ensure_order_buffer(spmm_context* ctx, size_t n) {
@@ -133,8 +141,9 @@ spmm_status_t spmm_create(spmm_handle_t* handle) {
 
 spmm_status_t spmm_destroy(spmm_handle_t h) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
-  if (h->ws || h->order) (void)hipStreamSynchronize(h->stream);
+  if (h->ws || h->scratch || h->order) (void)hipStreamSynchronize(h->stream);
   if (h->ws) (void)hipFree(h->ws);
+  if (h->scratch) (void)hipFree(h->scratch);
   if (h->order) (void)hipFree(h->order);
   for (auto e : h->ev_start) (void)hipEventDestroy(e);
   for (auto e : h->ev_stop) (void)hipEventDestroy(e);

@@ -33,6 +33,10 @@ struct spmm_context {
   // Device workspace (grown, never shrunk; freed in spmm_destroy).
   void* ws = nullptr;
   size_t ws_bytes = 0;
+  // Kernel scratch (item records, segment partial tiles), apart from ws: ws may
+  // hold a staged (transposed) B that the kernel reading it must not overwrite.
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
   // Block-row order of the column-stream BSR kernels (mb ints, grown like ws).
   int* order = nullptr;
   size_t order_cap = 0;
@@ -50,6 +54,8 @@ namespace spmm {
 // Grow the handle workspace to at least `bytes`. Not graph-capture safe on
 // the first (growing) call; steady-state calls never allocate.
 spmm_status_t ensure_workspace(spmm_context* ctx, size_t bytes);
+// The same for the kernel scratch buffer.
+spmm_status_t ensure_scratch(spmm_context* ctx, size_t bytes);
 // The same for the block-row order buffer (at least n ints).
 spmm_status_t ensure_order_buffer(spmm_context* ctx, size_t n);
 

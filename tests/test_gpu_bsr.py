@@ -139,6 +139,32 @@ def test_bsrmm_f32(oracle, device, bs, direction, orders):
     assert_normwise(got, ref, absd, TOL_F32, f"bsr bs={bs} dir={direction} orders={orders}")
 
 
+def test_segments_with_staged_col_major_b(oracle, device):
+    """Column-major B is staged (transposed) into the handle workspace before
+    the bs 32 column stream runs; on a shallow grid with one long block row
+    that kernel also splits the row into segments whose partial tiles need
+    scratch memory. The partials live in their own buffer (ctx->scratch), so
+    they cannot overwrite the staged B: one block row of 400 blocks (7
+    segments) among 39 short ones, against the oracle."""
+    rng = np.random.default_rng(77)
+    mb, kb, bs, n = 40, 400, 32, 128
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.008)
+    rows = [ci[rp[i]:rp[i + 1]] for i in range(mb)]
+    rows[5] = np.arange(kb, dtype=np.int32)
+    rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    v = rng.uniform(-1, 1, rp[-1] * bs * bs).astype(np.float32)
+    Bd = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    B = np.ascontiguousarray(Bd.T)
+    drp, dci, dv, dB = _dev(rp, ci, v, B.reshape(-1))
+    C = torch.full((mb * bs, n), float("nan"), device=device)
+    _ops().bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=kb * bs, order_b=1, C=C,
+                 ldc=n)
+    torch.cuda.synchronize()
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, Bd, n, 0)
+    assert_normwise(C.cpu().numpy(), ref, absd, TOL_F32, "segments + staged col-major B")
+
+
 @pytest.mark.parametrize("bs", [16, 32])
 @pytest.mark.parametrize("n", [1, 16, 33, 128, 512])
 @pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.5, 2.0)])
