@@ -2315,7 +2315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // 128-B lines (the 16-B form reads 16 half lines per copy, the other halves one copy
 // later) and the transposed reads (16 rows at a 528-B pitch) stay conflict-free.
 template <bool CROW, int P, int NA, int DA, int COLS = 256, int CAP = 64, int DIAG = 0,
-          bool BUILD = false, bool FLC = false>
+          bool BUILD = false, bool FLC = false, bool FLR = false>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
@@ -2332,6 +2332,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   constexpr int kT = COLS / 16;           // 16-column MFMA tiles per wave
   constexpr int kCopies = COLS / 32;      // copies per item (16 rows x 4 chunks each)
   static_assert(!FLC || COLS == 256, "full-line copies: 256 columns");
+  static_assert(!FLR || (COLS == 256 && !FLC), "two-row copies: 256 columns");
   constexpr int kRowP = 528;              // FLC row pitch
   constexpr int kStage = FLC ? 16 * kRowP : 16 * COLS * 2;  // one item: 16 B rows x COLS fp16
   // A-fragment buffer row: CAP entries + a dummy entry (index CAP) + pad; 136 / 104 B rows put
@@ -2363,6 +2364,20 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       FLC ? lds0 + kStg + (unsigned)kRowP * (4 * g + ((lane >> 2) & 3)) + 8u * (lane & 3)
           : lds0 + kStg + 256u * ((lane & 3) >> 1) + 16u * (4 * g + ((lane >> 2) & 3)) +
                 8u * (lane & 1);
+  // FLR: copy j brings item rows 2j (lanes 0-31) and 2j + 1 (lanes 32-63) whole, so each copy
+  // reads 8 whole 128-B lines; lane k of row R loads chunk (k - R) & 31, which puts chunk c of
+  // row R at 16-B slot (c + R) & 31 of its 512-B stage row: the 16 rows of one chunk sit in 16
+  // different bank slots, and the transposed reads take one address per t (tra).
+  unsigned boffr[8], tra[16];
+  if constexpr (FLR) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      boffr[j] = 2u * (unsigned)min(jt + 8 * (((lane & 31) - 2 * j - (lane >> 5)) & 31), n - 8);
+    const int R = 4 * g + ((lane >> 2) & 3);
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      tra[t] = lds0 + kStg + 512u * R + 16u * ((2 * t + ((lane & 3) >> 1) + R) & 31) + 8u * (lane & 1);
+  }
   // FLC: 4 B (2 columns) per lane and copy, the row's two halves
   const unsigned boffl = 2u * (unsigned)min(jt + 2 * lane, n - 2);
   const unsigned boffh = 2u * (unsigned)min(jt + 128 + 2 * lane, n - 2);
@@ -2505,7 +2520,38 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       if (kind[s]) {
         wait_vm_older(nis - stamp[s]);
         f16x4 fb[kT];
-        if constexpr (FLC) {
+        if constexpr (FLR) {
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
+              : "v"(tra[0]), "v"(tra[1]), "v"(tra[2]), "v"(tra[3]), "v"(tra[4]), "v"(tra[5]),
+                "v"(tra[6]), "v"(tra[7]), "n"(s * kStage)
+              : "memory");
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[8]), "=&v"(fb[9]), "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]),
+                "=&v"(fb[13]), "=&v"(fb[14]), "=&v"(fb[15])
+              : "v"(tra[8]), "v"(tra[9]), "v"(tra[10]), "v"(tra[11]), "v"(tra[12]), "v"(tra[13]),
+                "v"(tra[14]), "v"(tra[15]), "n"(s * kStage)
+              : "memory");
+        } else if constexpr (FLC) {
           asm volatile(
               "ds_read_b64_tr_b16 %0, %16\n\t"
               "ds_read_b64_tr_b16 %1, %16 offset:32\n\t"
@@ -2622,7 +2668,21 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
             npend = npend > 16 ? npend - 16 : 0;
             continue;
           }
-          if constexpr (FLC) {
+          if constexpr (FLR) {
+            int rw[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) rw[e] = __builtin_amdgcn_readlane(r, e);
+            const bool hi = lane >= 32;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int e = 2 * j + (hi ? 1 : 0);
+              const int re = hi ? rw[2 * j + 1] : rw[2 * j];
+              const char* be = e < cnt && !(DIAG & 2) ? reinterpret_cast<const char*>(B) + (size_t)re * ldb2 : zrow;
+              __builtin_amdgcn_global_load_lds((gbl_void_t)(be + boffr[j]),
+                                               (lds_void_t)(stage + 1024 * j), 16, 0, 0);
+            }
+            nis += 8;
+          } else if constexpr (FLC) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
               const int re = __builtin_amdgcn_readlane(r, e);
@@ -3560,8 +3620,10 @@ constexpr int kBsr16F16LdsDefault = 4725;
 // per wave): products stand-in K = 512 6.89 ms vs 7.08 for 4725.
 constexpr int kBsr16F16LdsWide = 4825;
 // Column stream (bsr16_f16_cs_kernel, 2 item stages, NA = 8, DA = 4): products
-// stand-in K = 512 4.57 ms vs 5.94 for 4825 (profiles/r02_cs16_v3_sweep.jsonl).
-constexpr int kBsr16F16Cs = 5021;
+// stand-in K = 512 4.57 ms vs 5.94 for 4825 (profiles/r02_cs16_v3_sweep.jsonl);
+// with two whole B rows per 16-B copy (FLR, 6121): 4.09 vs 4.48-4.49 for 5021 on
+// the same box, bit-identical (profiles/r02_is16/sweeps.txt).
+constexpr int kBsr16F16Cs = 6121;
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -3689,7 +3751,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
     int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8) || var / 100 == 50 ||
-                     var / 100 == 51 || var / 100 == 53 || var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 60)
+                     var / 100 == 51 || var / 100 == 53 || var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 61)
                  ? (dense_blocks ? kBsr32LdsDense
                                  : ((size_t)ldb * 128 < (1u << 31) ? kBsr32LdsDefault
                                                                      : kBsr32LdsDefaultWideLdb))
@@ -3828,7 +3890,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
     const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45 ||
                            var / 100 == 50 || var / 100 == 51 || var / 100 == 53 ||
-                           var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 60)
+                           var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 61)
                        ? kBsr16LdsDefault
                        : var;
 #define L(D)                                                                                     \
@@ -4013,6 +4075,8 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       CS16(9708, 2, 8, 4, 256, 64, 8) CS16(9706, 2, 8, 4, 256, 64, 6) CS16(9715, 2, 8, 4, 256, 64, 15)
       // 60PN: 50PN with full-line copies (FLC)
       CS16(6021, 2, 8, 4, 256, 64, 0, false, true)
+      // 61PN: 50PN with two whole rows per 16-B copy (FLR)
+      CS16(6121, 2, 8, 4, 256, 64, 0, false, false, true) CS16(6131, 3, 8, 4, 256, 64, 0, false, false, true)
 #undef CS16
       // item stream (bsr16_f16_is_kernel): 55PR = P item stages, R records ahead, 256
       // columns; 56PR: 128 columns. First launch: the builder (the column stream's walk,
