@@ -1546,7 +1546,6 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs_kernel(
 //    loop has no scalar loads (an SMEM load in flight would make each
 //    lgkmcnt(0) of the LDS reads wait for it too).
 // ---------------------------------------------------------------------------
-constexpr int kIsRec = 576;  // item record: 16 B-row indices + the 16 x 16 fp16 A fragment
 // DIAG (diagnostic builds, wrong results, timing only): bit 0 no MFMA, bit 1
 // every B row from the L2-resident zero row, bit 2 every A copy from block k0.
 // O32: the B-row loads take the block's panel base in SGPRs and the row
@@ -2307,6 +2306,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // DIAG (diagnostic builds, wrong results, timing only): bit 0 no MFMA, bit 1 every B row
 // from the L2-resident zero row, bit 2 every A copy from the row's first block, bit 3 no
 // item copies at all (the stage is read stale).
+constexpr int kIsRec = 576;  // item record: 16 B-row indices + the 16 x 16 fp16 A fragment
 // BUILD (the item-stream builder, bsr16_f16_is_kernel's first launch): the same walk over
 // the block row, once for all columns; each emitted item is stored as a 576-B record
 // (kIsRec) instead of being copied and multiplied, and nitems[br] gets the item count.
@@ -3622,8 +3622,10 @@ constexpr int kBsr16F16LdsWide = 4825;
 // Column stream (bsr16_f16_cs_kernel, 2 item stages, NA = 8, DA = 4): products
 // stand-in K = 512 4.57 ms vs 5.94 for 4825 (profiles/r02_cs16_v3_sweep.jsonl);
 // with two whole B rows per 16-B copy (FLR, 6121): 4.09 vs 4.48-4.49 for 5021 on
-// the same box, bit-identical (profiles/r02_is16/sweeps.txt).
-constexpr int kBsr16F16Cs = 6121;
+// the same box, bit-identical (profiles/r02_is16/sweeps.txt); with the 48-entry
+// pending list and a 4-slot A ring (6104: 19.7 KB, 8 waves per CU instead of 7)
+// 4.04 vs 4.18-4.19 for 6121 on one box.
+constexpr int kBsr16F16Cs = 6104;
 constexpr int kBsr16Default = 8;     // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
@@ -4077,6 +4079,8 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       CS16(6021, 2, 8, 4, 256, 64, 0, false, true)
       // 61PN: 50PN with two whole rows per 16-B copy (FLR)
       CS16(6121, 2, 8, 4, 256, 64, 0, false, false, true) CS16(6131, 3, 8, 4, 256, 64, 0, false, false, true)
+      CS16(6122, 2, 16, 8, 256, 64, 0, false, false, true) CS16(6104, 2, 4, 0, 256, 48, 0, false, false, true)
+      CS16(6120, 2, 8, 2, 256, 64, 0, false, false, true)
 #undef CS16
       // item stream (bsr16_f16_is_kernel): 55PR = P item stages, R records ahead, 256
       // columns; 56PR: 128 columns. First launch: the builder (the column stream's walk,
