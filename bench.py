@@ -34,6 +34,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -79,23 +80,59 @@ WORKLOADS = {
 METRIC = "SpMM GFLOP/s (2*nnz*K/t) + achieved HBM GB/s, ogbn-products K=128"
 
 
-BSR_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_bytes", "bytes.jsonl")
+BSR_TRAFFIC = os.path.join(ROOT, "profiles", "r03_pmc_bytes", "bytes.jsonl")
 
 
-def bsr_traffic(workload: str, kernel: str):
-    """PMC HBM bytes per launch of a BSR workload's kernel (tools/pmc_bytes.sh:
-    FETCH_SIZE x calibration + WRITE_SIZE, MI355X_MICROARCH.md §HBM), the last
-    matching record of profiles/r02_pmc_bytes/bytes.jsonl, or None."""
+def kernel_source_tag() -> str:
+    """First 16 hex digits of the SHA-256 of the BSR kernel source: counter
+    bytes recorded for one build of the kernels are not reused for another."""
+    import hashlib
+    try:
+        with open(os.path.join(ROOT, "spmm-denseblock_amd", "csrc", "bsr_kernels.hip"), "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return "unknown"
+
+
+def bsr_traffic(key: dict):
+    """PMC HBM bytes per launch of a BSR / hybrid workload's kernel
+    (tools/pmc_bytes.sh: FETCH_SIZE x calibration + WRITE_SIZE,
+    MI355X_MICROARCH.md §HBM): the last record of BSR_TRAFFIC whose workload,
+    kernel, K, dtype, nnzb, variant and kernel-source tag all equal `key`'s,
+    else None (a record of another shape or build is never used)."""
     rec = None
     try:
         with open(BSR_TRAFFIC) as f:
             for line in f:
                 r = json.loads(line)
-                if r.get("workload") == workload and r.get("kernel") == kernel:
+                if all(r.get(k) == v for k, v in key.items()):
                     rec = r
     except (OSError, ValueError):
         return None
     return rec and rec.get("counter_bytes_per_launch")
+
+
+def csr_roofline(n_rows: int, ci: np.ndarray, K: int, kms: float) -> dict:
+    """Roofline fields of a CSR line: SURVEY.md §8(d)'s gather model (one
+    B-row read per nonzero) while its rate stays under the HBM peak; when B is
+    cache-resident (the gather rate would pass the peak: re-reads served by
+    L2 / MALL, e.g. the arxiv stand-in's 87-MB B) the compulsory bytes
+    instead — the arrays, each distinct B row once, C once — with the gather
+    model's rate kept beside it."""
+    nnz = int(ci.size)
+    gather = csr_bytes(n_rows, nnz, K)
+    t = kms / 1e3
+    if gather / t / 1e9 <= HBM_PEAK_GBPS:
+        return {"achieved": round(gather / t / 1e9, 1),
+                "frac": round(gather / t / 1e9 / HBM_PEAK_GBPS, 4),
+                "algorithmic_bytes_per_launch": gather,
+                "bytes_model": "SURVEY 8d gather: one B row per nonzero"}
+    b_rows = int(np.unique(ci).size)
+    comp = 4 * (n_rows + 1) + 8 * nnz + 4 * K * b_rows + 4 * K * n_rows
+    return {"achieved": round(comp / t / 1e9, 1), "frac": round(comp / t / 1e9 / HBM_PEAK_GBPS, 4),
+            "algorithmic_bytes_per_launch": comp,
+            "bytes_model": "compulsory (B cache-resident): arrays, each distinct B row once, C once",
+            "gather_model_bytes": gather, "gather_model_GBps": round(gather / t / 1e9, 1)}
 
 
 def csr_bytes(n_rows: int, nnz: int, K: int) -> int:
@@ -162,6 +199,34 @@ def _time_prefix(run, n: int, budget_s: float):
     return rows, times
 
 
+def _spread(ts) -> dict:
+    """min / median / max of per-call times (s) and (max - min) / median."""
+    a = np.asarray(ts, dtype=np.float64)
+    med = float(np.median(a))
+    return {"min_s": round(float(a.min()), 6), "median_s": round(med, 6),
+            "max_s": round(float(a.max()), 6),
+            "spread": round(float((a.max() - a.min()) / med), 4) if med > 0 else None}
+
+
+def _batched_samples(run, min_sample_s: float = 0.1, nsamples: int = 11):
+    """Per-call times of `run` from samples of back-to-back calls, each sample
+    at least min_sample_s long (a short call's median otherwise measures
+    thread wake-up, not the loop), after a warm-up sample."""
+    run()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        run()
+    one = max((time.perf_counter() - t0) / 3, 1e-6)
+    reps = max(1, int(np.ceil(min_sample_s / one)))
+    ts = []
+    for _ in range(nsamples + 1):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run()
+        ts.append((time.perf_counter() - t0) / reps)
+    return reps, ts[1:]
+
+
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -174,8 +239,10 @@ def _cpu_model() -> str:
 
 
 def _host_cpus() -> dict:
-    """Threads this process may run on (affinity / cgroup cpuset) and the
-    machine's physical cores (unique (package, core) pairs in /proc/cpuinfo)."""
+    """Threads this process may run on (affinity / cgroup cpuset), the
+    physical cores among them (unique (package, core) pairs in sysfs), and
+    the machine's physical cores (unique (package, core) pairs in
+    /proc/cpuinfo)."""
     phys, pkg = set(), None
     try:
         with open("/proc/cpuinfo") as f:
@@ -186,17 +253,28 @@ def _host_cpus() -> dict:
                     phys.add((pkg, line.split(":", 1)[1].strip()))
     except OSError:
         pass
-    return {"affinity_cpus": len(os.sched_getaffinity(0)),
-            "machine_physical_cores": len(phys) or None,
-            "machine_logical_cpus": os.cpu_count()}
+    aff = sorted(os.sched_getaffinity(0))
+    mine = set()
+    for c in aff:
+        topo = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            with open(topo + "physical_package_id") as f1, open(topo + "core_id") as f2:
+                mine.add((f1.read().strip(), f2.read().strip()))
+        except OSError:
+            mine.add(("cpu", c))
+    return {"affinity_cpus": len(aff), "physical_cores_in_affinity": len(mine),
+            "machine_physical_cores": len(phys) or None, "machine_logical_cpus": os.cpu_count()}
 
 
-def cpu_baseline_config1(L, reps: int = 21) -> dict:
+def cpu_baseline_config1(L) -> dict:
     """BASELINE configs[0] / BASELINE.md §2 row 1 as stated: spmm.cc csr_spmm
     (oracle_spmm_cc_csr: OpenMP rows, k-outer, double, unit values) on
     randomCSRMatrix(16384, 16384, 2^-10) + randomDenseMatrix(16384, 32) from a
-    fresh mt19937_64(1234) (the reference generator's stream, bit-exact),
-    median of `reps` after one warm-up; coo_spmm (spmm.cc:27-43) beside it."""
+    fresh mt19937_64(1234) (the reference generator's stream, bit-exact).
+    One call takes well under a millisecond, so each of 11 samples times a
+    loop of back-to-back calls of at least 100 ms (after a warm-up sample);
+    min / median / max per call are reported. coo_spmm (spmm.cc:27-43)
+    beside it."""
     from helpers import ptr
     from spmm_hip import prep
     m, K = 16384, 32
@@ -211,31 +289,39 @@ def cpu_baseline_config1(L, reps: int = 21) -> dict:
                                                                 ptr(out))),
                       ("coo_spmm", lambda: L.oracle_spmm_cc_coo(m, K, ix.size, ptr(row), ptr(ix),
                                                                 ptr(B), K, ptr(out)))):
-        run()
-        ts = []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            run()
-            ts.append(time.perf_counter() - t0)
-        med = float(np.median(ts))
-        res[name] = {"seconds": round(med, 6), "GFLOPs": round(2.0 * ci.size * K / med / 1e9, 3)}
+        reps, ts = _batched_samples(run)
+        sp = _spread(ts)
+        res[name] = {"GFLOPs": round(2.0 * ci.size * K / sp["median_s"] / 1e9, 3),
+                     "calls_per_sample": reps, **sp}
     return {"value": res["csr_spmm"]["GFLOPs"], "unit": "GFLOP/s", "kind": "port",
             "cores": int(L.oracle_num_threads()),
             "sample": (f"BASELINE config 1: spmm.cc csr_spmm restated on randomCSRMatrix(16384, "
                        f"16384, 2^-10) ({ci.size} nnz, mt19937_64(1234)), K=32, double, unit "
-                       f"values, median of {reps} after a warm-up"), **res}
+                       f"values; 11 samples of {res['csr_spmm']['calls_per_sample']} back-to-back "
+                       f"calls (>= 100 ms each), median per call"), **res}
 
 
-def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0) -> dict:
-    """spmm.cc csr_spmm restated (oracle_spmm_cc_csr: OpenMP rows, k-outer,
+def cpu_baseline_child(args) -> None:
+    """One thread count of the CPU baseline, in a process of its own (the
+    parent sets OMP_NUM_THREADS / OMP_PROC_BIND / OMP_PLACES before the
+    OpenMP runtime starts). Regenerates the workload's graph (same generator
+    and seed as the GPU leg) and prints one JSON line.
+
+    spmm.cc csr_spmm restated (oracle_spmm_cc_csr: OpenMP rows, k-outer,
     double, unit values) on the SAME graph: a growing row prefix until about
-    budget_s of CPU work, or the whole graph repeated, median of the repeats.
-    Also the fp32-weighted variant at the same shape: the
-    oracle's sequential-FMA csrmm on U(-1,1) values, same prefix rule."""
+    budget_s of CPU work, or the whole graph repeated, median of the
+    repeats. Also the fp32-weighted variant at the same shape:
+    the oracle's sequential-FMA csrmm on U(-1,1) values, same prefix rule;
+    and BASELINE config 1 (cpu_baseline_config1)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from helpers import load_oracle, ptr
+    from spmm_hip import prep
     L = load_oracle()
+    W = WORKLOADS[args.workload]
+    K = args.K or W["K"]
+    rp, ci = prep.powerlaw_csr(W["n"], W["nnz"], W["max_deg"], 2.3, 1234)
     n = rp.size - 1
+    budget_s = args.cpu_budget
     Bd = np.random.default_rng(1).uniform(-1, 1, (n, K))  # double, as spmm.cc
     ip64, ix64 = rp.astype(np.int64), ci.astype(np.int64)
     out = np.empty((n, K))
@@ -243,29 +329,64 @@ def cpu_baseline(rp: np.ndarray, ci: np.ndarray, K: int, budget_s: float = 10.0)
         lambda r: L.oracle_spmm_cc_csr(r, K, ptr(ip64), ptr(ix64), ptr(Bd), K, ptr(out)),
         n, budget_s)
     del out, Bd
-    med = float(np.median(times))
+    sp = _spread(times)
     nnz_s = int(rp[rows])
-    res = {"value": round(2.0 * nnz_s * K / med / 1e9, 3), "unit": "GFLOP/s",
+    res = {"value": round(2.0 * nnz_s * K / sp["median_s"] / 1e9, 3), "unit": "GFLOP/s",
            "cores": int(L.oracle_num_threads()), "kind": "port", "cpu_model": _cpu_model(),
+           "omp_env": {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND",
+                                                      "OMP_PLACES")},
            "sample": (f"spmm.cc csr_spmm restated (double, unit values, k-outer, OpenMP) on "
                       f"{'all' if rows == n else 'the first'} {rows} rows ({nnz_s} nnz) of the "
                       f"same synthetic graph, K={K}; median of {len(times)} runs "
-                      f"({med:.3f} s each, {sum(times):.1f} s total)")}
+                      f"({sp['median_s']:.3f} s each, {sum(times):.1f} s total)"), **sp}
     Bf = np.random.default_rng(1).uniform(-1, 1, (n, K)).astype(np.float32)
     vf = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
     outf = np.empty((n, K), np.float32)
     rows, times = _time_prefix(
         lambda r: L.oracle_csrmm_f32(r, K, ptr(rp), ptr(ci), ptr(vf), 0, ptr(Bf), K, 0, 1.0, 0.0,
                                      ptr(outf), K, 0), n, budget_s)
-    med = float(np.median(times))
+    sp = _spread(times)
     nnz_s = int(rp[rows])
     res["fp32_weighted"] = {
-        "value": round(2.0 * nnz_s * K / med / 1e9, 3), "unit": "GFLOP/s",
+        "value": round(2.0 * nnz_s * K / sp["median_s"] / 1e9, 3), "unit": "GFLOP/s",
         "sample": (f"fp32 values, sequential FMA per element (oracle_csrmm_f32, OpenMP rows) on "
                    f"{'all' if rows == n else 'the first'} {rows} rows ({nnz_s} nnz), K={K}; "
-                   f"median of {len(times)} runs ({med:.3f} s each)")}
-    res.update(_host_cpus())
+                   f"median of {len(times)} runs ({sp['median_s']:.3f} s each)"), **sp}
+    del Bf, vf, outf
     res["config1"] = cpu_baseline_config1(L)
+    print(json.dumps(res), flush=True)
+
+
+def cpu_baseline(args, K: int) -> dict:
+    """BASELINE.md §2's CPU protocol on the GPU box's host: OpenMP threads =
+    the physical cores this process may run on (all 128 of the box when the
+    affinity mask is the whole machine), one per core (OMP_PROC_BIND=close,
+    OMP_PLACES=cores). The box's one-GPU CPU share, 16 threads bound the same
+    way, is the labelled second entry. Each thread count runs in a child
+    process of its own (cpu_baseline_child), so the OpenMP runtime starts
+    with that environment."""
+    hc = _host_cpus()
+    counts = [("all_physical_cores", hc["physical_cores_in_affinity"])]
+    if hc["physical_cores_in_affinity"] != 16:
+        counts.append(("gpu_share_16_threads", 16))
+    legs = {}
+    for label, T in counts:
+        env = dict(os.environ, OMP_NUM_THREADS=str(T), OMP_PROC_BIND="close", OMP_PLACES="cores")
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child",
+                            "--workload", args.workload, "--K", str(K), "--cpu-budget",
+                            str(args.cpu_budget)], env=env, capture_output=True, text=True,
+                           timeout=900)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            legs[label] = {"error": f"rc {r.returncode}: {r.stderr[-400:]}"}
+        else:
+            legs[label] = json.loads(lines[-1])
+    res = dict(legs["all_physical_cores"])
+    res["protocol"] = ("BASELINE.md §2: OMP_NUM_THREADS = physical cores in this process's "
+                       "affinity, OMP_PROC_BIND=close, OMP_PLACES=cores")
+    for label, _ in counts[1:]:
+        res[label] = legs[label]
+    res.update(hc)
     return res
 
 
@@ -381,8 +502,7 @@ def run_csr_weak(args, W, world, rank, dev, dist):
                     "GBps_per_rank": round(recv / float(ag[0]) / 1e9, 1),
                     "note": "timed after the step loop, not part of value"}
         del full
-    kbytes = csr_bytes(n, nnz, K)
-    achieved = kbytes / (kms / 1e3) / 1e9
+    crf = csr_roofline(n, ci, K, kms)
     vec = 4 if K > 128 and K % 4 == 0 else (2 if K > 64 and K % 2 == 0 else 1)
     rec = dict(
         value=2.0 * float(tot[0]) * K * args.steps / elapsed / 1e9,
@@ -395,11 +515,9 @@ def run_csr_weak(args, W, world, rank, dev, dist):
                 "n_per_rank": n, "nnz_per_rank": nnz, "n_total": ncols,
                 "nnz_total": int(tot[0]), "K": K, "parallelism": f"rows{world}",
                 "waves_per_cu": args.waves_per_cu or 16, "csr_options": args.csr_options},
-        roofline={"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                  "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                  "kernel": f"csr_mergepath_kernel<{vec}>", "kernel_ms": round(kms, 4),
-                  "kernel_ms_max_rank": round(kms_max, 4),
-                  "algorithmic_bytes_per_launch": kbytes},
+        roofline={"bound": "hbm", "peak": HBM_PEAK_GBPS, "unit": "GB/s", **crf,
+                  "traffic": None, "kernel": f"csr_mergepath_kernel<{vec}>",
+                  "kernel_ms": round(kms, 4), "kernel_ms_max_rank": round(kms_max, 4)},
         exchange=exchange, gen_seconds=round(t_gen, 2))
     return rec, None
 
@@ -476,8 +594,7 @@ def run_csr(args, W, world, rank, dev, dist):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kms_max = float(t[0]), float(t[1])
-    kbytes = csr_bytes(shard.rows, int(shard.colind.size), K)
-    achieved = kbytes / (kms / 1e3) / 1e9
+    crf = csr_roofline(shard.rows, shard.colind, K, kms)
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -501,14 +618,13 @@ def run_csr(args, W, world, rank, dev, dist):
                 "exchange_chunks": nch, "hip_graph": bool(GRAPH and world == 1),
                 "waves_per_cu": args.waves_per_cu or 16,
                 "csr_options": args.csr_options, "layout_BC": args.csr_layout},
-        roofline={"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                  "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        roofline={"bound": "hbm", "peak": HBM_PEAK_GBPS, "unit": "GB/s", **crf,
                   "traffic": traffic, "kernel": f"csr_mergepath_kernel<{vec}>",
-                  "kernel_ms": round(kms, 4), "kernel_ms_max_rank": round(kms_max, 4),
-                  "algorithmic_bytes_per_launch": kbytes},
+                  "kernel_ms": round(kms, 4), "kernel_ms_max_rank": round(kms_max, 4)},
         gen_seconds=round(t_gen, 2))
-    if world > 1:
-        # compute and collective reported separately.
+    if dist.is_initialized() and nch > 1 or world > 1:
+        # compute and collective reported separately (a world-1
+        # torch.distributed launch with --chunks > 1 rehearses it through RCCL).
         #  kernel_ms (roofline): this rank's kernels per step, max over ranks;
         #  allgather_ms: the step's all-gathers alone (no compute), max over ranks;
         #  collective_ms_exposed: step minus the slowest rank's kernel time, the
@@ -528,6 +644,7 @@ def run_csr(args, W, world, rank, dev, dist):
         recv = (world - 1) * (out.numel() // world) * 4
         rec["allgather_ms"] = round(float(ag[0]), 4)
         rec["allgather_bytes_received_per_rank"] = int(recv)
+        rec["allgather_bytes_per_rank_buffer"] = int(out.numel() * 4)
         rec["allgather_GBps_per_rank"] = round(recv / (float(ag[0]) / 1e3) / 1e9, 1)
         rec["collective_ms_exposed"] = round(rec["ms_per_step"] - kms_max, 4)
         rec["rows_per_rank"] = [int(b) for b in np.diff(shard.bounds)]
@@ -624,6 +741,7 @@ def run_bsr(args, W, world, rank, dev, dist):
     active_cols = int(torch.unique((d_r // bs) * n + d_c).numel())
     active_pairs = int(torch.unique(((d_r // bs) * mb + d_c // bs) * (bs // 2) +
                                     (d_c % bs) % (bs // 2)).numel())
+    b_rows = int(torch.unique(d_c).numel())  # distinct B rows the product touches
     del d_r, d_c
     # output columns per workgroup (bs 32: 128; bs 16: 256)
     tile = 128 if bs == 32 else 256
@@ -644,11 +762,23 @@ def run_bsr(args, W, world, rank, dev, dist):
         mfma_flops = dense_flops
     peak = MFMA_PEAK_TFLOPS[dt]
     kbytes = bsr_bytes(mb, nnzb, bs, K, s)
-    # bytes the column-masked kernel must move: A values and block columns per
-    # column tile, the B rows of nonzero columns, the C write
+    # Compulsory bytes (the roofline): the block values and the BSR index
+    # arrays once per column tile of the kernel, every distinct B row the
+    # product touches once, the C write once.
+    comp_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + s * nnzb * bs * bs) + s * b_rows * K +
+                  4 * mb * bs * K)
+    # Upper byte model (round 2's roofline): the same A and indices, the B
+    # rows of every (block row, nonzero column) pair with no reuse between
+    # block rows, and C.
     cm_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + s * nnzb * bs * bs) + s * active_cols * K +
                 4 * mb * bs * K) if cm else kbytes
     t = kms / 1e3
+    kname = (("bsr32_f32_cs2_kernel" if bs == 32 else "bsr16_f16_cs_kernel" if cs16 else
+              "bsr16_cm_kernel") if cm else f"bsr{bs} register-fragment kernel")
+    tkey = {"workload": args.workload, "kernel": kname, "K": K, "dtype": dt, "nnzb": nnzb,
+            "layout_BC": args.bsr_layout,
+            "variant": os.environ.get("SPMM_BSR_VARIANT", "default"),
+            "kernel_src": kernel_source_tag()}
     rec = dict(
         value=2.0 * nnz * K * args.steps / elapsed / 1e9, ms_per_step=elapsed / args.steps * 1e3,
         dtype=dt,
@@ -661,23 +791,24 @@ def run_bsr(args, W, world, rank, dev, dist):
                 "block_fill": round(nnz / (nnzb * bs * bs), 4),
                 "active_column_fraction": round(active_cols / (nnzb * bs), 4),
                 "active_pair_fraction": round(active_pairs / (nnzb * bs / 2), 4),
-                "parallelism": "single"},
-        roofline={"bound": "hbm", "achieved": round(cm_bytes / t / 1e9, 1),
+                "distinct_B_rows": b_rows, "parallelism": "single"},
+        roofline={"bound": "hbm", "achieved": round(comp_bytes / t / 1e9, 1),
                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                  "frac": round(cm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4),
-                  "traffic": None if args.bsr_layout != "row" else bsr_traffic(
-                      args.workload, "bsr32_f32_cs2_kernel" if bs == 32 else
-                      "bsr16_f16_cs_kernel" if cs16 else "bsr16_cm_kernel"),
-                  "kernel": (("bsr32_f32_cs2_kernel" if bs == 32 else
-                              "bsr16_f16_cs_kernel" if cs16 else
-                              f"bsr16_cm_kernel<{'f32' if dt == 'fp32' else 'f16'}>")
-                             + (" (column-major C epilogue, B staged row-major)"
-                                if args.bsr_layout == "col" else "") if cm else
-                             f"bsr{bs} register-fragment kernel"),
+                  "frac": round(comp_bytes / t / 1e9 / HBM_PEAK_GBPS, 4),
+                  "traffic": bsr_traffic(tkey),
+                  "kernel": kname + (" (column-major C epilogue, B staged row-major)"
+                                     if args.bsr_layout == "col" and cm else ""),
                   "kernel_ms": round(kms, 4),
-                  "bytes_per_launch": cm_bytes, "bytes_model": (
-                      "A values + block columns per column tile, B rows of nonzero A columns, "
-                      "C write" if cm else "SURVEY 8d full-panel model"),
+                  "bytes_per_launch": comp_bytes,
+                  "bytes_model": ("compulsory: A values + BSR indices once per column tile, "
+                                  "each distinct B row once, C write once"),
+                  "bytes_model_upper": cm_bytes,
+                  "bytes_model_upper_desc": (
+                      "A values + indices per column tile, the B rows of every (block row, "
+                      "nonzero column) pair (no reuse between block rows), C write" if cm else
+                      "SURVEY 8d full-panel model"),
+                  "upper_GBps": round(cm_bytes / t / 1e9, 1),
+                  "traffic_key": tkey,
                   "mfma_executed_flops_per_launch": mfma_flops,
                   "mfma_executed_TFLOPs": round(mfma_flops / t / 1e12, 2),
                   "mfma_peak": peak, "mfma_frac": round(mfma_flops / t / 1e12 / peak, 4),
@@ -689,9 +820,10 @@ def run_bsr(args, W, world, rank, dev, dist):
     tr = rec["roofline"]["traffic"]
     if tr:
         # the PMC bytes (profiled launch) over this run's kernel time: the HBM
-        # rate the kernel actually drives, beside the byte-model rate above
+        # rate the kernel actually drives, beside the compulsory-byte rate above
         rec["roofline"]["traffic_GBps"] = round(tr / t / 1e9, 1)
         rec["roofline"]["traffic_frac"] = round(tr / t / 1e9 / HBM_PEAK_GBPS, 4)
+        rec["roofline"]["traffic_over_compulsory"] = round(tr / comp_bytes, 3)
     return rec, None
 
 
@@ -745,24 +877,52 @@ def run_hybrid(args, W, world, rank, dev, dist):
                                              C=C, ldc=K, handle=h2), h2, 5, 2, 1, dist)
     ms = elapsed / args.steps * 1e3
     useful = 2.0 * nnz * K
+    nb, nc = int(bci.size), int(cci.size)
+    b_rows = int(np.unique(ci).size)  # distinct B rows the product touches
+    # Compulsory bytes (the roofline): the BSR part's block values and index
+    # arrays and the CSR remainder's arrays once, every distinct B row once,
+    # the C write once. Upper model: both parts' own models summed (the BSR
+    # part's full B panels, one B row per remainder nonzero).
+    comp_bytes = (4 * (mb + 1) + 4 * nb + 4 * nb * bs * bs + 4 * (n + 1) + 8 * nc +
+                  4 * b_rows * K + 4 * mb * bs * K)
+    upper = csr_bytes(n, nc, K) + bsr_bytes(mb, nb, bs, K, 4)
+    t = (float(kt.sum(axis=1).mean()) if kt is not None else ms) / 1e3
+    kname = ("bsr32_f32_lds_kernel" if fused else "bsr MFMA kernel + csr_mergepath")
+    tkey = {"workload": args.workload, "kernel": kname, "K": K, "dtype": "fp32", "nnzb": nb,
+            "csr_remainder_nnz": nc, "hybrid_options": hopt,
+            "variant": os.environ.get("SPMM_BSR_VARIANT", "default"),
+            "kernel_src": kernel_source_tag()}
     rec = dict(
         value=useful * args.steps / elapsed / 1e9, ms_per_step=ms, dtype="fp32",
         data=data,
         config={"workload": f"{args.workload}: divide(bs={bs}, density={dens}) + hybrid "
                             f"BSR-MFMA/CSR K={K}", "n": n, "nnz": nnz, "K": K, "bs": bs,
-                "nnzb": int(bci.size), "csr_remainder_nnz": int(cci.size),
-                "bsr_fill": round((nnz - cci.size) / max(1, bci.size * bs * bs), 4),
+                "nnzb": nb, "csr_remainder_nnz": nc,
+                "bsr_fill": round((nnz - nc) / max(1, nb * bs * bs), 4),
+                "distinct_B_rows": b_rows,
                 "parallelism": "single", "hybrid_options": hopt, "fused": bool(fused)},
-        roofline={"bound": "hbm", "achieved": round(
-            (csr_bytes(n, int(cci.size), K) + bsr_bytes(mb, int(bci.size), bs, K, 4)) /
-            (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": None, "traffic": None,
-            "kernel": ("bsr32_f32_lds_kernel<HYB> (fused)" if fused else
-                       "bsr MFMA kernel + csr_mergepath")},
+        roofline={"bound": "hbm", "achieved": round(comp_bytes / t / 1e9, 1),
+                  "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                  "frac": round(comp_bytes / t / 1e9 / HBM_PEAK_GBPS, 4),
+                  "traffic": bsr_traffic(tkey),
+                  "kernel": ("bsr32_f32_lds_kernel<HYB> (fused)" if fused else
+                             "bsr MFMA kernel + csr_mergepath"),
+                  "kernel_ms": round(t * 1e3, 4),
+                  "bytes_per_launch": comp_bytes,
+                  "bytes_model": ("compulsory: BSR part values + indices, CSR remainder "
+                                  "arrays, each distinct B row once, C write once"),
+                  "bytes_model_upper": upper,
+                  "bytes_model_upper_desc": ("SURVEY 8d: BSR part full panels + one B row "
+                                             "per remainder nonzero"),
+                  "upper_GBps": round(upper / t / 1e9, 1), "traffic_key": tkey},
         csr_same_matrix_ms=round(csr_ms, 4), divide_host_seconds=round(t_div, 2),
         plan=plan, reorder=reorder,
         part_kernel_ms=None if kt is None else [round(float(x), 4) for x in kt.mean(axis=0)])
-    rec["roofline"]["frac"] = round(rec["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
+    tr = rec["roofline"]["traffic"]
+    if tr:
+        rec["roofline"]["traffic_GBps"] = round(tr / t / 1e9, 1)
+        rec["roofline"]["traffic_frac"] = round(tr / t / 1e9 / HBM_PEAK_GBPS, 4)
+        rec["roofline"]["traffic_over_compulsory"] = round(tr / comp_bytes, 3)
     if kt is not None and parts == 2 and bs == 32:
         # The BSR part runs every MFMA step of its dense blocks and is bound by
         # the MFMA pipe (DESIGN.md §4a PMC), not by HBM.
@@ -810,6 +970,9 @@ def main() -> None:
                     help="SPMM_HYBRID_* flags (0 = library default, 1 = force fused, 2 = force two launches, "
                          "+4 = split-bf16 products in the dense-block part)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=6.0,
+                    help="seconds of CPU work per cpu_baseline leg (row prefix rule)")
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (DESIGN.md §7)")
     ap.add_argument("--graph", action="store_true",
@@ -817,6 +980,10 @@ def main() -> None:
     args = ap.parse_args()
     global GRAPH
     GRAPH = args.graph
+    if args.cpu_baseline_child:
+        args.workload = args.workload or "products_csr"
+        cpu_baseline_child(args)
+        return
 
     import torch
     import torch.distributed as dist
@@ -845,7 +1012,7 @@ def main() -> None:
     if rank == 0:
         cpu = None
         if (csr_inputs is not None and world == 1 and not args.no_cpu_baseline):
-            cpu = cpu_baseline(*csr_inputs)
+            cpu = cpu_baseline(args, csr_inputs[2])
         out = {"metric": METRIC if args.workload == "products_csr" else
                f"SpMM GFLOP/s (2*nnz*K/t), {args.workload}",
                "value": round(rec.pop("value"), 2), "unit": "GFLOP/s", "n_gpus": world,
@@ -857,9 +1024,8 @@ def main() -> None:
                "vs_baseline": None}
         out.update(rec)
         rf = out.get("roofline") or {}
-        if rf.get("unit") == "GB/s" and (rf.get("frac") or 0) > 1.0:
-            rf["note"] = ("algorithmic bytes above the HBM peak: re-reads served from L2 / MALL "
-                          "(SURVEY.md §8d)")
+        if (rf.get("frac") or 0) > 1.0:  # never reached: every model above is bounded
+            rf["note"] = "fraction above 1: the byte model is not the work"
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

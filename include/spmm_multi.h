@@ -42,11 +42,20 @@ extern "C" {
 typedef struct spmm_multi* spmm_multi_t;
 
 /* devices: ngpu device ordinals (NULL = 0 .. ngpu-1). Restores the caller's
- * current device before returning. RCCL failures map to
+ * current device before returning. RCCL is loaded here, at run time
+ * (librccl.so.1): without it this returns SPMM_STATUS_NOT_INITIALIZED and
+ * the rest of the library is unaffected. RCCL failures map to
  * SPMM_STATUS_EXECUTION_FAILED. */
 spmm_status_t spmm_multi_create(spmm_multi_t* ctx, int ngpu, const int* devices);
 spmm_status_t spmm_multi_destroy(spmm_multi_t ctx);
 int spmm_multi_size(spmm_multi_t ctx);
+/* Stream ordering with the caller: streams[p] (a hipStream_t on device p,
+ * or NULL = none) for every part, kept until changed; NULL clears all.
+ * When set, spmm_csr_f32_multi first makes part p's compute stream wait for
+ * the work already queued on streams[p] (the producers of B, the CSR arrays
+ * and C), and at the end makes streams[p] wait for part p's last
+ * all-gather, so work queued on streams[p] afterwards sees all of C. */
+spmm_status_t spmm_multi_set_user_streams(spmm_multi_t ctx, void* const* streams);
 /* The compute stream of part p (a hipStream_t; the call's results on device
  * p are complete once this stream is). */
 spmm_status_t spmm_multi_get_stream(spmm_multi_t ctx, int part, void** stream);

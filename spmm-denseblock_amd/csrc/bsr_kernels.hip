@@ -1558,7 +1558,8 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs_kernel(
 // The first column's A read is complete before the next block's A copy can
 // reuse its slot: advancing reads the new block's mask with lgkmcnt(0) before
 // it issues that copy (NA = 3: the copy of block k + 3 lands in block k's slot).
-template <bool CROW, int XM, int P, int NA, int DIAG = 0, bool O32 = false, bool PK = false>
+template <bool CROW, int XM, int P, int NA, int DIAG = 0, bool O32 = false, bool PK = false,
+          bool ANT = false>
 __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -1600,7 +1601,7 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       __builtin_amdgcn_global_load_lds((gbl_void_t)(src + a_src[q & 1] + 512 * (q >> 1)),
-                                       (lds_void_t)(dst + 256 * q), 16, 0, 0);
+                                       (lds_void_t)(dst + 256 * q), 16, 0, ANT ? 2 : 0);
   };
   unsigned moff[8];
 #pragma unroll
@@ -2315,7 +2316,7 @@ constexpr int kIsRec = 576;  // item record: 16 B-row indices + the 16 x 16 fp16
 // 128-B lines (the 16-B form reads 16 half lines per copy, the other halves one copy
 // later) and the transposed reads (16 rows at a 528-B pitch) stay conflict-free.
 template <bool CROW, int P, int NA, int DA, int COLS = 256, int CAP = 64, int DIAG = 0,
-          bool BUILD = false, bool FLC = false, bool FLR = false>
+          bool BUILD = false, bool FLC = false, bool FLR = false, bool TT = false>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
@@ -2345,9 +2346,27 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int lane = threadIdx.x;
   const int g = lane >> 4, r16 = lane & 15, h = lane >> 5;
-  const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
+  // TT: the column tiles of one block row are neighbouring waves of one XCD
+  // (a one-dimensional grid of mb x tiles waves, tiles fastest inside each
+  // XCD chunk), so the second tile's A blocks and block columns come from the
+  // XCD's L2 while the first tile's wave is still streaming them.
+  int br, tile;
+  if constexpr (TT) {
+    const int nt = (n + COLS - 1) / COLS;
+    if (order) {
+      br = order[blockIdx.x / nt];
+      tile = blockIdx.x % nt;
+    } else {
+      const int w = xcd_block_row(blockIdx.x, mb * nt, 32 * nt);
+      br = w / nt;
+      tile = w % nt;
+    }
+  } else {
+    br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
+    tile = blockIdx.y;
+  }
   int nit = 0;  // BUILD: items stored
-  const int jt = blockIdx.y * COLS;
+  const int jt = tile * COLS;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const unsigned lds0 = lds_addr(smem);
   const unsigned abuf = lds0 + kAbuf;
@@ -3753,12 +3772,13 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // columns set the mask buys nothing and its deeper B ring wins (reddit
     // stand-in hybrid: 0.81 vs 0.96 ms).
     int lv = var < 0 || ((var % 1000) / 100 >= 6 && (var % 1000) / 100 <= 8) || var / 100 == 50 ||
-                     var / 100 == 51 || var / 100 == 53 || var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 61)
+                     var / 100 == 51 || var / 100 == 53 || var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 61) ||
+                     var / 100 == 63
                  ? (dense_blocks ? kBsr32LdsDense
                                  : ((size_t)ldb * 128 < (1u << 31) ? kBsr32LdsDefault
                                                                      : kBsr32LdsDefaultWideLdb))
                  : var;
-    if ((lv == 4556 || lv == 4558 || lv == 4554 || lv == 4516 || lv == 4518) &&
+    if ((lv == 4556 || lv == 4558 || lv == 4554 || lv == 4516 || lv == 4518 || lv == 4416) &&
         (size_t)ldb * 128 >= (1u << 31))
       lv = kBsr32LdsDefaultWideLdb;  // O32 needs 32-row panels addressable in 31 bits
 #define L(D, X)                                                                                   \
@@ -3859,6 +3879,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       CS2(4556, 6, 3, 0, true) CS2(4558, 8, 3, 0, true) CS2(4554, 4, 3, 0, true)
       // 457P... taken by CS; 4516 / 4518: O32 + cross-block pairs (PK), P = 6 / 8
       CS2(4516, 6, 3, 0, true, true) CS2(4518, 8, 3, 0, true, true)
+      // 4416: 4516 with the A copies non-temporal (nt: A is read once, keep L2 for B rows)
+      CS2(4416, 6, 3, 0, true, true, true)
       // diagnostics (wrong results): 960D = (6, 3) with DIAG D
       CS2(9601, 6, 3, 1) CS2(9602, 6, 3, 2) CS2(9604, 6, 3, 4) CS2(9606, 6, 3, 6)
       CS2(9607, 6, 3, 7)
@@ -3892,7 +3914,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // 42xx / 52xx select bs = 32 kernels: the bs = 16 default here
     const int lv = var < 0 || (var % 1000) / 100 == 2 || var / 100 == 44 || var / 100 == 45 ||
                            var / 100 == 50 || var / 100 == 51 || var / 100 == 53 ||
-                           var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 61)
+                           var / 100 == 97 || (var / 100 >= 55 && var / 100 <= 61) || var / 100 == 63
                        ? kBsr16LdsDefault
                        : var;
 #define L(D)                                                                                     \
@@ -4082,6 +4104,26 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       CS16(6122, 2, 16, 8, 256, 64, 0, false, false, true) CS16(6104, 2, 4, 0, 256, 48, 0, false, false, true)
       CS16(6120, 2, 8, 2, 256, 64, 0, false, false, true)
 #undef CS16
+      // 63xx: 61xx with the column tiles of a block row side by side on one XCD (TT)
+#define CS16T(V, P, A, D, COLS, ...)                                                              \
+  case V: {                                                                                       \
+    const int* ord = nullptr;                                                                     \
+    const int nt = (n + COLS - 1) / COLS;                                                         \
+    if (const spmm_status_t st = block_row_order(ctx, mb, nt, rowptr, &ord)) {                    \
+      timing_end(ctx, slot);                                                                      \
+      return st;                                                                                  \
+    }                                                                                             \
+    if (crow) hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, P, A, D, COLS, ##__VA_ARGS__, true>), \
+                                 dim3(mb * nt), dim3(64), 0, ctx->stream, mb, n, rowptr, colind,  \
+                                 val, B, ldb, alpha, beta, C, ldc, ord, nullptr, nullptr);        \
+    else hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, P, A, D, COLS, ##__VA_ARGS__, true>),     \
+                            dim3(mb * nt), dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val,  \
+                            B, ldb, alpha, beta, C, ldc, ord, nullptr, nullptr);                  \
+    break;                                                                                        \
+  }
+      CS16T(6304, 2, 4, 0, 256, 48, 0, false, false, true)
+      CS16T(6321, 2, 8, 4, 256, 64, 0, false, false, true)
+#undef CS16T
       // item stream (bsr16_f16_is_kernel): 55PR = P item stages, R records ahead, 256
       // columns; 56PR: 128 columns. First launch: the builder (the column stream's walk,
       // NA = 8, DA = 4) into the workspace.

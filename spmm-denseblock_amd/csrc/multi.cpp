@@ -9,9 +9,17 @@
 // queued on the compute stream right away and overlaps chunk c's exchange.
 // At the end each compute stream waits for its collective stream, so a
 // caller that synchronises the compute stream sees all of C.
+//
+// RCCL is resolved at run time (dlopen of librccl.so.1 on the first
+// spmm_multi_create): the single-GPU entry points of libspmm_hip.so never
+// need it, so the library loads on a system without RCCL, and only
+// spmm_multi_create reports SPMM_STATUS_NOT_INITIALIZED there. The header is
+// included for the types only.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -27,6 +35,8 @@ struct spmm_multi {
   std::vector<std::vector<hipEvent_t>> chunk_done;  // [p][c]: chunk c's kernel finished
   std::vector<hipEvent_t> t0, t_comp, t_end;         // timing, per part
   std::vector<hipEvent_t> coll_done;                 // [p]: last all-gather finished
+  std::vector<hipEvent_t> user_in;                   // [p]: caller's stream reached the call
+  std::vector<hipStream_t> user;                     // [p]: caller streams (spmm_multi_set_user_streams)
   bool timing = false;
 };
 
@@ -42,6 +52,34 @@ spmm_status_t from_nccl(ncclResult_t r) {
   return r == ncclSuccess ? SPMM_STATUS_SUCCESS : SPMM_STATUS_EXECUTION_FAILED;
 }
 
+// The RCCL entry points this file uses, resolved once from librccl.
+struct Rccl {
+  decltype(&ncclCommInitAll) comm_init_all = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  bool ok = false;
+};
+
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+    if (!h) return;
+    r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
+    r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
+    r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
+    r.ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.all_gather;
+  });
+  return r;
+}
+
 #define SPMM_TRY_HIP(x)                                 \
   do {                                                  \
     hipError_t e_ = (x);                                \
@@ -53,11 +91,11 @@ void release(spmm_multi* c) {
     if (p < (int)c->dev.size()) (void)hipSetDevice(c->dev[p]);
     if (p < (int)c->compute.size() && c->compute[p]) (void)hipStreamSynchronize(c->compute[p]);
     if (p < (int)c->coll.size() && c->coll[p]) (void)hipStreamSynchronize(c->coll[p]);
-    if (p < (int)c->comm.size() && c->comm[p]) (void)ncclCommDestroy(c->comm[p]);
+    if (p < (int)c->comm.size() && c->comm[p]) (void)rccl().comm_destroy(c->comm[p]);
     if (p < (int)c->handle.size() && c->handle[p]) (void)spmm_destroy(c->handle[p]);
     if (p < (int)c->chunk_done.size())
       for (auto e : c->chunk_done[p]) (void)hipEventDestroy(e);
-    for (auto* v : {&c->t0, &c->t_comp, &c->t_end, &c->coll_done})
+    for (auto* v : {&c->t0, &c->t_comp, &c->t_end, &c->coll_done, &c->user_in})
       if (p < (int)v->size() && (*v)[p]) (void)hipEventDestroy((*v)[p]);
     if (p < (int)c->compute.size() && c->compute[p]) (void)hipStreamDestroy(c->compute[p]);
     if (p < (int)c->coll.size() && c->coll[p]) (void)hipStreamDestroy(c->coll[p]);
@@ -75,6 +113,7 @@ spmm_status_t spmm_multi_create(spmm_multi_t* out, int ngpu, const int* devices)
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SPMM_STATUS_NOT_INITIALIZED;
   if (ngpu < 1 || ngpu > ndev) return SPMM_STATUS_INVALID_VALUE;
+  if (!rccl().ok) return SPMM_STATUS_NOT_INITIALIZED;  // no usable librccl on this system
   std::vector<int> dev(ngpu);
   for (int p = 0; p < ngpu; ++p) {
     dev[p] = devices ? devices[p] : p;
@@ -96,6 +135,8 @@ spmm_status_t spmm_multi_create(spmm_multi_t* out, int ngpu, const int* devices)
   c->t_comp.assign(ngpu, nullptr);
   c->t_end.assign(ngpu, nullptr);
   c->coll_done.assign(ngpu, nullptr);
+  c->user_in.assign(ngpu, nullptr);
+  c->user.assign(ngpu, nullptr);
   spmm_status_t st = SPMM_STATUS_SUCCESS;
   for (int p = 0; p < ngpu && st == SPMM_STATUS_SUCCESS; ++p) {
     hipError_t e = hipSetDevice(dev[p]);
@@ -104,6 +145,7 @@ spmm_status_t spmm_multi_create(spmm_multi_t* out, int ngpu, const int* devices)
     for (auto* v : {&c->t0, &c->t_comp, &c->t_end})
       if (e == hipSuccess) e = hipEventCreate(&(*v)[p]);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->coll_done[p], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->user_in[p], hipEventDisableTiming);
     if (e != hipSuccess) {
       st = spmm::from_hip(e);
       break;
@@ -111,7 +153,8 @@ spmm_status_t spmm_multi_create(spmm_multi_t* out, int ngpu, const int* devices)
     st = spmm_create(&c->handle[p]);
     if (st == SPMM_STATUS_SUCCESS) st = spmm_set_stream(c->handle[p], c->compute[p]);
   }
-  if (st == SPMM_STATUS_SUCCESS) st = from_nccl(ncclCommInitAll(c->comm.data(), ngpu, dev.data()));
+  if (st == SPMM_STATUS_SUCCESS)
+    st = from_nccl(rccl().comm_init_all(c->comm.data(), ngpu, dev.data()));
   if (st != SPMM_STATUS_SUCCESS) {
     release(c);
     return st;
@@ -128,6 +171,13 @@ spmm_status_t spmm_multi_destroy(spmm_multi_t c) {
 }
 
 int spmm_multi_size(spmm_multi_t c) { return c ? c->ngpu : 0; }
+
+spmm_status_t spmm_multi_set_user_streams(spmm_multi_t c, void* const* streams) {
+  if (!c) return SPMM_STATUS_NOT_INITIALIZED;
+  for (int p = 0; p < c->ngpu; ++p)
+    c->user[p] = streams ? reinterpret_cast<hipStream_t>(streams[p]) : nullptr;
+  return SPMM_STATUS_SUCCESS;
+}
 
 spmm_status_t spmm_multi_get_stream(spmm_multi_t c, int part, void** stream) {
   if (!c) return SPMM_STATUS_NOT_INITIALIZED;
@@ -171,6 +221,13 @@ spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int*
       ev.push_back(e);
     }
   }
+  // inputs produced on the caller's streams are complete before any kernel reads them
+  for (int p = 0; p < P; ++p) {
+    if (!c->user[p]) continue;
+    SPMM_TRY_HIP(hipSetDevice(c->dev[p]));
+    SPMM_TRY_HIP(hipEventRecord(c->user_in[p], c->user[p]));
+    SPMM_TRY_HIP(hipStreamWaitEvent(c->compute[p], c->user_in[p], 0));
+  }
   for (int ch = 0; ch < chunks; ++ch) {
     for (int p = 0; p < P; ++p) {
       SPMM_TRY_HIP(hipSetDevice(c->dev[p]));
@@ -190,14 +247,17 @@ spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int*
       SPMM_TRY_HIP(hipEventRecord(c->chunk_done[p][ch], c->compute[p]));
       SPMM_TRY_HIP(hipStreamWaitEvent(c->coll[p], c->chunk_done[p][ch], 0));
     }
-    if (P > 1) {
-      spmm_status_t st = from_nccl(ncclGroupStart());
+    // in-place all-gather of chunk ch, on one device too (a one-rank RCCL
+    // communicator: the same call, stream and event chain as at P > 1)
+    {
+      const Rccl& R = rccl();
+      spmm_status_t st = from_nccl(R.group_start());
       for (int p = 0; p < P && st == SPMM_STATUS_SUCCESS; ++p) {
         float* base = C[p] + (size_t)ch * P * slot;
-        st = from_nccl(ncclAllGather(base + (size_t)p * slot, base, slot, ncclFloat, c->comm[p],
-                                     c->coll[p]));
+        st = from_nccl(R.all_gather(base + (size_t)p * slot, base, slot, ncclFloat, c->comm[p],
+                                    c->coll[p]));
       }
-      const spmm_status_t st2 = from_nccl(ncclGroupEnd());
+      const spmm_status_t st2 = from_nccl(R.group_end());
       if (st != SPMM_STATUS_SUCCESS) return st;
       if (st2 != SPMM_STATUS_SUCCESS) return st2;
     }
@@ -207,6 +267,8 @@ spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int*
     SPMM_TRY_HIP(hipEventRecord(c->coll_done[p], c->coll[p]));
     SPMM_TRY_HIP(hipStreamWaitEvent(c->compute[p], c->coll_done[p], 0));
     if (c->timing) SPMM_TRY_HIP(hipEventRecord(c->t_end[p], c->compute[p]));
+    // later work on the caller's stream sees all of C
+    if (c->user[p]) SPMM_TRY_HIP(hipStreamWaitEvent(c->user[p], c->coll_done[p], 0));
   }
   return SPMM_STATUS_SUCCESS;
 }

@@ -110,6 +110,7 @@ _PROTOS = {
     "spmm_multi_destroy": (c_int, [_P]),
     "spmm_multi_size": (c_int, [_P]),
     "spmm_multi_get_stream": (c_int, [_P, c_int, POINTER(c_void_p)]),
+    "spmm_multi_set_user_streams": (c_int, [_P, _P]),
     "spmm_multi_slot_rows": (c_int, [c_int, _P, c_int]),
     "spmm_csr_f32_multi": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P, _P, _P, _P, c_int, _P,
                                    c_int, c_int]),

@@ -298,15 +298,40 @@ class MultiGPU:
               ldc: int, chunks: int = 1) -> None:
         """parts[p] = (rowptr, colind, val) tensors on device p (rowptr of the
         part's rows, indexing colind / val directly); Bs[p] B replicas; Cs[p]
-        the [chunks * world * slot_rows, ldc] outputs (include/spmm_multi.h)."""
+        the [chunks * world * slot_rows, ldc] outputs (include/spmm_multi.h).
+        Ordered against each device's current torch stream: the kernels start
+        after the work already queued there, and work queued there afterwards
+        sees all of C (spmm_multi_set_user_streams)."""
         P = len(self.devices)
+        if not (len(parts) == len(part_nnz) == len(Bs) == len(Cs) == P) or len(bounds) != P + 1:
+            raise ValueError(f"MultiGPU.csrmm: {P} parts expected")
+        if chunks < 1 or ldc < n or ldb < n:
+            raise ValueError("MultiGPU.csrmm: chunks >= 1, ldb >= n and ldc >= n")
+        slot = self.slot_rows(bounds, chunks)
+        need_c = chunks * P * slot * ldc
         for p in range(P):
             rp, ci, v = parts[p]
             for t, dt, nm in ((rp, torch.int32, "rowptr"), (ci, torch.int32, "colind"),
                               (v, torch.float32, "val"), (Bs[p], torch.float32, "B"),
                               (Cs[p], torch.float32, "C")):
                 _need(t, dt, nm)
+                if t.device.index != self.devices[p]:
+                    raise ValueError(f"part {p}: {nm} is on {t.device}, expected "
+                                     f"cuda:{self.devices[p]}")
+            rows = int(bounds[p + 1]) - int(bounds[p])
+            if rp.numel() < rows + 1:
+                raise ValueError(f"part {p}: rowptr has {rp.numel()} entries, needs {rows + 1}")
+            if Cs[p].numel() < need_c:
+                raise ValueError(f"part {p}: C has {Cs[p].numel()} floats, the chunk-major "
+                                 f"output needs chunks * world * slot_rows * ldc = {need_c}")
+            if k > 0 and Bs[p].numel() < (k - 1) * ldb + n:
+                raise ValueError(f"part {p}: B has {Bs[p].numel()} floats, needs "
+                                 f"{(k - 1) * ldb + n}")
         vp = lambda ts: (c_void_p * P)(*[_ptr(t) for t in ts])  # noqa: E731
+        streams = (c_void_p * P)(*[torch.cuda.current_stream(d).cuda_stream
+                                   for d in self.devices])
+        check(lib().spmm_multi_set_user_streams(self._c, streams),
+              "spmm_multi_set_user_streams")
         b = (c_int * (P + 1))(*[int(x) for x in bounds])
         nz = (c_int * P)(*[int(x) for x in part_nnz])
         check(lib().spmm_csr_f32_multi(self._c, m, n, k, b, vp([q[0] for q in parts]),

@@ -1,6 +1,7 @@
 """bench.py helpers that need no GPU: the BSR workloads' PMC traffic lookup
-(profiles/r02_pmc_bytes/bytes.jsonl) and the reorder-in-the-loop
-graph builder on a small community graph."""
+(profiles/r03_pmc_bytes/bytes.jsonl), the CSR roofline rule,
+the CPU-baseline timing helpers and the reorder-in-the-loop graph builder
+ on a small community graph."""
 from __future__ import annotations
 
 import importlib.util
@@ -25,18 +26,68 @@ def _bench():
     return mod
 
 
-def test_bsr_traffic_lookup_matches_the_committed_records():
+KEY = {"workload": "products_bsr16_f16", "kernel": "bsr16_f16_cs_kernel", "K": 512,
+       "dtype": "fp16", "nnzb": 5040000, "layout_BC": "row", "variant": "default",
+       "kernel_src": "0123456789abcdef"}
+
+
+def test_bsr_traffic_lookup_needs_every_key(tmp_path, monkeypatch):
+    """Counter bytes are used only for the exact workload, kernel, K, dtype,
+    nnzb, variant and kernel build they were measured on (a
+    --K 256 run must not divide K = 512 bytes by its own time)."""
     b = _bench()
-    recs = [json.loads(line) for line in open(b.BSR_TRAFFIC)]
-    assert recs, "committed PMC byte records"
-    for wl, kern in {(r["workload"], r["kernel"]) for r in recs}:
-        want = [r for r in recs if r["workload"] == wl and r["kernel"] == kern][-1]
-        got = b.bsr_traffic(wl, kern)
-        assert got == want["counter_bytes_per_launch"] and got > 0
-        # FETCH_SIZE x calibration + WRITE_SIZE (MI355X_MICROARCH.md HBM recipe)
-        assert abs(want["fetch_size_bytes_raw"] * want["fetch_correction"] +
-                   want["write_size_bytes"] - got) < 1e-3 * got
-    assert b.bsr_traffic("no_such_workload", "bsr32_f32_cs2_kernel") is None
+    f = tmp_path / "bytes.jsonl"
+    recs = [dict(KEY, counter_bytes_per_launch=111), dict(KEY, K=256, counter_bytes_per_launch=222),
+            dict(KEY, counter_bytes_per_launch=333)]  # the last matching record wins
+    f.write_text("".join(json.dumps(r) + "\n" for r in recs))
+    monkeypatch.setattr(b, "BSR_TRAFFIC", str(f))
+    assert b.bsr_traffic(KEY) == 333
+    assert b.bsr_traffic(dict(KEY, K=256)) == 222
+    for k, v in (("K", 128), ("dtype", "fp32"), ("nnzb", 1), ("variant", "6104"),
+                 ("kernel_src", "fedcba9876543210"), ("layout_BC", "col"),
+                 ("workload", "products_rcm_bsr16_f16")):
+        assert b.bsr_traffic(dict(KEY, **{k: v})) is None, k
+    monkeypatch.setattr(b, "BSR_TRAFFIC", str(tmp_path / "missing.jsonl"))
+    assert b.bsr_traffic(KEY) is None
+
+
+def test_committed_traffic_records_are_consistent():
+    """Every committed record carries the full lookup key and its counter
+    bytes are FETCH_SIZE x calibration + WRITE_SIZE (MI355X_MICROARCH.md HBM
+    recipe)."""
+    b = _bench()
+    if not os.path.exists(b.BSR_TRAFFIC):
+        return
+    for line in open(b.BSR_TRAFFIC):
+        r = json.loads(line)
+        assert {"workload", "kernel", "K", "dtype", "nnzb", "variant", "kernel_src"} <= set(r)
+        got = r["counter_bytes_per_launch"]
+        assert got > 0
+        assert abs(r["fetch_size_bytes_raw"] * r["fetch_correction"] +
+                   r["write_size_bytes"] - got) < 1e-3 * got
+
+
+def test_csr_roofline_never_above_the_peak():
+    b = _bench()
+    ci = np.random.default_rng(0).integers(0, 1000, 50000).astype(np.int32)
+    # a slow launch: the gather model
+    r = b.csr_roofline(1000, ci, 128, 10.0)
+    assert r["bytes_model"].startswith("SURVEY") and r["frac"] <= 1
+    assert r["algorithmic_bytes_per_launch"] == b.csr_bytes(1000, ci.size, 128)
+    # a launch faster than the gather model allows (B cache-resident): compulsory bytes
+    r = b.csr_roofline(1000, ci, 128, 1e-4)
+    assert r["bytes_model"].startswith("compulsory")
+    assert r["algorithmic_bytes_per_launch"] == 4 * 1001 + 8 * ci.size + 4 * 128 * 1000 * 2
+    assert r["gather_model_GBps"] > b.HBM_PEAK_GBPS
+
+
+def test_batched_samples_and_spread():
+    b = _bench()
+    calls = []
+    reps, ts = b._batched_samples(lambda: calls.append(1), min_sample_s=0.001, nsamples=5)
+    assert len(ts) == 5 and reps >= 1 and len(calls) == 4 + 6 * reps
+    sp = b._spread([1.0, 2.0, 3.0])
+    assert sp["median_s"] == 2.0 and sp["spread"] == 1.0
 
 
 def test_community_graph_reorder_record():

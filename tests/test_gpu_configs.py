@@ -149,9 +149,11 @@ def test_config4_products_k256_row_shards(oracle, device, products_k256):
 @pytest.mark.parametrize("chunks", [1, 4])
 def test_config4_native_multi_entry(oracle, device, products_k256, chunks):
     """spmm_csr_f32_multi (include/spmm_multi.h) over ncclCommInitAll on this
-    box's one GPU: one chunk is the same kernel on the same rows as the
-    whole-matrix call (bit-identical); four chunks overlap the exchange with
-    the compute and agree within the fp32 bar."""
+    box's one GPU: every chunk goes through the in-place ncclAllGather of a
+    one-rank communicator and its event chain, as at P > 1. One chunk is the
+    same kernel on the same rows as the whole-matrix call (bit-identical);
+    four chunks overlap the exchange with the compute and agree within the
+    fp32 bar."""
     from spmm_hip import ops, prep
     rp, ci, v, K = products_k256
     n = rp.size - 1
@@ -179,3 +181,48 @@ def test_config4_native_multi_entry(oracle, device, products_k256, chunks):
         absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B.abs())
         assert bool(((got - Cw).abs() <= 2 * TOL_F32 * absd + 1e-30).all())
     mg.close()
+
+
+def test_config4_native_multi_checks_outputs(device):
+    """MultiGPU.csrmm refuses a C shorter than the chunk-major output and a
+    tensor on another device before anything is launched (the kernel and the
+    in-place all-gather would write past a short C)."""
+    from spmm_hip import ops
+    mg = ops.MultiGPU([device.index or 0])
+    rp = torch.tensor([0, 1, 2], dtype=torch.int32, device=device)
+    ci = torch.tensor([0, 1], dtype=torch.int32, device=device)
+    v = torch.ones(2, device=device)
+    B = torch.ones((2, 8), device=device)
+    short = torch.empty((3, 8), device=device)  # 4 chunks x 1 slot row x 8 needed = 32
+    with pytest.raises(ValueError, match="chunk-major"):
+        mg.csrmm([0, 2], [(rp, ci, v)], [2], [B], [short], m=2, n=8, k=2, ldb=8, ldc=8,
+                 chunks=4)
+    with pytest.raises(ValueError, match="HIP device"):
+        mg.csrmm([0, 2], [(rp, ci, v)], [2], [B.cpu()], [short], m=2, n=8, k=2, ldb=8, ldc=8)
+    ok = torch.empty((2, 8), device=device)
+    mg.csrmm([0, 2], [(rp, ci, v)], [2], [B], [ok], m=2, n=8, k=2, ldb=8, ldc=8)
+    torch.cuda.synchronize()  # ordered on the current stream: no explicit mg.synchronize()
+    assert torch.equal(ok, torch.ones((2, 8), device=device))
+    mg.close()
+
+
+def test_config4_torch_distributed_world1(tmp_path):
+    """bench.py's N > 1 exchange path through RCCL on this one GPU: a fresh
+    child process initialises torch.distributed (nccl backend) at world 1
+    before any GPU call, then the in-place all-gather (chunks = 1, bit-identical
+    to the whole-matrix kernel) and chunked_spmm with 4 async all-gathers
+    overlapping the next chunk's kernel (within the fp32 bar)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29541", RANK="0",
+               LOCAL_RANK="0", WORLD_SIZE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_world1_child.py")
+    r = subprocess.run([sys.executable, "-u", child], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    print(res)
+    assert res["backend"] == "nccl" and res["world"] == 1
+    assert res["chunks1_bit_identical"]
+    assert res["chunks4_within_bar"] and res["chunks4_no_nan"], res
+    assert res["allgather_ms"] > 0

@@ -2,7 +2,9 @@
 """Counter bytes of each workload's dominant kernel from tools/pmc_bytes.sh's
 passes: FETCH_SIZE (KiB per dispatch) x the calibration factor + WRITE_SIZE,
 per launch, against the kernel-trace mean duration of the same kernel, and
-beside the bench line's own byte model (roofline.bytes_per_launch).
+beside the bench line's own byte model (roofline.bytes_per_launch). Each
+record carries the bench line's roofline.traffic_key, the exact shape
+bench.py will use it for.
 
     python tools/bytes_summary.py gpurun_out/pmcb WORKLOAD [WORKLOAD ...]
 Prints one JSON line per workload."""
@@ -42,14 +44,17 @@ def main():
     for wl in wls:
         b = bench_line(os.path.join(o, f"kt_{wl}.log"))
         rf = b["roofline"]
-        kname = rf["kernel"].split("<")[0].split(" ")[0]
+        key = rf.get("traffic_key") or {"workload": wl}
+        kname = key.get("kernel", rf["kernel"]).split("<")[0].split(" ")[0]
         dur = one(os.path.join(o, f"kt_{wl}"), kname, "duration_ns") * 1e-9
         fetch = one(os.path.join(o, f"fetch_{wl}"), kname, "FETCH_SIZE") * 1024
         write = one(os.path.join(o, f"write_{wl}"), kname, "WRITE_SIZE") * 1024
         hbm = fetch * factor + write
         model = rf.get("bytes_per_launch") or rf.get("algorithmic_bytes_per_launch")
+        # the bench line's lookup key (workload, kernel, K, dtype, nnzb, variant,
+        # kernel source tag): bench.py uses these bytes only for that exact run shape
         print(json.dumps({
-            "workload": wl, "kernel": kname, "kernel_trace_ms": round(dur * 1e3, 4),
+            **key, "kernel_trace_ms": round(dur * 1e3, 4),
             "bench_kernel_ms": rf.get("kernel_ms"),
             "fetch_size_bytes_raw": round(fetch), "fetch_correction": round(factor, 4),
             "write_size_bytes": round(write), "counter_bytes_per_launch": round(hbm),
@@ -57,7 +62,8 @@ def main():
             "counter_frac_of_8TBps": round(hbm / dur / HBM_PEAK, 4),
             "model_bytes_per_launch": model,
             "model_frac": rf.get("frac"),
-            "model_over_counter": round(model / hbm, 3) if model else None}))
+            "model_over_counter": round(model / hbm, 3) if model else None,
+            "upper_model_bytes": rf.get("bytes_model_upper")}))
 
 
 if __name__ == "__main__":
