@@ -358,6 +358,23 @@ spmm_status_t spmm_hybrid_csrmm_f32(spmm_handle_t handle, int m, int n, int k, f
                                     const float* bsrVal, int nnzb, const float* B, int ldb,
                                     float beta, float* C, int ldc);
 
+/* The same with explicit storage orders: divide.cu's own call shape
+ * (divide.cu:218-230, 348-373) is csrmm2 + bsrmm onto a column-major z
+ * (ldc = nb*bs) with alpha = beta = 1, B column-major (transB = N, ldb >= k)
+ * or row-major (transB = T, ldb >= n). Row-major B and C are
+ * spmm_hybrid_csrmm_f32. Otherwise two stream-ordered launches: a
+ * column-major B is transposed once into the handle's scratch (zero rows
+ * past k, so ldb need only cover the k real rows), the BSR part writes C in
+ * orderC with beta, then the CSR remainder accumulates. A column-major C
+ * needs ldc >= ceil(m/bs)*bs when nnzb > 0 (>= m otherwise). */
+spmm_status_t spmm_hybrid_csrmm_ex_f32(spmm_handle_t handle, int m, int n, int k, float alpha,
+                                       const int* csrRowPtr, const int* csrColInd,
+                                       const float* csrVal, int csrNnz, int blockDim,
+                                       const int* bsrRowPtr, const int* bsrColInd,
+                                       const float* bsrVal, int nnzb, const float* B, int ldb,
+                                       spmm_order_t orderB, float beta, float* C, int ldc,
+                                       spmm_order_t orderC);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

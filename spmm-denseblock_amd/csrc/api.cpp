@@ -380,3 +380,68 @@ extern "C" spmm_status_t spmm_hybrid_csrmm_f32(
   return csrmm_impl(handle, m, n, k, csrNnz, alpha, csrRowPtr, csrColInd, csrVal, 0, B, ldb,
                     SPMM_ORDER_ROW, csr_beta, C, ldc, SPMM_ORDER_ROW);
 }
+
+// divide.cu's own call shape (divide.cu:218-230, 348-373): csrmm2 and bsrmm
+// back to back onto one column-major z (ldc = nb*bs) with alpha = beta = 1,
+// B column-major (transB = N, ldb = n) or row-major (transB = T, ldb = dim).
+// Row-major B and C keep spmm_hybrid_csrmm_f32 (fused when it pays). Any
+// column-major operand runs as two stream-ordered launches: a column-major B
+// is transposed once into a row-major (ceil(k/bs)*bs) x n copy in the handle's
+// scratch, zero rows past k (so the BSR part never reads past the caller's B:
+// the reference's ldb = n is short of nb*bs when bs does not divide n); the
+// BSR part runs the dense-block MFMA kernel on it, writing C in the caller's
+// order through its own epilogue (beta), then the CSR remainder accumulates
+// (beta = 1; a column-major C through the workspace transpose).
+extern "C" spmm_status_t spmm_hybrid_csrmm_ex_f32(
+    spmm_handle_t handle, int m, int n, int k, float alpha, const int* csrRowPtr,
+    const int* csrColInd, const float* csrVal, int csrNnz, int blockDim, const int* bsrRowPtr,
+    const int* bsrColInd, const float* bsrVal, int nnzb, const float* B, int ldb,
+    spmm_order_t orderB, float beta, float* C, int ldc, spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if ((orderB != SPMM_ORDER_ROW && orderB != SPMM_ORDER_COL) ||
+      (orderC != SPMM_ORDER_ROW && orderC != SPMM_ORDER_COL))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (orderB == SPMM_ORDER_ROW && orderC == SPMM_ORDER_ROW)
+    return spmm_hybrid_csrmm_f32(handle, m, n, k, alpha, csrRowPtr, csrColInd, csrVal, csrNnz,
+                                 blockDim, bsrRowPtr, bsrColInd, bsrVal, nnzb, B, ldb, beta, C,
+                                 ldc);
+  if (m < 0 || n < 0 || k < 0 || csrNnz < 0 || nnzb < 0 || blockDim <= 0)
+    return SPMM_STATUS_INVALID_VALUE;
+  if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  if (!csrRowPtr || !C || (k > 0 && !B)) return SPMM_STATUS_INVALID_VALUE;
+  if (nnzb > 0 && (!bsrRowPtr || !bsrColInd || !bsrVal)) return SPMM_STATUS_INVALID_VALUE;
+  if (csrNnz > 0 && (!csrColInd || !csrVal)) return SPMM_STATUS_INVALID_VALUE;
+  const int mb = (m + blockDim - 1) / blockDim, kb = (k + blockDim - 1) / blockDim;
+  const long long rows_c = nnzb > 0 ? (long long)mb * blockDim : m;
+  if (orderB == SPMM_ORDER_COL ? ldb < (k > 0 ? k : 1) : ldb < n) return SPMM_STATUS_INVALID_VALUE;
+  if (orderC == SPMM_ORDER_COL ? ldc < rows_c : ldc < n) return SPMM_STATUS_INVALID_VALUE;
+  const float* Bx = B;
+  int ldbx = ldb;
+  if (orderB == SPMM_ORDER_COL && k > 0) {
+    const size_t rows_b = nnzb > 0 ? (size_t)kb * blockDim : (size_t)k;
+    spmm_status_t st = ensure_scratch(handle, rows_b * n * sizeof(float));
+    if (st != SPMM_STATUS_SUCCESS) return st;
+    float* Bt = static_cast<float*>(handle->scratch);
+    // B (k x n col-major) is an (n x k) row-major matrix with ld ldb
+    st = launch_transpose(handle, n, k, B, ldb, Bt, n, 0.f);
+    if (st != SPMM_STATUS_SUCCESS) return st;
+    if (rows_b > (size_t)k) {
+      const hipError_t e = hipMemsetAsync(Bt + (size_t)k * n, 0,
+                                          (rows_b - k) * n * sizeof(float), handle->stream);
+      if (e != hipSuccess) return from_hip(e);
+    }
+    Bx = Bt;
+    ldbx = n;
+  }
+  float csr_beta = beta;
+  if (nnzb > 0) {
+    spmm_status_t st = launch_bsrmm_f32(handle, SPMM_DIRECTION_ROW, mb, kb, n, nnzb, blockDim,
+                                        alpha, bsrRowPtr, bsrColInd, bsrVal, Bx, ldbx,
+                                        SPMM_ORDER_ROW, beta, C, ldc, orderC,
+                                        /*dense_blocks=*/true);
+    if (st != SPMM_STATUS_SUCCESS) return st;
+    csr_beta = 1.f;
+  }
+  return csrmm_impl(handle, m, n, k, csrNnz, alpha, csrRowPtr, csrColInd, csrVal, 0, Bx, ldbx,
+                    SPMM_ORDER_ROW, csr_beta, C, ldc, orderC);
+}

@@ -122,6 +122,9 @@ _PROTOS = {
                                  POINTER(c_double)]),
     "spmm_hybrid_csrmm_f32": (c_int, [_P, c_int, c_int, c_int, c_float, _P, _P, _P, c_int, c_int,
                                       _P, _P, _P, c_int, _P, c_int, c_float, _P, c_int]),
+    "spmm_hybrid_csrmm_ex_f32": (c_int, [_P, c_int, c_int, c_int, c_float, _P, _P, _P, c_int,
+                                         c_int, _P, _P, _P, c_int, _P, c_int, c_int, c_float, _P,
+                                         c_int, c_int]),
     # spmm_host.h
     "spmm_host_free": (None, [_P]),
     "spmm_host_rng_seed": (None, [c_uint64]),

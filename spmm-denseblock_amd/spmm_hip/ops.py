@@ -185,11 +185,13 @@ def bsrmm_f16(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: 
 
 def hybrid_csrmm(csr: tuple, bsr: tuple, B: torch.Tensor, *, m: int, n: int, k: int, bs: int,
                  ldb: int, C: torch.Tensor, ldc: int, alpha: float = 1.0, beta: float = 0.0,
+                 order_b: int = ORDER_ROW, order_c: int = ORDER_ROW,
                  handle: Handle | None = None) -> torch.Tensor:
     """Dense-block + CSR-remainder SpMM (divide.cu:348-373) on one stream:
     csr = (rowptr, colind, val), bsr = (rowptr, colind, val) from
-    prep.divide; row-major B and C (padded to whole blocks when the BSR part
-    is non-empty)."""
+    prep.divide. Row-major B and C (padded to whole blocks when the BSR part
+    is non-empty): spmm_hybrid_csrmm_f32; other storage orders (divide.cu's
+    column-major z, transB = N / T): spmm_hybrid_csrmm_ex_f32."""
     crp, cci, cv = csr
     brp, bci, bv = bsr
     for t, dt, nm in ((crp, torch.int32, "csr_rowptr"), (cci, torch.int32, "csr_colind"),
@@ -198,10 +200,16 @@ def hybrid_csrmm(csr: tuple, bsr: tuple, B: torch.Tensor, *, m: int, n: int, k: 
                       (B, torch.float32, "B"), (C, torch.float32, "C")):
         _need(t, dt, nm)
     h = handle or default_handle()
-    check(lib().spmm_hybrid_csrmm_f32(h.raw, m, n, k, alpha, _ptr(crp), _ptr(cci), _ptr(cv),
-                                      cci.numel(), bs, _ptr(brp), _ptr(bci), _ptr(bv),
-                                      bci.numel(), _ptr(B), ldb, beta, _ptr(C), ldc),
-          "spmm_hybrid_csrmm_f32")
+    if order_b == ORDER_ROW and order_c == ORDER_ROW:
+        check(lib().spmm_hybrid_csrmm_f32(h.raw, m, n, k, alpha, _ptr(crp), _ptr(cci), _ptr(cv),
+                                          cci.numel(), bs, _ptr(brp), _ptr(bci), _ptr(bv),
+                                          bci.numel(), _ptr(B), ldb, beta, _ptr(C), ldc),
+              "spmm_hybrid_csrmm_f32")
+    else:
+        check(lib().spmm_hybrid_csrmm_ex_f32(h.raw, m, n, k, alpha, _ptr(crp), _ptr(cci),
+                                             _ptr(cv), cci.numel(), bs, _ptr(brp), _ptr(bci),
+                                             _ptr(bv), bci.numel(), _ptr(B), ldb, order_b, beta,
+                                             _ptr(C), ldc, order_c), "spmm_hybrid_csrmm_ex_f32")
     return C
 
 

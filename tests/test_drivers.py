@@ -245,3 +245,42 @@ def test_compat_header_drivers_on_the_kats(golden, T):
     for g, w in zip(got, want):
         assert np.array_equal(g, w), (g, w)
     assert r.stdout.count("status SPMM_STATUS_SUCCESS") == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("impl,tb,n", [("rocsparse", 0, 8000), ("cusparse", 1, 8000),
+                                       ("hybrid", 0, 8000), ("hybrid", 1, 7990),
+                                       ("rocsparse", 0, 7990)])
+def test_divide_cli(tmp_path, impl, tb, n):
+    """divide.cu:195-378 reproduced: divide_matrix at density 0.05, then
+    csrmm2 + bsrmm (or the library's hybrid call) accumulating into the
+    column-major z with alpha = beta = 1, transB N (y column-major) or T (y
+    row-major); its lines, and z against the f64 oracle of the whole
+    unit-valued product. n = 7990 is not a multiple of bs = 32 (the driver
+    then reads y with ldb = n1, printed)."""
+    from spmm_hip import prep
+    rp, ci = prep.community_csr(n, 40.0, 64, 256, 0.9, 3)
+    os.makedirs(tmp_path / "tmp", exist_ok=True)
+    prep.dump_csr(str(tmp_path / "tmp" / "cm"), rp, ci)
+    dump = str(tmp_path / "C.bin")
+    dim, bs = 64, 32
+    out = _run(["divide", "cm", bs, dim, impl, tb, 0.05], tmp_path,
+               env={"SPMM_DRIVER_DUMP": dump})
+    assert "csr nnz = " in out and "bsr nnzb = " in out and out.rstrip().endswith("end")
+    assert ("hybrid cost time" in out) if impl == "hybrid" else (
+        "csrmm cost time" in out and "bsrmm cost time" in out and "total cost time" in out)
+    nb = (n + bs - 1) // bs
+    n1 = nb * bs
+    # the split itself: divide_matrix's counts (host restatement, bit-exact with divide.cu)
+    _, _, _, brp, _, _ = prep.divide(n, rp, ci, np.ones(ci.size, np.float32), bs, 0.05)
+    csr_nnz = int(out.split("csr nnz = ")[1].split()[0])
+    assert int(out.split("bsr nnzb = ")[1].split()[0]) == int(brp[-1]) and csr_nnz < ci.size
+    prep.rng_seed(1234)
+    y = prep.random_dense_matrix(n1, dim).reshape(-1)
+    if tb == 1:
+        B = y.reshape(n1, dim)  # row-major, ldb = dim
+    else:
+        ldb = n1 if n1 != n else n
+        assert ("note: ldb = n1" in out) == (n1 != n)
+        B = np.ascontiguousarray(y[:ldb * dim].reshape(dim, ldb).T)  # column-major
+    _check_dump(dump, rp, ci, B, f"divide {impl} transB={tb} n={n}")

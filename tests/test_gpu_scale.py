@@ -1,16 +1,25 @@
-"""Path B at BASELINE's full sizes, through
-size-independent properties: the BSR, hybrid and CSR kernels are three
-independent implementations of the same product, so at full scale each BSR
-result must agree with the CSR kernel's within the fp32 bar, with the
-magnitude bound |A|.|B| itself computed on the device (the CSR kernel on
-|val|, |B|). The small-size tests pin each kernel to the oracle; these check
-that nothing breaks at 10^8 nonzeros (index widths, grid sizes, tails)."""
+"""Path B at BASELINE's full sizes.
+
+Two checks per result:
+* sampled rows against the f64 oracle (oracle_csrmm_f64 on the same CSR
+  values the BSR / hybrid arrays were built from: the product is the same
+  matrix's), as the reference's own differential bar does
+  (check_result.cu:233-246): every row of the longest block row, of a
+  segmented block row where the launch splits rows (seg_build_kernel), of the
+  block rows launched first and last (XCD-chunked order, and longest-first on
+  shallow grids), and 1,500 random rows;
+* every row against the CSR kernel, an independent implementation of the
+  same product, within the fp32 bar, with the magnitude bound |A|.|B|
+  computed on the device (the CSR kernel on |val|, |B|).
+The small-size tests pin each kernel to the oracle element by element; these
+check that nothing breaks at 10^8 nonzeros (index widths, grid sizes, tails,
+segments, launch orders)."""
 from __future__ import annotations
 
 import numpy as np
 import pytest
 
-from helpers import TOL_F16_ACC, TOL_F32
+from helpers import TOL_F16_ACC, TOL_F32, assert_normwise, oracle_csrmm_f64
 
 pytestmark = pytest.mark.gpu
 
@@ -26,6 +35,57 @@ def _dev(*arrs):
     return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
 
 
+def _xcd_block_row(b: int, mb: int, xm: int = 32) -> int:
+    """bsr_kernels.hip xcd_block_row: block row of wave b in the XCD-chunked order."""
+    full = mb // (8 * xm) * (8 * xm)
+    if b >= full:
+        return b
+    x, i = b % 8, b // 8
+    return ((i // xm) * 8 + x) * xm + i % xm
+
+
+def _sample_rows(brp: np.ndarray, bs: int, n: int, seed: int, extra_block_rows=()) -> np.ndarray:
+    """Rows to check against the oracle: the longest and shortest block rows,
+    the first and last block rows of the XCD-chunked launch order, any extra
+    block rows (segmented ones), and 1,500 random rows."""
+    nbr = np.diff(brp)
+    mb = nbr.size
+    brs = {int(np.argmax(nbr)), int(np.argmin(nbr)), 0, _xcd_block_row(mb - 1, mb), mb - 1}
+    brs |= {int(b) for b in extra_block_rows}
+    rows = [np.arange(b * bs, min((b + 1) * bs, n)) for b in sorted(brs)]
+    rows.append(np.random.default_rng(seed).choice(n, 1500, replace=False))
+    return np.unique(np.concatenate(rows))
+
+
+def _segmented_block_rows(brp: np.ndarray, num_cus: int = 256) -> list[int]:
+    """Block rows the bs = 32 launch cuts into segments (cs2_segments: a
+    shallow grid whose longest row exceeds twice the mean load per wave slot;
+    rows longer than L blocks are split): the shortest and the longest such."""
+    nbr = np.diff(brp)
+    nnzb, slots = int(nbr.sum()), 12 * num_cus
+    if nbr.size > 8 * slots or nbr.max() <= 2 * (nnzb + slots - 1) // slots:
+        return []
+    L = max(64, (nnzb + 2 * slots - 1) // (2 * slots))
+    seg = np.nonzero(nbr > L)[0]
+    return [] if seg.size == 0 else [int(seg[np.argmin(nbr[seg])]), int(seg[np.argmax(nbr[seg])])]
+
+
+def _check_oracle_rows(oracle, got, rp, ci, v, B, rows, tol, what):
+    """got[rows] against the f64 oracle of the same rows of the CSR product;
+    only the B rows those rows touch leave the device."""
+    K = B.shape[1]
+    deg = np.diff(rp)
+    sub_rp = np.concatenate([[0], np.cumsum(deg[rows])]).astype(np.int32)
+    sub_ci = np.concatenate([ci[rp[r]:rp[r + 1]] for r in rows])
+    sub_v = np.concatenate([v[rp[r]:rp[r + 1]] for r in rows]).astype(np.float32)
+    ucols, inv = np.unique(sub_ci, return_inverse=True)
+    Bsub = B[torch.from_numpy(ucols.astype(np.int64)).to(B.device)].float().cpu().numpy()
+    ref, absd = oracle_csrmm_f64(oracle, rows.size, K, sub_rp, inv.astype(np.int32), sub_v, Bsub,
+                                 K, 0)
+    g = got[torch.from_numpy(rows.astype(np.int64)).to(got.device)].cpu().numpy()
+    assert_normwise(g, ref, absd, tol, f"{what}: {rows.size} sampled rows vs the f64 oracle")
+
+
 def _within(got, ref, absd, tol, what):
     err = (got - ref).abs()
     bound = tol * absd + 1e-30
@@ -33,9 +93,10 @@ def _within(got, ref, absd, tol, what):
     assert bad == 0, f"{what}: {bad} elements outside {tol} x |A||B| (max err {float(err.max())})"
 
 
-def test_reddit_scale_bsr32_and_hybrid_vs_csr(device):
+def test_reddit_scale_bsr32_and_hybrid_vs_csr(oracle, device):
     """Config 3 (reddit stand-in, 115 M nnz, bs = 32, K = 128): device csr2bsr
-    -> LDS MFMA kernel, and divide -> hybrid, both against the CSR kernel."""
+    -> the column-stream MFMA kernel, and divide -> hybrid, each against
+    sampled oracle rows and the CSR kernel."""
     from spmm_hip import prep
     ops = _ops()
     n, K, bs = 232965, 128, 32
@@ -53,6 +114,9 @@ def test_reddit_scale_bsr32_and_hybrid_vs_csr(device):
     Cb = torch.empty((mb * bs, K), device=device)
     ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=Cb, ldc=K)
     torch.cuda.synchronize()
+    brp_h = brp.cpu().numpy()
+    rows = _sample_rows(brp_h, bs, n, 11, _segmented_block_rows(brp_h))
+    _check_oracle_rows(oracle, Cb, rp, ci, v, B, rows, TOL_F32, "reddit bs32 BSR")
     _within(Cb[:n], Cc, absd, 2 * TOL_F32, "reddit bs32 BSR vs CSR")
     assert not bool(Cb[n:].any()), "padding rows of C must be zero"
     del brp, bci, bval
@@ -66,14 +130,17 @@ def test_reddit_scale_bsr32_and_hybrid_vs_csr(device):
         ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=Ch,
                          ldc=K, handle=h)
         torch.cuda.synchronize()
+        _check_oracle_rows(oracle, Ch, rp, ci, v, B, _sample_rows(parts[3], bs, n, 12), TOL_F32,
+                           f"reddit hybrid (flags {flags})")
         _within(Ch[:n], Cc, absd, 2 * TOL_F32, f"reddit hybrid (flags {flags}) vs CSR")
         h.close()
 
 
-def test_products_scale_bsr16_f16_vs_csr(device):
+def test_products_scale_bsr16_f16_vs_csr(oracle, device):
     """Config 5 (products stand-in, bs = 16, fp16 A and B, K = 512): the
-    fp16 MFMA kernel against the CSR kernel run on the same fp16-rounded
-    values in fp32 (both accumulate in fp32)."""
+    fp16 MFMA kernel against sampled oracle rows (the exact product of the
+    same fp16 values) and against the CSR kernel run on the same
+    fp16-rounded values in fp32 (both accumulate in fp32)."""
     from spmm_hip import prep
     ops = _ops()
     n, K, bs = 2449029, 512, 16
@@ -93,11 +160,13 @@ def test_products_scale_bsr16_f16_vs_csr(device):
     ops.bsrmm_f16(brp, bci, bval16, B16, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=Cb, ldc=K)
     torch.cuda.synchronize()
     assert int(bci.numel()) > 4_000_000
+    rows = _sample_rows(brp.cpu().numpy(), bs, n, 13)
+    _check_oracle_rows(oracle, Cb, rp, ci, v, B16, rows, TOL_F16_ACC, "products bs16 fp16 BSR")
     _within(Cb[:n], Cc, absd, 2 * TOL_F16_ACC, "products bs16 fp16 BSR vs CSR")
 
 
 @pytest.mark.parametrize("bs", [32, 16])
-def test_reordered_reddit_scale_bsr_vs_csr(device, bs):
+def test_reordered_reddit_scale_bsr_vs_csr(oracle, device, bs):
     """Configs 3 / 5 with the reorder step in the loop (reorder_graph.cc:26-49
     then run_bsrmm.cu): the reddit stand-in with scrambled node ids, the
     in-repo RCM (spmm_reorder_rcm), the permutation applied, device csr2bsr,
@@ -132,6 +201,13 @@ def test_reordered_reddit_scale_bsr_vs_csr(device, bs):
                       ldc=K)
         tol = 2 * TOL_F16_ACC
     torch.cuda.synchronize()
+    brp_h = brp.cpu().numpy()
+    seg = _segmented_block_rows(brp_h) if bs == 32 else []
+    if bs == 32:
+        assert seg, "the RCM-reordered reddit stand-in must exercise the segmented rows"
+    rows = _sample_rows(brp_h, bs, n, 14 + bs, seg)
+    _check_oracle_rows(oracle, Cb, rp, ci, v, B, rows, TOL_F32 if bs == 32 else TOL_F16_ACC,
+                       f"RCM-reordered reddit bs{bs} BSR")
     _within(Cb[:n], Cc, absd, tol, f"RCM-reordered reddit bs{bs} BSR vs CSR")
     assert not bool(Cb[n:].any()), "padding rows of C must be zero"
     if bs == 32:
@@ -143,4 +219,6 @@ def test_reordered_reddit_scale_bsr_vs_csr(device, bs):
         Ch = torch.empty((mb * bs, K), device=device)
         ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=Ch, ldc=K)
         torch.cuda.synchronize()
+        _check_oracle_rows(oracle, Ch, rp, ci, v, B, _sample_rows(parts[3], bs, n, 15), TOL_F32,
+                           "RCM-reordered reddit hybrid")
         _within(Ch[:n], Cc, absd, 2 * TOL_F32, "RCM-reordered reddit hybrid vs CSR")

@@ -9,8 +9,9 @@ tail of a block row and the count then covered a B copy; a GPU rerun loop
 caught it about one run in four. These tests read the stream instead:
 
 * every stage hand-off wait keeps in flight only what its kernel plans for
-  (CM4: exactly the one A prefetch load; every other ring: LDS-DMA copies) and
-  retires an LDS-DMA copy as its youngest operation, on every path;
+  (LDS-DMA copies) and retires an LDS-DMA copy as its youngest operation, on
+  every path (round 1's CM4 kernel, whose ring kept exactly one A prefetch
+  load, was removed in round 3; the checker still handles that form);
 * no copy loop holds a vmcnt(0) that drains the copies of the blocks ahead in
   the middle of an iteration (hipcc put one before every fp16 B-fragment read
   until those reads went through inline asm);
@@ -40,23 +41,19 @@ def bsr_asm() -> str:
         return f.read()
 
 
+# The LDS-DMA kernels the library ships (bsr_kernels.hip dispatch): every
+# instantiation of each family must be audited.
+SHIPPED_DMA = {"bsr32_f32_lds_kernel": 6, "bsr32_f32_cs2_kernel": 6, "bsr16_cm_kernel": 4,
+               "bsr16_f16_cs_kernel": 4}
+
+
 def test_every_stage_handoff_wait(bsr_asm):
     res = iv.audit(bsr_asm)
-    assert len(res) >= 40, f"expected the LDS-staged kernels, found {len(res)}"
+    for fam, cnt in SHIPPED_DMA.items():
+        got = sum(fam in k for k in res)
+        assert got == cnt, f"{fam}: {got} LDS-DMA instantiations audited, expected {cnt}"
     bad = {k: v for k, v in res.items() if v}
     assert not bad, "\n".join(f"{k}: {v}" for k, v in bad.items())
-
-
-def test_cm4_keeps_exactly_the_a_prefetch(bsr_asm):
-    funcs = iv.split_functions(bsr_asm)
-    cm4 = [k for k in funcs if "bsr32_f32_cm4_kernel" in k]
-    assert len(cm4) == 2  # row- and column-major C
-    for k in cm4:
-        waits = [r for r in iv.counted_waits(k, funcs[k]) if r["handoff"]]
-        # three unrolled steps + two tail steps
-        assert len(waits) >= 5, waits
-        for r in waits:
-            assert r["n"] == 1 and r["window"][0] == ["load"] and r["window"][1] == ["dma"], r
 
 
 def test_no_copy_loop_drains(bsr_asm):
@@ -125,16 +122,18 @@ _Z5drainv:
     assert len(iv.loop_drains(body)) == 1
 
 
-def test_column_stream_counts_only_its_copies(bsr_asm):
-    """bsr32_f32_cs_kernel waits with counts computed at run time from the
-    number of copies it issued (one per B item, four per A block). That is
-    exact only if every vector-memory operation of its loops is one of those
-    LDS-DMA copies and the compiler adds no waits of its own: no VGPR load,
-    store or spill (scratch) in a copy loop, and every vmcnt wait there is one
-    of the hand-placed ones (inline asm)."""
+@pytest.mark.parametrize("kernel", ["bsr32_f32_cs2_kernel", "bsr16_f16_cs_kernel"])
+def test_column_stream_counts_only_its_copies(bsr_asm, kernel):
+    """The column streams wait with counts computed at run time from the
+    number of vector-memory operations they issued (A copies, B rows or
+    item copies, block-column chunks). That is exact only if every such
+    operation in a copy loop is one the wave counts — an LDS-DMA copy or an
+    inline-asm load — and the compiler adds no waits of its own: no
+    compiler-generated VGPR load, store or spill (scratch) in a copy loop,
+    and every vmcnt wait there one of the hand-placed ones (inline asm)."""
     funcs = iv.split_functions(bsr_asm)
-    cs = [k for k in funcs if "bsr32_f32_cs_kernel" in k]
-    assert len(cs) >= 2, "column-stream instantiations"
+    cs = [k for k in funcs if kernel in k]
+    assert len(cs) >= 4, "column-stream instantiations"
     for k in cs:
         body = funcs[k]
         assert not any(line.strip().startswith("scratch_") for _, line in body), f"{k}: spills"
@@ -148,11 +147,12 @@ def test_column_stream_counts_only_its_copies(bsr_asm):
                 continue
             for no, mn, ops in b.insts:
                 c = iv.classify(mn, ops)
-                assert c in (None, "dma"), f"{k} line {no}: {mn} {ops} in a copy loop"
+                assert c in (None, "dma") or (c == "load" and no in b.asm_lines), \
+                    f"{k} line {no}: {mn} {ops} in a copy loop"
                 n_dma += c == "dma"
                 if mn == "s_waitcnt" and "vmcnt" in ops:
                     assert no in b.asm_lines, f"{k} line {no}: compiler-placed {mn} {ops}"
-        assert n_dma >= 8, (k, n_dma)
+        assert n_dma >= 4, (k, n_dma)
 
 
 def _vregs(ops: str) -> set:
@@ -165,9 +165,8 @@ def _vregs(ops: str) -> set:
     return out
 
 
-@pytest.mark.parametrize("kernel,tag", [("bsr32_f32_cs2_kernel", "ELi0ELb"),
-                                        ("bsr16_f16_cs_kernel", "")])
-def test_column_stream_registers_in_flight_are_asm_only(bsr_asm, kernel, tag):
+@pytest.mark.parametrize("kernel", ["bsr32_f32_cs2_kernel", "bsr16_f16_cs_kernel"])
+def test_column_stream_registers_in_flight_are_asm_only(bsr_asm, kernel):
     """bsr32_f32_cs2_kernel loads B rows, block-column chunks and A columns
     (bsr16_f16_cs_kernel: block-column chunks) with inline asm that does not
     wait, so hipcc believes their registers hold data at once. They are safe only if nothing but inline asm touches them
@@ -177,8 +176,7 @@ def test_column_stream_registers_in_flight_are_asm_only(bsr_asm, kernel, tag):
     flight; any compiler-generated instruction that reads or writes one of
     them (a copy, a spill, a reuse) fails the test."""
     funcs = iv.split_functions(bsr_asm)
-    # shipped instantiations only (DIAG = 0; the diagnostic builds are timing tools)
-    cs2 = [k for k in funcs if kernel in k and tag in k]
+    cs2 = [k for k in funcs if kernel in k]
     assert len(cs2) >= 2, f"{kernel} instantiations"
     for k in cs2:
         body = funcs[k]
