@@ -1152,7 +1152,7 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   }
   // nothing is in flight after the last round; the full wait makes that
   // visible to the register check (tests/test_isa_waits.py)
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : : "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : "v"(cnext) : "memory");
 
   if constexpr (CROW) {
     const int col = jt + 4 * j;
@@ -1804,9 +1804,10 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     }
     if (fin) break;
   }
-  // nothing is in flight after the last round (a block-column chunk may be);
-  // the full wait makes that visible to the register check (tests/test_isa_waits.py)
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // nothing is in flight after the last round (a block-column chunk may be: its
+  // register stays live until this full wait, which also makes the drain visible to the
+  // register check, tests/test_isa_waits.py)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : : "v"(cnext) : "memory");
 
   if constexpr (!CROW) {
     // column-major C: the 16 x COLS tile through LDS, then 4 whole 64-B column
@@ -2132,9 +2133,12 @@ constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 //  offsets, cross-block pairs, nt A copies): products stand-in 3.07 ms
 //  against 3.15 without nt A (4516, round 2's default), reddit 1.93 / 2.04
 //  (profiles/r03_var_sweep.jsonl). 4496: the same without 32-bit offsets,
-//  for 32 * ldb * 4 >= 2^31. 4126: the full-panel LDS kernel (D = 2, 40 KB,
-//  4 workgroups per CU), the default for blocks known to be dense (the
-//  hybrid's BSR part, MFMA-pipe bound: products part 1.71 vs 1.87 ms at D = 3).
+//  for 32 * ldb * 4 >= 2^31. 4126, not selectable: the full-panel LDS kernel
+//  (D = 2, 40 KB, 4 workgroups per CU), the default for blocks known to be
+//  dense (the hybrid's BSR part, MFMA-pipe bound: products part 1.71 vs 1.87
+//  ms at D = 3). It computes the dense block product (an inf / NaN in a B row
+//  only explicit zeros meet reaches C), so it fails the column-sparse parity
+//  case the column streams pass and is not offered as an override.
 constexpr int kBsr32Cs = 4416;
 constexpr int kBsr32CsNoNt = 4516;
 constexpr int kBsr32CsWideLdb = 4496;
@@ -2269,8 +2273,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     const dim3 grid(mb, (n + 127) / 128);
     const bool narrow = (size_t)ldb * 128 < (1u << 31);  // 32-row panels addressable in 31 bits
     int lv = dense_blocks ? kBsr32Dense : kBsr32Cs;
-    if (var == kBsr32CsNoNt || var == kBsr32CsWideLdb || var == kBsr32Dense || var == kBsr32Cs)
-      lv = var;
+    if (var == kBsr32CsNoNt || var == kBsr32CsWideLdb || var == kBsr32Cs) lv = var;
     if (!narrow && (lv == kBsr32Cs || lv == kBsr32CsNoNt)) lv = kBsr32CsWideLdb;
     if (lv == kBsr32Dense) {
       // split-bf16 (opt-in, SPMM_HYBRID_SPLIT_BF16): wave-pair split-K for row-major C
@@ -2394,7 +2397,6 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                int ldb, spmm_order_t orderB, float beta, float* C, int ldc,
                                spmm_order_t orderC) {
   (void)kb;
-  (void)nnzb;
   if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   const _Float16* val = reinterpret_cast<const _Float16*>(val16);
   const _Float16* B = reinterpret_cast<const _Float16*>(B16);
@@ -2407,7 +2409,8 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   if (bs == 16 && rowd && brow && n >= 8 && n % 8 == 0 && ldb % 8 == 0 && aligned(val, 16) &&
       aligned(B, 16)) {
     int lv = n >= 128 ? kBsr16F16Cs : kBsr16F16Cm;
-    if (var == kBsr16F16Cm || (n >= 128 && (var == kBsr16F16Cs || var == kBsr16F16CsNoNt)))
+    if (var == kBsr16F16Cm ||
+        (n >= 128 && (var == kBsr16F16Cs || var == kBsr16F16CsNoNt)))
       lv = var;
     if (lv == kBsr16F16Cm) {
       const dim3 grid(mb, (n + 255) / 256);

@@ -206,6 +206,54 @@ def test_bsrmm_f16(oracle, device, n, direction, ob):
     assert_normwise(C.cpu().numpy(), ref, absd, TOL_F16_ACC, f"f16 n={n}")
 
 
+@pytest.mark.parametrize("n", [136, 264, 392])
+@pytest.mark.parametrize("oc", [0, 1])
+@pytest.mark.parametrize("ob", [0, 1])
+def test_bsrmm_f16_column_stream_shapes(oracle, device, n, oc, ob):
+    """The shipped fp16 column streams (n >= 128) on the paths the defaults
+    take besides n % 256 == 0: a ragged last column tile (n = 136, 264, 392:
+    the clamped row offsets and the tail column guard), ldb > n, column-major
+    C (the LDS-tile epilogue), alpha / beta != (1, 0) (the beta epilogue), and
+    a column-major B staged row-major through the workspace; rows longer than
+    one 64-block chunk and an empty block row."""
+    rng = np.random.default_rng(n * 7 + 2 * oc + ob)
+    mb, kb, bs = 23, 90, 16
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.8, empty_rows=(4,))
+    v16 = v.astype(np.float16)
+    Bd = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float16)
+    if ob == 0:
+        ldb = n + 8
+        Bm = np.zeros((kb * bs, ldb), np.float16)
+        Bm[:, :n] = Bd
+    else:
+        ldb = kb * bs + 8
+        Bm = np.zeros((n, ldb), np.float16)
+        Bm[:, :kb * bs] = Bd.T
+    m = mb * bs
+    alpha, beta = 0.5, 1.5
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    ldc = n + 4 if oc == 0 else m + 4
+    Cm = np.zeros((m, ldc) if oc == 0 else (n, ldc), np.float32)
+    if oc == 0:
+        Cm[:, :n] = C0
+    else:
+        Cm[:, :m] = C0.T
+    drp, dci, dv, dB, dC = _dev(rp, ci, v16, Bm.reshape(-1), Cm.reshape(-1))
+    _ops().bsrmm_f16(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=ldb, order_b=ob, C=dC,
+                     ldc=ldc, order_c=oc, alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    got = dC.cpu().numpy().reshape(Cm.shape)
+    got = got[:, :n] if oc == 0 else got[:, :m].T
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v16, Bd, n, 0, half=True)
+    ref = alpha * ref + beta * C0.astype(np.float64)
+    absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+    assert_normwise(got, ref, absd, TOL_F16_ACC, f"f16 column stream n={n} oc={oc} ob={ob}")
+    # the padding columns of C are untouched
+    pad = dC.cpu().numpy().reshape(Cm.shape)[:, n:] if oc == 0 else \
+        dC.cpu().numpy().reshape(Cm.shape)[:, m:]
+    assert np.array_equal(pad, Cm[:, n:] if oc == 0 else Cm[:, m:])
+
+
 def test_csr_vs_bsr_differential(oracle, device):
     """check_result.cu:103-116,233-246: csrmm2(T) vs bsrmm(T) after csr2bsr,
     m = 32768, p = 0.01, bs = 4, K = 64, B = +-0.5 alternating, eps 1e-4."""
