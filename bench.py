@@ -262,8 +262,16 @@ def _host_cpus() -> dict:
                 mine.add((f1.read().strip(), f2.read().strip()))
         except OSError:
             mine.add(("cpu", c))
+    quota = None  # cgroup v2 CPU bandwidth limit ("max 100000" = none)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = "none" if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     return {"affinity_cpus": len(aff), "physical_cores_in_affinity": len(mine),
-            "machine_physical_cores": len(phys) or None, "machine_logical_cpus": os.cpu_count()}
+            "machine_physical_cores": len(phys) or None, "machine_logical_cpus": os.cpu_count(),
+            "cgroup_cpu_quota_cpus": quota}
 
 
 def cpu_baseline_config1(L) -> dict:

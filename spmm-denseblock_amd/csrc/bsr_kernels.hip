@@ -1525,7 +1525,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // ANT: the A copies are non-temporal (nt): each tile's wave reads A from HBM anyway, and
 // its lines should not displace the B rows neighbouring block rows share in L2 (products
 // stand-in 4.03 -> 3.88 ms, profiles/r03_var_sweep.jsonl).
-template <bool CROW, int P, int NA, int DA, int CAP = 48, bool ANT = false>
+template <bool CROW, int P, int NA, int DA, int CAP = 48, bool ANT = false, bool CST = false>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
@@ -1547,6 +1547,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   constexpr int kStg = kAbuf + 16 * kAbRow;  // offset of the item stages
   constexpr int kLds = kStg + P * kStage;
   static_assert(kLds >= COLS * 16 * 4, "column-major C tile fits");
+  static_assert(!CST || kLds >= 16 * (COLS + 4) * 4, "row-major C tile fits");
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int lane = threadIdx.x;
   const int g = lane >> 4, r16 = lane & 15, h = lane >> 5;
@@ -1824,6 +1825,42 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       if (jt + jl < n) {
         float* p = C + (size_t)(jt + jl) * ldc + row;
         *p = epi(tile[jl * 16 + r16], alpha, beta, p);
+      }
+    }
+    return;
+  }
+  if constexpr (CST) {
+    // row-major C through LDS: the 16 x COLS tile (row pitch COLS + 4 floats: the two
+    // half-waves' rows in different banks), then each row as 64 lanes x 16 B (1 KB per
+    // store instruction; the register layout stores 4 x 64-B row pieces per instruction:
+    // products stand-in 3.91-4.04 -> 3.79-3.90 ms, profiles/r03_epilogue_ab.txt)
+    constexpr int kTp = COLS + 4;
+    float* tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int t = 0; t < kT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tile[(4 * g + e) * kTp + 16 * t + r16] = acc[t][e];
+    __builtin_amdgcn_s_waitcnt(0);
+    const int col = jt + 4 * lane;
+    if (col < n) {
+      const bool vec = (ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
+#pragma unroll 4
+      for (int rr = 0; rr < 16; ++rr) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(tile + rr * kTp + 4 * lane);
+        float* p = C + ((size_t)br * 16 + rr) * ldc + col;
+        if (vec) {
+          if (beta == 0.f) {
+            v *= alpha;
+          } else {
+            const f32x4 c = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
+          }
+          *reinterpret_cast<f32x4*>(p) = v;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) p[i] = epi(v[i], alpha, beta, p + i);
+        }
       }
     }
     return;
@@ -2145,8 +2182,10 @@ constexpr int kBsr32CsWideLdb = 4496;
 constexpr int kBsr32Dense = 4126;
 //  bs 16 fp16, n >= 128 (bsr16_f16_cs_kernel: 2 item stages, 4 A slots, a
 //  48-entry pending list, whole-row copies, nt A copies; 19.7 KB of LDS, 8
-//  waves per CU): products stand-in K = 512 3.88 ms against 4.03 without nt A
-//  (6104, round 2's default). Below 128 columns, and 4725: the column-masked
+//  waves per CU), row-major C through an LDS tile (1-KB row stores): products
+//  stand-in K = 512 3.79-3.90 ms against 3.91-4.04 storing from the MFMA
+//  register layout (profiles/r03_epilogue_ab.txt); 6104 is the same without nt A (4.03 against 3.88
+//  before the staged epilogue). Below 128 columns, and 4725: the column-masked
 //  block kernel (bsr16_cm_kernel, at least 8 waves per SIMD).
 constexpr int kBsr16F16Cs = 6404;
 constexpr int kBsr16F16CsNoNt = 6104;
@@ -2427,19 +2466,19 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
         timing_end(ctx, slot);
         return st;
       }
-#define CS16_LAUNCH(ANT)                                                                         \
+#define CS16_LAUNCH(...)                                                                         \
   do {                                                                                           \
     if (crow)                                                                                    \
-      hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, 2, 4, 0, 48, ANT>), gc, dim3(64), 0,         \
+      hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, 2, 4, 0, 48, __VA_ARGS__>), gc, dim3(64), 0, \
                          ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
                          ord);                                                                   \
     else                                                                                         \
-      hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, 2, 4, 0, 48, ANT>), gc, dim3(64), 0,        \
-                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
-                         ord);                                                                   \
+      hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, 2, 4, 0, 48, __VA_ARGS__>), gc, dim3(64),   \
+                         0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C,     \
+                         ldc, ord);                                                              \
   } while (0)
-      if (lv == kBsr16F16Cs) CS16_LAUNCH(true);
-      else CS16_LAUNCH(false);
+      if (lv == kBsr16F16Cs) CS16_LAUNCH(true, true);
+      else CS16_LAUNCH(false, true);
 #undef CS16_LAUNCH
     }
   } else if (bs == 16 && vec_ok) {
