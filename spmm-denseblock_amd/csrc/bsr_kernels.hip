@@ -1519,9 +1519,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // 2j + 1 (lanes 32-63) whole, so each copy reads 8 whole 128-B lines (a chunk-major form
 // read 16 half lines per copy, the other halves one copy later: the L1 / TA work per byte
 // was the cost). The stage is row-major (512-B rows); lane k of row R loads
-// chunk (k - R) & 31, which puts chunk c of row R at 16-B slot (c + R) & 31 of its row, so
-// the 16 rows of one chunk sit in 16 different bank slots and the transposed reads take
-// one address per t (tra).
+// chunk (k - 2R) & 31, which puts chunk c of row R at 16-B slot (c + 2R) & 31 of its row,
+// so the transposed reads are conflict-free and take one address per t (tra).
 // ANT: the A copies are non-temporal (nt): each tile's wave reads A from HBM anyway, and
 // its lines should not displace the B rows neighbouring block rows share in L2 (products
 // stand-in 4.03 -> 3.88 ms, profiles/r03_var_sweep.jsonl).
@@ -1560,16 +1559,23 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   const size_t ldb2 = (size_t)ldb * 2;
   const char* const zrow = reinterpret_cast<const char*>(g_zero_row) - 2 * (size_t)jt;
   // transposed B reads: lane (g, q = (lane >> 2) & 3, p = lane & 3) reads row R = 4g + q,
-  // columns 16t + 4p .. + 3: chunk 2t + p / 2 at byte 8 (p & 1), in slot (chunk + R) & 31
+  // columns 16t + 4p .. + 3: chunk 2t + p / 2 at byte 8 (p & 1), in slot (chunk + 2R) & 31.
+  // Chunk c of row R sits at slot (c + 2R) & 31, so the 32 lanes of a transposed read's lane
+  // group (rows 8i .. 8i + 7, chunks 2t, 2t + 1) hit 16 distinct 16-B slots mod 256 B:
+  // conflict-free (with c + R, rows R and R + 1 collided on one slot, 2-way: products stand-in
+  // 3.79-3.81 -> 3.78-3.80 ms, profiles/r03_swz_ep_lgk_ab.txt)
+  constexpr int kSw = 2;
   unsigned boffr[8], tra[16];
 #pragma unroll
   for (int j = 0; j < 8; ++j)
-    boffr[j] = 2u * (unsigned)min(jt + 8 * (((lane & 31) - 2 * j - (lane >> 5)) & 31), n - 8);
+    boffr[j] =
+        2u * (unsigned)min(jt + 8 * (((lane & 31) - kSw * (2 * j + (lane >> 5))) & 31), n - 8);
   {
     const int R = 4 * g + ((lane >> 2) & 3);
 #pragma unroll
     for (int t = 0; t < 16; ++t)
-      tra[t] = lds0 + kStg + 512u * R + 16u * ((2 * t + ((lane & 3) >> 1) + R) & 31) + 8u * (lane & 1);
+      tra[t] = lds0 + kStg + 512u * R + 16u * ((2 * t + ((lane & 3) >> 1) + kSw * R) & 31) +
+               8u * (lane & 1);
   }
 
   int nis = 0;  // vector-memory operations issued by this wave
@@ -1707,7 +1713,8 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     const bool fin = !more;
 #pragma unroll
     for (int s = 0; s < P; ++s) {
-      // consume the item issued P slots ago
+      // consume the item issued P slots ago (issuing the next item into the stage before
+      // the MFMAs, once its fragments are in registers, measured 2.5 % slower)
       if (kind[s]) {
         wait_vm_older(nis - stamp[s]);
         f16x4 fb[kT];
