@@ -1524,12 +1524,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // ANT: the A copies are non-temporal (nt): each tile's wave reads A from HBM anyway, and
 // its lines should not displace the B rows neighbouring block rows share in L2 (products
 // stand-in 4.03 -> 3.88 ms, profiles/r03_var_sweep.jsonl).
-template <bool CROW, int P, int NA, int DA, int CAP = 48, bool ANT = false, bool CST = false>
+template <bool CROW, int P, int NA, int DA, int CAP = 48, bool ANT = false, bool CST = false,
+          int COLS = 256>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
     float beta, float* __restrict__ C, int ldc, const int* __restrict__ order) {
-  constexpr int COLS = 256;  // output columns per wave
+  // COLS: output columns per wave, 256 or 512 (W512: a stage row is a whole 1-KB B row, one
+  // copy per row, and the block row's A values and walk serve all 512 columns)
+  static_assert(COLS == 256 || COLS == 512, "columns per wave");
+  constexpr int kRowB = COLS * 2;     // bytes per stage row
+  constexpr int kCh = COLS / 8;       // 16-B chunks per stage row
+  constexpr int kRpc = 1024 / kRowB;  // stage rows per copy (2 or 1)
+  constexpr int kCp = 16 / kRpc;      // copies per item
   // the pair copied at block kr (blocks kr + DA + 2, + 3) overwrites blocks
   // kr + DA + 2 - NA, + 3 - NA, which must be read already (< kr)
   static_assert((NA & (NA - 1)) == 0 && DA % 2 == 0 && NA >= DA + 4 && P >= 2 && P <= 6,
@@ -1565,17 +1572,17 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   // conflict-free (with c + R, rows R and R + 1 collided on one slot, 2-way: products stand-in
   // 3.79-3.81 -> 3.78-3.80 ms, profiles/r03_swz_ep_lgk_ab.txt)
   constexpr int kSw = 2;
-  unsigned boffr[8], tra[16];
+  unsigned boffr[kCp], tra[kT];
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    boffr[j] =
-        2u * (unsigned)min(jt + 8 * (((lane & 31) - kSw * (2 * j + (lane >> 5))) & 31), n - 8);
+  for (int j = 0; j < kCp; ++j)
+    boffr[j] = 2u * (unsigned)min(
+                        jt + 8 * (((lane % kCh) - kSw * (kRpc * j + lane / kCh)) & (kCh - 1)), n - 8);
   {
     const int R = 4 * g + ((lane >> 2) & 3);
 #pragma unroll
-    for (int t = 0; t < 16; ++t)
-      tra[t] = lds0 + kStg + 512u * R + 16u * ((2 * t + ((lane & 3) >> 1) + kSw * R) & 31) +
-               8u * (lane & 1);
+    for (int t = 0; t < kT; ++t)
+      tra[t] = lds0 + kStg + (unsigned)kRowB * R +
+               16u * ((2 * t + ((lane & 3) >> 1) + kSw * R) & (kCh - 1)) + 8u * (lane & 1);
   }
 
   int nis = 0;  // vector-memory operations issued by this wave
@@ -1717,40 +1724,46 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       // the MFMAs, once its fragments are in registers, measured 2.5 % slower)
       if (kind[s]) {
         wait_vm_older(nis - stamp[s]);
-        f16x4 fb[kT];
-        asm volatile(
-            "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
-              "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
-            : "v"(tra[0]), "v"(tra[1]), "v"(tra[2]), "v"(tra[3]), "v"(tra[4]), "v"(tra[5]),
-              "v"(tra[6]), "v"(tra[7]), "n"(s * kStage)
-            : "memory");
-        asm volatile(
-            "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(fb[8]), "=&v"(fb[9]), "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]),
-              "=&v"(fb[13]), "=&v"(fb[14]), "=&v"(fb[15])
-            : "v"(tra[8]), "v"(tra[9]), "v"(tra[10]), "v"(tra[11]), "v"(tra[12]), "v"(tra[13]),
-              "v"(tra[14]), "v"(tra[15]), "n"(s * kStage)
-            : "memory");
 #pragma unroll
-        for (int t = 0; t < kT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[t], 0, 0, 0);
+        for (int hh = 0; hh < kT / 16; ++hh) {
+          f16x4 fb[16];
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+                "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
+              : "v"(tra[16 * hh]), "v"(tra[16 * hh + 1]), "v"(tra[16 * hh + 2]),
+                "v"(tra[16 * hh + 3]), "v"(tra[16 * hh + 4]), "v"(tra[16 * hh + 5]),
+                "v"(tra[16 * hh + 6]), "v"(tra[16 * hh + 7]), "n"(s * kStage)
+              : "memory");
+          asm volatile(
+              "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+              "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(fb[8]), "=&v"(fb[9]), "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]),
+                "=&v"(fb[13]), "=&v"(fb[14]), "=&v"(fb[15])
+              : "v"(tra[16 * hh + 8]), "v"(tra[16 * hh + 9]), "v"(tra[16 * hh + 10]),
+                "v"(tra[16 * hh + 11]), "v"(tra[16 * hh + 12]), "v"(tra[16 * hh + 13]),
+                "v"(tra[16 * hh + 14]), "v"(tra[16 * hh + 15]), "n"(s * kStage)
+              : "memory");
+#pragma unroll
+          for (int t = 0; t < 16; ++t)
+            acc[16 * hh + t] =
+                __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[16 * hh + t], 0, 0, 0);
+        }
       }
       // produce the next item into slot s: read blocks until 16 columns are
       // pending or the blocks run out
@@ -1784,16 +1797,16 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
             int rw[16];
 #pragma unroll
             for (int e = 0; e < 16; ++e) rw[e] = __builtin_amdgcn_readlane(r, e);
-            const bool hi = lane >= 32;
+            const bool hi = kRpc == 2 && lane >= 32;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const int e = 2 * j + (hi ? 1 : 0);
-              const int re = hi ? rw[2 * j + 1] : rw[2 * j];
+            for (int j = 0; j < kCp; ++j) {
+              const int e = kRpc * j + (hi ? 1 : 0);
+              const int re = kRpc == 1 ? rw[j] : (hi ? rw[2 * j + 1] : rw[2 * j]);
               const char* be = e < cnt ? reinterpret_cast<const char*>(B) + (size_t)re * ldb2 : zrow;
               __builtin_amdgcn_global_load_lds((gbl_void_t)(be + boffr[j]),
                                                (lds_void_t)(stage + 1024 * j), 16, 0, 0);
             }
-            nis += 8;
+            nis += kCp;
           }
           unsigned y0 = y[0], y1 = y[1];
           if (cnt < 16) {  // padded entries: stale values (NaN / inf) must not meet the zero rows
@@ -1848,12 +1861,14 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) tile[(4 * g + e) * kTp + 16 * t + r16] = acc[t][e];
     __builtin_amdgcn_s_waitcnt(0);
-    const int col = jt + 4 * lane;
-    if (col < n) {
-      const bool vec = (ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
+    const bool vec = (ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
+#pragma unroll
+    for (int cc = 0; cc < COLS; cc += 256) {
+      const int col = jt + cc + 4 * lane;
+      if (col >= n) break;
 #pragma unroll 4
       for (int rr = 0; rr < 16; ++rr) {
-        f32x4 v = *reinterpret_cast<const f32x4*>(tile + rr * kTp + 4 * lane);
+        f32x4 v = *reinterpret_cast<const f32x4*>(tile + rr * kTp + cc + 4 * lane);
         float* p = C + ((size_t)br * 16 + rr) * ldc + col;
         if (vec) {
           if (beta == 0.f) {
@@ -2456,7 +2471,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       aligned(B, 16)) {
     int lv = n >= 128 ? kBsr16F16Cs : kBsr16F16Cm;
     if (var == kBsr16F16Cm ||
-        (n >= 128 && (var == kBsr16F16Cs || var == kBsr16F16CsNoNt)))
+        (n >= 128 && (var == kBsr16F16Cs || var == kBsr16F16CsNoNt || var == 6444)))
       lv = var;
     if (lv == kBsr16F16Cm) {
       const dim3 grid(mb, (n + 255) / 256);
@@ -2467,7 +2482,8 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
         hipLaunchKernelGGL((bsr16_cm_kernel<_Float16, false, 2, 5, 8>), grid, dim3(256), 0,
                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
     } else {
-      const dim3 gc(mb, (n + 255) / 256);
+      const int cols = lv == 6444 ? 512 : 256;
+      const dim3 gc(mb, (n + cols - 1) / cols);
       const int* ord = nullptr;
       if (const spmm_status_t st = block_row_order(ctx, mb, gc.y, rowptr, &ord)) {
         timing_end(ctx, slot);
@@ -2485,6 +2501,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
                          ldc, ord);                                                              \
   } while (0)
       if (lv == kBsr16F16Cs) CS16_LAUNCH(true, true);
+      else if (lv == 6444) CS16_LAUNCH(true, true, 512);
       else CS16_LAUNCH(false, true);
 #undef CS16_LAUNCH
     }
