@@ -1530,12 +1530,15 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
     float beta, float* __restrict__ C, int ldc, const int* __restrict__ order) {
-  // COLS: output columns per wave, 256 or 512 (W512: a stage row is a whole 1-KB B row, one
-  // copy per row, and the block row's A values and walk serve all 512 columns)
-  static_assert(COLS == 256 || COLS == 512, "columns per wave");
+  // COLS: output columns per wave (the launcher uses 256). 512 makes a stage row one whole
+  // 1-KB B row and serves all 512 columns with one A copy and one walk per block row; 128
+  // quarters the stage. Both pass the parity subset and lose on the products stand-in, K =
+  // 512: 4.37 ms at 512 (4 waves per CU by LDS) and 4.87 at 128 (4 tiles of A and walk per
+  // block row), against 3.77-3.89 at 256 (profiles/r03_cols_per_wave_ab.txt)
+  static_assert(COLS == 128 || COLS == 256 || COLS == 512, "columns per wave");
   constexpr int kRowB = COLS * 2;     // bytes per stage row
   constexpr int kCh = COLS / 8;       // 16-B chunks per stage row
-  constexpr int kRpc = 1024 / kRowB;  // stage rows per copy (2 or 1)
+  constexpr int kRpc = 1024 / kRowB;  // stage rows per copy (4, 2 or 1)
   constexpr int kCp = 16 / kRpc;      // copies per item
   // the pair copied at block kr (blocks kr + DA + 2, + 3) overwrites blocks
   // kr + DA + 2 - NA, + 3 - NA, which must be read already (< kr)
@@ -1725,7 +1728,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       if (kind[s]) {
         wait_vm_older(nis - stamp[s]);
 #pragma unroll
-        for (int hh = 0; hh < kT / 16; ++hh) {
+        for (int hh = 0; hh < (kT + 15) / 16; ++hh) {
           f16x4 fb[16];
           asm volatile(
               "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
@@ -1743,7 +1746,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
                 "v"(tra[16 * hh + 3]), "v"(tra[16 * hh + 4]), "v"(tra[16 * hh + 5]),
                 "v"(tra[16 * hh + 6]), "v"(tra[16 * hh + 7]), "n"(s * kStage)
               : "memory");
-          asm volatile(
+          if constexpr (kT >= 16) asm volatile(
               "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
               "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
               "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
@@ -1755,12 +1758,13 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
               "s_waitcnt lgkmcnt(0)"
               : "=&v"(fb[8]), "=&v"(fb[9]), "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]),
                 "=&v"(fb[13]), "=&v"(fb[14]), "=&v"(fb[15])
-              : "v"(tra[16 * hh + 8]), "v"(tra[16 * hh + 9]), "v"(tra[16 * hh + 10]),
-                "v"(tra[16 * hh + 11]), "v"(tra[16 * hh + 12]), "v"(tra[16 * hh + 13]),
-                "v"(tra[16 * hh + 14]), "v"(tra[16 * hh + 15]), "n"(s * kStage)
+              : "v"(tra[(16 * hh + 8) % kT]), "v"(tra[(16 * hh + 9) % kT]),
+                "v"(tra[(16 * hh + 10) % kT]), "v"(tra[(16 * hh + 11) % kT]),
+                "v"(tra[(16 * hh + 12) % kT]), "v"(tra[(16 * hh + 13) % kT]),
+                "v"(tra[(16 * hh + 14) % kT]), "v"(tra[(16 * hh + 15) % kT]), "n"(s * kStage)
               : "memory");
 #pragma unroll
-          for (int t = 0; t < 16; ++t)
+          for (int t = 0; t < (kT < 16 ? kT : 16); ++t)
             acc[16 * hh + t] =
                 __builtin_amdgcn_mfma_f32_16x16x16f16(fa[s], fb[t], acc[16 * hh + t], 0, 0, 0);
         }
@@ -1797,11 +1801,13 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
             int rw[16];
 #pragma unroll
             for (int e = 0; e < 16; ++e) rw[e] = __builtin_amdgcn_readlane(r, e);
-            const bool hi = kRpc == 2 && lane >= 32;
+            const int sub = lane / (64 / kRpc);  // this lane's row within a copy
 #pragma unroll
             for (int j = 0; j < kCp; ++j) {
-              const int e = kRpc * j + (hi ? 1 : 0);
-              const int re = kRpc == 1 ? rw[j] : (hi ? rw[2 * j + 1] : rw[2 * j]);
+              const int e = kRpc * j + sub;
+              int re = rw[kRpc * j];
+#pragma unroll
+              for (int u = 1; u < kRpc; ++u) re = sub == u ? rw[kRpc * j + u] : re;
               const char* be = e < cnt ? reinterpret_cast<const char*>(B) + (size_t)re * ldb2 : zrow;
               __builtin_amdgcn_global_load_lds((gbl_void_t)(be + boffr[j]),
                                                (lds_void_t)(stage + 1024 * j), 16, 0, 0);
@@ -1862,13 +1868,16 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       for (int e = 0; e < 4; ++e) tile[(4 * g + e) * kTp + 16 * t + r16] = acc[t][e];
     __builtin_amdgcn_s_waitcnt(0);
     const bool vec = (ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
+    constexpr int kLpr = COLS >= 256 ? 64 : COLS / 4;  // lanes per row piece
+    constexpr int kRpp = 64 / kLpr;                    // rows per store instruction
 #pragma unroll
-    for (int cc = 0; cc < COLS; cc += 256) {
-      const int col = jt + cc + 4 * lane;
+    for (int cc = 0; cc < COLS; cc += 4 * kLpr) {
+      const int col = jt + cc + 4 * (lane % kLpr);
       if (col >= n) break;
 #pragma unroll 4
-      for (int rr = 0; rr < 16; ++rr) {
-        f32x4 v = *reinterpret_cast<const f32x4*>(tile + rr * kTp + cc + 4 * lane);
+      for (int r0 = 0; r0 < 16; r0 += kRpp) {
+        const int rr = r0 + lane / kLpr;
+        f32x4 v = *reinterpret_cast<const f32x4*>(tile + rr * kTp + cc + 4 * (lane % kLpr));
         float* p = C + ((size_t)br * 16 + rr) * ldc + col;
         if (vec) {
           if (beta == 0.f) {
@@ -2471,7 +2480,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
       aligned(B, 16)) {
     int lv = n >= 128 ? kBsr16F16Cs : kBsr16F16Cm;
     if (var == kBsr16F16Cm ||
-        (n >= 128 && (var == kBsr16F16Cs || var == kBsr16F16CsNoNt || var == 6444)))
+        (n >= 128 && (var == kBsr16F16Cs || var == kBsr16F16CsNoNt)))
       lv = var;
     if (lv == kBsr16F16Cm) {
       const dim3 grid(mb, (n + 255) / 256);
@@ -2482,8 +2491,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
         hipLaunchKernelGGL((bsr16_cm_kernel<_Float16, false, 2, 5, 8>), grid, dim3(256), 0,
                            ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
     } else {
-      const int cols = lv == 6444 ? 512 : 256;
-      const dim3 gc(mb, (n + cols - 1) / cols);
+      const dim3 gc(mb, (n + 255) / 256);
       const int* ord = nullptr;
       if (const spmm_status_t st = block_row_order(ctx, mb, gc.y, rowptr, &ord)) {
         timing_end(ctx, slot);
@@ -2501,7 +2509,6 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
                          ldc, ord);                                                              \
   } while (0)
       if (lv == kBsr16F16Cs) CS16_LAUNCH(true, true);
-      else if (lv == 6444) CS16_LAUNCH(true, true, 512);
       else CS16_LAUNCH(false, true);
 #undef CS16_LAUNCH
     }
