@@ -209,13 +209,15 @@ def test_bsrmm_f16(oracle, device, n, direction, ob):
 @pytest.mark.parametrize("n", [136, 264, 392])
 @pytest.mark.parametrize("oc", [0, 1])
 @pytest.mark.parametrize("ob", [0, 1])
-def test_bsrmm_f16_column_stream_shapes(oracle, device, n, oc, ob):
+@pytest.mark.parametrize("cpad", [4, 1])
+def test_bsrmm_f16_column_stream_shapes(oracle, device, n, oc, ob, cpad):
     """The shipped fp16 column streams (n >= 128) on the paths the defaults
     take besides n % 256 == 0: a ragged last column tile (n = 136, 264, 392:
     the clamped row offsets and the tail column guard), ldb > n, column-major
     C (the LDS-tile epilogue), alpha / beta != (1, 0) (the beta epilogue), and
     a column-major B staged row-major through the workspace; rows longer than
-    one 64-block chunk and an empty block row."""
+    one 64-block chunk and an empty block row. cpad = 1 makes ldc odd, so the
+    row-major LDS-tile epilogue takes its per-element store path."""
     rng = np.random.default_rng(n * 7 + 2 * oc + ob)
     mb, kb, bs = 23, 90, 16
     rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.8, empty_rows=(4,))
@@ -232,7 +234,7 @@ def test_bsrmm_f16_column_stream_shapes(oracle, device, n, oc, ob):
     m = mb * bs
     alpha, beta = 0.5, 1.5
     C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
-    ldc = n + 4 if oc == 0 else m + 4
+    ldc = n + cpad if oc == 0 else m + cpad
     Cm = np.zeros((m, ldc) if oc == 0 else (n, ldc), np.float32)
     if oc == 0:
         Cm[:, :n] = C0
