@@ -2338,8 +2338,11 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   const bool vec_ok = aligned(val, 16) && (brow || (aligned(B, 16) && ldb % 4 == 0));
   const int slot = timing_begin(ctx);
   const int var = variant_override();
+  // the column stream stores row-major C as 16-B row pieces (and its segment fix-up too):
+  // C and ldc must keep them aligned, else the fragment kernel's scalar stores serve
+  const bool c16 = !crow || (aligned(C, 16) && ldc % 4 == 0);
   if (bs == 32 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 && aligned(val, 16) &&
-      aligned(B, 16)) {
+      aligned(B, 16) && (dense_blocks || c16)) {
     const dim3 grid(mb, (n + 127) / 128);
     const bool narrow = (size_t)ldb * 128 < (1u << 31);  // 32-row panels addressable in 31 bits
     int lv = dense_blocks ? kBsr32Dense : kBsr32Cs;

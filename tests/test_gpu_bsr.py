@@ -139,6 +139,34 @@ def test_bsrmm_f32(oracle, device, bs, direction, orders):
     assert_normwise(got, ref, absd, TOL_F32, f"bsr bs={bs} dir={direction} orders={orders}")
 
 
+@pytest.mark.parametrize("cpad,coff", [(1, 0), (4, 1), (0, 2)])
+def test_bsrmm_f32_bs32_unaligned_row_major_c(oracle, device, cpad, coff):
+    """Row-major C whose rows are not 16-B aligned (odd ldc, or C starting 1 or
+    2 floats into its buffer): the bs 32 column stream stores 16-B row pieces,
+    so these calls take the fragment kernel's scalar stores; alpha / beta and
+    the padding columns are checked."""
+    rng = np.random.default_rng(41 + cpad + 7 * coff)
+    mb, kb, bs, n = 19, 27, 32, 136
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.3, empty_rows=(2,))
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    m, ldc = mb * bs, n + cpad
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    Cm = np.full(coff + m * ldc, 7.0, np.float32)
+    Cm[coff:].reshape(m, ldc)[:, :n] = C0
+    drp, dci, dv, dB, dC = _dev(rp, ci, v, B.reshape(-1), Cm)
+    alpha, beta = -0.75, 0.5
+    _ops().bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC[coff:], ldc=ldc,
+                 alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    out = dC.cpu().numpy()
+    got = out[coff:].reshape(m, ldc)
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
+    ref = alpha * ref + beta * C0.astype(np.float64)
+    absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+    assert_normwise(got[:, :n], ref, absd, TOL_F32, f"bs32 cpad={cpad} coff={coff}")
+    assert np.all(got[:, n:] == 7.0) and np.all(out[:coff] == 7.0)
+
+
 def test_segments_with_staged_col_major_b(oracle, device):
     """Column-major B is staged (transposed) into the handle workspace before
     the bs 32 column stream runs; on a shallow grid with one long block row
