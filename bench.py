@@ -58,6 +58,13 @@ WORKLOADS = {
     # community-ordered products stand-in
     "products_bsr32": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                            p_in=0.97, bs=32, K=128, dtype="fp32"),
+    # the same products and reddit BSR products on the analysed column stream
+    # (spmm_bsr32_analysis_f32 once per matrix, outside the timed region, like
+    # cuSPARSE's SpMM preprocess; spmm_bsrmm_analysed_f32 timed)
+    "products_bsr32_an": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                              p_in=0.97, bs=32, K=128, dtype="fp32", analysed=True),
+    "reddit_bsr32_an": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
+                            p_in=0.99, bs=32, K=128, dtype="fp32", analysed=True),
     "products_hybrid32": dict(kind="hybrid", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                               p_in=0.97, bs=32, K=128, density="auto"),
     # §8f rank 2 in the loop: scrambled ids -> in-repo RCM -> divide + hybrid
@@ -707,6 +714,28 @@ def run_bsr(args, W, world, rank, dev, dist):
     B = (torch.rand((mb * bs, K), device=dev, generator=g) * 2 - 1).to(tdt)
     h = ops.Handle()
     fn = ops.bsrmm if dt == "fp32" else ops.bsrmm_f16
+    an = bool(W.get("analysed"))
+    analysis_ms = None
+    if an:
+        if dt != "fp32" or bs != 32:
+            raise SystemExit("the analysed column stream is bs 32 fp32")
+        masks = torch.empty(nnzb, dtype=torch.int32, device=dev)
+        vcol = torch.empty(nnzb * 1024, device=dev)
+        ts = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ops.bsr32_analysis(d_bv, nnzb=nnzb, masks=masks, val_col=vcol, handle=h)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        analysis_ms = min(ts) * 1e3
+        del d_bv
+
+        def fn(rp_, ci_, _v, B_, *, mb, kb, n, bs, ldb, C, ldc, order_b=ops.ORDER_ROW,
+               order_c=ops.ORDER_ROW, handle=None):
+            ops.bsrmm_analysed(rp_, ci_, vcol, masks, B_, mb=mb, kb=kb, n=n, ldb=ldb,
+                               order_b=order_b, C=C, ldc=ldc, order_c=order_c, handle=handle)
+        d_bv = None
     if args.bsr_layout == "col":
         # cusparseSbsrmm's transB = N layout (run_bsrmm.cu:70-71): B and C
         # column-major with ld = mb*bs.
@@ -773,12 +802,14 @@ def run_bsr(args, W, world, rank, dev, dist):
     # Compulsory bytes (the roofline): the block values and the BSR index
     # arrays once per column tile of the kernel, every distinct B row the
     # product touches once, the C write once.
-    comp_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + s * nnzb * bs * bs) + s * b_rows * K +
+    # (analysed: the masks and only the nonzero columns' values, column-major)
+    a_bytes = (4 * nnzb + s * active_cols * bs) if an else s * nnzb * bs * bs
+    comp_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + a_bytes) + s * b_rows * K +
                   4 * mb * bs * K)
     # Upper byte model (round 2's roofline): the same A and indices, the B
     # rows of every (block row, nonzero column) pair with no reuse between
     # block rows, and C.
-    cm_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + s * nnzb * bs * bs) + s * active_cols * K +
+    cm_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + a_bytes) + s * active_cols * K +
                 4 * mb * bs * K) if cm else kbytes
     t = kms / 1e3
     kname = (("bsr32_f32_cs2_kernel" if bs == 32 else "bsr16_f16_cs_kernel" if cs16 else
@@ -793,7 +824,8 @@ def run_bsr(args, W, world, rank, dev, dist):
         data=data,
         config={"workload": f"{args.workload}: " + (f"scrambled ids -> {reorder['method']} -> "
                                                     if reorder else "") +
-                            f"csr2bsr bs={bs} + bsrmm K={K} {dt}", "n": n,
+                            f"csr2bsr bs={bs} + " + ("analysis + bsrmm_analysed" if an else "bsrmm") +
+                            f" K={K} {dt}", "n": n,
                 "layout_BC": args.bsr_layout,
                 "nnz": nnz, "K": K, "bs": bs, "nnzb": nnzb,
                 "block_fill": round(nnz / (nnzb * bs * bs), 4),
@@ -804,12 +836,15 @@ def run_bsr(args, W, world, rank, dev, dist):
                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                   "frac": round(comp_bytes / t / 1e9 / HBM_PEAK_GBPS, 4),
                   "traffic": bsr_traffic(tkey),
-                  "kernel": kname + (" (column-major C epilogue, B staged row-major)"
-                                     if args.bsr_layout == "col" and cm else ""),
+                  "kernel": kname + (" (analysed: column masks, column-major A)" if an else "") +
+                            (" (column-major C epilogue, B staged row-major)"
+                             if args.bsr_layout == "col" and cm else ""),
                   "kernel_ms": round(kms, 4),
                   "bytes_per_launch": comp_bytes,
                   "bytes_model": ("compulsory: A values + BSR indices once per column tile, "
-                                  "each distinct B row once, C write once"),
+                                  "each distinct B row once, C write once" +
+                                  ("; analysed: masks + the nonzero columns' values" if an
+                                   else "")),
                   "bytes_model_upper": cm_bytes,
                   "bytes_model_upper_desc": (
                       "A values + indices per column tile, the B rows of every (block row, "
@@ -824,6 +859,7 @@ def run_bsr(args, W, world, rank, dev, dist):
                   "full_panel_model_bytes_per_launch": kbytes,
                   "full_panel_model_GBps": round(kbytes / t / 1e9, 1)},
         csr_same_matrix_ms=round(csr_ms, 4), csr2bsr_host_seconds=round(t_conv, 2),
+        analysis_ms=round(analysis_ms, 4) if an else None,
         gen_seconds=round(t_gen, 2), reorder=reorder)
     tr = rec["roofline"]["traffic"]
     if tr:

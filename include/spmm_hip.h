@@ -181,6 +181,31 @@ spmm_status_t spmm_bsrmm_ex_f32(spmm_handle_t handle, spmm_direction_t dir, int 
                                 spmm_order_t orderB, float beta, float* C, int ldc,
                                 spmm_order_t orderC);
 
+/* Analysis for the bs = 32 column stream (an extension: rocsparse_bsrmm.h:102-256
+ * has no analysis step; this follows rocSPARSE's bsrmv analysis / cuSPARSE's
+ * SpMM preprocess pattern). Once per matrix, on the handle's stream:
+ *   masks[k]  bit c set iff column c of block k holds a value other than +-0
+ *             (NaN and inf count), nnzb words;
+ *   valCol    dir = ROW: a column-major copy of the blocks, nnzb * 1024 floats
+ *             (may be null for dir = COLUMN, whose blocks already are).
+ * Caller-owned buffers. INVALID_VALUE for a bad dir, nnzb < 0 or a null
+ * pointer that is needed. */
+spmm_status_t spmm_bsr32_analysis_f32(spmm_handle_t handle, spmm_direction_t dir, int nnzb,
+                                      const float* bsrVal, unsigned* masks, float* valCol);
+
+/* C(mb*32 x n) = alpha * A * B(kb*32 x n) + beta * C on the analysis: valCol are
+ * the column-major blocks (valCol from spmm_bsr32_analysis_f32, or bsrVal of a
+ * COLUMN-direction matrix) and masks their column masks. A column of a block
+ * with no value other than +-0 is skipped, as the shipped column streams do; the
+ * kernel reads only the nonzero columns' values. Same checks and quick returns
+ * as spmm_bsrmm_ex_f32 with blockDim 32; layouts the analysed kernel cannot
+ * take run the COLUMN-direction kernels on valCol. */
+spmm_status_t spmm_bsrmm_analysed_f32(spmm_handle_t handle, int mb, int kb, int n, int nnzb,
+                                      float alpha, const int* bsrRowPtr, const int* bsrColInd,
+                                      const float* valCol, const unsigned* masks, const float* B,
+                                      int ldb, spmm_order_t orderB, float beta, float* C,
+                                      int ldc, spmm_order_t orderC);
+
 /* fp16 A and B (IEEE binary16 bit patterns), fp32 accumulate and fp32 C.
  * bs = 16 runs on v_mfma_f32_16x16x32_f16 with two blocks per instruction. */
 spmm_status_t spmm_bsrmm_ex_f16(spmm_handle_t handle, spmm_direction_t dir, int mb, int kb,

@@ -829,6 +829,54 @@ __global__ __launch_bounds__(256) void seg_fixup_kernel(int n, const int4* __res
   }
 }
 
+// Analysis for the analysed bs = 32 column stream (spmm_bsr32_analysis_f32): per
+// block the mask of its nonzero columns (bit c: a value other than +-0 in column
+// c, NaN and inf included, as the column streams' own masks) and, for ROW blocks,
+// a column-major copy of the values. One wave per block, four per workgroup.
+//  * ROW: lane (j, h) loads row j, columns 16h .. 16h + 15 (four 16-B loads); a
+//    ballot per column pair (i, 16 + i) gives both bits; the copy writes column
+//    16h + i of every row as one 128-B line per half-wave.
+//  * COLUMN: lane L loads floats 16L .. 16L + 15 = column L / 2, half L & 1; one
+//    ballot, lanes 2c and 2c + 1 folded into bit c.
+__global__ __launch_bounds__(256) void bsr32_analysis_kernel(int nnzb, int rowdir,
+                                                             const float* __restrict__ val,
+                                                             unsigned* __restrict__ masks,
+                                                             float* __restrict__ val_col) {
+  const int lane = threadIdx.x & 63;
+  const long long k = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= nnzb) return;
+  const float* blk = val + (size_t)k * 1024;
+  unsigned msk = 0;
+  if (rowdir) {
+    const int j = lane & 31, h = lane >> 5;
+    f32x4 x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = *reinterpret_cast<const f32x4*>(blk + j * 32 + 16 * h + 4 * q);
+    float* dst = val_col + (size_t)k * 1024;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = x[i >> 2][i & 3];
+      const unsigned long long b = __builtin_amdgcn_ballot_w64((__float_as_uint(v) & 0x7fffffffu) != 0u);
+      msk |= ((unsigned)b != 0u ? 1u : 0u) << i;
+      msk |= ((unsigned)(b >> 32) != 0u ? 1u : 0u) << (16 + i);
+      dst[(16 * h + i) * 32 + j] = v;
+    }
+  } else {
+    f32x4 x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = *reinterpret_cast<const f32x4*>(blk + 16 * lane + 4 * q);
+    unsigned t = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t |= __float_as_uint(x[q][e]) & 0x7fffffffu;
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(t != 0u);
+#pragma unroll
+    for (int c = 0; c < 32; ++c) msk |= (((b >> (2 * c)) & 3ull) != 0ull ? 1u : 0u) << c;
+  }
+  if (lane == 0) masks[k] = msk;
+}
+
 // Longest-first block-row order for the one-wave-per-block-row kernels (the
 // column streams). Their waves run as long as their block rows; when the grid
 // is only a few waves per slot deep, dispatching in block-row order leaves a
@@ -908,17 +956,27 @@ __global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int
 // never again, so its lines should not displace the B rows that neighbouring
 // block rows share in the XCD's L2 (products stand-in 3.15 -> 3.07 ms, reddit
 // 2.04 -> 1.93, profiles/r03_var_sweep.jsonl).
-template <bool CROW, int XM, int P, int NA, bool O32 = false, bool PK = false, bool ANT = false>
+// MSK (the analysed form, spmm_bsrmm_analysed_f32): the blocks are column-major
+// (COLUMN direction, or the column-major copy spmm_bsr32_analysis_f32 made of ROW
+// blocks) and masks[k] holds block k's nonzero columns, computed once per matrix.
+// No A ring and no mask reads: per item the wave loads only its nonzero columns'
+// A values, one 128-B line per column (lane j: row j), straight into registers
+// beside the B rows, and the masks come 64 blocks at a time like the block
+// columns. A's bytes fall from the whole block to the nonzero columns (products
+// stand-in: 7.5 of 32 columns), and the kernel needs no LDS (row-major C).
+template <bool CROW, int XM, int P, int NA, bool O32 = false, bool PK = false, bool ANT = false,
+          bool MSK = false>
 __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc, const int* __restrict__ order,
-    const int4* __restrict__ segs = nullptr, float* __restrict__ part = nullptr) {
+    const int4* __restrict__ segs = nullptr, float* __restrict__ part = nullptr,
+    const unsigned* __restrict__ masks = nullptr) {
   static_assert(NA >= 2 && NA <= 4 && P >= 2 && P <= 16, "ring depths");
   constexpr int DA = NA - 1;  // A blocks in flight ahead of the producer's block
   // (column-major C reuses the LDS for a 128 x 36-float tile)
   __shared__ __attribute__((aligned(16)))
-  float smem[CROW || NA * 1024 >= 128 * 36 ? NA * 1024 : 128 * 36];
+  float smem[MSK && CROW ? 4 : (CROW || NA * 1024 >= 128 * 36 ? NA * 1024 : 128 * 36)];
   const int lane = threadIdx.x;
   const int j = lane & 31, h = lane >> 5;
   // a segment of a block row (seg_build_kernel; row-major C only) or a whole row
@@ -999,20 +1057,28 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   bool more = true;
   const char* bblk = reinterpret_cast<const char*>(B);
   int ccur = 0, cnext = 0, cstamp = 0;  // block-column chunks (cnext: in flight)
+  unsigned mcur = 0, mnext = 0;         // MSK: the same chunks of the column masks
+  const float* ablk = val;              // MSK: the current block's column-major values
   auto load_cols = [&](int kstart) {
     const unsigned off = 4u * (unsigned)min(kstart + lane, k1 - 1);
     asm volatile("global_load_dword %0, %1, %2" : "=&v"(cnext) : "v"(off), "s"(colind) : "memory");
+    if constexpr (MSK) {
+      asm volatile("global_load_dword %0, %1, %2" : "=&v"(mnext) : "v"(off), "s"(masks) : "memory");
+      ++nis;
+    }
     cstamp = ++nis;
   };
   if (k0 < k1) load_cols(k0);
+  if constexpr (!MSK) {
 #pragma unroll
-  for (int d = 0; d < DA; ++d) {
-    if (k0 + d < k1) {
-      issue_a(k0 + d, d);
-      nis += 4;
-      ast[d] = nis;
-    } else {
-      ast[d] = -64;
+    for (int d = 0; d < DA; ++d) {
+      if (k0 + d < k1) {
+        issue_a(k0 + d, d);
+        nis += 4;
+        ast[d] = nis;
+      } else {
+        ast[d] = -64;
+      }
     }
   }
   int kind[P], stamp[P];
@@ -1032,14 +1098,25 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     aslot = aslot + 1 == NA ? 0 : aslot + 1;
     const int kr = k - k0;
     if ((kr & 63) == 0) {  // next block-column chunk
-      asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
-                   : "=&v"(ccur)
-                   : "s"(nis - cstamp), "v"(cnext)
-                   : "scc", "memory");
+      if constexpr (MSK)
+        asm volatile(SPMM_VM_LADDER("%2") "v_mov_b32 %0, %3\n\tv_mov_b32 %1, %4"
+                     : "=&v"(ccur), "=&v"(mcur)
+                     : "s"(nis - cstamp), "v"(cnext), "v"(mnext)
+                     : "scc", "memory");
+      else
+        asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
+                     : "=&v"(ccur)
+                     : "s"(nis - cstamp), "v"(cnext)
+                     : "scc", "memory");
       if (k + 64 < k1) load_cols(k + 64);
     }
     const int bc = __builtin_amdgcn_readlane(ccur, kr & 63);
     bblk = reinterpret_cast<const char*>(B) + (size_t)bc * 32 * ldb4;
+    if constexpr (MSK) {
+      m = (unsigned)__builtin_amdgcn_readlane((int)mcur, kr & 63);
+      ablk = val + (size_t)k * 1024;
+      return;
+    }
     wait_vm_older(nis - ast[0]);  // A(k) landed
 #pragma unroll
     for (int d = 0; d + 1 < DA; ++d) ast[d] = ast[d + 1];
@@ -1051,6 +1128,14 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     } else {
       ast[DA - 1] = -64;
     }
+  };
+  // MSK: this lane's A value of column c of the current block (row j) into r (in flight)
+  auto load_acol = [&](float& r, int c) {
+    asm volatile("global_load_dword %0, %1, %2"
+                 : "=&v"(r)
+                 : "v"(4u * (unsigned)(32 * c + j)), "s"(ablk)
+                 : "memory");
+    ++nis;
   };
   // LDS address of this lane's A value of column c of the current block
   auto acol = [&](int c) -> unsigned {
@@ -1115,14 +1200,20 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
           m &= m - 1u;
           if constexpr (PK) {
             // first column: A read and B load now, from this block
-            asm volatile("ds_read_b32 %0, %1" : "=&v"(ra0[s]) : "v"(acol(c0)) : "memory");
+            if constexpr (MSK)
+              load_acol(ra0[s], c0);
+            else
+              asm volatile("ds_read_b32 %0, %1" : "=&v"(ra0[s]) : "v"(acol(c0)) : "memory");
             load_row(rb0[s], c0);
             kind[s] = 1;
             while (m == 0u && k + 1 < k1) advance();  // pair with the next block's first column
             if (m != 0u) {
               const int c1 = __builtin_ctz(m);
               m &= m - 1u;
-              asm volatile("ds_read_b32 %0, %1" : "=&v"(ra1[s]) : "v"(acol(c1)) : "memory");
+              if constexpr (MSK)
+                load_acol(ra1[s], c1);
+              else
+                asm volatile("ds_read_b32 %0, %1" : "=&v"(ra1[s]) : "v"(acol(c1)) : "memory");
               load_row(rb1[s], c1);
               kind[s] = 2;
             }
@@ -1132,10 +1223,15 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
               c1 = __builtin_ctz(m);
               m &= m - 1u;
             }
-            asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3"
-                         : "=&v"(ra0[s]), "=&v"(ra1[s])
-                         : "v"(acol(c0)), "v"(acol(c1))
-                         : "memory");
+            if constexpr (MSK) {
+              load_acol(ra0[s], c0);
+              load_acol(ra1[s], c1);
+            } else {
+              asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3"
+                           : "=&v"(ra0[s]), "=&v"(ra1[s])
+                           : "v"(acol(c0)), "v"(acol(c1))
+                           : "memory");
+            }
             load_row(rb0[s], c0);
             kind[s] = 1;
             if (c1 != c0) {
@@ -1152,7 +1248,13 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   }
   // nothing is in flight after the last round; the full wait makes that
   // visible to the register check (tests/test_isa_waits.py)
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : "v"(cnext) : "memory");
+  if constexpr (MSK)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)"
+                 : "+a"(u0), "+a"(u1)
+                 : "v"(cnext), "v"(mnext)
+                 : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : "v"(cnext) : "memory");
 
   if constexpr (CROW) {
     const int col = jt + 4 * j;
@@ -2325,11 +2427,19 @@ bool aligned(const void* p, int bytes) { return reinterpret_cast<uintptr_t>(p) %
 
 namespace spmm {
 
+spmm_status_t launch_bsr32_analysis(spmm_context* ctx, spmm_direction_t dir, int nnzb,
+                                    const float* val, unsigned* masks, float* val_col) {
+  if (nnzb == 0) return SPMM_STATUS_SUCCESS;
+  hipLaunchKernelGGL(bsr32_analysis_kernel, dim3((nnzb + 3) / 4), dim3(256), 0, ctx->stream, nnzb,
+                     dir == SPMM_DIRECTION_ROW ? 1 : 0, val, masks, val_col);
+  return from_hip(hipGetLastError());
+}
+
 spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, int kb, int n,
                                int nnzb, int bs, float alpha, const int* rowptr,
                                const int* colind, const float* val, const float* B, int ldb,
                                spmm_order_t orderB, float beta, float* C, int ldc,
-                               spmm_order_t orderC, bool dense_blocks) {
+                               spmm_order_t orderC, bool dense_blocks, const unsigned* masks) {
   (void)kb;
   if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   const bool rowd = dir == SPMM_DIRECTION_ROW;
@@ -2341,8 +2451,10 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   // the column stream stores row-major C as 16-B row pieces (and its segment fix-up too):
   // C and ldc must keep them aligned, else the fragment kernel's scalar stores serve
   const bool c16 = !crow || (aligned(C, 16) && ldc % 4 == 0);
-  if (bs == 32 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 && aligned(val, 16) &&
-      aligned(B, 16) && (dense_blocks || c16)) {
+  // the analysed column stream: COLUMN blocks with their column masks
+  const bool msk = masks && bs == 32 && !rowd && !dense_blocks && c16;
+  if (bs == 32 && (rowd || msk) && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 &&
+      aligned(val, 16) && aligned(B, 16) && (dense_blocks || c16)) {
     const dim3 grid(mb, (n + 127) / 128);
     const bool narrow = (size_t)ldb * 128 < (1u << 31);  // 32-row panels addressable in 31 bits
     int lv = dense_blocks ? kBsr32Dense : kBsr32Cs;
@@ -2389,13 +2501,15 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     if (crow)                                                                                    \
       hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, 6, 3, __VA_ARGS__>), g2, dim3(64), 0,   \
                          ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
-                         ord, sg, pt);                                                           \
+                         ord, sg, pt, masks);                                                    \
     else                                                                                         \
       hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, 6, 3, __VA_ARGS__>), g2, dim3(64), 0,  \
                          ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
-                         ord, nullptr, nullptr);                                                 \
+                         ord, nullptr, nullptr, masks);                                          \
   } while (0)
-      if (lv == kBsr32Cs) CS2_LAUNCH(true, true, true);
+      if (msk && narrow) CS2_LAUNCH(true, true, true, true);
+      else if (msk) CS2_LAUNCH(false, true, true, true);
+      else if (lv == kBsr32Cs) CS2_LAUNCH(true, true, true);
       else if (lv == kBsr32CsNoNt) CS2_LAUNCH(true, true, false);
       else CS2_LAUNCH(false, true, true);  // kBsr32CsWideLdb
 #undef CS2_LAUNCH

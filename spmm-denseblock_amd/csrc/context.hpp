@@ -91,7 +91,11 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                int nnzb, int bs, float alpha, const int* rowptr,
                                const int* colind, const float* val, const float* B, int ldb,
                                spmm_order_t orderB, float beta, float* C, int ldc,
-                               spmm_order_t orderC, bool dense_blocks = false);
+                               spmm_order_t orderC, bool dense_blocks = false,
+                               const unsigned* masks = nullptr);
+// spmm_bsr32_analysis_f32: column masks (+ a column-major copy of ROW blocks)
+spmm_status_t launch_bsr32_analysis(spmm_context* ctx, spmm_direction_t dir, int nnzb,
+                                    const float* val, unsigned* masks, float* val_col);
 
 // Fused hybrid (bs = 32, row-major B and C): one launch, BSR MFMA part plus the
 // CSR remainder per block row (bsr_kernels.hip). C holds ceil(m/32)*32 rows.

@@ -166,6 +166,56 @@ def bsrmm(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torc
     return C
 
 
+def bsr32_analysis(val: torch.Tensor, *, nnzb: int, direction: int = DIRECTION_ROW,
+                   masks: torch.Tensor | None = None, val_col: torch.Tensor | None = None,
+                   handle: Handle | None = None):
+    """Column masks of the bs = 32 blocks (int32 words, bit c = column c holds a
+    value other than +-0) and, for ROW blocks, their column-major copy
+    (spmm_bsr32_analysis_f32). Returns (masks, val_col); val_col is val itself
+    for COLUMN blocks."""
+    _need(val, torch.float32, "val")
+    if val.numel() < nnzb * 1024:
+        raise ValueError(f"val holds {val.numel()} floats, {nnzb} blocks need {nnzb * 1024}")
+    if masks is None:
+        masks = torch.empty(max(nnzb, 1), dtype=torch.int32, device=val.device)
+    if direction == DIRECTION_ROW and val_col is None:
+        val_col = torch.empty(max(nnzb, 1) * 1024, dtype=torch.float32, device=val.device)
+    _need(masks, torch.int32, "masks")
+    if masks.numel() < nnzb:
+        raise ValueError("masks holds fewer than nnzb words")
+    if direction == DIRECTION_ROW:
+        _need(val_col, torch.float32, "val_col")
+        if val_col.numel() < nnzb * 1024:
+            raise ValueError("val_col holds fewer than nnzb * 1024 floats")
+    h = handle or default_handle()
+    check(lib().spmm_bsr32_analysis_f32(h.raw, direction, nnzb, _ptr(val), _ptr(masks),
+                                        _ptr(val_col) if direction == DIRECTION_ROW else None),
+          "spmm_bsr32_analysis_f32")
+    return masks, (val_col if direction == DIRECTION_ROW else val)
+
+
+def bsrmm_analysed(rowptr: torch.Tensor, colind: torch.Tensor, val_col: torch.Tensor,
+                   masks: torch.Tensor, B: torch.Tensor, *, mb: int, kb: int, n: int, ldb: int,
+                   order_b: int = ORDER_ROW, C: torch.Tensor, ldc: int,
+                   order_c: int = ORDER_ROW, alpha: float = 1.0, beta: float = 0.0,
+                   handle: Handle | None = None) -> torch.Tensor:
+    """C(mb*32 x n) = alpha * A * B + beta * C on bsr32_analysis's output
+    (spmm_bsrmm_analysed_f32)."""
+    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                      (val_col, torch.float32, "val_col"), (masks, torch.int32, "masks"),
+                      (B, torch.float32, "B"), (C, torch.float32, "C")):
+        _need(t, dt, nm)
+    nnzb = colind.numel()
+    if val_col.numel() < nnzb * 1024 or masks.numel() < nnzb:
+        raise ValueError("val_col / masks are shorter than the matrix's nnzb blocks")
+    h = handle or default_handle()
+    check(lib().spmm_bsrmm_analysed_f32(h.raw, mb, kb, n, nnzb, alpha, _ptr(rowptr),
+                                        _ptr(colind), _ptr(val_col), _ptr(masks), _ptr(B), ldb,
+                                        order_b, beta, _ptr(C), ldc, order_c),
+          "spmm_bsrmm_analysed_f32")
+    return C
+
+
 def bsrmm_f16(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torch.Tensor, *,
               mb: int, kb: int, n: int, bs: int, ldb: int, order_b: int = ORDER_ROW,
               C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW, alpha: float = 1.0,

@@ -628,3 +628,122 @@ def test_column_sparse_blocks(oracle, device, bs, dtype, n, layout):
     got = run(Bbad)
     assert np.isfinite(got).all(), "explicit zeros must not turn inf / NaN of B into NaN"
     assert_normwise(got, ref, absd, tol, what + ", non-finite B")
+
+
+def _masks_np(v, bs=32):
+    """Column masks of row-major blocks as the analysis defines them (bit c: a
+    value other than +-0 in column c; NaN and inf count)."""
+    vb = v.reshape(-1, bs, bs)
+    nz = (vb.view(np.uint32) & 0x7fffffff) != 0
+    cols = nz.any(axis=1)  # [nnzb, bs]
+    return (cols.astype(np.uint64) << np.arange(bs, dtype=np.uint64)).sum(axis=1).astype(np.uint32)
+
+
+@pytest.mark.parametrize("direction", [0, 1])
+def test_bsr32_analysis(device, direction):
+    """spmm_bsr32_analysis_f32: the column masks (explicit zero blocks, -0.0,
+    NaN and inf entries included) and, for ROW blocks, the column-major copy."""
+    rng = np.random.default_rng(5 + direction)
+    rp, ci, v = _column_sparse_bsr(rng, 17, 40, 32, 0.4)
+    vb = v.reshape(-1, 32, 32).copy()
+    nnzb = vb.shape[0]
+    vb[1, 3, 7] = -0.0
+    vb[2, 0, 31] = np.nan
+    vb[4, 31, 0] = np.inf
+    v = vb.reshape(-1)
+    src = v if direction == 0 else np.ascontiguousarray(vb.transpose(0, 2, 1)).reshape(-1)
+    (dv,) = _dev(src)
+    masks, vcol = _ops().bsr32_analysis(dv, nnzb=nnzb, direction=direction)
+    torch.cuda.synchronize()
+    want = _masks_np(v)
+    got = masks.cpu().numpy()[:nnzb].view(np.uint32)
+    assert np.array_equal(got, want)
+    colmajor = np.ascontiguousarray(vb.transpose(0, 2, 1)).reshape(-1)
+    assert np.array_equal(vcol.cpu().numpy()[:nnzb * 1024].view(np.uint32),
+                          colmajor.view(np.uint32))
+
+
+@pytest.mark.parametrize("orders", [(0, 0), (1, 1), (0, 1), (1, 0)])
+@pytest.mark.parametrize("n", [96, 136, 130])
+@pytest.mark.parametrize("direction", [0, 1])
+def test_bsrmm_analysed(oracle, device, orders, n, direction):
+    """spmm_bsrmm_analysed_f32 against the fp64 oracle: column-sparse blocks,
+    an empty block row and one of 300 blocks (several 64-block chunks, and
+    segments on this shallow grid), alpha / beta, every B / C order; n = 130
+    (n % 4 != 0) takes the COLUMN-direction fallback kernels on the same
+    analysis. Then inf / NaN in B rows that only empty columns meet: C stays
+    finite, as with the other column streams."""
+    ob, oc = orders
+    rng = np.random.default_rng(n + 10 * ob + 100 * oc + direction)
+    mb, kb, bs = 23, 320, 32
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.1)
+    # block row 5: 300 blocks
+    rows = [ci[rp[i]:rp[i + 1]] for i in range(mb)]
+    vals = [v.reshape(-1, bs * bs)[rp[i]:rp[i + 1]] for i in range(mb)]
+    rows[5] = np.sort(rng.choice(kb, 300, replace=False)).astype(np.int32)
+    _, _, extra = _column_sparse_bsr(rng, 1, 300, bs, 1.0)
+    vals[5] = extra.reshape(-1, bs * bs)[:300]
+    rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    v = np.concatenate(vals).reshape(-1).astype(np.float32)
+    nnzb = ci.size
+    K, m = kb * bs, mb * bs
+    Bd = rng.uniform(-1, 1, (K, n)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    alpha, beta = 0.5, -1.5
+    ops = _ops()
+    src = v if direction == 0 else np.ascontiguousarray(
+        v.reshape(-1, bs, bs).transpose(0, 2, 1)).reshape(-1)
+    drp, dci, dv = _dev(rp, ci, src)
+    masks, vcol = ops.bsr32_analysis(dv, nnzb=nnzb, direction=direction)
+
+    def run(Bh):
+        B = Bh if ob == 0 else np.ascontiguousarray(Bh.T)
+        Cm = C0 if oc == 0 else np.ascontiguousarray(C0.T)
+        dB, dC = _dev(B.reshape(-1), Cm.reshape(-1))
+        ops.bsrmm_analysed(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n,
+                           ldb=n if ob == 0 else K, order_b=ob, C=dC, ldc=n if oc == 0 else m,
+                           order_c=oc, alpha=alpha, beta=beta)
+        torch.cuda.synchronize()
+        got = dC.cpu().numpy().reshape((m, n) if oc == 0 else (n, m))
+        return got if oc == 0 else got.T
+
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, Bd, n, 0)
+    ref = alpha * ref + beta * C0.astype(np.float64)
+    absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+    what = f"analysed n={n} orders={orders} dir={direction}"
+    assert_normwise(run(Bd), ref, absd, TOL_F32, what)
+    if n % 4:
+        return  # the fallback kernels compute the dense block product
+    vb = v.reshape(-1, bs, bs)
+    used = np.zeros(K, bool)
+    for br in range(mb):
+        for k in range(rp[br], rp[br + 1]):
+            used[ci[k] * bs + np.nonzero(np.any(vb[k] != 0, axis=0))[0]] = True
+    unused = np.nonzero(~used)[0]
+    assert unused.size > 0
+    Bbad = Bd.copy()
+    Bbad[unused[0::2]] = np.inf
+    Bbad[unused[1::2]] = np.nan
+    got = run(Bbad)
+    assert np.isfinite(got).all()
+    assert_normwise(got, ref, absd, TOL_F32, what + ", non-finite B")
+
+
+def test_bsrmm_analysed_matches_column_stream(device):
+    """The analysed stream is the shipped bs 32 column stream with A read from
+    the column-major copy: the same items in the same order, so the same
+    result bit for bit (row-major B and C)."""
+    rng = np.random.default_rng(77)
+    mb, kb, bs, n = 40, 200, 32, 256
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.15)
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B.reshape(-1))
+    ops = _ops()
+    C1 = torch.empty((mb * bs, n), device=device)
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=C1, ldc=n)
+    masks, vcol = ops.bsr32_analysis(dv, nnzb=ci.size)
+    C2 = torch.empty((mb * bs, n), device=device)
+    ops.bsrmm_analysed(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n, ldb=n, C=C2, ldc=n)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2)

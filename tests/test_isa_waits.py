@@ -20,6 +20,7 @@ caught it about one run in four. These tests read the stream instead:
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
 
@@ -138,8 +139,13 @@ def test_column_stream_counts_only_its_copies(bsr_asm, kernel):
         body = funcs[k]
         assert not any(line.strip().startswith("scratch_") for _, line in body), f"{k}: spills"
         blocks = iv.build_cfg(body)
+        # the analysed bs 32 form (MSK, 8th template argument) copies nothing into LDS:
+        # its loops are the ones with inline-asm loads
+        msk = re.search(r"cs2_kernelI(?:L[bi]\d+E){7}Lb1E", k) is not None
         loops = {b.header for b in blocks
-                 if b.in_loop and any(iv.classify(mn, ops) == "dma" for _, mn, ops in b.insts)}
+                 if b.in_loop and any(iv.classify(mn, ops) == "dma" or
+                                      (msk and iv.classify(mn, ops) == "load" and no in b.asm_lines)
+                                      for no, mn, ops in b.insts)}
         assert loops, k
         n_dma = 0
         for b in blocks:
@@ -152,7 +158,7 @@ def test_column_stream_counts_only_its_copies(bsr_asm, kernel):
                 n_dma += c == "dma"
                 if mn == "s_waitcnt" and "vmcnt" in ops:
                     assert no in b.asm_lines, f"{k} line {no}: compiler-placed {mn} {ops}"
-        assert n_dma >= 4, (k, n_dma)
+        assert msk or n_dma >= 4, (k, n_dma)
 
 
 def _vregs(ops: str) -> set:
