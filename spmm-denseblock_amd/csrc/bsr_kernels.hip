@@ -2507,8 +2507,22 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                          ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
                          ord, nullptr, nullptr, masks);                                          \
   } while (0)
-      if (msk && narrow) CS2_LAUNCH(true, true, true, true);
-      else if (msk) CS2_LAUNCH(false, true, true, true);
+#define MSK_LAUNCH(O32_)                                                                         \
+  do {                                                                                           \
+    if (crow)                                                                                    \
+      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, 6, 3, O32_, true, true, true>), g2,     \
+                         dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha,    \
+                         beta, C, ldc, ord, sg, pt, masks);                                      \
+    else                                                                                         \
+      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, 6, 3, O32_, true, true, true>), g2,    \
+                         dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha,    \
+                         beta, C, ldc, ord, nullptr, nullptr, masks);                            \
+  } while (0)
+      // (4, 8 or 10 items in flight: 2.11-2.15 / 2.11-2.12 / 2.43 ms against 2.11 at 6 on
+      // the products stand-in, profiles/r03_analysed_sweep.txt)
+      if (msk && narrow) MSK_LAUNCH(true);
+      else if (msk) MSK_LAUNCH(false);
+#undef MSK_LAUNCH
       else if (lv == kBsr32Cs) CS2_LAUNCH(true, true, true);
       else if (lv == kBsr32CsNoNt) CS2_LAUNCH(true, true, false);
       else CS2_LAUNCH(false, true, true);  // kBsr32CsWideLdb

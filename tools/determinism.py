@@ -55,6 +55,13 @@ def main():
                 ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K)
                 return C
             bad += check("bsr32 fp32 K=128 (column stream, CS2)", run, reps)
+            masks, vcol = ops.bsr32_analysis(bval, nnzb=bci.numel())
+
+            def run_an():
+                ops.bsrmm_analysed(brp, bci, vcol, masks, B, mb=mb, kb=mb, n=K, ldb=K, C=C, ldc=K)
+                return C
+            bad += check("bsr32 fp32 K=128 (analysed column stream)", run_an, reps)
+            del masks, vcol
         else:
             bv16, B16 = bval.half(), B.half()
             del bval, B
