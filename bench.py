@@ -76,6 +76,12 @@ WORKLOADS = {
     # upper bound a perfect reorderer reaches.
     "reddit_rcm_bsr32": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
                              p_in=0.99, bs=32, K=128, dtype="fp32", reorder="rcm"),
+    "reddit_rcm_bsr32_an": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
+                                p_in=0.99, bs=32, K=128, dtype="fp32", reorder="rcm",
+                                analysed=True),
+    "products_rcm_bsr32_an": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                                  p_in=0.97, bs=32, K=128, dtype="fp32", reorder="rcm",
+                                  analysed=True),
     "products_rcm_bsr16_f16": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                    p_in=0.97, bs=16, K=512, dtype="fp16", reorder="rcm"),
     "products_rcm_bsr32": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
