@@ -747,3 +747,30 @@ def test_bsrmm_analysed_matches_column_stream(device):
     ops.bsrmm_analysed(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n, ldb=n, C=C2, ldc=n)
     torch.cuda.synchronize()
     assert torch.equal(C1, C2)
+
+
+def test_bsr32_analysis_argument_checks(device):
+    """Status codes of the analysis entries (the reference's INVALID_VALUE /
+    quick-return conventions, rocsparse_bsrmm.h:110-176)."""
+    from spmm_hip._lib import lib
+    h = _ops().default_handle()
+    v = torch.zeros(2048, device=device)
+    m = torch.zeros(2, dtype=torch.int32, device=device)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    L = lib()
+    assert L.spmm_bsr32_analysis_f32(h.raw, 5, 2, P(v), P(m), P(v)) == 3      # bad dir
+    assert L.spmm_bsr32_analysis_f32(h.raw, 0, -1, P(v), P(m), P(v)) == 3     # nnzb < 0
+    assert L.spmm_bsr32_analysis_f32(h.raw, 0, 2, P(v), P(m), None) == 3      # ROW needs valCol
+    assert L.spmm_bsr32_analysis_f32(h.raw, 1, 2, P(v), P(m), None) == 0      # COLUMN does not
+    assert L.spmm_bsr32_analysis_f32(h.raw, 0, 0, None, None, None) == 0      # quick return
+    rp = torch.tensor([0, 2], dtype=torch.int32, device=device)
+    ci = torch.tensor([0, 1], dtype=torch.int32, device=device)
+    B = torch.zeros(64 * 8, device=device)
+    C = torch.full((32 * 8,), 3.0, device=device)
+    args = (h.raw, 1, 2, 8, 2, 1.0, P(rp), P(ci), P(v))
+    assert L.spmm_bsrmm_analysed_f32(*args, None, P(B), 8, 0, 0.0, P(C), 8, 0) == 3  # masks
+    assert L.spmm_bsrmm_analysed_f32(*args, P(m), P(B), 4, 0, 0.0, P(C), 8, 0) == 3  # ldb < n
+    assert L.spmm_bsrmm_analysed_f32(h.raw, 0, 2, 8, 2, 1.0, None, None, None, None, None, 8, 0,
+                                     0.0, None, 8, 0) == 0                            # quick
+    torch.cuda.synchronize()
+    assert torch.all(C == 3.0)
