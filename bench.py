@@ -65,6 +65,8 @@ WORKLOADS = {
                               p_in=0.97, bs=32, K=128, dtype="fp32", analysed=True),
     "reddit_bsr32_an": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
                             p_in=0.99, bs=32, K=128, dtype="fp32", analysed=True),
+    "products_bsr16_f16_an": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                                  p_in=0.97, bs=16, K=512, dtype="fp16", analysed=True),
     "products_hybrid32": dict(kind="hybrid", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                               p_in=0.97, bs=32, K=128, density="auto"),
     # §8f rank 2 in the loop: scrambled ids -> in-repo RCM -> divide + hybrid
@@ -82,6 +84,9 @@ WORKLOADS = {
     "products_rcm_bsr32_an": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                   p_in=0.97, bs=32, K=128, dtype="fp32", reorder="rcm",
                                   analysed=True),
+    "products_rcm_bsr16_f16_an": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                                      p_in=0.97, bs=16, K=512, dtype="fp16", reorder="rcm",
+                                      analysed=True),
     "products_rcm_bsr16_f16": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                    p_in=0.97, bs=16, K=512, dtype="fp16", reorder="rcm"),
     "products_rcm_bsr32": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
@@ -723,15 +728,17 @@ def run_bsr(args, W, world, rank, dev, dist):
     an = bool(W.get("analysed"))
     analysis_ms = None
     if an:
-        if dt != "fp32" or bs != 32:
-            raise SystemExit("the analysed column stream is bs 32 fp32")
+        if (bs, dt) not in ((32, "fp32"), (16, "fp16")):
+            raise SystemExit("the analysed column streams are bs 32 fp32 and bs 16 fp16")
         masks = torch.empty(nnzb, dtype=torch.int32, device=dev)
-        vcol = torch.empty(nnzb * 1024, device=dev)
+        vcol = torch.empty(nnzb * bs * bs, dtype=tdt, device=dev)
+        analysis = ops.bsr32_analysis if bs == 32 else ops.bsr16_analysis
+        product = ops.bsrmm_analysed if bs == 32 else ops.bsrmm_analysed_f16
         ts = []
         for _ in range(3):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            ops.bsr32_analysis(d_bv, nnzb=nnzb, masks=masks, val_col=vcol, handle=h)
+            analysis(d_bv, nnzb=nnzb, masks=masks, val_col=vcol, handle=h)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         analysis_ms = min(ts) * 1e3
@@ -739,8 +746,8 @@ def run_bsr(args, W, world, rank, dev, dist):
 
         def fn(rp_, ci_, _v, B_, *, mb, kb, n, bs, ldb, C, ldc, order_b=ops.ORDER_ROW,
                order_c=ops.ORDER_ROW, handle=None):
-            ops.bsrmm_analysed(rp_, ci_, vcol, masks, B_, mb=mb, kb=kb, n=n, ldb=ldb,
-                               order_b=order_b, C=C, ldc=ldc, order_c=order_c, handle=handle)
+            product(rp_, ci_, vcol, masks, B_, mb=mb, kb=kb, n=n, ldb=ldb, order_b=order_b, C=C,
+                    ldc=ldc, order_c=order_c, handle=handle)
         d_bv = None
     if args.bsr_layout == "col":
         # cusparseSbsrmm's transB = N layout (run_bsrmm.cu:70-71): B and C

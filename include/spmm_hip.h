@@ -206,6 +206,21 @@ spmm_status_t spmm_bsrmm_analysed_f32(spmm_handle_t handle, int mb, int kb, int 
                                       int ldb, spmm_order_t orderB, float beta, float* C,
                                       int ldc, spmm_order_t orderC);
 
+/* The same analysis for bs = 16 fp16 blocks: masks[k] bit c (c < 16), and for
+ * ROW blocks a column-major fp16 copy (nnzb * 256 halves). */
+spmm_status_t spmm_bsr16_analysis_f16(spmm_handle_t handle, spmm_direction_t dir, int nnzb,
+                                      const uint16_t* bsrVal, unsigned* masks, uint16_t* valCol);
+
+/* C(mb*16 x n, fp32) = alpha * A * B(kb*16 x n, fp16) + beta * C on the bs = 16
+ * analysis (fp16 A and B, fp32 accumulate), as spmm_bsrmm_ex_f16 with blockDim 16:
+ * n >= 128 runs the analysed column stream, other shapes the COLUMN-direction
+ * kernels on valCol. */
+spmm_status_t spmm_bsrmm_analysed_f16(spmm_handle_t handle, int mb, int kb, int n, int nnzb,
+                                      float alpha, const int* bsrRowPtr, const int* bsrColInd,
+                                      const uint16_t* valCol, const unsigned* masks,
+                                      const uint16_t* B, int ldb, spmm_order_t orderB,
+                                      float beta, float* C, int ldc, spmm_order_t orderC);
+
 /* fp16 A and B (IEEE binary16 bit patterns), fp32 accumulate and fp32 C.
  * bs = 16 runs on v_mfma_f32_16x16x32_f16 with two blocks per instruction. */
 spmm_status_t spmm_bsrmm_ex_f16(spmm_handle_t handle, spmm_direction_t dir, int mb, int kb,

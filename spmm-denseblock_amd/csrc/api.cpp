@@ -233,6 +233,41 @@ spmm_status_t spmm_bsrmm_analysed_f32(spmm_handle_t handle, int mb, int kb, int 
   return launch(B, ldb, orderB);
 }
 
+spmm_status_t spmm_bsr16_analysis_f16(spmm_handle_t handle, spmm_direction_t dir, int nnzb,
+                                      const uint16_t* bsrVal, unsigned* masks, uint16_t* valCol) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if ((dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) || nnzb < 0)
+    return SPMM_STATUS_INVALID_VALUE;
+  if (nnzb == 0) return SPMM_STATUS_SUCCESS;
+  if (!bsrVal || !masks || (dir == SPMM_DIRECTION_ROW && !valCol))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (reinterpret_cast<uintptr_t>(bsrVal) % 8 != 0) return SPMM_STATUS_INVALID_VALUE;
+  return launch_bsr16_analysis(handle, dir, nnzb, bsrVal, masks, valCol);
+}
+
+spmm_status_t spmm_bsrmm_analysed_f16(spmm_handle_t handle, int mb, int kb, int n, int nnzb,
+                                      float alpha, const int* bsrRowPtr, const int* bsrColInd,
+                                      const uint16_t* valCol, const unsigned* masks,
+                                      const uint16_t* B, int ldb, spmm_order_t orderB,
+                                      float beta, float* C, int ldc, spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  bool quick = false;
+  spmm_status_t st = bsr_checks(mb, kb, n, nnzb, 16, bsrRowPtr, bsrColInd, valCol, B, ldb,
+                                orderB, C, ldc, orderC, &quick);
+  if (st != SPMM_STATUS_SUCCESS || quick) return st;
+  if (!masks) return SPMM_STATUS_INVALID_VALUE;
+  const auto launch = [&](const uint16_t* Bx, int ldbx, spmm_order_t obx) {
+    return launch_bsrmm_f16(handle, SPMM_DIRECTION_COLUMN, mb, kb, n, nnzb, 16, alpha, bsrRowPtr,
+                            bsrColInd, valCol, Bx, ldbx, obx, beta, C, ldc, orderC, masks);
+  };
+  if (orderB == SPMM_ORDER_COL && n >= 128 && n % 8 == 0)
+    return bsrmm_staged<uint16_t>(handle, kb, n, 16, B, ldb, orderB,
+                                  [&](const uint16_t* Bx, int ldbx) {
+                                    return launch(Bx, ldbx, SPMM_ORDER_ROW);
+                                  });
+  return launch(B, ldb, orderB);
+}
+
 spmm_status_t spmm_bsrmm_ex_f16(spmm_handle_t handle, spmm_direction_t dir, int mb, int kb, int n,
                                 int nnzb, int blockDim, float alpha, const int* bsrRowPtr,
                                 const int* bsrColInd, const uint16_t* bsrVal, const uint16_t* B,

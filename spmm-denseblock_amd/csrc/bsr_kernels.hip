@@ -877,6 +877,40 @@ __global__ __launch_bounds__(256) void bsr32_analysis_kernel(int nnzb, int rowdi
   if (lane == 0) masks[k] = msk;
 }
 
+// The same analysis for bs = 16 fp16 (spmm_bsr16_analysis_f16): one wave per block
+// (512 B), lane L holding 4 halves. ROW: lane (r = L / 4, q = L % 4) holds row r,
+// columns 4q .. 4q + 3, and writes them to the column-major copy; COLUMN: lane L
+// holds column L / 4, rows 4 (L % 4) .. + 3.
+__global__ __launch_bounds__(256) void bsr16_analysis_kernel(int nnzb, int rowdir,
+                                                             const uint16_t* __restrict__ val,
+                                                             unsigned* __restrict__ masks,
+                                                             uint16_t* __restrict__ val_col) {
+  const int lane = threadIdx.x & 63;
+  const long long k = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= nnzb) return;
+  typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+  const u16x4 x = *reinterpret_cast<const u16x4*>(val + (size_t)k * 256 + 4 * lane);
+  unsigned msk = 0;
+  if (rowdir) {
+    const int r = lane >> 2, q = lane & 3;
+    uint16_t* dst = val_col + (size_t)k * 256;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const unsigned long long b = __builtin_amdgcn_ballot_w64((x[e] & 0x7fffu) != 0u);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+        msk |= ((b & (0x1111111111111111ull << qq)) != 0ull ? 1u : 0u) << (4 * qq + e);
+      dst[(4 * q + e) * 16 + r] = x[e];
+    }
+  } else {
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(
+        ((x[0] | x[1] | x[2] | x[3]) & 0x7fffu) != 0u);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) msk |= (((b >> (4 * c)) & 15ull) != 0ull ? 1u : 0u) << c;
+  }
+  if (lane == 0) masks[k] = msk;
+}
+
 // Longest-first block-row order for the one-wave-per-block-row kernels (the
 // column streams). Their waves run as long as their block rows; when the grid
 // is only a few waves per slot deep, dispatching in block-row order leaves a
@@ -1626,12 +1660,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // ANT: the A copies are non-temporal (nt): each tile's wave reads A from HBM anyway, and
 // its lines should not displace the B rows neighbouring block rows share in L2 (products
 // stand-in 4.03 -> 3.88 ms, profiles/r03_var_sweep.jsonl).
+// MSK (the analysed form, spmm_bsrmm_analysed_f16): the blocks are column-major and
+// masks[k] holds block k's nonzero columns (spmm_bsr16_analysis_f16, once per matrix).
+// The masks come 64 blocks at a time beside the block columns, so the walk reads no A
+// values to find them (no ds_read / ballot round trip), and the A values a block pushes
+// (lane (g, c): rows 4g .. 4g + 3 of column c, 8 contiguous bytes) come one pair of
+// blocks ahead into registers instead of an LDS ring: 2 KB less LDS per wave.
 template <bool CROW, int P, int NA, int DA, int CAP = 48, bool ANT = false, bool CST = false,
-          int COLS = 256>
+          int COLS = 256, bool MSK = false>
 __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
-    float beta, float* __restrict__ C, int ldc, const int* __restrict__ order) {
+    float beta, float* __restrict__ C, int ldc, const int* __restrict__ order,
+    const unsigned* __restrict__ masks = nullptr) {
   // COLS: output columns per wave (the launcher uses 256). 512 makes a stage row one whole
   // 1-KB B row and serves all 512 columns with one A copy and one walk per block row; 128
   // quarters the stage. Both pass the parity subset and lose on the products stand-in, K =
@@ -1654,7 +1695,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   // A-fragment buffer row: CAP entries + a dummy entry (index CAP) + pad; 136 / 104 B rows put
   // the four row groups' writes in different banks
   constexpr int kAbRow = CAP == 64 ? 136 : 104;
-  constexpr int kAbuf = NA * 512;   // offset of the A-fragment buffer
+  constexpr int kAbuf = MSK ? 0 : NA * 512;   // offset of the A-fragment buffer
   constexpr int kStg = kAbuf + 16 * kAbRow;  // offset of the item stages
   constexpr int kLds = kStg + P * kStage;
   static_assert(kLds >= COLS * 16 * 4, "column-major C tile fits");
@@ -1693,10 +1734,31 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   int nis = 0;  // vector-memory operations issued by this wave
   // block columns: 64 at a time in one VGPR (lane l: colind[k0 + 64c + l]), the next chunk in flight
   int ccur = 0, cnext = 0, cstamp = 0;
+  unsigned mcur = 0, mnext = 0;  // MSK: the masks of the same chunks
   auto load_cols = [&](int kstart) {
     const unsigned off = 4u * (unsigned)min(kstart + lane, k1 - 1);
     asm volatile("global_load_dword %0, %1, %2" : "=&v"(cnext) : "v"(off), "s"(colind) : "memory");
+    if constexpr (MSK) {
+      asm volatile("global_load_dword %0, %1, %2" : "=&v"(mnext) : "v"(off), "s"(masks) : "memory");
+      ++nis;
+    }
     cstamp = ++nis;
+  };
+  // MSK: the A values of the pair of blocks in flight (an*: asm-only registers) and of the
+  // pair being pushed (ac*); lane (g, c): rows 4g .. 4g + 3 of column c
+  typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
+  u32x2a an0 = {0u, 0u}, an1 = {0u, 0u}, ac0 = {0u, 0u}, ac1 = {0u, 0u};
+  int astamp = -64;
+  auto issue_a_reg = [&](int kr_) {  // blocks k0 + kr_, + 1 (clamped)
+    const unsigned o0 = 2u * (unsigned)(min(k0 + kr_, k1 - 1) * 256 + 16 * r16 + 4 * g);
+    const unsigned o1 = 2u * (unsigned)(min(k0 + kr_ + 1, k1 - 1) * 256 + 16 * r16 + 4 * g);
+    asm volatile("global_load_dwordx2 %0, %2, %4\n\t"
+                 "global_load_dwordx2 %1, %3, %4"
+                 : "=&v"(an0), "=&v"(an1)
+                 : "v"(o0), "v"(o1), "s"(val)
+                 : "memory");
+    nis += 2;
+    astamp = nis;
   };
   auto issue_a = [&](int kr) {  // blocks k0 + kr, k0 + kr + 1 (kr even) -> slots kr, kr + 1
     const int blk = min(k0 + kr + h, k1 - 1);
@@ -1707,13 +1769,17 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   };
   if (k0 < k1) load_cols(k0);
   int ast[DA / 2 + 1];  // count at each A pair in flight
+  if constexpr (MSK) {
+    if (k0 < k1) issue_a_reg(0);
+  } else {
 #pragma unroll
-  for (int q = 0; q <= DA / 2; ++q) {
-    if (k0 + 2 * q < k1) {
-      issue_a(2 * q);
-      ast[q] = nis;
-    } else {
-      ast[q] = -64;
+    for (int q = 0; q <= DA / 2; ++q) {
+      if (k0 + 2 * q < k1) {
+        issue_a(2 * q);
+        ast[q] = nis;
+      } else {
+        ast[q] = -64;
+      }
     }
   }
 
@@ -1725,15 +1791,43 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   // list. One LDS round trip reads both blocks' values, one more pushes both.
   auto advance2 = [&]() {
     if ((kr & 63) == 0) {  // next block-column chunk
-      asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
-                   : "=&v"(ccur)
-                   : "s"(nis - cstamp), "v"(cnext)
-                   : "scc", "memory");
+      if constexpr (MSK)
+        asm volatile(SPMM_VM_LADDER("%2") "v_mov_b32 %0, %3\n\tv_mov_b32 %1, %4"
+                     : "=&v"(ccur), "=&v"(mcur)
+                     : "s"(nis - cstamp), "v"(cnext), "v"(mnext)
+                     : "scc", "memory");
+      else
+        asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
+                     : "=&v"(ccur)
+                     : "s"(nis - cstamp), "v"(cnext)
+                     : "scc", "memory");
       if (k0 + kr + 64 < k1) load_cols(k0 + kr + 64);
     }
     const bool two = k0 + kr + 1 < k1;
     const int bc0 = __builtin_amdgcn_readlane(ccur, kr & 63);
     const int bc1 = __builtin_amdgcn_readlane(ccur, (kr + 1) & 63);
+    unsigned m[2];
+    unsigned x[8];
+    if constexpr (MSK) {
+      m[0] = (unsigned)__builtin_amdgcn_readlane((int)mcur, kr & 63) & 0xffffu;
+      m[1] = two ? (unsigned)__builtin_amdgcn_readlane((int)mcur, (kr + 1) & 63) & 0xffffu : 0u;
+      // pair kr / 2 landed: its A values become current, the next pair goes in flight
+      asm volatile(SPMM_VM_LADDER("%4") "v_mov_b64 %0, %2\n\tv_mov_b64 %1, %3"
+                   : "=&v"(ac0), "=&v"(ac1)
+                   : "v"(an0), "v"(an1), "s"(nis - astamp)
+                   : "scc", "memory");
+      if (k0 + kr + 2 < k1) issue_a_reg(kr + 2);
+      kr += 2;
+      if ((m[0] | m[1]) == 0u) return;
+      x[0] = ac0[0];
+      x[1] = ac0[0] >> 16;
+      x[2] = ac0[1];
+      x[3] = ac0[1] >> 16;
+      x[4] = ac1[0];
+      x[5] = ac1[0] >> 16;
+      x[6] = ac1[1];
+      x[7] = ac1[1] >> 16;
+    } else {
     wait_vm_older(nis - ast[0]);  // pair kr / 2 landed
 #pragma unroll
     for (int q = 0; q < DA / 2; ++q) ast[q] = ast[q + 1];
@@ -1743,7 +1837,6 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     } else {
       ast[DA / 2] = -64;
     }
-    unsigned x[8];
     asm volatile(
         "ds_read_u16 %0, %8\n\t"
         "ds_read_u16 %1, %8 offset:32\n\t"
@@ -1759,7 +1852,6 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
         : "v"(lds0 + 512u * (unsigned)(kr & (NA - 1)) + 128u * g + 2u * r16)
         : "memory");
     kr += 2;
-    unsigned m[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const unsigned long long b =
@@ -1768,6 +1860,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
       m[u] = (w | (w >> 16)) & 0xffffu;
     }
     if (!two) m[1] = 0u;  // the pair's second copy repeated the last block
+    }
     const int cnt0 = __builtin_popcount(m[0]), cnt1 = __builtin_popcount(m[1]);
     if (cnt0 + cnt1 == 0) return;
     // lane c < 16 with bit c set -> entry ebase + npend (+ cnt0) + popcount(mask below c);
@@ -1936,7 +2029,13 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   // nothing is in flight after the last round (a block-column chunk may be: its
   // register stays live until this full wait, which also makes the drain visible to the
   // register check, tests/test_isa_waits.py)
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : : "v"(cnext) : "memory");
+  if constexpr (MSK)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)"
+                 :
+                 : "v"(cnext), "v"(mnext), "v"(an0), "v"(an1)
+                 : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : : "v"(cnext) : "memory");
 
   if constexpr (!CROW) {
     // column-major C: the 16 x COLS tile through LDS, then 4 whole 64-B column
@@ -2435,6 +2534,14 @@ spmm_status_t launch_bsr32_analysis(spmm_context* ctx, spmm_direction_t dir, int
   return from_hip(hipGetLastError());
 }
 
+spmm_status_t launch_bsr16_analysis(spmm_context* ctx, spmm_direction_t dir, int nnzb,
+                                    const uint16_t* val, unsigned* masks, uint16_t* val_col) {
+  if (nnzb == 0) return SPMM_STATUS_SUCCESS;
+  hipLaunchKernelGGL(bsr16_analysis_kernel, dim3((nnzb + 3) / 4), dim3(256), 0, ctx->stream, nnzb,
+                     dir == SPMM_DIRECTION_ROW ? 1 : 0, val, masks, val_col);
+  return from_hip(hipGetLastError());
+}
+
 spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, int kb, int n,
                                int nnzb, int bs, float alpha, const int* rowptr,
                                const int* colind, const float* val, const float* B, int ldb,
@@ -2596,7 +2703,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                int nnzb, int bs, float alpha, const int* rowptr,
                                const int* colind, const uint16_t* val16, const uint16_t* B16,
                                int ldb, spmm_order_t orderB, float beta, float* C, int ldc,
-                               spmm_order_t orderC) {
+                               spmm_order_t orderC, const unsigned* masks) {
   (void)kb;
   if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   const _Float16* val = reinterpret_cast<const _Float16*>(val16);
@@ -2607,12 +2714,15 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   const bool vec_ok = aligned(val, 16) && (brow || (aligned(B, 16) && ldb % 8 == 0));
   const int slot = timing_begin(ctx);
   const int var = variant_override();
-  if (bs == 16 && rowd && brow && n >= 8 && n % 8 == 0 && ldb % 8 == 0 && aligned(val, 16) &&
-      aligned(B, 16)) {
+  // the analysed column stream: COLUMN blocks with their column masks, n >= 128
+  const bool msk = masks && bs == 16 && !rowd && n >= 128;
+  if (bs == 16 && (rowd || msk) && brow && n >= 8 && n % 8 == 0 && ldb % 8 == 0 &&
+      aligned(val, 16) && aligned(B, 16)) {
     int lv = n >= 128 ? kBsr16F16Cs : kBsr16F16Cm;
     if (var == kBsr16F16Cm ||
         (n >= 128 && (var == kBsr16F16Cs || var == kBsr16F16CsNoNt)))
       lv = var;
+    if (msk) lv = kBsr16F16Cs;  // COLUMN blocks: only the analysed stream reads them here
     if (lv == kBsr16F16Cm) {
       const dim3 grid(mb, (n + 255) / 256);
       if (crow)
@@ -2633,13 +2743,14 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
     if (crow)                                                                                    \
       hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, 2, 4, 0, 48, __VA_ARGS__>), gc, dim3(64), 0, \
                          ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
-                         ord);                                                                   \
+                         ord, masks);                                                            \
     else                                                                                         \
       hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, 2, 4, 0, 48, __VA_ARGS__>), gc, dim3(64),   \
                          0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C,     \
-                         ldc, ord);                                                              \
+                         ldc, ord, masks);                                                       \
   } while (0)
-      if (lv == kBsr16F16Cs) CS16_LAUNCH(true, true);
+      if (msk) CS16_LAUNCH(true, true, 256, true);
+      else if (lv == kBsr16F16Cs) CS16_LAUNCH(true, true);
       else CS16_LAUNCH(false, true);
 #undef CS16_LAUNCH
     }

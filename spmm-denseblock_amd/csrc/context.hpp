@@ -116,6 +116,8 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                int nnzb, int bs, float alpha, const int* rowptr,
                                const int* colind, const uint16_t* val, const uint16_t* B,
                                int ldb, spmm_order_t orderB, float beta, float* C, int ldc,
-                               spmm_order_t orderC);
+                               spmm_order_t orderC, const unsigned* masks = nullptr);
+spmm_status_t launch_bsr16_analysis(spmm_context* ctx, spmm_direction_t dir, int nnzb,
+                                    const uint16_t* val, unsigned* masks, uint16_t* val_col);
 
 }  // namespace spmm

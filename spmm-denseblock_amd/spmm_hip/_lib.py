@@ -85,6 +85,9 @@ _PROTOS = {
     "spmm_bsr32_analysis_f32": (c_int, [_P, c_int, c_int, _P, _P, _P]),
     "spmm_bsrmm_analysed_f32": (c_int, [_P, c_int, c_int, c_int, c_int, c_float, _P, _P, _P, _P,
                                         _P, c_int, c_int, c_float, _P, c_int, c_int]),
+    "spmm_bsr16_analysis_f16": (c_int, [_P, c_int, c_int, _P, _P, _P]),
+    "spmm_bsrmm_analysed_f16": (c_int, [_P, c_int, c_int, c_int, c_int, c_float, _P, _P, _P, _P,
+                                        _P, c_int, c_int, c_float, _P, c_int, c_int]),
     "spmm_gespmm_csrmm_f64": (c_int, [c_int, c_int, _P, _P, _P, _P, _P, _P]),
     "spmm_csrmm_ex_f64": (c_int, [_P, c_int, c_int, c_int, c_int, c_double, _P, _P, _P, c_int,
                                   _P, c_int, c_int, c_double, _P, c_int, c_int]),

@@ -216,6 +216,53 @@ def bsrmm_analysed(rowptr: torch.Tensor, colind: torch.Tensor, val_col: torch.Te
     return C
 
 
+def bsr16_analysis(val: torch.Tensor, *, nnzb: int, direction: int = DIRECTION_ROW,
+                   masks: torch.Tensor | None = None, val_col: torch.Tensor | None = None,
+                   handle: Handle | None = None):
+    """bs = 16 fp16 form of bsr32_analysis (spmm_bsr16_analysis_f16): masks
+    (int32, bit c < 16) and, for ROW blocks, the column-major fp16 copy."""
+    _need(val, torch.float16, "val")
+    if val.numel() < nnzb * 256:
+        raise ValueError(f"val holds {val.numel()} halves, {nnzb} blocks need {nnzb * 256}")
+    if masks is None:
+        masks = torch.empty(max(nnzb, 1), dtype=torch.int32, device=val.device)
+    if direction == DIRECTION_ROW and val_col is None:
+        val_col = torch.empty(max(nnzb, 1) * 256, dtype=torch.float16, device=val.device)
+    _need(masks, torch.int32, "masks")
+    if masks.numel() < nnzb:
+        raise ValueError("masks holds fewer than nnzb words")
+    if direction == DIRECTION_ROW:
+        _need(val_col, torch.float16, "val_col")
+        if val_col.numel() < nnzb * 256:
+            raise ValueError("val_col holds fewer than nnzb * 256 halves")
+    h = handle or default_handle()
+    check(lib().spmm_bsr16_analysis_f16(h.raw, direction, nnzb, _ptr(val), _ptr(masks),
+                                        _ptr(val_col) if direction == DIRECTION_ROW else None),
+          "spmm_bsr16_analysis_f16")
+    return masks, (val_col if direction == DIRECTION_ROW else val)
+
+
+def bsrmm_analysed_f16(rowptr: torch.Tensor, colind: torch.Tensor, val_col: torch.Tensor,
+                       masks: torch.Tensor, B: torch.Tensor, *, mb: int, kb: int, n: int,
+                       ldb: int, order_b: int = ORDER_ROW, C: torch.Tensor, ldc: int,
+                       order_c: int = ORDER_ROW, alpha: float = 1.0, beta: float = 0.0,
+                       handle: Handle | None = None) -> torch.Tensor:
+    """fp16 A and B, fp32 C, on bsr16_analysis's output (spmm_bsrmm_analysed_f16)."""
+    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                      (val_col, torch.float16, "val_col"), (masks, torch.int32, "masks"),
+                      (B, torch.float16, "B"), (C, torch.float32, "C")):
+        _need(t, dt, nm)
+    nnzb = colind.numel()
+    if val_col.numel() < nnzb * 256 or masks.numel() < nnzb:
+        raise ValueError("val_col / masks are shorter than the matrix's nnzb blocks")
+    h = handle or default_handle()
+    check(lib().spmm_bsrmm_analysed_f16(h.raw, mb, kb, n, nnzb, alpha, _ptr(rowptr),
+                                        _ptr(colind), _ptr(val_col), _ptr(masks), _ptr(B), ldb,
+                                        order_b, beta, _ptr(C), ldc, order_c),
+          "spmm_bsrmm_analysed_f16")
+    return C
+
+
 def bsrmm_f16(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torch.Tensor, *,
               mb: int, kb: int, n: int, bs: int, ldb: int, order_b: int = ORDER_ROW,
               C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW, alpha: float = 1.0,

@@ -774,3 +774,115 @@ def test_bsr32_analysis_argument_checks(device):
                                      0.0, None, 8, 0) == 0                            # quick
     torch.cuda.synchronize()
     assert torch.all(C == 3.0)
+
+
+def _masks16_np(v16):
+    vb = v16.reshape(-1, 16, 16)
+    nz = (vb.view(np.uint16) & 0x7fff) != 0
+    cols = nz.any(axis=1)
+    return (cols.astype(np.uint32) << np.arange(16, dtype=np.uint32)).sum(axis=1).astype(np.uint32)
+
+
+@pytest.mark.parametrize("direction", [0, 1])
+def test_bsr16_analysis(device, direction):
+    """spmm_bsr16_analysis_f16: masks (-0.0, NaN, inf included) and the
+    column-major fp16 copy of ROW blocks."""
+    rng = np.random.default_rng(15 + direction)
+    rp, ci, v = _column_sparse_bsr(rng, 19, 50, 16, 0.4)
+    vb = v.astype(np.float16).reshape(-1, 16, 16).copy()
+    nnzb = vb.shape[0]
+    vb[1, 3, 7] = -0.0
+    vb[2, 0, 15] = np.nan
+    vb[4, 15, 0] = np.inf
+    src = vb.reshape(-1) if direction == 0 else np.ascontiguousarray(
+        vb.transpose(0, 2, 1)).reshape(-1)
+    (dv,) = _dev(src)
+    masks, vcol = _ops().bsr16_analysis(dv, nnzb=nnzb, direction=direction)
+    torch.cuda.synchronize()
+    assert np.array_equal(masks.cpu().numpy()[:nnzb].view(np.uint32), _masks16_np(vb))
+    colmajor = np.ascontiguousarray(vb.transpose(0, 2, 1)).reshape(-1)
+    assert np.array_equal(vcol.cpu().numpy()[:nnzb * 256].view(np.uint16),
+                          colmajor.view(np.uint16))
+
+
+@pytest.mark.parametrize("orders", [(0, 0), (1, 1), (0, 1)])
+@pytest.mark.parametrize("n", [128, 264, 512, 120])
+@pytest.mark.parametrize("direction", [0, 1])
+def test_bsrmm_analysed_f16(oracle, device, orders, n, direction):
+    """spmm_bsrmm_analysed_f16 against the fp64 oracle (fp16 inputs): column-
+    sparse blocks, an empty block row, one of 300 blocks (several 64-block
+    chunks), alpha / beta, B / C orders; n = 120 (< 128) takes the COLUMN-
+    direction fallback. Then inf / NaN in B rows only empty columns meet."""
+    ob, oc = orders
+    rng = np.random.default_rng(3 * n + 10 * ob + 100 * oc + direction)
+    mb, kb, bs = 21, 320, 16
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.1)
+    rows = [ci[rp[i]:rp[i + 1]] for i in range(mb)]
+    vals = [v.reshape(-1, bs * bs)[rp[i]:rp[i + 1]] for i in range(mb)]
+    rows[5] = np.sort(rng.choice(kb, 300, replace=False)).astype(np.int32)
+    _, _, extra = _column_sparse_bsr(rng, 1, 300, bs, 1.0)
+    vals[5] = extra.reshape(-1, bs * bs)[:300]
+    rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    v16 = np.concatenate(vals).reshape(-1).astype(np.float16)
+    nnzb = ci.size
+    K, m = kb * bs, mb * bs
+    Bd = rng.uniform(-1, 1, (K, n)).astype(np.float16)
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    alpha, beta = 0.5, -1.5
+    ops = _ops()
+    src = v16 if direction == 0 else np.ascontiguousarray(
+        v16.reshape(-1, bs, bs).transpose(0, 2, 1)).reshape(-1)
+    drp, dci, dv = _dev(rp, ci, src)
+    masks, vcol = ops.bsr16_analysis(dv, nnzb=nnzb, direction=direction)
+
+    def run(Bh):
+        B = Bh if ob == 0 else np.ascontiguousarray(Bh.T)
+        Cm = C0 if oc == 0 else np.ascontiguousarray(C0.T)
+        dB, dC = _dev(B.reshape(-1), Cm.reshape(-1))
+        ops.bsrmm_analysed_f16(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n,
+                               ldb=n if ob == 0 else K, order_b=ob, C=dC,
+                               ldc=n if oc == 0 else m, order_c=oc, alpha=alpha, beta=beta)
+        torch.cuda.synchronize()
+        got = dC.cpu().numpy().reshape((m, n) if oc == 0 else (n, m))
+        return got if oc == 0 else got.T
+
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v16, Bd, n, 0, half=True)
+    ref = alpha * ref + beta * C0.astype(np.float64)
+    absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+    what = f"analysed f16 n={n} orders={orders} dir={direction}"
+    assert_normwise(run(Bd), ref, absd, TOL_F16_ACC, what)
+    if n < 128:
+        return  # the fallback kernels compute the dense block product
+    vb = v16.reshape(-1, bs, bs)
+    used = np.zeros(K, bool)
+    for br in range(mb):
+        for k in range(rp[br], rp[br + 1]):
+            used[ci[k] * bs + np.nonzero(np.any(vb[k] != 0, axis=0))[0]] = True
+    unused = np.nonzero(~used)[0]
+    assert unused.size > 0
+    Bbad = Bd.copy()
+    Bbad[unused[0::2]] = np.inf
+    Bbad[unused[1::2]] = np.nan
+    got = run(Bbad)
+    assert np.isfinite(got).all()
+    assert_normwise(got, ref, absd, TOL_F16_ACC, what + ", non-finite B")
+
+
+def test_bsrmm_analysed_f16_matches_column_stream(device):
+    """Same items in the same order as the shipped fp16 column stream: the
+    same result bit for bit."""
+    rng = np.random.default_rng(78)
+    mb, kb, bs, n = 40, 300, 16, 512
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.15)
+    v16 = v.astype(np.float16)
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float16)
+    drp, dci, dv, dB = _dev(rp, ci, v16, B.reshape(-1))
+    ops = _ops()
+    C1 = torch.empty((mb * bs, n), device=device)
+    ops.bsrmm_f16(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=C1, ldc=n)
+    masks, vcol = ops.bsr16_analysis(dv, nnzb=ci.size)
+    C2 = torch.empty((mb * bs, n), device=device)
+    ops.bsrmm_analysed_f16(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n, ldb=n, C=C2, ldc=n)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2)
