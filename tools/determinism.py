@@ -70,6 +70,14 @@ def main():
                 ops.bsrmm_f16(brp, bci, bv16, B16, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K)
                 return C
             bad += check("bsr16 fp16 K=512 (column stream, CS16)", run, reps)
+            masks16, vcol16 = ops.bsr16_analysis(bv16, nnzb=bci.numel())
+
+            def run_an16():
+                ops.bsrmm_analysed_f16(brp, bci, vcol16, masks16, B16, mb=mb, kb=mb, n=K, ldb=K,
+                                       C=C, ldc=K)
+                return C
+            bad += check("bsr16 fp16 K=512 (analysed column stream)", run_an16, reps)
+            del masks16, vcol16
             del bv16, B16
         del brp, bci, C
         torch.cuda.empty_cache()

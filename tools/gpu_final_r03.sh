@@ -19,7 +19,7 @@ echo "== kernel trace"
 fi
 if [[ $PH == *b* ]]; then
 : > $O/workloads.jsonl
-for w in ${WLS:-reddit_bsr32 products_bsr32 products_bsr32_an reddit_bsr32_an products_bsr16_f16 reddit_rcm_bsr32 products_rcm_bsr32 products_rcm_bsr16_f16 reddit_hybrid32 products_hybrid32 reddit_rcm_hybrid32 arxiv_csr products_csr_k256}; do
+for w in ${WLS:-reddit_bsr32 products_bsr32 products_bsr32_an reddit_bsr32_an products_bsr16_f16 products_bsr16_f16_an products_rcm_bsr32_an reddit_rcm_bsr32_an products_rcm_bsr16_f16_an reddit_rcm_bsr32 products_rcm_bsr32 products_rcm_bsr16_f16 reddit_hybrid32 products_hybrid32 reddit_rcm_hybrid32 arxiv_csr products_csr_k256}; do
   timeout -k 10 300 python bench.py --workload $w --steps 20 --warmup 5 --no-cpu-baseline > $O/bw.log 2>&1; rc=$?; stop $rc
   [ $rc -eq 0 ] || { tail -5 $O/bw.log; continue; }
   grep '^{' $O/bw.log >> $O/workloads.jsonl
