@@ -1302,11 +1302,26 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
       }
       return;
     }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA -> AGPR read
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const size_t row = (size_t)br * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
       f32x4* p = reinterpret_cast<f32x4*>(C + row * ldc + col);
       f32x4 v = {u0[e], u1[e], u0[16 + e], u1[16 + e]};
+      {
+        // each row's four accumulators read just before its store: hipcc otherwise copies
+        // all 64 out of the AGPRs at once, and those 64 VGPRs set the kernel's register
+        // count (148: 3 waves per SIMD; the loop itself needs fewer than 60 besides the
+        // accumulators). Analysed products 2.14 -> 2.04 ms at 4 waves per SIMD
+        // (profiles/r03_analysed_4waves.txt)
+        asm volatile("v_accvgpr_read_b32 %0, %4\n\t"
+                     "v_accvgpr_read_b32 %1, %5\n\t"
+                     "v_accvgpr_read_b32 %2, %6\n\t"
+                     "v_accvgpr_read_b32 %3, %7"
+                     : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3])
+                     : "a"(u0[e]), "a"(u1[e]), "a"(u0[16 + e]), "a"(u1[16 + e])
+                     : "memory");
+      }
       if (beta == 0.f) {
         v *= alpha;
       } else {
