@@ -49,6 +49,10 @@ MFMA_PEAK_TFLOPS = {"fp32": 157.3, "fp16": 2500.0}  # dense (no sparsity)
 WORKLOADS = {
     "products_csr": dict(kind="csr", n=2449029, nnz=61859140, max_deg=17481, K=128),
     "products_csr_k256": dict(kind="csr", n=2449029, nnz=61859140, max_deg=17481, K=256),
+    # the headline product on hot-column cache hints (spmm_csr_hot_analysis once
+    # per matrix, timed apart as analysis_ms; spmm_csrmm_hot_f32 in the step)
+    "products_csr_hot": dict(kind="csr", n=2449029, nnz=61859140, max_deg=17481, K=128,
+                             hot=True),
     "arxiv_csr": dict(kind="csr", n=169343, nnz=1166243, max_deg=13161, K=128),
     "reddit_bsr32": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
                          bs=32, K=128, dtype="fp32"),
@@ -217,6 +221,12 @@ def _time_prefix(run, n: int, budget_s: float):
     return rows, times
 
 
+def _progress(msg: str) -> None:
+    """One line on stderr per finished CPU-baseline leg (a long silent run
+    looks hung to a watchdog)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _spread(ts) -> dict:
     """min / median / max of per-call times (s) and (max - min) / median."""
     a = np.asarray(ts, dtype=np.float64)
@@ -297,10 +307,13 @@ def cpu_baseline_config1(L) -> dict:
     (oracle_spmm_cc_csr: OpenMP rows, k-outer, double, unit values) on
     randomCSRMatrix(16384, 16384, 2^-10) + randomDenseMatrix(16384, 32) from a
     fresh mt19937_64(1234) (the reference generator's stream, bit-exact).
-    One call takes well under a millisecond, so each of 11 samples times a
-    loop of back-to-back calls of at least 100 ms (after a warm-up sample);
-    min / median / max per call are reported. coo_spmm (spmm.cc:27-43)
-    beside it."""
+    One call takes well under a millisecond, so each of 5 samples times a
+    loop of back-to-back calls of at least 1 s (after a warm-up sample):
+    the box's cgroup grants 16 CPUs of time per 100-ms CFS period, so 128
+    threads run stop-go, and a sample must span many periods for its mean
+    to be the throttled rate rather than the phase it landed in (100-ms
+    samples spread 15-180 % in round 3). min / median / max per call are
+    reported. coo_spmm (spmm.cc:27-43) beside it."""
     from helpers import ptr
     from spmm_hip import prep
     m, K = 16384, 32
@@ -315,7 +328,8 @@ def cpu_baseline_config1(L) -> dict:
                                                                 ptr(out))),
                       ("coo_spmm", lambda: L.oracle_spmm_cc_coo(m, K, ix.size, ptr(row), ptr(ix),
                                                                 ptr(B), K, ptr(out)))):
-        reps, ts = _batched_samples(run)
+        reps, ts = _batched_samples(run, min_sample_s=1.0, nsamples=5)
+        _progress(f"config1 {name} done")
         sp = _spread(ts)
         res[name] = {"GFLOPs": round(2.0 * ci.size * K / sp["median_s"] / 1e9, 3),
                      "calls_per_sample": reps, **sp}
@@ -323,8 +337,8 @@ def cpu_baseline_config1(L) -> dict:
             "cores": int(L.oracle_num_threads()),
             "sample": (f"BASELINE config 1: spmm.cc csr_spmm restated on randomCSRMatrix(16384, "
                        f"16384, 2^-10) ({ci.size} nnz, mt19937_64(1234)), K=32, double, unit "
-                       f"values; 11 samples of {res['csr_spmm']['calls_per_sample']} back-to-back "
-                       f"calls (>= 100 ms each), median per call"), **res}
+                       f"values; 5 samples of {res['csr_spmm']['calls_per_sample']} back-to-back "
+                       f"calls (>= 1 s each), median per call"), **res}
 
 
 def cpu_baseline_child(args) -> None:
@@ -355,6 +369,7 @@ def cpu_baseline_child(args) -> None:
         lambda r: L.oracle_spmm_cc_csr(r, K, ptr(ip64), ptr(ix64), ptr(Bd), K, ptr(out)),
         n, budget_s)
     del out, Bd
+    _progress(f"cpu_baseline csr_spmm ({os.environ.get('OMP_NUM_THREADS')} threads) done")
     sp = _spread(times)
     nnz_s = int(rp[rows])
     res = {"value": round(2.0 * nnz_s * K / sp["median_s"] / 1e9, 3), "unit": "GFLOP/s",
@@ -379,6 +394,7 @@ def cpu_baseline_child(args) -> None:
                    f"{'all' if rows == n else 'the first'} {rows} rows ({nnz_s} nnz), K={K}; "
                    f"median of {len(times)} runs ({sp['median_s']:.3f} s each)"), **sp}
     del Bf, vf, outf
+    _progress("cpu_baseline fp32_weighted done")
     res["config1"] = cpu_baseline_config1(L)
     print(json.dumps(res), flush=True)
 
@@ -400,11 +416,11 @@ def cpu_baseline(args, K: int) -> dict:
         env = dict(os.environ, OMP_NUM_THREADS=str(T), OMP_PROC_BIND="close", OMP_PLACES="cores")
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child",
                             "--workload", args.workload, "--K", str(K), "--cpu-budget",
-                            str(args.cpu_budget)], env=env, capture_output=True, text=True,
-                           timeout=900)
+                            str(args.cpu_budget)], env=env, stdout=subprocess.PIPE,
+                           stderr=None, text=True, timeout=900)
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
         if r.returncode != 0 or not lines:
-            legs[label] = {"error": f"rc {r.returncode}: {r.stderr[-400:]}"}
+            legs[label] = {"error": f"rc {r.returncode} (child stderr above)"}
         else:
             legs[label] = json.loads(lines[-1])
     res = dict(legs["all_physical_cores"])
@@ -574,6 +590,20 @@ def run_csr(args, W, world, rank, dev, dist):
     nch = args.chunks or (4 if world > 1 else 1)
     if nch > 1 and not dist.is_initialized():
         raise SystemExit("--chunks > 1 at N = 1 needs a torch.distributed launcher")
+    hot = bool(W.get("hot"))
+    analysis_ms = None
+    if hot:
+        if world > 1 or nch > 1 or args.csr_layout == "col":
+            raise SystemExit("the hot-column line is the 1-GPU row-major product")
+        ts = []
+        for _ in range(3):  # once per matrix; timed apart from the step
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            d_tag = ops.csr_hot_analysis(d_ci, n=K, k=n, handle=h)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        analysis_ms = min(ts) * 1e3
+        hot_share = float((d_tag < 0).float().mean())
     if nch > 1:
         # the all-gather of chunk c overlaps the compute of chunk c + 1
         out = torch.empty((nch, world, sdist.chunk_rows(shard, nch), K), device=dev)
@@ -603,10 +633,13 @@ def run_csr(args, W, world, rank, dev, dist):
     else:
         out = torch.empty((world * mr, K), device=dev)
         C_slot = out[rank * mr: rank * mr + shard.rows]
+        product, ci_step = ops.csrmm, d_ci
+        if hot:
+            product, ci_step = ops.csrmm_hot, d_tag
 
         def step():
-            ops.csrmm(d_rp, d_ci, d_v, B, m=shard.rows, n=K, k=n, ldb=K, C=C_slot, ldc=K,
-                      handle=h)
+            product(d_rp, ci_step, d_v, B, m=shard.rows, n=K, k=n, ldb=K, C=C_slot, ldc=K,
+                    handle=h)
             if world > 1:
                 sdist.gather(out, shard, compact=False)
 
@@ -622,7 +655,7 @@ def run_csr(args, W, world, rank, dev, dist):
     elapsed, kms_max = float(t[0]), float(t[1])
     crf = csr_roofline(shard.rows, shard.colind, K, kms)
     traffic = None
-    if os.path.exists(args.traffic_json):
+    if os.path.exists(args.traffic_json) and not hot:  # bytes of the plain kernel only
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
@@ -645,9 +678,15 @@ def run_csr(args, W, world, rank, dev, dist):
                 "waves_per_cu": args.waves_per_cu or 16,
                 "csr_options": args.csr_options, "layout_BC": args.csr_layout},
         roofline={"bound": "hbm", "peak": HBM_PEAK_GBPS, "unit": "GB/s", **crf,
-                  "traffic": traffic, "kernel": f"csr_mergepath_kernel<{vec}>",
+                  "traffic": traffic,
+                  "kernel": f"csr_mergepath_kernel<{vec}>" + (" (hot-column hints)" if hot else ""),
                   "kernel_ms": round(kms, 4), "kernel_ms_max_rank": round(kms_max, 4)},
         gen_seconds=round(t_gen, 2))
+    if hot:
+        rec["analysis_ms"] = round(analysis_ms, 4)
+        rec["hot_gather_share"] = round(hot_share, 4)
+        rec["config"]["workload"] += (" on hot-column cache hints (spmm_csr_hot_analysis once, "
+                                      "analysis_ms apart; spmm_csrmm_hot_f32 per step)")
     if dist.is_initialized() and nch > 1 or world > 1:
         # compute and collective reported separately (a world-1
         # torch.distributed launch with --chunks > 1 rehearses it through RCCL).

@@ -148,6 +148,31 @@ spmm_status_t spmm_csrmm_ex_f32(spmm_handle_t handle, int m, int n, int k, int n
                                 const float* B, int ldb, spmm_order_t orderB, float beta,
                                 float* C, int ldc, spmm_order_t orderC);
 
+/* Hot-column analysis for the CSR gathers (an extension, once per matrix like
+ * cuSPARSE's SpMM preprocess; the reference's gespmm_csrmm.h / csrmm.cu have
+ * none). Counts every column's nonzeros on the device and writes
+ *   csrColIndHot[i] = csrColInd[i] | 0x80000000  if column csrColInd[i] is hot,
+ *                     csrColInd[i]               otherwise,
+ * hot = among the columns with the most nonzeros whose gathered B-row pieces
+ * (n floats, at most one merge-path column tile) fit in hotBytes (0 = the
+ * default below: half the 256-MB MALL). Requires column indices < 2^31 - 1.
+ * Caller-owned output (nnz ints); scratch comes from the handle. */
+#define SPMM_CSR_HOT_BYTES_DEFAULT (128ll << 20)
+spmm_status_t spmm_csr_hot_analysis(spmm_handle_t handle, int n, int k, int nnz,
+                                    const int* csrColInd, spmm_index_base_t base,
+                                    long long hotBytes, int* csrColIndHot);
+
+/* spmm_csrmm_ex_f32 on the tagged column indices of spmm_csr_hot_analysis:
+ * hot columns' B rows are gathered with the default cache policy, every other
+ * row non-temporal, so the long tail of rarely used rows does not evict the hub
+ * rows from L2 and the MALL. Same arithmetic, order and result as
+ * spmm_csrmm_ex_f32 on the untagged indices (bit-identical), same checks. */
+spmm_status_t spmm_csrmm_hot_f32(spmm_handle_t handle, int m, int n, int k, int nnz,
+                                 float alpha, const int* csrRowPtr, const int* csrColIndHot,
+                                 const float* csrVal, spmm_index_base_t base, const float* B,
+                                 int ldb, spmm_order_t orderB, float beta, float* C, int ldc,
+                                 spmm_order_t orderC);
+
 /* ------------------------------------------------------------------------ */
 /* Path B: BSR x dense                                                         */
 /* ------------------------------------------------------------------------ */

@@ -19,7 +19,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, float alpha,
                          const int* rowptr, const int* colind, const float* val, int base,
                          const float* B, int ldb, spmm_order_t orderB, float beta, float* C,
-                         int ldc, spmm_order_t orderC) {
+                         int ldc, spmm_order_t orderC, bool hot = false) {
   WsLayout L;
   L.carry_bytes = csrmm_carry_bytes(ctx, m, n, nullptr);
   L.b_off = align256(L.carry_bytes);
@@ -48,11 +48,11 @@ spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, f
   }
   if (orderC == SPMM_ORDER_ROW) {
     return launch_csrmm_rowmajor(ctx, m, n, rowptr, colind, val, base, Bx, ldbx, alpha, beta, C,
-                                 ldc, carry_val, carry_row, nnz_hint);
+                                 ldc, carry_val, carry_row, nnz_hint, hot);
   }
   float* Ct = reinterpret_cast<float*>(ws + L.c_off);
   st = launch_csrmm_rowmajor(ctx, m, n, rowptr, colind, val, base, Bx, ldbx, alpha, 0.f, Ct, n,
-                             carry_val, carry_row, nnz_hint);
+                             carry_val, carry_row, nnz_hint, hot);
   if (st != SPMM_STATUS_SUCCESS) return st;
   // C (m x n col-major, ldc) is an (n x m) row-major matrix with ld ldc.
   return launch_transpose(ctx, m, n, Ct, n, C, ldc, beta);
@@ -127,6 +127,44 @@ spmm_status_t spmm_csrmm_ex_f32(spmm_handle_t handle, int m, int n, int k, int n
   if (orderC == SPMM_ORDER_ROW ? ldc < n : ldc < m) return SPMM_STATUS_INVALID_VALUE;
   return csrmm_impl(handle, m, n, k, nnz, alpha, csrRowPtr, csrColInd, csrVal, (int)base, B, ldb,
                     orderB, beta, C, ldc, orderC);
+}
+
+spmm_status_t spmm_csr_hot_analysis(spmm_handle_t handle, int n, int k, int nnz,
+                                    const int* csrColInd, spmm_index_base_t base,
+                                    long long hotBytes, int* csrColIndHot) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (n < 0 || k < 0 || nnz < 0 || hotBytes < 0) return SPMM_STATUS_INVALID_VALUE;
+  if (base != SPMM_INDEX_BASE_ZERO && base != SPMM_INDEX_BASE_ONE)
+    return SPMM_STATUS_INVALID_VALUE;
+  if (nnz == 0) return SPMM_STATUS_SUCCESS;
+  if (!csrColInd || !csrColIndHot || k == 0) return SPMM_STATUS_INVALID_VALUE;
+  // one gathered B-row piece: the merge-path kernel's column tile (64 / 128 / 256
+  // floats) or the whole row when n is narrower
+  const long long tile = n > 128 ? 256 : (n > 64 ? 128 : 64);
+  const long long piece = 4 * (n > 0 && n < tile ? n : tile);
+  const long long hot_rows = (hotBytes ? hotBytes : SPMM_CSR_HOT_BYTES_DEFAULT) / piece;
+  return launch_csr_hot_analysis(handle, k, nnz, csrColInd, (int)base, hot_rows, csrColIndHot);
+}
+
+spmm_status_t spmm_csrmm_hot_f32(spmm_handle_t handle, int m, int n, int k, int nnz, float alpha,
+                                 const int* csrRowPtr, const int* csrColIndHot,
+                                 const float* csrVal, spmm_index_base_t base, const float* B,
+                                 int ldb, spmm_order_t orderB, float beta, float* C, int ldc,
+                                 spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (m < 0 || n < 0 || k < 0 || nnz < 0) return SPMM_STATUS_INVALID_VALUE;
+  if (base != SPMM_INDEX_BASE_ZERO && base != SPMM_INDEX_BASE_ONE)
+    return SPMM_STATUS_INVALID_VALUE;
+  if ((orderB != SPMM_ORDER_ROW && orderB != SPMM_ORDER_COL) ||
+      (orderC != SPMM_ORDER_ROW && orderC != SPMM_ORDER_COL))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  if (!csrRowPtr || !C || (k > 0 && !B) || (nnz > 0 && (!csrColIndHot || !csrVal)))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (orderB == SPMM_ORDER_ROW ? ldb < n : ldb < (k > 0 ? k : 1)) return SPMM_STATUS_INVALID_VALUE;
+  if (orderC == SPMM_ORDER_ROW ? ldc < n : ldc < m) return SPMM_STATUS_INVALID_VALUE;
+  return csrmm_impl(handle, m, n, k, nnz, alpha, csrRowPtr, csrColIndHot, csrVal, (int)base, B,
+                    ldb, orderB, beta, C, ldc, orderC, true);
 }
 
 spmm_status_t spmm_scsrmm2(spmm_handle_t handle, spmm_operation_t transA,

@@ -79,7 +79,11 @@ inline spmm_status_t from_hip(hipError_t e) {
 spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* rowptr,
                                     const int* colind, const float* val, int base,
                                     const float* B, int ldb, float alpha, float beta, float* C,
-                                    int ldc, float* carry_val, int* carry_row, int nnz_hint);
+                                    int ldc, float* carry_val, int* carry_row, int nnz_hint,
+                                    bool hot = false);
+// spmm_csr_hot_analysis: colind_out = colind with bit 31 set on hot columns
+spmm_status_t launch_csr_hot_analysis(spmm_context* ctx, int k, long long nnz, const int* colind,
+                                      int base, long long hot_rows, int* colind_out);
 size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n, int* nwaves_out);
 
 spmm_status_t launch_transpose16(spmm_context* ctx, int rows, int cols, const uint16_t* src,

@@ -72,6 +72,18 @@ __device__ __forceinline__ void vset(typename Vec<VEC>::T& v, int c, float x) {
   if constexpr (VEC == 1) v = x; else v[c] = x;
 }
 
+// One B-row piece by a raw buffer load with cache policy AUX (0 default, 2 nt).
+template <int VEC, int AUX>
+__device__ __forceinline__ typename Vec<VEC>::T bload(__amdgpu_buffer_rsrc_t rs, int off) {
+  if constexpr (VEC == 1) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, AUX));
+  } else if constexpr (VEC == 2) {
+    return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, AUX));
+  } else {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX));
+  }
+}
+
 // Waits for a pending load into `x` right here. Used on the (rare) reload
 // paths so that the common path that merges with them after a branch does
 // not inherit a conservative vmcnt(0) for the reloaded register.
@@ -124,7 +136,7 @@ __device__ __forceinline__ int merge_search2(const int* __restrict__ rowptr, int
   return lo;
 }
 
-template <int VEC, bool NT>
+template <int VEC, bool NT, bool HOT = false, int CA = 2>
 __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
     int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, int base, const float* __restrict__ B, int ldb, float alpha,
@@ -251,8 +263,24 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
         const int l = lb + u / kR;
         vdst[u] = rdlanef(valv[u % kR], l);
         // Wave-uniform row base (SGPRs) + per-lane column offset.
-        const float* rowp = Bb + (size_t)rdlane(colv[u % kR], l) * ldb;
-        const vec x = vload<VEC>(rowp + col_ld);
+        const int cr = rdlane(colv[u % kR], l);
+        const float* rowp = Bb + (size_t)(HOT ? (cr & 0x7fffffff) : cr) * ldb;
+        vec x;
+        if constexpr (HOT) {
+          // tagged colind (spmm_csr_hot_analysis): bit 31 marks a column whose B
+          // row is worth keeping in L2; every other row is streamed (nt), so the
+          // long tail of once-per-wave rows does not evict the hubs
+          // (buffer loads: the cache policy is an immediate of the intrinsic, so the two
+          // arms stay two instructions; plain loads were merged into one, nt dropped)
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<float*>(rowp), 0, 0x7fffffff, 0x00020000);
+          if (cr < 0)
+            x = bload<VEC, 0>(rs, 4 * col_ld);
+          else
+            x = bload<VEC, CA>(rs, 4 * col_ld);
+        } else {
+          x = vload<VEC>(rowp + col_ld);
+        }
 #pragma unroll
         for (int c = 0; c < VEC; ++c) dst[u][c] = vget<VEC>(x, c);
       }
@@ -681,9 +709,110 @@ int csr_nwaves(spmm_context* ctx, int m, long long nnz) {
   return (int)nw;
 }
 
+// ---------------------------------------------------------------------------
+// spmm_csr_hot_analysis (once per matrix): which columns' B rows the gathers
+// keep in the caches. Count the nonzeros of every column, histogram the counts
+// (kHotBins bins, the last one open-ended), pick the count threshold that keeps
+// at most hot_rows columns above it, and write colind | bit 31 for the hot ones.
+// ---------------------------------------------------------------------------
+constexpr int kHotBins = 8192;
+
+__global__ __launch_bounds__(256) void col_count_kernel(long long nnz, const int* __restrict__ colind,
+                                                       int base, int k, unsigned* __restrict__ cnt) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nnz;
+       i += (long long)gridDim.x * 256) {
+    const int c = colind[i] - base;
+    if ((unsigned)c < (unsigned)k) atomicAdd(cnt + c, 1u);
+  }
+}
+
+// per-workgroup LDS histogram of the counts (most columns share a few small
+// counts: global atomics on those bins would serialise), flushed once
+__global__ __launch_bounds__(256) void count_hist_kernel(int k, const unsigned* __restrict__ cnt,
+                                                        unsigned* __restrict__ hist) {
+  __shared__ unsigned h[kHotBins];
+  for (int b = threadIdx.x; b < kHotBins; b += 256) h[b] = 0;
+  __syncthreads();
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < k; c += gridDim.x * 256)
+    atomicAdd(h + min(cnt[c], (unsigned)(kHotBins - 1)), 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < kHotBins; b += 256)
+    if (h[b]) atomicAdd(hist + b, h[b]);
+}
+
+// thr = the smallest bin t with (columns in bins >= t) <= hot_rows; a column is
+// hot iff min(count, kHotBins - 1) >= thr (thr = kHotBins: none; nonzero-free
+// columns are never gathered, so thr = 0 only when every column fits)
+__global__ __launch_bounds__(1024) void hot_select_kernel(const unsigned* __restrict__ hist,
+                                                         long long hot_rows,
+                                                         unsigned* __restrict__ thr) {
+  constexpr int kPer = kHotBins / 1024;
+  __shared__ unsigned long long part[1024];
+  const int t = threadIdx.x;
+  const int top = kHotBins - kPer * t - 1;  // thread t owns bins top .. top - kPer + 1
+  unsigned long long s = 0;
+  for (int j = 0; j < kPer; ++j) s += hist[top - j];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const unsigned long long v = t >= o ? part[t - o] : 0ull;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const unsigned long long above = t ? part[t - 1] : 0ull;  // columns in the bins above mine
+  if (above <= (unsigned long long)hot_rows && part[t] > (unsigned long long)hot_rows) {
+    unsigned long long c = above;
+    int b = top;
+    for (; b > top - kPer; --b) {
+      if (c + hist[b] > (unsigned long long)hot_rows) break;
+      c += hist[b];
+    }
+    *thr = (unsigned)(b + 1);
+  }
+  if (t == 1023 && part[t] <= (unsigned long long)hot_rows) *thr = 0u;
+}
+
+__global__ __launch_bounds__(256) void hot_tag_kernel(long long nnz, const int* __restrict__ colind,
+                                                     int base, int k,
+                                                     const unsigned* __restrict__ cnt,
+                                                     const unsigned* __restrict__ thr,
+                                                     int* __restrict__ out) {
+  const unsigned t = *thr;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nnz;
+       i += (long long)gridDim.x * 256) {
+    const int ci = colind[i];
+    const int c = ci - base;
+    const bool hot = (unsigned)c < (unsigned)k && min(cnt[c], (unsigned)(kHotBins - 1)) >= t;
+    out[i] = hot ? (int)((unsigned)ci | 0x80000000u) : ci;
+  }
+}
+
 }  // namespace
 
 namespace spmm {
+
+spmm_status_t launch_csr_hot_analysis(spmm_context* ctx, int k, long long nnz, const int* colind,
+                                      int base, long long hot_rows, int* colind_out) {
+  // scratch: counts (k words), histogram, threshold
+  const size_t cnt_bytes = ((size_t)k * 4 + 255) & ~(size_t)255;
+  spmm_status_t st = ensure_scratch(ctx, cnt_bytes + kHotBins * 4 + 256);
+  if (st != SPMM_STATUS_SUCCESS) return st;
+  unsigned* cnt = static_cast<unsigned*>(ctx->scratch);
+  unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(ctx->scratch) + cnt_bytes);
+  unsigned* thr = hist + kHotBins;
+  hipError_t e = hipMemsetAsync(cnt, 0, cnt_bytes + kHotBins * 4, ctx->stream);
+  if (e != hipSuccess) return from_hip(e);
+  const int grid = ctx->num_cus * 8;
+  hipLaunchKernelGGL(col_count_kernel, dim3(grid), dim3(256), 0, ctx->stream, nnz, colind, base, k,
+                     cnt);
+  hipLaunchKernelGGL(count_hist_kernel, dim3(ctx->num_cus), dim3(256), 0, ctx->stream, k, cnt,
+                     hist);
+  hipLaunchKernelGGL(hot_select_kernel, dim3(1), dim3(1024), 0, ctx->stream, hist, hot_rows, thr);
+  hipLaunchKernelGGL(hot_tag_kernel, dim3(grid), dim3(256), 0, ctx->stream, nnz, colind, base, k,
+                     cnt, thr, colind_out);
+  return from_hip(hipGetLastError());
+}
 
 size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n, int* nwaves_out) {
   // The grid does not depend on nnz beyond the cap: size it for the cap.
@@ -699,7 +828,8 @@ size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n, int* nwaves_out) {
 spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* rowptr,
                                     const int* colind, const float* val, int base,
                                     const float* B, int ldb, float alpha, float beta, float* C,
-                                    int ldc, float* carry_val, int* carry_row, int nnz_hint) {
+                                    int ldc, float* carry_val, int* carry_row, int nnz_hint,
+                                    bool hot) {
   if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   const int vec = pick_vec(n, B, ldb, C, ldc);
   const int tile = kWave * vec;
@@ -709,7 +839,7 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   dim3 block(kWG);
   const int slot = timing_begin(ctx);
   const bool nt = (ctx->csr_flags & SPMM_CSR_NT_STREAMS) != 0;
-  const bool grouped = n <= kGroupMaxK && n % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
+  const bool grouped = !hot && n <= kGroupMaxK && n % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
                       reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
                       reinterpret_cast<uintptr_t>(C) % 16 == 0 &&
                       (ctx->csr_flags & SPMM_CSR_SEQUENTIAL_ROWS) == 0;
@@ -759,7 +889,24 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
 #define SPMM_LAUNCH_MP(V, N)                                                                   \
   hipLaunchKernelGGL((csr_mergepath_kernel<V, N>), grid, block, 0, ctx->stream, m, n, rowptr, \
                      colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw)
-  if (vec == 4) {
+#define SPMM_LAUNCH_HOT(V)                                                                     \
+  hipLaunchKernelGGL((csr_mergepath_kernel<V, true, true>), grid, block, 0, ctx->stream, m, n, \
+                     rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
+                     carry_row, nw)
+#define SPMM_LAUNCH_HOTA(CA)                                                                   \
+  hipLaunchKernelGGL((csr_mergepath_kernel<2, true, true, CA>), grid, block, 0, ctx->stream, m, \
+                     n, rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,    \
+                     carry_row, nw)
+  static const int hot_aux = [] {
+    const char* e = getenv("SPMM_CSR_HOT_AUX");  // probe only: cache policy of cold rows
+    return e ? atoi(e) : 2;
+  }();
+  if (hot && vec == 2 && hot_aux != 2) {
+    if (hot_aux == 1) SPMM_LAUNCH_HOTA(1); else if (hot_aux == 16) SPMM_LAUNCH_HOTA(16);
+    else if (hot_aux == 18) SPMM_LAUNCH_HOTA(18); else SPMM_LAUNCH_HOTA(3);
+  } else if (hot) {
+    if (vec == 4) SPMM_LAUNCH_HOT(4); else if (vec == 2) SPMM_LAUNCH_HOT(2); else SPMM_LAUNCH_HOT(1);
+  } else if (vec == 4) {
     if (nt) SPMM_LAUNCH_MP(4, true); else SPMM_LAUNCH_MP(4, false);
   } else if (vec == 2) {
     if (nt) SPMM_LAUNCH_MP(2, true); else SPMM_LAUNCH_MP(2, false);
@@ -767,6 +914,8 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
     if (nt) SPMM_LAUNCH_MP(1, true); else SPMM_LAUNCH_MP(1, false);
   }
 #undef SPMM_LAUNCH_MP
+#undef SPMM_LAUNCH_HOT
+#undef SPMM_LAUNCH_HOTA
   timing_end(ctx, slot);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return from_hip(e);

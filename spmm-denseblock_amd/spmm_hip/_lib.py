@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_uint64, c_void_p
+from ctypes import c_longlong, POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_uint64, c_void_p
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(PKG_DIR)
@@ -75,6 +75,9 @@ _PROTOS = {
                              _P, _P, _P, _P, c_int, POINTER(c_float), _P, c_int]),
     "spmm_csrmm_ex_f32": (c_int, [_P, c_int, c_int, c_int, c_int, c_float, _P, _P, _P, c_int,
                                   _P, c_int, c_int, c_float, _P, c_int, c_int]),
+    "spmm_csr_hot_analysis": (c_int, [_P, c_int, c_int, c_int, _P, c_int, c_longlong, _P]),
+    "spmm_csrmm_hot_f32": (c_int, [_P, c_int, c_int, c_int, c_int, c_float, _P, _P, _P, c_int,
+                                   _P, c_int, c_int, c_float, _P, c_int, c_int]),
     "spmm_sbsrmm": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                             POINTER(c_float), _P, _P, _P, _P, c_int, _P, c_int,
                             POINTER(c_float), _P, c_int]),

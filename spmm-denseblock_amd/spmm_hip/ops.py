@@ -147,6 +147,43 @@ def csrmm(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torc
     return C
 
 
+def csr_hot_analysis(colind: torch.Tensor, *, n: int, k: int, base: int = 0,
+                     hot_bytes: int = 0, out: torch.Tensor | None = None,
+                     handle: Handle | None = None) -> torch.Tensor:
+    """spmm_csr_hot_analysis: colind with bit 31 set on the hot columns (the
+    most used B rows whose n-float pieces fit in hot_bytes; 0 = the library
+    default). Once per matrix; feed the result to csrmm_hot."""
+    _need(colind, torch.int32, "colind")
+    if out is None:
+        out = torch.empty_like(colind)
+    _need(out, torch.int32, "out")
+    if out.numel() < colind.numel():
+        raise ValueError("out is shorter than colind")
+    h = handle or default_handle()
+    check(lib().spmm_csr_hot_analysis(h.raw, n, k, colind.numel(), _ptr(colind), base, hot_bytes,
+                                      _ptr(out)), "spmm_csr_hot_analysis")
+    return out
+
+
+def csrmm_hot(rowptr: torch.Tensor, colind_hot: torch.Tensor, val: torch.Tensor,
+              B: torch.Tensor, *, m: int | None = None, n: int, k: int, ldb: int,
+              order_b: int = ORDER_ROW, C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW,
+              alpha: float = 1.0, beta: float = 0.0, base: int = 0,
+              handle: Handle | None = None) -> torch.Tensor:
+    """csrmm on the tagged indices of csr_hot_analysis (spmm_csrmm_hot_f32):
+    the same result, bit for bit, with cache hints on the B-row gathers."""
+    for t, d, nm in ((rowptr, torch.int32, "rowptr"), (colind_hot, torch.int32, "colind_hot"),
+                     (val, torch.float32, "val"), (B, torch.float32, "B"),
+                     (C, torch.float32, "C")):
+        _need(t, d, nm)
+    h = handle or default_handle()
+    m = rowptr.numel() - 1 if m is None else m
+    check(lib().spmm_csrmm_hot_f32(h.raw, m, n, k, colind_hot.numel(), alpha, _ptr(rowptr),
+                                   _ptr(colind_hot), _ptr(val), base, _ptr(B), ldb, order_b, beta,
+                                   _ptr(C), ldc, order_c), "spmm_csrmm_hot_f32")
+    return C
+
+
 def bsrmm(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torch.Tensor, *,
           mb: int, kb: int, n: int, bs: int, ldb: int, order_b: int = ORDER_ROW,
           C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW, alpha: float = 1.0,
