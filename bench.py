@@ -241,10 +241,17 @@ def _batched_samples(run, min_sample_s: float = 0.1, nsamples: int = 11):
     at least min_sample_s long (a short call's median otherwise measures
     thread wake-up, not the loop), after a warm-up sample."""
     run()
-    t0 = time.perf_counter()
-    for _ in range(3):
+    # per-call time from a loop of at least a quarter second: a few calls can
+    # land in a throttled period (cgroup CPU quota) and read 10x slow, which
+    # made round 3's "1-s" samples 0.11 s long
+    t0, calls = time.perf_counter(), 0
+    while True:
         run()
-    one = max((time.perf_counter() - t0) / 3, 1e-6)
+        calls += 1
+        dt = time.perf_counter() - t0
+        if dt >= min(0.25, min_sample_s):
+            break
+    one = max(dt / calls, 1e-6)
     reps = max(1, int(np.ceil(min_sample_s / one)))
     ts = []
     for _ in range(nsamples + 1):

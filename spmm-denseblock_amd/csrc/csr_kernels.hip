@@ -136,7 +136,7 @@ __device__ __forceinline__ int merge_search2(const int* __restrict__ rowptr, int
   return lo;
 }
 
-template <int VEC, bool NT, bool HOT = false, int CA = 2>
+template <int VEC, bool NT, bool HOT = false>
 __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
     int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, int base, const float* __restrict__ B, int ldb, float alpha,
@@ -268,16 +268,18 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
         vec x;
         if constexpr (HOT) {
           // tagged colind (spmm_csr_hot_analysis): bit 31 marks a column whose B
-          // row is worth keeping in L2; every other row is streamed (nt), so the
-          // long tail of once-per-wave rows does not evict the hubs
-          // (buffer loads: the cache policy is an immediate of the intrinsic, so the two
-          // arms stay two instructions; plain loads were merged into one, nt dropped)
+          // row is worth keeping in L2 / MALL; every other row is streamed (nt), so
+          // the long tail of rarely used rows does not evict the hubs (products
+          // stand-in, K = 128: 4.30 -> 4.21 ms at the default 128-MB budget; sc0 /
+          // sc1 cold loads change nothing, nt on every row 6.5 ms: DESIGN.md §3b).
+          // Buffer loads: the cache policy is an immediate of the intrinsic, so the
+          // two arms stay two instructions (plain loads were merged, nt dropped).
           const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
               const_cast<float*>(rowp), 0, 0x7fffffff, 0x00020000);
           if (cr < 0)
             x = bload<VEC, 0>(rs, 4 * col_ld);
           else
-            x = bload<VEC, CA>(rs, 4 * col_ld);
+            x = bload<VEC, 2>(rs, 4 * col_ld);
         } else {
           x = vload<VEC>(rowp + col_ld);
         }
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
 // in G interleaved chains — within the fp32 bar, not bit-identical to the
 // sequential order (SPMM_CSR_SEQUENTIAL_ROWS keeps the main kernel).
 // Carries use the VEC = 1 fix-up (columns 0..31 of a slot).
-template <bool NT, int LPG, int PD>
+template <bool NT, int LPG, int PD, bool HOT = false>
 __global__ __launch_bounds__(kWG) void csr_group_kernel(
     int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, int base, const float* __restrict__ B, int ldb, float alpha,
@@ -446,6 +448,9 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
     }
   };
   auto load_b = [&](int c) {
+    // hot-tagged indices (spmm_csrmm_hot_f32): the tag is dropped here; each lane
+    // group gathers its own row, so a per-row policy would split every load in two
+    if constexpr (HOT) c &= 0x7fffffff;
     return *reinterpret_cast<const f32x4*>(Bb + (size_t)c * ldb + col_ld);
   };
   // One step's products: groups before a row end inside the step belong to
@@ -839,7 +844,7 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   dim3 block(kWG);
   const int slot = timing_begin(ctx);
   const bool nt = (ctx->csr_flags & SPMM_CSR_NT_STREAMS) != 0;
-  const bool grouped = !hot && n <= kGroupMaxK && n % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
+  const bool grouped = n <= kGroupMaxK && n % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
                       reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
                       reinterpret_cast<uintptr_t>(C) % 16 == 0 &&
                       (ctx->csr_flags & SPMM_CSR_SEQUENTIAL_ROWS) == 0;
@@ -850,7 +855,11 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
       return e ? atoi(e) : 0;
     }();
 #define SPMM_LAUNCH_GRP_PD(L, PD)                                                              \
-  if (nt)                                                                                      \
+  if (hot)                                                                                     \
+    hipLaunchKernelGGL((csr_group_kernel<true, L, PD, true>), g8, block, 0, ctx->stream, m, n,  \
+                       rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
+                       carry_row, nw);                                                          \
+  else if (nt)                                                                                 \
     hipLaunchKernelGGL((csr_group_kernel<true, L, PD>), g8, block, 0, ctx->stream, m, n,        \
                        rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
                        carry_row, nw);                                                          \
@@ -893,18 +902,7 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   hipLaunchKernelGGL((csr_mergepath_kernel<V, true, true>), grid, block, 0, ctx->stream, m, n, \
                      rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
                      carry_row, nw)
-#define SPMM_LAUNCH_HOTA(CA)                                                                   \
-  hipLaunchKernelGGL((csr_mergepath_kernel<2, true, true, CA>), grid, block, 0, ctx->stream, m, \
-                     n, rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,    \
-                     carry_row, nw)
-  static const int hot_aux = [] {
-    const char* e = getenv("SPMM_CSR_HOT_AUX");  // probe only: cache policy of cold rows
-    return e ? atoi(e) : 2;
-  }();
-  if (hot && vec == 2 && hot_aux != 2) {
-    if (hot_aux == 1) SPMM_LAUNCH_HOTA(1); else if (hot_aux == 16) SPMM_LAUNCH_HOTA(16);
-    else if (hot_aux == 18) SPMM_LAUNCH_HOTA(18); else SPMM_LAUNCH_HOTA(3);
-  } else if (hot) {
+  if (hot) {
     if (vec == 4) SPMM_LAUNCH_HOT(4); else if (vec == 2) SPMM_LAUNCH_HOT(2); else SPMM_LAUNCH_HOT(1);
   } else if (vec == 4) {
     if (nt) SPMM_LAUNCH_MP(4, true); else SPMM_LAUNCH_MP(4, false);
@@ -915,7 +913,6 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   }
 #undef SPMM_LAUNCH_MP
 #undef SPMM_LAUNCH_HOT
-#undef SPMM_LAUNCH_HOTA
   timing_end(ctx, slot);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return from_hip(e);
