@@ -689,6 +689,27 @@ def run_csr(args, W, world, rank, dev, dist):
                   "kernel": f"csr_mergepath_kernel<{vec}>" + (" (hot-column hints)" if hot else ""),
                   "kernel_ms": round(kms, 4), "kernel_ms_max_rank": round(kms_max, 4)},
         gen_seconds=round(t_gen, 2))
+    if (not hot and world == 1 and nch == 1 and args.csr_layout != "col"
+            and args.workload == "products_csr" and not args.no_hot_side):
+        # Beside the drop-in line (not `value`): the same product on the
+        # hot-column cache hints, analysis once, timed apart.
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d_tag = ops.csr_hot_analysis(d_ci, n=K, k=n, handle=h)
+        torch.cuda.synchronize()
+        a_ms = (time.perf_counter() - t0) * 1e3
+
+        def step_hot():
+            ops.csrmm_hot(d_rp, d_tag, d_v, B, m=shard.rows, n=K, k=n, ldb=K, C=C_slot, ldc=K,
+                          handle=h)
+        e_hot, kt_hot = timed_loop(step_hot, h, args.steps, args.warmup, world, dist, raw=True)
+        k_hot = float(np.sum(kt_hot)) / args.steps if kt_hot else float("nan")
+        rec["hot_column_hints"] = {
+            "entry": "spmm_csr_hot_analysis once + spmm_csrmm_hot_f32 per step (bit-identical C)",
+            "value": round(2.0 * nnz * K * args.steps / e_hot / 1e9, 2), "unit": "GFLOP/s",
+            "ms_per_step": round(e_hot / args.steps * 1e3, 4), "kernel_ms": round(k_hot, 4),
+            "analysis_ms_first_call": round(a_ms, 3),
+            "frac_algorithmic": csr_roofline(shard.rows, shard.colind, K, k_hot)["frac"]}
     if hot:
         rec["analysis_ms"] = round(analysis_ms, 4)
         rec["hot_gather_share"] = round(hot_share, 4)
@@ -1058,6 +1079,8 @@ def main() -> None:
                     help="B/C storage for CSR workloads (col = cusparseScsrmm, run_csrmm.cu)")
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--csr-options", type=int, default=None, help="SPMM_CSR_* flags")
+    ap.add_argument("--no-hot-side", action="store_true",
+                    help="skip the hot-column side measurement of the products_csr line")
     ap.add_argument("--chunks", type=int, default=0,
                     help="row chunks per rank whose all-gathers overlap the next chunk's compute "
                          "(default 4 when N > 1; 1 = compute, then one all-gather; > 1 at N = 1 "

@@ -45,7 +45,16 @@ def main():
         if bs == 32:
             Bn = B[:n].contiguous()
             bad += check("csr K=128", lambda: ops.gespmm_csrmm(drp, dci, dv, Bn), reps)
-            del Bn
+            tag = ops.csr_hot_analysis(dci, n=K, k=n)
+            bad += check("csr hot-column tags", lambda: ops.csr_hot_analysis(dci, n=K, k=n), 2)
+            Ch = torch.empty((n, K), device=dev)
+
+            def run_hot():
+                ops.csrmm_hot(drp, tag, dv, Bn, n=K, k=n, ldb=K, C=Ch, ldc=K)
+                return Ch
+            bad += check("csr K=128 (hot-column hints)", run_hot, reps)
+            bad += int((run_hot() != ops.gespmm_csrmm(drp, dci, dv, Bn)).sum())
+            del Bn, tag, Ch
         bad += check(f"csr2bsr bs={bs} (values)",
                      lambda: ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)[2], 2)
         brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
