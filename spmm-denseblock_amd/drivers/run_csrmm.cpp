@@ -2,7 +2,8 @@
 // Reference CLI of run_csrmm.cu:46-171 on the HIP engine. Reads
 // tmp/<graph>_indptr.txt / _indices.txt, values 1.0, B = randomDenseMatrix
 // (mt19937_64 seeded 1234), times 10 epochs with events on stream 0 and
-// prints the reference's lines. impl: gespmm (gespmm_csrmm<float>),
+// prints the reference's lines. impl: gespmm (gespmm_csrmm<float>), gespmm_hot
+// (the same layout on hot-column hints, tagged once before the epochs),
 // cusparseScsrmm (col-major B and C), cusparseScsrmm2 (transposeB picks the
 // B layout, col-major C) — all served by libspmm_hip.so.
 // --gpus N (impl gespmm; not in the reference, which is single-GPU): the rows
@@ -120,7 +121,7 @@ int main(int argc, char* argv[]) {
   argc = (int)pos.size();
   argv = pos.data();
   if (argc < 5) {
-    printf("usage: %s <graph> <dim> <gespmm|cusparseScsrmm|cusparseScsrmm2> <transposeB> "
+    printf("usage: %s <graph> <dim> <gespmm|gespmm_hot|cusparseScsrmm|cusparseScsrmm2> <transposeB> "
            "[--gpus N] [--chunks C]\n",
            argv[0]);
     return 1;
@@ -171,11 +172,22 @@ int main(int argc, char* argv[]) {
   // For the cuSPARSE-shaped impls a column-major B of the same values is
   // needed (transposeB == 0); gespmm always reads B row-major.
   float* d_yc = nullptr;
-  if (impl != "gespmm" && transposeB == 0) {
+  if (impl != "gespmm" && impl != "gespmm_hot" && transposeB == 0) {
     std::vector<float> yc((size_t)n * dim);
     for (int r = 0; r < n; ++r)
       for (int c = 0; c < dim; ++c) yc[(size_t)c * n + r] = y[(size_t)r * dim + c];
     d_yc = mem.upload(yc.data(), yc.size());
+  }
+  // gespmm_hot (not in the reference): gespmm's layout on hot-column cache hints,
+  // the columns tagged once before the epochs (spmm_csr_hot_analysis)
+  int* d_ci_hot = nullptr;
+  if (impl == "gespmm_hot") {
+    d_ci_hot = mem.alloc<int>(ci.size());
+    EventTimer ta;
+    ta.start();
+    HANDLE_SPMM_ERROR(spmm_csr_hot_analysis(handle, dim, n, nnz, d_ci, SPMM_INDEX_BASE_ZERO, 0,
+                                            d_ci_hot));
+    printf("hot-column analysis time: %3.10f ms\n", ta.stop_ms());
   }
   printf("csrmm...\n");
   const int epoch = 10;
@@ -185,6 +197,10 @@ int main(int argc, char* argv[]) {
     tm.start();
     if (impl == "gespmm") {
       gespmm_csrmm<float>(n, dim, d_rp, d_ci, d_val, d_y, d_z);
+    } else if (impl == "gespmm_hot") {
+      HANDLE_SPMM_ERROR(spmm_csrmm_hot_f32(handle, n, dim, n, nnz, 1.f, d_rp, d_ci_hot, d_val,
+                                           SPMM_INDEX_BASE_ZERO, d_y, dim, SPMM_ORDER_ROW, 0.f,
+                                           d_z, dim, SPMM_ORDER_ROW));
     } else if (impl == "cusparseScsrmm") {
       assert(transposeB == 0);
       HANDLE_SPMM_ERROR(spmm_scsrmm(handle, SPMM_OPERATION_NON_TRANSPOSE, n, dim, n, nnz, &alpha,
@@ -209,7 +225,7 @@ int main(int argc, char* argv[]) {
   {  // C back to the host, row-major (the cusparse forms write it col-major)
     std::vector<float> zc((size_t)n * dim), z((size_t)n * dim);
     HANDLE_ERROR(hipMemcpy(zc.data(), d_z, zc.size() * sizeof(float), hipMemcpyDeviceToHost));
-    if (impl == "gespmm") z = zc;
+    if (impl == "gespmm" || impl == "gespmm_hot") z = zc;
     else
       for (int r = 0; r < n; ++r)
         for (int c = 0; c < dim; ++c) z[(size_t)r * dim + c] = zc[(size_t)c * n + r];

@@ -90,7 +90,7 @@ def test_rabbit_reorder_cli(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("impl,tb", [("gespmm", 0), ("cusparseScsrmm", 0),
+@pytest.mark.parametrize("impl,tb", [("gespmm", 0), ("gespmm_hot", 0), ("cusparseScsrmm", 0),
                                      ("cusparseScsrmm2", 1)])
 def test_run_csrmm_cli(tmp_path, impl, tb):
     """run_csrmm.cu:46-171's CLI and lines, and its C checked against the
@@ -103,6 +103,8 @@ def test_run_csrmm_cli(tmp_path, impl, tb):
     out = _run(["run_csrmm", "pl", 64, impl, tb], tmp_path, env={"SPMM_DRIVER_DUMP": dump})
     assert "n=20000 nnz=200000" in out and "average csrmm cost time" in out
     assert out.rstrip().endswith("end")
+    if impl == "gespmm_hot":
+        assert "hot-column analysis time" in out
     prep.rng_seed(1234)
     B = prep.random_dense_matrix(20000, 64)
     _check_dump(dump, rp, ci, B, f"run_csrmm {impl}")
