@@ -82,6 +82,10 @@ def test_status_strings_and_host_side_checks():
     assert L.spmm_bsr32_analysis_f32(None, 0, 4, None, None, None) == 1
     assert L.spmm_bsrmm_analysed_f32(None, 1, 1, 4, 1, 1.0, None, None, None, None, None, 4, 0,
                                      0.0, None, 4, 0) == 1
+    # the hot-column CSR entries likewise
+    assert L.spmm_csr_hot_analysis(None, 128, 4, 4, None, 0, 0, None) == 1
+    assert L.spmm_csrmm_hot_f32(None, 1, 1, 1, 0, 1.0, None, None, None, 0, None, 1, 0, 0.0,
+                                None, 1, 0) == 1
     d = ctypes.c_void_p()
     assert L.spmm_create_mat_descr(ctypes.byref(d)) == 0
     assert L.spmm_set_mat_index_base(d, 1) == 0
