@@ -662,7 +662,7 @@ def run_csr(args, W, world, rank, dev, dist):
     elapsed, kms_max = float(t[0]), float(t[1])
     crf = csr_roofline(shard.rows, shard.colind, K, kms)
     traffic = None
-    hot_bytes = os.path.join(ROOT, "profiles", "r03_final_b", "pmcb", "csr_bytes.jsonl")
+    hot_bytes = os.path.join(ROOT, "profiles", "r03_final_c", "pmcb", "csr_bytes.jsonl")
     if hot and K == W["K"] and nnz == W["nnz"] and world == 1 and os.path.exists(hot_bytes):
         # counter bytes of the hot kernel on this workload's own shape (tools/pmc_bytes.sh)
         with open(hot_bytes) as f:

@@ -38,6 +38,11 @@ spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, f
 
   const float* Bx = B;
   int ldbx = ldb;
+  // hot-tagged indices: one buffer resource for all of B when every row offset
+  // fits 32 bits (the kernel then passes the row in soffset)
+  auto hot_mode = [&](int ld) {
+    return !hot ? 0 : ((long long)(k + base) * ld + n) * 4 + 64 < (1ll << 32) ? 2 : 1;
+  };
   if (orderB == SPMM_ORDER_COL) {
     // B (k x n col-major) is an (n x k) row-major matrix with ld ldb.
     float* Bt = reinterpret_cast<float*>(ws + L.b_off);
@@ -48,11 +53,11 @@ spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, f
   }
   if (orderC == SPMM_ORDER_ROW) {
     return launch_csrmm_rowmajor(ctx, m, n, rowptr, colind, val, base, Bx, ldbx, alpha, beta, C,
-                                 ldc, carry_val, carry_row, nnz_hint, hot);
+                                 ldc, carry_val, carry_row, nnz_hint, hot_mode(ldbx));
   }
   float* Ct = reinterpret_cast<float*>(ws + L.c_off);
   st = launch_csrmm_rowmajor(ctx, m, n, rowptr, colind, val, base, Bx, ldbx, alpha, 0.f, Ct, n,
-                             carry_val, carry_row, nnz_hint, hot);
+                             carry_val, carry_row, nnz_hint, hot_mode(ldbx));
   if (st != SPMM_STATUS_SUCCESS) return st;
   // C (m x n col-major, ldc) is an (n x m) row-major matrix with ld ldc.
   return launch_transpose(ctx, m, n, Ct, n, C, ldc, beta);

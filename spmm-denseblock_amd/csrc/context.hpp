@@ -80,7 +80,7 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
                                     const int* colind, const float* val, int base,
                                     const float* B, int ldb, float alpha, float beta, float* C,
                                     int ldc, float* carry_val, int* carry_row, int nnz_hint,
-                                    bool hot = false);
+                                    int hot = 0);  // 1: hot-tagged colind; 2: and B below 4 GB
 // spmm_csr_hot_analysis: colind_out = colind with bit 31 set on hot columns
 spmm_status_t launch_csr_hot_analysis(spmm_context* ctx, int k, long long nnz, const int* colind,
                                       int base, long long hot_rows, int* colind_out);

@@ -179,3 +179,38 @@ def test_hot_status_codes(device):
                                 None, 1, 0) == NOT_INITIALIZED
     assert L.spmm_csrmm_hot_f32(h.raw, -1, 1, 1, 0, 1.0, None, None, None, 0, None, 1, 0, 0.0,
                                 None, 1, 0) == INVALID_VALUE
+
+
+def test_hot_per_row_resource_beyond_4gb(device):
+    """B whose row offsets pass 4 GB (k * ldb * 4 > 2^32): the kernel then builds a
+    buffer resource per row (HOT = 1) instead of one for all of B with the row in
+    soffset (HOT = 2). Bit-identical to the plain kernel; fp64 reference on the GPU."""
+    ops = _ops()
+    m, k, n, ldb, nnz = 20000, 1_100_000, 128, 1024, 200_000
+    g = torch.Generator(device=device)
+    g.manual_seed(7)
+    B = torch.rand((k, ldb), device=device, generator=g) * 2 - 1  # 4.5 GB
+    rows = torch.sort(torch.randint(0, m, (nnz,), device=device, generator=g)).values
+    ci = torch.randint(0, k, (nnz,), device=device, generator=g, dtype=torch.int32)
+    ci[:50] = k - 1  # the last rows of B, past the 4-GB offset
+    rows[:50] = 0
+    rows = torch.sort(rows).values
+    rp = torch.zeros(m + 1, dtype=torch.int64, device=device)
+    rp[1:] = torch.cumsum(torch.bincount(rows, minlength=m), 0)
+    rp = rp.to(torch.int32)
+    v = torch.rand(nnz, device=device, generator=g) * 2 - 1
+    tag = ops.csr_hot_analysis(ci, n=n, k=k, hot_bytes=20000 * 512)
+    assert 0 < int((tag < 0).sum()) < nnz
+    C1 = torch.empty((m, n), device=device)
+    C2 = torch.empty((m, n), device=device)
+    ops.csrmm(rp, ci, v, B, n=n, k=k, ldb=ldb, C=C1, ldc=n)
+    ops.csrmm_hot(rp, tag, v, B, n=n, k=k, ldb=ldb, C=C2, ldc=n)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2)
+    ref = torch.zeros((m, n), dtype=torch.float64, device=device)
+    ref.index_add_(0, rows, v.double()[:, None] * B[ci.long(), :n].double())
+    absd = torch.zeros_like(ref).index_add_(0, rows, (v.double()[:, None] *
+                                                      B[ci.long(), :n].double()).abs())
+    assert_normwise(C2.cpu().numpy(), ref.cpu().numpy(), absd.cpu().numpy(), TOL_F32,
+                    "hot csrmm, B past 4 GB")
+    del B

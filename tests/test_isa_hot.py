@@ -36,10 +36,17 @@ def _bodies(asm: str, pattern: str) -> dict[str, str]:
     return out
 
 
+def _hot_mode(name: str) -> int:
+    # csr_mergepath_kernel<VEC, NT, HOT>: mangled ...ILi<VEC>ELb<NT>ELi<HOT>EE...
+    m = re.search(r"ILi(\d)ELb([01])ELi(\d)EE", name)
+    assert m, name
+    return int(m.group(3))
+
+
 def test_hot_kernels_keep_both_policies(csr_asm):
-    # csr_mergepath_kernel<VEC, NT = true, HOT = true>: mangled ...ILi{1,2,4}ELb1ELb1E...
-    hot = {k: v for k, v in _bodies(csr_asm, "csr_mergepath_kernel").items() if "ELb1ELb1E" in k}
-    assert len(hot) == 3, f"expected VEC 1 / 2 / 4 hot instantiations, found {sorted(hot)}"
+    # HOT = 1 (a resource per row) and HOT = 2 (one resource, the row in soffset)
+    hot = {k: v for k, v in _bodies(csr_asm, "csr_mergepath_kernel").items() if _hot_mode(k)}
+    assert len(hot) == 6, f"expected VEC 1 / 2 / 4 x HOT 1 / 2 instantiations, found {sorted(hot)}"
     for name, body in hot.items():
         loads = re.findall(r"^\s*buffer_load_dword\S*\s[^\n]*$", body, re.M)
         nt = [ln for ln in loads if re.search(r"\bnt\b", ln)]
@@ -50,7 +57,7 @@ def test_hot_kernels_keep_both_policies(csr_asm):
 
 def test_plain_kernels_have_no_buffer_gathers(csr_asm):
     plain = {k: v for k, v in _bodies(csr_asm, "csr_mergepath_kernel").items()
-             if "ELb1ELb1E" not in k}
+             if not _hot_mode(k)}
     assert plain
     for name, body in plain.items():
         assert "buffer_load" not in body, f"{name}: the plain kernel changed its gathers"
