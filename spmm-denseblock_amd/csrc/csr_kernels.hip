@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
           // tagged colind (spmm_csr_hot_analysis): bit 31 marks a column whose B
           // row is worth keeping in L2 / MALL; every other row is streamed (nt), so
           // the long tail of rarely used rows does not evict the hubs (products
-          // stand-in, K = 128: 4.30 -> 4.21 ms at the default 128-MB budget; sc0 /
+          // stand-in, K = 128: 4.29 -> 4.14 ms at the default 128-MB budget; sc0 /
           // sc1 cold loads change nothing, nt on every row 6.5 ms: DESIGN.md §3b).
           // Buffer loads: the cache policy is an immediate of the intrinsic, so the
           // two arms stay two instructions (plain loads were merged, nt dropped).
