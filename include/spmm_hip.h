@@ -156,7 +156,9 @@ spmm_status_t spmm_csrmm_ex_f32(spmm_handle_t handle, int m, int n, int k, int n
  * hot = among the columns with the most nonzeros whose gathered B-row pieces
  * (n floats, at most one merge-path column tile) fit in hotBytes (0 = the
  * default below: half the 256-MB MALL). Requires column indices < 2^31 - 1.
- * Caller-owned output (nnz ints); scratch comes from the handle. */
+ * Caller-owned output (nnz ints); scratch comes from the handle. The tagged
+ * array is input for spmm_csrmm_hot_f32 only: every other entry reads it as
+ * negative (out-of-range) column indices. */
 #define SPMM_CSR_HOT_BYTES_DEFAULT (128ll << 20)
 spmm_status_t spmm_csr_hot_analysis(spmm_handle_t handle, int n, int k, int nnz,
                                     const int* csrColInd, spmm_index_base_t base,
