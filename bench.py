@@ -103,6 +103,23 @@ METRIC = "SpMM GFLOP/s (2*nnz*K/t) + achieved HBM GB/s, ogbn-products K=128"
 
 
 BSR_TRAFFIC = os.path.join(ROOT, "profiles", "r03_pmc_bytes", "bytes.jsonl")
+# counter bytes of the CSR kernels per workload (tools/pmc_bytes.sh)
+CSR_TRAFFIC = os.path.join(ROOT, "profiles", "r03_final_c", "pmcb", "csr_bytes.jsonl")
+
+
+def csr_counter_bytes(workload: str):
+    """PMC bytes per launch (FETCH_SIZE x calibration + WRITE_SIZE) recorded
+    for a CSR workload's kernel in CSR_TRAFFIC, else None."""
+    rec = None
+    try:
+        with open(CSR_TRAFFIC) as f:
+            for line in f:
+                r = json.loads(line)
+                if r.get("workload") == workload:
+                    rec = r.get("counter_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+    return rec
 
 
 def kernel_source_tag() -> str:
@@ -114,6 +131,15 @@ def kernel_source_tag() -> str:
             return hashlib.sha256(f.read()).hexdigest()[:16]
     except OSError:
         return "unknown"
+
+
+def bsr_variant() -> str:
+    """The BSR kernel variant the library runs: SPMM_BSR_VARIANT only in a
+    TUNING build (spmm_get_build_options), which alone reads it."""
+    from spmm_hip import _lib
+    if _lib.lib().spmm_get_build_options() & _lib.BUILD_TUNING:
+        return os.environ.get("SPMM_BSR_VARIANT", "default")
+    return "default"
 
 
 def bsr_traffic(key: dict):
@@ -662,14 +688,9 @@ def run_csr(args, W, world, rank, dev, dist):
     elapsed, kms_max = float(t[0]), float(t[1])
     crf = csr_roofline(shard.rows, shard.colind, K, kms)
     traffic = None
-    hot_bytes = os.path.join(ROOT, "profiles", "r03_final_c", "pmcb", "csr_bytes.jsonl")
-    if hot and K == W["K"] and nnz == W["nnz"] and world == 1 and os.path.exists(hot_bytes):
+    if hot and K == W["K"] and nnz == W["nnz"] and world == 1:
         # counter bytes of the hot kernel on this workload's own shape (tools/pmc_bytes.sh)
-        with open(hot_bytes) as f:
-            for line in f:
-                r = json.loads(line)
-                if r.get("workload") == args.workload:
-                    traffic = r.get("counter_bytes_per_launch")
+        traffic = csr_counter_bytes(args.workload)
         if traffic and crf.get("gather_model_GBps"):
             # The gather rate passed the peak (MALL-served re-reads), and the
             # compulsory model (~3 GB) says nothing about this kernel: its own
@@ -678,7 +699,8 @@ def run_csr(args, W, world, rank, dev, dist):
             crf.update(achieved=round(traffic / t_s / 1e9, 1),
                        frac=round(traffic / t_s / 1e9 / HBM_PEAK_GBPS, 4),
                        bytes_model=("counter bytes of this kernel on this shape (FETCH_SIZE x "
-                                    "calibration + WRITE_SIZE, profiles/r03_final_c/pmcb)"),
+                                    "calibration + WRITE_SIZE, " +
+                                    os.path.relpath(CSR_TRAFFIC, ROOT) + ")"),
                        compulsory_bytes=crf["algorithmic_bytes_per_launch"],
                        algorithmic_bytes_per_launch=crf["gather_model_bytes"],
                        gather_model_frac=round(crf["gather_model_GBps"] / HBM_PEAK_GBPS, 4))
@@ -724,15 +746,24 @@ def run_csr(args, W, world, rank, dev, dist):
                           handle=h)
         e_hot, kt_hot = timed_loop(step_hot, h, args.steps, args.warmup, world, dist, raw=True)
         k_hot = float(np.sum(kt_hot)) / args.steps if kt_hot else float("nan")
-        rec["hot_column_hints"] = {
+        side = {
             "entry": "spmm_csr_hot_analysis once + spmm_csrmm_hot_f32 per step (bit-identical C)",
             "value": round(2.0 * nnz * K * args.steps / e_hot / 1e9, 2), "unit": "GFLOP/s",
             "ms_per_step": round(e_hot / args.steps * 1e3, 4), "kernel_ms": round(k_hot, 4),
             "analysis_ms_first_call": round(a_ms, 3),
-            # SURVEY 8(d)'s gather model (one B row per nonzero); above 1 where the
-            # MALL serves the re-reads
-            "gather_model_frac": round(csr_bytes(shard.rows, int(shard.colind.size), K) /
-                                       (k_hot / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
+            # SURVEY 8(d)'s gather model (one B row per nonzero) passes the peak
+            # here (the MALL serves the re-reads), so it is a rate, not a fraction
+            "gather_model_GBps": round(csr_bytes(shard.rows, int(shard.colind.size), K) /
+                                       (k_hot / 1e3) / 1e9, 1)}
+        hot_tr = csr_counter_bytes("products_csr_hot")
+        if hot_tr:
+            # the roofline of this kernel: its own counter bytes, as products_csr_hot
+            side.update(counter_bytes_per_launch=hot_tr,
+                        achieved=round(hot_tr / (k_hot / 1e3) / 1e9, 1),
+                        frac=round(hot_tr / (k_hot / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                        bytes_model="counter bytes of the hot kernel (" +
+                                    os.path.relpath(CSR_TRAFFIC, ROOT) + ")")
+        rec["hot_column_hints"] = side
     if hot:
         rec["analysis_ms"] = round(analysis_ms, 4)
         rec["hot_gather_share"] = round(hot_share, 4)
@@ -919,7 +950,7 @@ def run_bsr(args, W, world, rank, dev, dist):
               "bsr16_cm_kernel") if cm else f"bsr{bs} register-fragment kernel")
     tkey = {"workload": args.workload, "kernel": kname, "K": K, "dtype": dt, "nnzb": nnzb,
             "layout_BC": args.bsr_layout,
-            "variant": os.environ.get("SPMM_BSR_VARIANT", "default"),
+            "variant": bsr_variant(),
             "kernel_src": kernel_source_tag()}
     rec = dict(
         value=2.0 * nnz * K * args.steps / elapsed / 1e9, ms_per_step=elapsed / args.steps * 1e3,
@@ -971,6 +1002,40 @@ def run_bsr(args, W, world, rank, dev, dist):
         rec["roofline"]["traffic_GBps"] = round(tr / t / 1e9, 1)
         rec["roofline"]["traffic_frac"] = round(tr / t / 1e9 / HBM_PEAK_GBPS, 4)
         rec["roofline"]["traffic_over_compulsory"] = round(tr / comp_bytes, 3)
+    if (not an and args.bsr_layout == "row" and not args.no_analysed_side and
+            (bs, dt) in ((32, "fp32"), (16, "fp16"))):
+        # Beside the drop-in line (not `value`): the same product on the analysed
+        # entry (column masks + column-major A once per matrix, timed apart).
+        del d_rp, d_ci, d_v, B32, C2
+        masks = torch.empty(nnzb, dtype=torch.int32, device=dev)
+        vcol = torch.empty(nnzb * bs * bs, dtype=tdt, device=dev)
+        analysis = ops.bsr32_analysis if bs == 32 else ops.bsr16_analysis
+        product = ops.bsrmm_analysed if bs == 32 else ops.bsrmm_analysed_f16
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        analysis(d_bv, nnzb=nnzb, masks=masks, val_col=vcol, handle=h)
+        torch.cuda.synchronize()
+        a_ms = (time.perf_counter() - t0) * 1e3
+        del d_bv
+        e_an, k_an = timed_loop(
+            lambda: product(d_brp, d_bci, vcol, masks, B, mb=mb, kb=mb, n=K, ldb=K, C=C, ldc=K,
+                            handle=h), h, args.steps, args.warmup, 1, dist)
+        a_bytes_an = 4 * nnzb + s * active_cols * bs
+        comp_an = (ntiles * (4 * (mb + 1) + 4 * nnzb + a_bytes_an) + s * b_rows * K +
+                   4 * mb * bs * K)
+        t_an = k_an / 1e3
+        rec["analysed_entry"] = {
+            "entry": ("spmm_bsr32_analysis_f32 once + spmm_bsrmm_analysed_f32 per step" if bs == 32
+                      else "spmm_bsr16_analysis_f16 once + spmm_bsrmm_analysed_f16 per step"),
+            "value": round(2.0 * nnz * K * args.steps / e_an / 1e9, 2), "unit": "GFLOP/s",
+            "ms_per_step": round(e_an / args.steps * 1e3, 4), "kernel_ms": round(k_an, 4),
+            "analysis_ms_first_call": round(a_ms, 3),
+            "bytes_per_launch": comp_an,
+            "achieved": round(comp_an / t_an / 1e9, 1),
+            "frac": round(comp_an / t_an / 1e9 / HBM_PEAK_GBPS, 4),
+            "bytes_model": "compulsory, analysed: masks + the nonzero columns' values",
+            "mfma_executed_TFLOPs": round(mfma_flops / t_an / 1e12, 2),
+            "mfma_frac": round(mfma_flops / t_an / 1e12 / peak, 4)}
     return rec, None
 
 
@@ -1037,7 +1102,7 @@ def run_hybrid(args, W, world, rank, dev, dist):
     kname = ("bsr32_f32_lds_kernel" if fused else "bsr MFMA kernel + csr_mergepath")
     tkey = {"workload": args.workload, "kernel": kname, "K": K, "dtype": "fp32", "nnzb": nb,
             "csr_remainder_nnz": nc, "hybrid_options": hopt,
-            "variant": os.environ.get("SPMM_BSR_VARIANT", "default"),
+            "variant": bsr_variant(),
             "kernel_src": kernel_source_tag()}
     rec = dict(
         value=useful * args.steps / elapsed / 1e9, ms_per_step=ms, dtype="fp32",
@@ -1104,6 +1169,8 @@ def main() -> None:
     ap.add_argument("--csr-options", type=int, default=None, help="SPMM_CSR_* flags")
     ap.add_argument("--no-hot-side", action="store_true",
                     help="skip the hot-column side measurement of the products_csr line")
+    ap.add_argument("--no-analysed-side", action="store_true",
+                    help="skip the analysed-entry side measurement of the bs 32 / bs 16 fp16 lines")
     ap.add_argument("--chunks", type=int, default=0,
                     help="row chunks per rank whose all-gathers overlap the next chunk's compute "
                          "(default 4 when N > 1; 1 = compute, then one all-gather; > 1 at N = 1 "

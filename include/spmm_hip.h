@@ -107,6 +107,36 @@ spmm_status_t spmm_set_csr_waves_per_cu(spmm_handle_t handle, int waves_per_cu);
 #define SPMM_CSR_SEQUENTIAL_ROWS 2
 spmm_status_t spmm_set_csr_options(spmm_handle_t handle, int flags);
 
+/* BSR kernel options (bit flags, per handle).
+ *
+ * The default contract of the BSR entries at bs 16 / 32 (the column streams,
+ * DESIGN.md §4) is COLUMN-GRANULAR: a column of a stored block whose values
+ * are all +-0 is skipped; every other column multiplies whole, its explicit
+ * zeros included. With finite B this is the dense block product exactly. With
+ * an inf / NaN in B row J*bs + c, rows of block row I get a non-finite value
+ * from it iff a stored block (I, J) holds a value other than +-0 in its
+ * column c: then every row of block row I does (0 * inf = NaN for the rows
+ * whose entry is an explicit zero), and if column c is all zeros none does.
+ *
+ * SPMM_BSR_DENSE_BLOCK_PRODUCT: cusparseSbsrmm's dense-block semantics
+ * (bsrmm.cu:141-144): every stored block multiplies as a dense
+ * bs x bs matrix, so an inf / NaN in B row J*bs + c reaches every row of every
+ * block row that stores a block (I, J), whatever that block's column c holds.
+ * Runs the full-panel kernels (bs 32 ROW blocks, row-major B: the LDS-staged
+ * MFMA kernel the hybrid uses for dense blocks; otherwise the register-
+ * fragment MFMA kernels) for spmm_bsrmm_ex_f32 / _f16, spmm_sbsrmm, the
+ * analysed entries (which then ignore the masks) and the hybrid's BSR part.
+ * Same result as the default on finite inputs, within the fp32 bar. */
+#define SPMM_BSR_DENSE_BLOCK_PRODUCT 1
+spmm_status_t spmm_set_bsr_options(spmm_handle_t handle, int flags);
+
+/* Build options of the loaded library (bit flags): SPMM_BUILD_TUNING is set
+ * in an A/B build (make TUNING=1), whose kernel choice the environment may
+ * override (SPMM_BSR_VARIANT, SPMM_BSR_ORDER, SPMM_CSR_GROUP_PD); a release
+ * build reads no environment variable. */
+#define SPMM_BUILD_TUNING 1
+int spmm_get_build_options(void);
+
 /* ------------------------------------------------------------------------ */
 /* Path A: CSR x dense                                                         */
 /* ------------------------------------------------------------------------ */
@@ -156,6 +186,10 @@ spmm_status_t spmm_csrmm_ex_f32(spmm_handle_t handle, int m, int n, int k, int n
  * hot = among the columns with the most nonzeros whose gathered B-row pieces
  * (n floats, at most one merge-path column tile) fit in hotBytes (0 = the
  * default below: half the 256-MB MALL). Requires column indices < 2^31 - 1.
+ * The piece size assumes 16-B aligned B and C with ld % 4 == 0 (the layout
+ * the kernel gathers 2 or 4 floats per lane from); with a misaligned B the
+ * kernel gathers one float per lane and the hot set is up to 4x smaller than
+ * hotBytes (results are unaffected: the tags are cache hints only).
  * Caller-owned output (nnz ints); scratch comes from the handle. The tagged
  * array is input for spmm_csrmm_hot_f32 only: every other entry reads it as
  * negative (out-of-range) column indices. */
@@ -215,8 +249,9 @@ spmm_status_t spmm_bsrmm_ex_f32(spmm_handle_t handle, spmm_direction_t dir, int 
  *             (NaN and inf count), nnzb words;
  *   valCol    dir = ROW: a column-major copy of the blocks, nnzb * 1024 floats
  *             (may be null for dir = COLUMN, whose blocks already are).
- * Caller-owned buffers. INVALID_VALUE for a bad dir, nnzb < 0 or a null
- * pointer that is needed. */
+ * Caller-owned buffers. INVALID_VALUE for a bad dir, nnzb < 0, a null
+ * pointer that is needed, or a valCol that overlaps bsrVal (the analysis
+ * reads whole blocks while it scatters their columns: no in-place form). */
 spmm_status_t spmm_bsr32_analysis_f32(spmm_handle_t handle, spmm_direction_t dir, int nnzb,
                                       const float* bsrVal, unsigned* masks, float* valCol);
 
@@ -234,7 +269,7 @@ spmm_status_t spmm_bsrmm_analysed_f32(spmm_handle_t handle, int mb, int kb, int 
                                       int ldc, spmm_order_t orderC);
 
 /* The same analysis for bs = 16 fp16 blocks: masks[k] bit c (c < 16), and for
- * ROW blocks a column-major fp16 copy (nnzb * 256 halves). */
+ * ROW blocks a column-major fp16 copy (nnzb * 256 halves); same checks. */
 spmm_status_t spmm_bsr16_analysis_f16(spmm_handle_t handle, spmm_direction_t dir, int nnzb,
                                       const uint16_t* bsrVal, unsigned* masks, uint16_t* valCol);
 
@@ -406,7 +441,7 @@ spmm_status_t spmm_dbsrmm(spmm_handle_t handle, spmm_direction_t dir, spmm_opera
  * so non-finite values propagate as in the fp32 path. The flag takes effect
  * only on the bs = 32 LDS-staged forms: the fused launch, and the two-launch
  * BSR part when n % 4 == 0, ldb % 4 == 0 and B / bsrVal are 16-byte aligned;
- * elsewhere (bs != 32, other layouts, a tuning SPMM_BSR_VARIANT override) the
+ * elsewhere (bs != 32, other layouts) the
  * dense-block part runs the plain fp32 MFMA kernel, with the same result
  * within the fp32 bar. */
 #define SPMM_HYBRID_SPLIT_BF16 4

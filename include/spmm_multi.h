@@ -49,12 +49,15 @@ typedef struct spmm_multi* spmm_multi_t;
 spmm_status_t spmm_multi_create(spmm_multi_t* ctx, int ngpu, const int* devices);
 spmm_status_t spmm_multi_destroy(spmm_multi_t ctx);
 int spmm_multi_size(spmm_multi_t ctx);
-/* Stream ordering with the caller: streams[p] (a hipStream_t on device p,
- * or NULL = none) for every part, kept until changed; NULL clears all.
- * When set, spmm_csr_f32_multi first makes part p's compute stream wait for
- * the work already queued on streams[p] (the producers of B, the CSR arrays
- * and C), and at the end makes streams[p] wait for part p's last
- * all-gather, so work queued on streams[p] afterwards sees all of C. */
+/* Stream ordering with the caller for the NEXT spmm_csr_f32_multi call:
+ * streams[p] is a hipStream_t on device p, a NULL entry being device p's
+ * legacy null (default) stream; streams == NULL means no ordering. That
+ * call first makes part p's compute stream wait for the work already queued
+ * on streams[p] (the producers of B, the CSR arrays and C), and at the end
+ * makes streams[p] wait for part p's last all-gather, so work queued on
+ * streams[p] afterwards sees all of C. The call then forgets the streams
+ * (set them again before every call that needs the ordering), so no handle
+ * is kept past the call it was given for. */
 spmm_status_t spmm_multi_set_user_streams(spmm_multi_t ctx, void* const* streams);
 /* The compute stream of part p (a hipStream_t; the call's results on device
  * p are complete once this stream is). */

@@ -94,6 +94,12 @@ spmm_status_t bsrmm_staged(spmm_context* ctx, int kb, int n, int bs, const T* B,
   return launch(Bt, n);
 }
 
+// [a, a + bytes) and [b, b + bytes) share a byte
+bool overlaps(const void* a, const void* b, size_t bytes) {
+  const uintptr_t x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
+  return x < y + bytes && y < x + bytes;
+}
+
 }  // namespace
 
 extern "C" {
@@ -249,6 +255,8 @@ spmm_status_t spmm_bsr32_analysis_f32(spmm_handle_t handle, spmm_direction_t dir
   if (!bsrVal || !masks || (dir == SPMM_DIRECTION_ROW && !valCol))
     return SPMM_STATUS_INVALID_VALUE;
   if (reinterpret_cast<uintptr_t>(bsrVal) % 16 != 0) return SPMM_STATUS_INVALID_VALUE;
+  if (dir == SPMM_DIRECTION_ROW && overlaps(bsrVal, valCol, (size_t)nnzb * 1024 * sizeof(float)))
+    return SPMM_STATUS_INVALID_VALUE;
   return launch_bsr32_analysis(handle, dir, nnzb, bsrVal, masks, valCol);
 }
 
@@ -285,6 +293,8 @@ spmm_status_t spmm_bsr16_analysis_f16(spmm_handle_t handle, spmm_direction_t dir
   if (!bsrVal || !masks || (dir == SPMM_DIRECTION_ROW && !valCol))
     return SPMM_STATUS_INVALID_VALUE;
   if (reinterpret_cast<uintptr_t>(bsrVal) % 8 != 0) return SPMM_STATUS_INVALID_VALUE;
+  if (dir == SPMM_DIRECTION_ROW && overlaps(bsrVal, valCol, (size_t)nnzb * 256 * sizeof(uint16_t)))
+    return SPMM_STATUS_INVALID_VALUE;
   return launch_bsr16_analysis(handle, dir, nnzb, bsrVal, masks, valCol);
 }
 

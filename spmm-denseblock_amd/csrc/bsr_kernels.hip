@@ -2407,11 +2407,12 @@ constexpr int kBsr32Default = 40;
 constexpr int kBsr16Default = 8;      // fp32 bs 16
 constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 
-// Shipped kernels of the ROW-block, row-major-B path, and the variants
-// SPMM_BSR_VARIANT may select instead (tuning A/B only). Every accepted value
-// is a kernel the BSR parity subset passes (tools/gpu_var.sh TESTV,
-// profiles/r03_var_tests.log); any other value selects the default, so no
-// environment setting can make this library compute a different product.
+// Shipped kernels of the ROW-block, row-major-B path, and the alternatives a
+// TUNING build (make TUNING=1, -DSPMM_TUNING) lets SPMM_BSR_VARIANT select for
+// A/B timing. A release build compiles the override out (variant_override()
+// is the constant -1), so no environment setting can change which kernel
+// computes a product; the parity subset of each alternative is on record per
+// value in profiles/r04_var_tests/ (tools/gpu_var.sh, a TUNING build).
 // History of the removed variants: DESIGN.md §4.
 //  bs 32 fp32 (bsr32_f32_cs2_kernel: 6 item slots, 3 A slots, 32-bit B-row
 //  offsets, cross-block pairs, nt A copies): products stand-in 3.07 ms
@@ -2420,9 +2421,9 @@ constexpr int kBsr16F16Default = 12;  // fp16 bs 16
 //  for 32 * ldb * 4 >= 2^31. 4126, not selectable: the full-panel LDS kernel
 //  (D = 2, 40 KB, 4 workgroups per CU), the default for blocks known to be
 //  dense (the hybrid's BSR part, MFMA-pipe bound: products part 1.71 vs 1.87
-//  ms at D = 3). It computes the dense block product (an inf / NaN in a B row
-//  only explicit zeros meet reaches C), so it fails the column-sparse parity
-//  case the column streams pass and is not offered as an override.
+//  ms at D = 3) and the kernel of SPMM_BSR_DENSE_BLOCK_PRODUCT. It computes
+//  the dense block product (an inf / NaN in a B row only explicit zeros meet
+//  reaches C).
 constexpr int kBsr32Cs = 4416;
 constexpr int kBsr32CsNoNt = 4516;
 constexpr int kBsr32CsWideLdb = 4496;
@@ -2440,6 +2441,7 @@ constexpr int kBsr16F16Cm = 4725;
 //  bs 16 fp32: the column-masked block kernel (products stand-in K = 512
 //  16.6 ms against 18.5 for the full-panel kernel).
 
+#ifdef SPMM_TUNING
 int variant_override() {
   static const int var = [] {
     const char* e = getenv("SPMM_BSR_VARIANT");
@@ -2447,13 +2449,25 @@ int variant_override() {
   }();
   return var;
 }
+// SPMM_BSR_ORDER=1 / 2 / 3 (below): scheduling A/B of the column streams
+int order_override() {
+  static const int force = [] {
+    const char* e = getenv("SPMM_BSR_ORDER");
+    return e ? atoi(e) : 0;
+  }();
+  return force;
+}
+#else
+constexpr int variant_override() { return -1; }
+constexpr int order_override() { return 0; }
+#endif
 #define SPMM_COMMA ,
 
 // Block-row order for the column-stream kernels: longest first when the grid
 // is at most kLptRounds waves per resident slot deep (a few long rows would
 // otherwise start last and run alone), else nullptr (the kernels' XCD-chunked
-// order, which keeps neighbouring block rows in one L2). SPMM_BSR_ORDER=1
-// forces longest first, 2 the XCD order (tuning). One launch of
+// order, which keeps neighbouring block rows in one L2). In a TUNING build
+// SPMM_BSR_ORDER=1 forces longest first, 2 the XCD order. One launch of
 // block_row_order_kernel into the handle's order buffer, in stream order.
 constexpr int kLptRounds = 8;
 
@@ -2467,10 +2481,7 @@ constexpr int kLptRounds = 8;
 spmm_status_t cs2_segments(spmm_context* ctx, int mb, int nnzb, int ntiles, const int* rowptr,
                            const int4** segs, const int4** splits, float** part, int* nseg,
                            int* nsplit) {
-  static const int force = [] {
-    const char* e = getenv("SPMM_BSR_ORDER");
-    return e ? atoi(e) : 0;
-  }();
+  const int force = order_override();
   *segs = nullptr;
   *splits = nullptr;
   *part = nullptr;
@@ -2499,10 +2510,7 @@ spmm_status_t cs2_segments(spmm_context* ctx, int mb, int nnzb, int ntiles, cons
 spmm_status_t block_row_order(spmm_context* ctx, int mb, int ntiles, const int* rowptr,
                               const int** order, long slots_per_cu = 12, const int* crp = nullptr,
                               int m = 0) {
-  static const int force = [] {
-    const char* e = getenv("SPMM_BSR_ORDER");
-    return e ? atoi(e) : 0;
-  }();
+  const int force = order_override();
   *order = nullptr;
   const long waves = (long)mb * ntiles, slots = slots_per_cu * ctx->num_cus;
   if (force == 2 || (force != 1 && force != 3 && waves > kLptRounds * slots))
@@ -2570,6 +2578,14 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   const bool vec_ok = aligned(val, 16) && (brow || (aligned(B, 16) && ldb % 4 == 0));
   const int slot = timing_begin(ctx);
   const int var = variant_override();
+  // SPMM_BSR_DENSE_BLOCK_PRODUCT: cusparseSbsrmm's dense-block semantics, the full-panel
+  // kernels only (no column masks); the split-bf16 option stays the hybrid's own
+  const bool hybrid_part = dense_blocks;
+  const bool dense_sem = (ctx->bsr_flags & SPMM_BSR_DENSE_BLOCK_PRODUCT) != 0;
+  if (dense_sem) {
+    dense_blocks = true;
+    masks = nullptr;
+  }
   // the column stream stores row-major C as 16-B row pieces (and its segment fix-up too):
   // C and ldc must keep them aligned, else the fragment kernel's scalar stores serve
   const bool c16 = !crow || (aligned(C, 16) && ldc % 4 == 0);
@@ -2580,13 +2596,17 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     const dim3 grid(mb, (n + 127) / 128);
     const bool narrow = (size_t)ldb * 128 < (1u << 31);  // 32-row panels addressable in 31 bits
     int lv = dense_blocks ? kBsr32Dense : kBsr32Cs;
-    if (var == kBsr32CsNoNt || var == kBsr32CsWideLdb || var == kBsr32Cs) lv = var;
+    // (a tuning override never replaces the dense-block kernel: the hybrid's
+    // column-major form stages B in the handle scratch the column stream's
+    // segments would reuse)
+    if (!dense_blocks && (var == kBsr32CsNoNt || var == kBsr32CsWideLdb || var == kBsr32Cs))
+      lv = var;
     if (!narrow && (lv == kBsr32Cs || lv == kBsr32CsNoNt)) lv = kBsr32CsWideLdb;
     if (lv == kBsr32Dense) {
       // split-bf16 (opt-in, SPMM_HYBRID_SPLIT_BF16): wave-pair split-K for row-major C
       // (products hybrid 1.86-1.87 vs 1.89 ms fused, reddit 0.80 vs 0.83,
       // profiles/r01_hybrid_split.jsonl), one k range per wave for column-major C
-      const bool split = dense_blocks && (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16);
+      const bool split = hybrid_part && (ctx->hybrid_flags & SPMM_HYBRID_SPLIT_BF16);
       if (split && crow)
         hipLaunchKernelGGL((bsr32_f32_lds_kernel<true, 2, 32, false, 24, true, true>), grid,
                            dim3(256), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha,
@@ -2660,7 +2680,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                       ctx->stream, rowd, brow, crow, mb, n, rowptr, colind, val, B, ldb, alpha,
                       beta, C, ldc);
   } else if (bs == 16 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 &&
-             aligned(val, 16) && aligned(B, 16)) {
+             aligned(val, 16) && aligned(B, 16) && !dense_sem) {
     const dim3 grid(mb, (n + 255) / 256);
     if (crow)
       hipLaunchKernelGGL((bsr16_cm_kernel<float, true, 2, 5>), grid, dim3(256), 0, ctx->stream, mb,
@@ -2729,10 +2749,12 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   const bool vec_ok = aligned(val, 16) && (brow || (aligned(B, 16) && ldb % 8 == 0));
   const int slot = timing_begin(ctx);
   const int var = variant_override();
+  // SPMM_BSR_DENSE_BLOCK_PRODUCT: the register-fragment kernel (dense blocks, no masks)
+  const bool dense_sem = (ctx->bsr_flags & SPMM_BSR_DENSE_BLOCK_PRODUCT) != 0;
   // the analysed column stream: COLUMN blocks with their column masks, n >= 128
-  const bool msk = masks && bs == 16 && !rowd && n >= 128;
+  const bool msk = masks && bs == 16 && !rowd && n >= 128 && !dense_sem;
   if (bs == 16 && (rowd || msk) && brow && n >= 8 && n % 8 == 0 && ldb % 8 == 0 &&
-      aligned(val, 16) && aligned(B, 16)) {
+      aligned(val, 16) && aligned(B, 16) && !dense_sem) {
     int lv = n >= 128 ? kBsr16F16Cs : kBsr16F16Cm;
     if (var == kBsr16F16Cm ||
         (n >= 128 && (var == kBsr16F16Cs || var == kBsr16F16CsNoNt)))

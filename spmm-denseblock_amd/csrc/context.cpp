@@ -234,4 +234,19 @@ spmm_status_t spmm_set_hybrid_options(spmm_handle_t h, int flags) {
   return SPMM_STATUS_SUCCESS;
 }
 
+spmm_status_t spmm_set_bsr_options(spmm_handle_t h, int flags) {
+  if (!h) return SPMM_STATUS_NOT_INITIALIZED;
+  if (flags & ~SPMM_BSR_DENSE_BLOCK_PRODUCT) return SPMM_STATUS_INVALID_VALUE;
+  h->bsr_flags = flags;
+  return SPMM_STATUS_SUCCESS;
+}
+
+int spmm_get_build_options(void) {
+#ifdef SPMM_TUNING
+  return SPMM_BUILD_TUNING;
+#else
+  return 0;
+#endif
+}
+
 }  // extern "C"

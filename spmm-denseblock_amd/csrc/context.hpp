@@ -29,6 +29,7 @@ struct spmm_context {
   int csr_waves_per_cu = 0;  // 0 = default
   int csr_flags = SPMM_CSR_NT_STREAMS;  // SPMM_CSR_* option bits (default: nt streams)
   int hybrid_flags = 0;                 // SPMM_HYBRID_* option bits
+  int bsr_flags = 0;                    // SPMM_BSR_* option bits
 
   // Device workspace (grown, never shrunk; freed in spmm_destroy).
   void* ws = nullptr;

@@ -863,10 +863,14 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
                       (ctx->csr_flags & SPMM_CSR_SEQUENTIAL_ROWS) == 0;
   if (grouped) {
     dim3 g8((nw + kWavesPerWG - 1) / kWavesPerWG, 1);
+#ifdef SPMM_TUNING
     static const int pd_env = [] {
-      const char* e = getenv("SPMM_CSR_GROUP_PD");  // tuning only
+      const char* e = getenv("SPMM_CSR_GROUP_PD");  // TUNING builds only
       return e ? atoi(e) : 0;
     }();
+#else
+    constexpr int pd_env = 0;
+#endif
 #define SPMM_LAUNCH_GRP_PD(L, PD)                                                              \
   if (hot)                                                                                     \
     hipLaunchKernelGGL((csr_group_kernel<true, L, PD, true>), g8, block, 0, ctx->stream, m, n,  \

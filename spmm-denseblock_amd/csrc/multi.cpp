@@ -37,6 +37,7 @@ struct spmm_multi {
   std::vector<hipEvent_t> coll_done;                 // [p]: last all-gather finished
   std::vector<hipEvent_t> user_in;                   // [p]: caller's stream reached the call
   std::vector<hipStream_t> user;                     // [p]: caller streams (spmm_multi_set_user_streams)
+  bool user_set = false;                             // `user` applies to the next call (NULL = stream 0)
   bool timing = false;
 };
 
@@ -172,8 +173,14 @@ spmm_status_t spmm_multi_destroy(spmm_multi_t c) {
 
 int spmm_multi_size(spmm_multi_t c) { return c ? c->ngpu : 0; }
 
+// A NULL entry is the device's legacy null stream (torch's default stream
+// reports cuda_stream == 0): the compute and collective streams are
+// non-blocking, so nothing would order them against it otherwise. The set
+// applies to the next spmm_csr_f32_multi call only, which then forgets it: a
+// caller that later destroys one of its streams leaves no dangling handle here.
 spmm_status_t spmm_multi_set_user_streams(spmm_multi_t c, void* const* streams) {
   if (!c) return SPMM_STATUS_NOT_INITIALIZED;
+  c->user_set = streams != nullptr;
   for (int p = 0; p < c->ngpu; ++p)
     c->user[p] = streams ? reinterpret_cast<hipStream_t>(streams[p]) : nullptr;
   return SPMM_STATUS_SUCCESS;
@@ -222,8 +229,9 @@ spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int*
     }
   }
   // inputs produced on the caller's streams are complete before any kernel reads them
-  for (int p = 0; p < P; ++p) {
-    if (!c->user[p]) continue;
+  const bool ordered = c->user_set;
+  c->user_set = false;  // consumed by this call
+  for (int p = 0; p < P && ordered; ++p) {
     SPMM_TRY_HIP(hipSetDevice(c->dev[p]));
     SPMM_TRY_HIP(hipEventRecord(c->user_in[p], c->user[p]));
     SPMM_TRY_HIP(hipStreamWaitEvent(c->compute[p], c->user_in[p], 0));
@@ -268,8 +276,9 @@ spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int*
     SPMM_TRY_HIP(hipStreamWaitEvent(c->compute[p], c->coll_done[p], 0));
     if (c->timing) SPMM_TRY_HIP(hipEventRecord(c->t_end[p], c->compute[p]));
     // later work on the caller's stream sees all of C
-    if (c->user[p]) SPMM_TRY_HIP(hipStreamWaitEvent(c->user[p], c->coll_done[p], 0));
+    if (ordered) SPMM_TRY_HIP(hipStreamWaitEvent(c->user[p], c->coll_done[p], 0));
   }
+  for (int p = 0; p < P; ++p) c->user[p] = nullptr;
   return SPMM_STATUS_SUCCESS;
 }
 

@@ -34,6 +34,8 @@ CSR_SEQUENTIAL_ROWS = 2
 HYBRID_FUSED = 1
 HYBRID_TWO_LAUNCH = 2
 HYBRID_SPLIT_BF16 = 4
+BSR_DENSE_BLOCK_PRODUCT = 1
+BUILD_TUNING = 1
 
 
 class SpmmError(RuntimeError):
@@ -68,6 +70,8 @@ _PROTOS = {
     "spmm_set_csr_waves_per_cu": (c_int, [_P, c_int]),
     "spmm_set_csr_options": (c_int, [_P, c_int]),
     "spmm_set_hybrid_options": (c_int, [_P, c_int]),
+    "spmm_set_bsr_options": (c_int, [_P, c_int]),
+    "spmm_get_build_options": (c_int, []),
     "spmm_gespmm_csrmm_f32": (c_int, [c_int, c_int, _P, _P, _P, _P, _P, _P]),
     "spmm_scsrmm": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, POINTER(c_float), _P,
                             _P, _P, _P, _P, c_int, POINTER(c_float), _P, c_int]),

@@ -72,6 +72,9 @@ class Handle:
     def set_hybrid_options(self, flags: int) -> None:
         check(lib().spmm_set_hybrid_options(self._h, flags), "spmm_set_hybrid_options")
 
+    def set_bsr_options(self, flags: int) -> None:
+        check(lib().spmm_set_bsr_options(self._h, flags), "spmm_set_bsr_options")
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             lib().spmm_destroy(self._h)

@@ -93,6 +93,21 @@ def test_status_strings_and_host_side_checks():
     assert L.spmm_destroy_mat_descr(d) == 0
 
 
+def test_release_build_reads_no_environment():
+    """The shipped library is a release build: its kernel choice cannot be
+    changed by SPMM_BSR_VARIANT / SPMM_BSR_ORDER / SPMM_CSR_GROUP_PD (those
+    are read only by a `make TUNING=1` A/B build), and the binary names none
+    of them."""
+    from spmm_hip import _lib
+    L = _lib.lib()
+    assert L.spmm_get_build_options() & _lib.BUILD_TUNING == 0
+    data = open(_lib.LIB_PATH, "rb").read()
+    for var in (b"SPMM_BSR_VARIANT", b"SPMM_BSR_ORDER", b"SPMM_CSR_GROUP_PD"):
+        assert var not in data, var
+    assert L.spmm_set_bsr_options(None, 1) == 1
+    assert L.spmm_get_version() == 100
+
+
 def test_no_silent_fallback_when_library_missing(monkeypatch):
     from spmm_hip import _lib
     monkeypatch.setattr(_lib, "_lib", None)

@@ -630,6 +630,65 @@ def test_column_sparse_blocks(oracle, device, bs, dtype, n, layout):
     assert_normwise(got, ref, absd, tol, what + ", non-finite B")
 
 
+@pytest.mark.parametrize("bs,dtype", [(32, "f32"), (16, "f32"), (16, "f16"), (8, "f32"),
+                                      (64, "f32")])
+@pytest.mark.parametrize("layout", ["row", "col"])
+def test_dense_block_product_option(oracle, device, bs, dtype, layout):
+    """SPMM_BSR_DENSE_BLOCK_PRODUCT (spmm_set_bsr_options): cusparseSbsrmm's
+    dense-block semantics. inf / NaN in B rows that only explicit zeros of
+    stored blocks meet give NaN in every row of those block rows (0 * inf),
+    exactly where the f64 dense-block oracle has them; every other element
+    matches the oracle within the bar. The default handle on the same inputs
+    keeps them finite (column-granular contract, test_column_sparse_blocks)."""
+    from spmm_hip._lib import BSR_DENSE_BLOCK_PRODUCT
+    ops = _ops()
+    rng = np.random.default_rng(7 * bs + (layout == "col"))
+    mb, kb, n = 13, 40, 136
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.3)
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    vb = v.reshape(-1, bs, bs)
+    used = np.zeros(kb * bs, bool)
+    stored = np.zeros(kb * bs, bool)
+    for k in range(rp[-1]):
+        used[ci[k] * bs + np.nonzero(np.any(vb[k] != 0, axis=0))[0]] = True
+        stored[ci[k] * bs: ci[k] * bs + bs] = True
+    cand = np.nonzero(stored & ~used)[0]
+    assert cand.size >= 2
+    B[cand[0]] = np.inf
+    B[cand[1]] = np.nan
+    if dtype == "f16":
+        v, B = v.astype(np.float16), B.astype(np.float16)
+    fn = ops.bsrmm if dtype == "f32" else ops.bsrmm_f16
+    m = mb * bs
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0, half=dtype == "f16")
+    for flags in (BSR_DENSE_BLOCK_PRODUCT, 0):
+        h = ops.Handle()
+        h.set_bsr_options(flags)
+        if layout == "row":
+            drp, dci, dv, dB = _dev(rp, ci, v, B.reshape(-1))
+            dC = torch.empty((m * n,), device=device)
+            fn(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n, handle=h)
+            torch.cuda.synchronize()
+            got = dC.cpu().numpy().reshape(m, n)
+        else:
+            drp, dci, dv, dB = _dev(rp, ci, v, np.ascontiguousarray(B.T).reshape(-1))
+            dC = torch.empty((n * m,), device=device)
+            fn(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=kb * bs, order_b=ops.ORDER_COL,
+               C=dC, ldc=m, order_c=ops.ORDER_COL, handle=h)
+            torch.cuda.synchronize()
+            got = dC.cpu().numpy().reshape(n, m).T
+        h.close()
+        what = f"bs={bs} {dtype} {layout} flags={flags}"
+        if flags:
+            assert np.isnan(ref).any()
+            assert np.array_equal(np.isnan(got), np.isnan(ref)), what + ": NaN pattern"
+            fin = ~np.isnan(ref)
+            assert_normwise(got[fin], ref[fin], absd[fin], TOL_F32 if dtype == "f32" else
+                            TOL_F16_ACC, what)
+        elif bs in (16, 32):  # the column streams / column-masked kernels skip empty columns
+            assert np.isfinite(got).all(), what + ": default contract keeps C finite"
+
+
 def _masks_np(v, bs=32):
     """Column masks of row-major blocks as the analysis defines them (bit c: a
     value other than +-0 in column c; NaN and inf count)."""

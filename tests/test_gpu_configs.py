@@ -206,6 +206,33 @@ def test_config4_native_multi_checks_outputs(device):
     mg.close()
 
 
+def test_config4_native_multi_orders_against_default_stream(device):
+    """MultiGPU.csrmm on torch's legacy default stream (cuda_stream == 0, the
+    NULL entry of spmm_multi_set_user_streams): the kernels start after a slow
+    producer of B queued there, and a copy of C queued there afterwards sees the
+    finished all-gather. No device-wide synchronize between the three: the
+    copy to the host waits for the default stream alone."""
+    from spmm_hip import ops
+    torch.cuda.set_stream(torch.cuda.default_stream(device))
+    assert torch.cuda.current_stream(device).cuda_stream == 0
+    m, K = 4096, 64
+    rp = torch.arange(0, 2 * m + 1, 2, dtype=torch.int32, device=device)  # 2 nnz per row
+    ci = (torch.arange(2 * m, dtype=torch.int32, device=device) * 7) % m
+    v = torch.ones(2 * m, device=device)
+    B = torch.zeros((m, K), device=device)
+    C = torch.zeros((2 * m, K), device=device)  # 2 chunks x 1 part x m / 2 rows
+    mg = ops.MultiGPU([device.index or 0])
+    torch.cuda.synchronize()
+    for rep in range(2):  # the ordering holds on every call, not only the first
+        torch.cuda._sleep(100_000_000)  # ~40-50 ms of spinning on the default stream
+        B.fill_(3.0 + rep)              # the producer of B, behind it
+        mg.csrmm([0, m], [(rp, ci, v)], [2 * m], [B], [C], m=m, n=K, k=m, ldb=K, ldc=K,
+                 chunks=2)
+        got = C[:m].cpu()  # queued on the default stream after the call
+        assert bool((got == 2 * (3.0 + rep)).all()), f"call {rep}: C read before the product"
+    mg.close()
+
+
 def test_config4_torch_distributed_world1(tmp_path):
     """bench.py's N > 1 exchange path through RCCL on this one GPU: a fresh
     child process initialises torch.distributed (nccl backend) at world 1

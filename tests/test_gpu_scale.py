@@ -222,3 +222,164 @@ def test_reordered_reddit_scale_bsr_vs_csr(oracle, device, bs):
         _check_oracle_rows(oracle, Ch, rp, ci, v, B, _sample_rows(parts[3], bs, n, 15), TOL_F32,
                            "RCM-reordered reddit hybrid")
         _within(Ch[:n], Cc, absd, 2 * TOL_F32, "RCM-reordered reddit hybrid vs CSR")
+
+
+# ---------------------------------------------------------------------------
+# The analysed entries at full size (spmm_bsr32_analysis_f32 +
+# spmm_bsrmm_analysed_f32, spmm_bsr16_analysis_f16 + spmm_bsrmm_analysed_f16):
+# the entries north_star's MFMA claim rests on, on the same stand-ins as the
+# drop-in tests above, with the same two checks, plus bit-identity with the
+# drop-in column stream on the same matrix (same items, order and segments).
+# ---------------------------------------------------------------------------
+def _graph(kind: str, reorder: bool):
+    """(rp, ci, n) of the reddit / products community stand-ins (bench.py
+    WORKLOADS), optionally with ids scrambled and the in-repo RCM applied."""
+    from spmm_hip import prep
+    if kind == "reddit":
+        n = 232965
+        rp, ci = prep.community_csr(n, 670.0, 512, 2048, 0.99, 1234)
+    else:
+        n = 2449029
+        rp, ci = prep.community_csr(n, 27.0, 32, 512, 0.97, 1234)
+    if reorder:
+        rp, ci = prep.permute_csr(rp, ci, np.random.default_rng(9).permutation(n).astype(np.int32))
+        rp, ci = prep.permute_csr(rp, ci, prep.reorder(rp, ci, "rcm"))
+    return rp, ci, n
+
+
+@pytest.mark.parametrize("kind,reorder", [("reddit", False), ("reddit", True),
+                                          ("products", False), ("products", True)])
+def test_analysed_bs32_full_size(oracle, device, kind, reorder):
+    """Config 3's bs 32 fp32 product on the analysed entry at full size:
+    reddit (1.8 M blocks), reddit after RCM (segmented outlier rows: the
+    segment partials and their fix-up), products (2.96 M blocks: the
+    column-major copy valCol is 12 GB, past 2^31 bytes, so every 64-bit block
+    offset is exercised) and products after RCM (10.5 M blocks, 43 GB of
+    valCol). Sampled rows against the f64 oracle (check_result.cu:233-246's
+    bar is 1e-5 relative here), every row against the CSR kernel, and C
+    bit-identical to the drop-in column stream on the same blocks."""
+    ops = _ops()
+    rp, ci, n = _graph(kind, reorder)
+    K, bs = 128, 32
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
+    drp, dci, dv = _dev(rp, ci, v)
+    mb = (n + bs - 1) // bs
+    B = torch.rand((mb * bs, K), device=device) * 2 - 1
+    Cc = ops.gespmm_csrmm(drp, dci, dv, B[:n].contiguous())
+    absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B[:n].abs().contiguous())
+    brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
+    del dci, dv
+    nnzb = int(bci.numel())
+    Cd = torch.empty((mb * bs, K), device=device)
+    ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=Cd, ldc=K)
+    masks, vcol = ops.bsr32_analysis(bval, nnzb=nnzb)
+    del bval
+    if kind == "products":
+        assert vcol.numel() * 4 > 2 ** 31, "valCol must pass 2^31 bytes"
+    Ca = torch.empty((mb * bs, K), device=device)
+    ops.bsrmm_analysed(brp, bci, vcol, masks, B, mb=mb, kb=mb, n=K, ldb=K, C=Ca, ldc=K)
+    torch.cuda.synchronize()
+    brp_h = brp.cpu().numpy()
+    seg = _segmented_block_rows(brp_h)
+    if kind == "reddit" and reorder:
+        assert seg, "the RCM-reordered reddit stand-in must exercise the segmented rows"
+    what = f"analysed bs32 {kind}{' RCM' if reorder else ''} (nnzb {nnzb})"
+    rows = _sample_rows(brp_h, bs, n, 21 + 2 * reorder + (kind == "products"), seg)
+    _check_oracle_rows(oracle, Ca, rp, ci, v, B, rows, TOL_F32, what)
+    _within(Ca[:n], Cc, absd, 2 * TOL_F32, what + " vs CSR")
+    assert not bool(Ca[n:].any()), "padding rows of C must be zero"
+    assert torch.equal(Ca, Cd), what + ": differs from the drop-in column stream"
+
+
+@pytest.mark.parametrize("reorder", [False, True])
+def test_analysed_bs16_f16_full_size(oracle, device, reorder):
+    """Config 5's bs 16 fp16 product (K = 512) on the analysed entry at full
+    size, on the products stand-in and after RCM (14.3 M blocks): sampled rows
+    against the f64 oracle of the same fp16 values, every row against the CSR
+    kernel on the fp16-rounded values, and C bit-identical to the drop-in
+    column stream."""
+    ops = _ops()
+    rp, ci, n = _graph("products", reorder)
+    K, bs = 512, 16
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float16).astype(np.float32)
+    drp, dci, dv = _dev(rp, ci, v)
+    mb = (n + bs - 1) // bs
+    B16 = (torch.rand((mb * bs, K), device=device) * 2 - 1).half()
+    Bf = B16[:n].float().contiguous()
+    Cc = ops.gespmm_csrmm(drp, dci, dv, Bf)
+    absd = ops.gespmm_csrmm(drp, dci, dv.abs(), Bf.abs())
+    del Bf
+    brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
+    del dci, dv
+    bval16 = bval.half()
+    del bval
+    nnzb = int(bci.numel())
+    Cd = torch.empty((mb * bs, K), device=device)
+    ops.bsrmm_f16(brp, bci, bval16, B16, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=Cd, ldc=K)
+    masks, vcol = ops.bsr16_analysis(bval16, nnzb=nnzb)
+    del bval16
+    Ca = torch.empty((mb * bs, K), device=device)
+    ops.bsrmm_analysed_f16(brp, bci, vcol, masks, B16, mb=mb, kb=mb, n=K, ldb=K, C=Ca, ldc=K)
+    torch.cuda.synchronize()
+    what = f"analysed bs16 fp16 products{' RCM' if reorder else ''} (nnzb {nnzb})"
+    rows = _sample_rows(brp.cpu().numpy(), bs, n, 31 + reorder)
+    _check_oracle_rows(oracle, Ca, rp, ci, v, B16, rows, TOL_F16_ACC, what)
+    _within(Ca[:n], Cc, absd, 2 * TOL_F16_ACC, what + " vs CSR")
+    assert torch.equal(Ca, Cd), what + ": differs from the drop-in column stream"
+
+
+def test_nonfinite_contract_full_size(device):
+    """The two non-finite contracts of Path B (include/spmm_hip.h,
+    spmm_set_bsr_options) at full size on the reddit stand-in, bs 32: three B
+    rows set to NaN. Expected NaN rows come from the block pattern on the host:
+      * default (column-granular): every row of block row I iff a stored block
+        (I, J) has a value other than +-0 in the column holding the NaN row;
+      * SPMM_BSR_DENSE_BLOCK_PRODUCT (cusparseSbsrmm's dense blocks): every row
+        of block row I iff a block (I, J) is stored at all.
+    Everything else is finite and equals the CSR kernel on B with those rows
+    zeroed, within the fp32 bar."""
+    from spmm_hip import prep
+    from spmm_hip._lib import BSR_DENSE_BLOCK_PRODUCT
+    ops = _ops()
+    rp, ci, n = _graph("reddit", False)
+    K, bs = 128, 32
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
+    mb = (n + bs - 1) // bs
+    # NaN rows: a hub column, a mid-popularity one and one past n's last block
+    deg = np.bincount(ci, minlength=n)
+    order = np.argsort(-deg, kind="stable")
+    nan_rows = np.array(sorted({int(order[0]), int(order[n // 50]), n - 1}), dtype=np.int64)
+    drp, dci, dv = _dev(rp, ci, v)
+    B = torch.rand((mb * bs, K), device=device) * 2 - 1
+    B0 = B.clone()
+    B0[torch.from_numpy(nan_rows).to(device)] = 0.0
+    B[torch.from_numpy(nan_rows).to(device)] = float("nan")
+    Cc = ops.gespmm_csrmm(drp, dci, dv, B0[:n].contiguous())
+    absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B0[:n].abs().contiguous())
+    brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
+    brp_h, bci_h = brp.cpu().numpy(), bci.cpu().numpy()
+    # column-granular: (block row, column) pairs holding a nonzero, from the CSR pattern
+    row_of = np.repeat(np.arange(n), np.diff(rp))
+    hit_col = np.zeros(mb, bool)
+    for r in nan_rows:
+        hit_col[np.unique(row_of[ci == r] // bs)] = True
+    blk_row_of = np.repeat(np.arange(mb), np.diff(brp_h))
+    hit_dense = np.zeros(mb, bool)
+    for r in nan_rows:
+        hit_dense[np.unique(blk_row_of[bci_h == r // bs])] = True
+    assert hit_dense.sum() > hit_col.sum() > 0, "the case must separate the two contracts"
+    for flags, hit in ((0, hit_col), (BSR_DENSE_BLOCK_PRODUCT, hit_dense)):
+        h = ops.Handle()
+        h.set_bsr_options(flags)
+        C = torch.empty((mb * bs, K), device=device)
+        ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K, handle=h)
+        torch.cuda.synchronize()
+        nanrow = torch.isnan(C).view(mb, bs * K)
+        want = torch.from_numpy(hit).to(device)
+        got_any, got_all = nanrow.any(dim=1), nanrow.all(dim=1)
+        assert torch.equal(got_any, want) and torch.equal(got_all, want), (
+            f"flags {flags}: NaN block rows {int(got_any.sum())} (whole: {int(got_all.sum())}), "
+            f"expected {int(want.sum())}")
+        keep = ~want.repeat_interleave(bs)[:n]
+        _within(C[:n][keep], Cc[keep], absd[keep], 2 * TOL_F32, f"flags {flags}: finite rows vs CSR")
+        h.close()

@@ -234,3 +234,66 @@ def test_column_stream_registers_in_flight_are_asm_only(bsr_asm, kernel):
             if ins[bi] is not None:
                 transfer(b, ins[bi], True)
         assert not errs, f"{k}: compiler touches in-flight registers: {errs[:5]}"
+
+
+# ---------------------------------------------------------------------------
+# Store-data hazard ("The sc1 store failure"): a VMEM store of
+# more than 64 bits reads its data VGPRs after it issues; a VALU write of them
+# within 2 wait states (gfx950) replaces the data. hipcc pads its own stores,
+# not those inside inline asm, so every shipped object is audited.
+# ---------------------------------------------------------------------------
+import isa_store_hazard as ish  # noqa: E402
+
+_ALL_ASM = [os.path.join(PKG, "build", f"{k}-hip-amdgcn-amd-amdhsa-gfx950.s")
+            for k in ("csr_kernels", "bsr_kernels", "convert_kernels", "f64_kernels")]
+
+
+def test_no_store_data_hazard_in_shipped_code():
+    if not all(os.path.exists(p) for p in _ALL_ASM):
+        subprocess.run(["make", "-C", PKG, "lib"], check=True, capture_output=True)
+    total = 0
+    for p in _ALL_ASM:
+        with open(p) as f:
+            res = ish.check(f.read())
+        total += len(res)
+        bad = {k: v for k, v in res.items() if v}
+        assert not bad, "\n".join(h for v in bad.values() for h in v)
+    assert total >= 40, f"only {total} functions with wide stores audited"
+
+
+_HAZARD_EXCERPT = """\
+_Z6kernelv:
+\tv_mov_b32 v8, s0
+\ts_nop 0
+\t;;#ASMSTART
+\tglobal_store_dwordx4 v[8:9], v[0:3], off sc1
+\t;;#ASMEND
+\t;;#ASMSTART
+\tv_accvgpr_read_b32 v2, a33
+\t;;#ASMEND
+\ts_nop 1
+\t;;#ASMSTART
+\tglobal_store_dwordx4 v[8:9], v[4:7], off sc1
+\ts_nop 1
+\t;;#ASMEND
+\tv_mov_b32 v5, 0
+\tbuffer_store_dwordx4 v[10:13], v8, s[0:3], 0 offen
+\ts_cbranch_scc1 .LBB0_2
+.LBB0_1:
+\ts_nop 3
+.LBB0_2:
+\tv_add_u32_e32 v12, 1, v12
+\ts_endpgm
+.Lfunc_end0:
+"""
+
+
+def test_store_hazard_checker_flags_the_pattern():
+    """An asm store followed at once by a VALU write of its data registers is
+    flagged (both the straight-line case and the branch that skips the pad);
+    a store whose string ends in s_nop 1 is clean."""
+    res = ish.check(_HAZARD_EXCERPT)
+    hz = res["_Z6kernelv"]
+    assert len(hz) == 2, hz
+    assert "v_accvgpr_read_b32 v2" in hz[0] and "inline asm" in hz[0]
+    assert "v_add_u32_e32 v12" in hz[1]
