@@ -95,6 +95,13 @@ WORKLOADS = {
                                    p_in=0.97, bs=16, K=512, dtype="fp16", reorder="rcm"),
     "products_rcm_bsr32": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                p_in=0.97, bs=32, K=128, dtype="fp32", reorder="rcm"),
+    # the block sizes benchmark.py:3-19 sweeps besides 16 / 32, on the reddit
+    # stand-in: bs 8 (lane-group VALU kernel) and bs 64 (the bs 32 column stream
+    # on 32 x 32 sub-blocks)
+    "reddit_bsr8": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
+                        bs=8, K=128, dtype="fp32"),
+    "reddit_bsr64": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
+                         bs=64, K=128, dtype="fp32"),
     # §8f next row: dense-block + CSR remainder (divide.cu) on the reddit stand-in
     "reddit_hybrid32": dict(kind="hybrid", n=232965, avg_deg=670.0, cmin=512, cmax=2048,
                             p_in=0.99, bs=32, K=128, density="auto"),
@@ -905,17 +912,19 @@ def run_bsr(args, W, world, rank, dev, dist):
     # row-major staged copy of B, with C written column-major by their
     # epilogue; the transposes are separate launches, outside
     # kernel_ms.
-    cm = bs in (16, 32) and K % (4 if dt == "fp32" else 8) == 0
+    cm = bs in (16, 32, 64) and K % (4 if dt == "fp32" else 8) == 0 and not (bs == 64 and dt != "fp32")
     d_r = torch.repeat_interleave(torch.arange(n, device=dev, dtype=torch.int64),
                                   torch.from_numpy(np.diff(rp)).to(dev))
     d_c = torch.from_numpy(ci).to(dev).to(torch.int64)
     active_cols = int(torch.unique((d_r // bs) * n + d_c).numel())
     active_pairs = int(torch.unique(((d_r // bs) * mb + d_c // bs) * (bs // 2) +
                                     (d_c % bs) % (bs // 2)).numel())
+    # bs 64 streams 32 x 32 sub-blocks: nonzero columns per 32-row half
+    active_cols32 = int(torch.unique((d_r // 32) * n + d_c).numel()) if bs == 64 else active_cols
     b_rows = int(torch.unique(d_c).numel())  # distinct B rows the product touches
     del d_r, d_c
     # output columns per workgroup (bs 32: 128; bs 16: 256)
-    tile = 128 if bs == 32 else 256
+    tile = 256 if bs == 16 else 128
     ntiles = (K + tile - 1) // tile
     dense_flops = 2.0 * nnzb * bs * bs * K    # SURVEY §8d "MFMA-executed" (dense blocks)
     cs16 = cm and bs == 16 and dt == "fp16" and K >= 128
@@ -923,6 +932,9 @@ def run_bsr(args, W, world, rank, dev, dist):
         # column stream: two v_mfma_f32_32x32x1_2b_f32 (32 rows x 64 columns,
         # k = 1) per nonzero column of a block and 128 output columns
         mfma_flops = active_cols * 2.0 * bs * K
+    elif cm and bs == 64:
+        # the same per nonzero column of a 32 x 32 sub-block
+        mfma_flops = active_cols32 * 2.0 * 32 * K
     elif cs16:
         # column stream: items of 16 nonzero columns packed across blocks, one
         # v_mfma_f32_16x16x16_f16 per item and 16 output columns (the last
@@ -946,8 +958,11 @@ def run_bsr(args, W, world, rank, dev, dist):
     cm_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + a_bytes) + s * active_cols * K +
                 4 * mb * bs * K) if cm else kbytes
     t = kms / 1e3
-    kname = (("bsr32_f32_cs2_kernel" if bs == 32 else "bsr16_f16_cs_kernel" if cs16 else
-              "bsr16_cm_kernel") if cm else f"bsr{bs} register-fragment kernel")
+    kname = (("bsr32_f32_cs2_kernel" if bs == 32 else
+              "bsr32_f32_cs2_kernel (bs 64 sub-blocks)" if bs == 64 else
+              "bsr16_f16_cs_kernel" if cs16 else "bsr16_cm_kernel") if cm else
+             f"bsr_small_kernel<{bs}>" if bs in (2, 4, 8) and dt == "fp32" else
+             f"bsr{bs} register-fragment kernel")
     tkey = {"workload": args.workload, "kernel": kname, "K": K, "dtype": dt, "nnzb": nnzb,
             "layout_BC": args.bsr_layout,
             "variant": bsr_variant(),
@@ -986,9 +1001,10 @@ def run_bsr(args, W, world, rank, dev, dist):
                       "SURVEY 8d full-panel model"),
                   "upper_GBps": round(cm_bytes / t / 1e9, 1),
                   "traffic_key": tkey,
-                  "mfma_executed_flops_per_launch": mfma_flops,
-                  "mfma_executed_TFLOPs": round(mfma_flops / t / 1e12, 2),
-                  "mfma_peak": peak, "mfma_frac": round(mfma_flops / t / 1e12 / peak, 4),
+                  "mfma_executed_flops_per_launch": mfma_flops if bs >= 16 else None,
+                  "mfma_executed_TFLOPs": round(mfma_flops / t / 1e12, 2) if bs >= 16 else None,
+                  "mfma_peak": peak,
+                  "mfma_frac": round(mfma_flops / t / 1e12 / peak, 4) if bs >= 16 else None,
                   "dense_block_equivalent_TFLOPs": round(dense_flops / t / 1e12, 2),
                   "full_panel_model_bytes_per_launch": kbytes,
                   "full_panel_model_GBps": round(kbytes / t / 1e9, 1)},

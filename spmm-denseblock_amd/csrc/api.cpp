@@ -21,7 +21,7 @@ spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, f
                          const float* B, int ldb, spmm_order_t orderB, float beta, float* C,
                          int ldc, spmm_order_t orderC, bool hot = false) {
   WsLayout L;
-  L.carry_bytes = csrmm_carry_bytes(ctx, m, n, nullptr);
+  L.carry_bytes = csrmm_carry_bytes(ctx, m, n);
   L.b_off = align256(L.carry_bytes);
   const size_t b_bytes = orderB == SPMM_ORDER_COL ? (size_t)k * n * sizeof(float) : 0;
   L.c_off = align256(L.b_off + b_bytes);
@@ -30,11 +30,6 @@ spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, f
   spmm_status_t st = ensure_workspace(ctx, L.total);
   if (st != SPMM_STATUS_SUCCESS) return st;
   char* ws = static_cast<char*>(ctx->ws);
-  int nw = 0;
-  csrmm_carry_bytes(ctx, m, n, &nw);
-  const int ntiles_max = (n + 63) / 64;
-  float* carry_val = reinterpret_cast<float*>(ws);
-  int* carry_row = reinterpret_cast<int*>(ws + (size_t)nw * ntiles_max * 64 * sizeof(float));
 
   const float* Bx = B;
   int ldbx = ldb;
@@ -53,18 +48,20 @@ spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, f
   }
   if (orderC == SPMM_ORDER_ROW) {
     return launch_csrmm_rowmajor(ctx, m, n, rowptr, colind, val, base, Bx, ldbx, alpha, beta, C,
-                                 ldc, carry_val, carry_row, nnz_hint, hot_mode(ldbx));
+                                 ldc, ws, nnz_hint, hot_mode(ldbx));
   }
   float* Ct = reinterpret_cast<float*>(ws + L.c_off);
   st = launch_csrmm_rowmajor(ctx, m, n, rowptr, colind, val, base, Bx, ldbx, alpha, 0.f, Ct, n,
-                             carry_val, carry_row, nnz_hint, hot_mode(ldbx));
+                             ws, nnz_hint, hot_mode(ldbx));
   if (st != SPMM_STATUS_SUCCESS) return st;
   // C (m x n col-major, ldc) is an (n x m) row-major matrix with ld ldc.
   return launch_transpose(ctx, m, n, Ct, n, C, ldc, beta);
 }
 
-// Column-major B and / or C with ROW blocks at bs 32 / 16 (cusparseSbsrmm's
-// transB = N layout, run_bsrmm.cu:70-71) run on the column-masked LDS kernels
+// Column-major B and / or C with ROW blocks at bs 16 / 32 / 64 and 2 / 4 / 8
+// fp32 (cusparseSbsrmm's transB = N layout, run_bsrmm.cu:70-71) run on the
+// row-major-B kernels (column streams, column-masked LDS kernels, the
+// lane-group kernel)
 // (DESIGN.md §4): B is transposed into a row-major workspace copy (the kernels
 // copy whole B-panel rows), C is written column-major by the kernels' own
 // LDS-transposed epilogue. The direct kernels for these layouts fetch B
@@ -73,7 +70,8 @@ spmm_status_t csrmm_impl(spmm_context* ctx, int m, int n, int k, int nnz_hint, f
 bool bsr_stage(spmm_direction_t dir, int bs, int n, int elem, spmm_order_t ob, spmm_order_t oc,
                const void* val) {
   const int vec = 16 / elem;  // elements per 16-byte copy
-  return dir == SPMM_DIRECTION_ROW && (bs == 16 || (bs == 32 && elem == 4)) &&
+  const bool f32_stream = elem == 4 && (bs == 2 || bs == 4 || bs == 8 || bs == 32 || bs == 64);
+  return dir == SPMM_DIRECTION_ROW && (bs == 16 || f32_stream) &&
          (ob == SPMM_ORDER_COL || oc == SPMM_ORDER_COL) && n >= vec && n % vec == 0 &&
          reinterpret_cast<uintptr_t>(val) % 16 == 0;
 }

@@ -924,20 +924,21 @@ __global__ __launch_bounds__(256) void bsr16_analysis_kernel(int nnzb, int rowdi
 // key is (32 x blocks + remainder entries) / 8: a dense block's MFMA work
 // weighs about as much as 32 remainder gathers.
 __device__ __forceinline__ int block_row_key(int i, const int* __restrict__ rowptr,
-                                             const int* __restrict__ crp, int m) {
-  const int nb = rowptr[i + 1] - rowptr[i];
+                                             const int* __restrict__ crp, int m, int sub) {
+  // sub: 32-row halves of bs-64 block rows (the SUB column stream), two sub-blocks each
+  const int nb = (rowptr[(i >> sub) + 1] - rowptr[i >> sub]) << sub;
   if (!crp) return min(nb, 1023);
   const int rem = crp[min(32 * i + 32, m)] - crp[32 * i];
   return min((32 * nb + rem) >> 3, 1023);
 }
 __global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int* __restrict__ rowptr,
                                                                const int* __restrict__ crp, int m,
-                                                               int* __restrict__ order) {
+                                                               int sub, int* __restrict__ order) {
   __shared__ int cnt[1024];
   const int t = threadIdx.x;
   cnt[t] = 0;
   __syncthreads();
-  for (int i = t; i < mb; i += 1024) atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m)], 1);
+  for (int i = t; i < mb; i += 1024) atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m, sub)], 1);
   __syncthreads();
   const int own = cnt[t];
   for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan
@@ -949,7 +950,7 @@ __global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int
   cnt[t] -= own;  // exclusive
   __syncthreads();
   for (int i = t; i < mb; i += 1024)
-    order[atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m)], 1)] = i;
+    order[atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m, sub)], 1)] = i;
 }
 
 // ---------------------------------------------------------------------------
@@ -998,8 +999,14 @@ __global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int
 // beside the B rows, and the masks come 64 blocks at a time like the block
 // columns. A's bytes fall from the whole block to the nonzero columns (products
 // stand-in: 7.5 of 32 columns), and the kernel needs no LDS (row-major C).
+// SUB (bs = 64 ROW blocks): a 64 x 64 block is four 32 x 32 sub-blocks with a
+// row stride of 64 floats, and the wave of 32-row block row br streams the
+// sub-blocks (br & 1, 0) and (br & 1, 1) of every block of bs-64 block row
+// br / 2, in that order, as if they were blocks of a bs-32 matrix whose
+// block columns are 2 bc and 2 bc + 1: virtual block index v, block v / 2,
+// sub-block column v & 1. mb is then the number of 32-row block rows.
 template <bool CROW, int XM, int P, int NA, bool O32 = false, bool PK = false, bool ANT = false,
-          bool MSK = false>
+          bool MSK = false, bool SUB = false>
 __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -1007,7 +1014,9 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     const int4* __restrict__ segs = nullptr, float* __restrict__ part = nullptr,
     const unsigned* __restrict__ masks = nullptr) {
   static_assert(NA >= 2 && NA <= 4 && P >= 2 && P <= 16, "ring depths");
+  static_assert(!(SUB && MSK), "the analysed stream is bs 32 only");
   constexpr int DA = NA - 1;  // A blocks in flight ahead of the producer's block
+  constexpr int LDA = SUB ? 64 : 32;  // row stride of a (sub-)block's values
   // (column-major C reuses the LDS for a 128 x 36-float tile)
   __shared__ __attribute__((aligned(16)))
   float smem[MSK && CROW ? 4 : (CROW || NA * 1024 >= 128 * 36 ? NA * 1024 : 128 * 36)];
@@ -1024,8 +1033,13 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     pidx = sg.w;
   } else {
     br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, XM);
-    k0 = rowptr[br];
-    k1 = rowptr[br + 1];
+    if constexpr (SUB) {  // virtual sub-block indices (above)
+      k0 = 2 * rowptr[br >> 1];
+      k1 = 2 * rowptr[(br >> 1) + 1];
+    } else {
+      k0 = rowptr[br];
+      k1 = rowptr[br + 1];
+    }
   }
   const int jt = blockIdx.y * 128;
   const unsigned lds_a = (unsigned)reinterpret_cast<uintptr_t>(smem);
@@ -1034,14 +1048,15 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int r = 8 * q + (lane >> 3);
-    a_src[q] = r * 32 + 4 * ((lane & 7) ^ ((r >> 1) & 7));
+    a_src[q] = r * LDA + 4 * ((lane & 7) ^ ((r >> 1) & 7));
   }
   auto issue_a = [&](int kk, int slot) {
-    const float* src = val + (size_t)kk * 1024;
+    const float* src = SUB ? val + (size_t)(kk >> 1) * 4096 + (br & 1) * 2048 + (kk & 1) * 32
+                           : val + (size_t)kk * 1024;
     float* dst = smem + slot * 1024;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((gbl_void_t)(src + a_src[q & 1] + 512 * (q >> 1)),
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(src + a_src[q & 1] + 16 * LDA * (q >> 1)),
                                        (lds_void_t)(dst + 256 * q), 16, 0, ANT ? 2 : 0);
   };
   unsigned moff[8];
@@ -1094,7 +1109,8 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   unsigned mcur = 0, mnext = 0;         // MSK: the same chunks of the column masks
   const float* ablk = val;              // MSK: the current block's column-major values
   auto load_cols = [&](int kstart) {
-    const unsigned off = 4u * (unsigned)min(kstart + lane, k1 - 1);
+    const unsigned off = SUB ? 4u * (unsigned)min((kstart >> 1) + lane, (k1 >> 1) - 1)
+                             : 4u * (unsigned)min(kstart + lane, k1 - 1);
     asm volatile("global_load_dword %0, %1, %2" : "=&v"(cnext) : "v"(off), "s"(colind) : "memory");
     if constexpr (MSK) {
       asm volatile("global_load_dword %0, %1, %2" : "=&v"(mnext) : "v"(off), "s"(masks) : "memory");
@@ -1131,7 +1147,8 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     ++k;
     aslot = aslot + 1 == NA ? 0 : aslot + 1;
     const int kr = k - k0;
-    if ((kr & 63) == 0) {  // next block-column chunk
+    constexpr int kChunkV = SUB ? 128 : 64;  // (virtual) blocks per block-column chunk
+    if ((kr & (kChunkV - 1)) == 0) {  // next block-column chunk
       if constexpr (MSK)
         asm volatile(SPMM_VM_LADDER("%2") "v_mov_b32 %0, %3\n\tv_mov_b32 %1, %4"
                      : "=&v"(ccur), "=&v"(mcur)
@@ -1142,9 +1159,10 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
                      : "=&v"(ccur)
                      : "s"(nis - cstamp), "v"(cnext)
                      : "scc", "memory");
-      if (k + 64 < k1) load_cols(k + 64);
+      if (k + kChunkV < k1) load_cols(k + kChunkV);
     }
-    const int bc = __builtin_amdgcn_readlane(ccur, kr & 63);
+    const int bc = SUB ? 2 * __builtin_amdgcn_readlane(ccur, (kr >> 1) & 63) + (kr & 1)
+                       : __builtin_amdgcn_readlane(ccur, kr & 63);
     bblk = reinterpret_cast<const char*>(B) + (size_t)bc * 32 * ldb4;
     if constexpr (MSK) {
       m = (unsigned)__builtin_amdgcn_readlane((int)mcur, kr & 63);
@@ -2367,6 +2385,127 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f16_mf
 }
 
 // ---------------------------------------------------------------------------
+// bs = 2 / 4 / 8, fp32, row-major B: a lane-group VALU kernel
+// (rocsparse_bsrmm.h:227-252 sends bs <= 8 to its large-blockdim kernel;
+// rocsparse_bsrmm_impl.h:315-389). A bs x bs block feeds too few rows per B row
+// for an MFMA tile (8 of 32), and the product is bound by the B-row gathers
+// (4 flop per gathered byte at bs 8), so the VALU does the FMAs at a small
+// fraction of its rate. One wave per (block row, 64 * VEC columns), four
+// independent waves per workgroup. Per block:
+//  * A: lane l < bs^2 holds element l of the block (one coalesced load), its
+//    column mask is one ballot, and a(r, c) comes to the FMAs by v_readlane;
+//  * B: one gather per block column: the 64 lanes read VEC floats each of row
+//    bc * bs + c (a whole 256 / 512-B row piece); a column whose values are all
+//    +-0 reads the L2-resident zero row instead, so every block issues the same
+//    bs gathers and the compiler's counted waits hold across the pipeline
+//    (the column-granular contract of include/spmm_hip.h);
+//  * pipeline: a ring of R = 4 block slots, A loaded two blocks ahead and the
+//    B gathers one block ahead of the FMAs (unrolled R times: static
+//    registers, no branch around a load).
+// Each output element is one sequential fp32 FMA chain, blocks in order and
+// columns in order inside a block: the oracle's bsrmm order bit for bit.
+// ---------------------------------------------------------------------------
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+template <int BS, int VEC, bool ROWD, bool CROW>
+__global__ __launch_bounds__(256) void bsr_small_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc) {
+  static_assert(BS == 2 || BS == 4 || BS == 8, "bs 2 / 4 / 8");
+  static_assert(VEC == 1 || VEC == 2, "VEC 1 / 2");
+  constexpr int E = BS * BS;
+  constexpr int R = 4;  // ring slots: A of block k + 2, B of block k + 1, FMAs of block k
+  typedef typename std::conditional<VEC == 2, f32x2v, float>::type vec;
+  const int lane = threadIdx.x & 63;
+  const int br = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (br >= mb) return;
+  const int col0 = blockIdx.y * 64 * VEC + lane * VEC;
+  const bool col_ok = col0 < n;
+  const int col_ld = col_ok ? col0 : 0;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  const int kl = k1 - 1;
+  const float* const zrow = g_zero_row + lane * VEC;
+
+  float acc[BS][VEC];
+#pragma unroll
+  for (int r = 0; r < BS; ++r)
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[r][v] = 0.f;
+
+  float av[R];      // A of a block: lane l < E holds element l
+  int bcol[R];      // its block column
+  vec x[R][BS];     // its B rows (zero row for empty columns)
+  auto load_a = [&](int k, int s) {
+    const int kk = min(k, kl);
+    av[s] = val[(size_t)kk * E + (lane < E ? lane : 0)];
+    bcol[s] = colind[kk];
+  };
+  auto load_b = [&](int s) {
+    const unsigned long long bits =
+        __builtin_amdgcn_ballot_w64(lane < E && (__float_as_uint(av[s]) & 0x7fffffffu) != 0u);
+    const float* base = B + (size_t)bcol[s] * BS * ldb + col_ld;
+#pragma unroll
+    for (int c = 0; c < BS; ++c) {
+      unsigned long long colbits = 0;
+#pragma unroll
+      for (int r = 0; r < BS; ++r) colbits |= 1ull << (ROWD ? r * BS + c : c * BS + r);
+      const float* p = (bits & colbits) ? base + (size_t)c * ldb : zrow;
+      x[s][c] = *reinterpret_cast<const vec*>(p);
+    }
+  };
+  auto fma_block = [&](int s) {
+#pragma unroll
+    for (int c = 0; c < BS; ++c) {
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        const float a = __int_as_float(
+            __builtin_amdgcn_readlane(__float_as_int(av[s]), ROWD ? r * BS + c : c * BS + r));
+        if constexpr (VEC == 1) {
+          acc[r][0] = __builtin_fmaf(a, x[s][c], acc[r][0]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[r][v] = __builtin_fmaf(a, x[s][c][v], acc[r][v]);
+        }
+      }
+    }
+  };
+
+  if (k0 < k1) {
+    load_a(k0, 0);
+    load_a(k0 + 1, 1);
+    load_b(0);
+    for (int k = k0; k < k1; k += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        // the loads run for blocks past the row's end too (clamped to its last
+        // block): no branch around a load, so the waits stay counted
+        load_a(k + u + 2, (u + 2) % R);
+        load_b((u + 1) % R);
+        if (k + u < k1) fma_block(u);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int r = 0; r < BS; ++r) {
+    const size_t row = (size_t)br * BS + r;
+    if (!col_ok) break;
+    if constexpr (CROW) {
+      float* p = C + row * ldc + col0;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) p[v] = epi(acc[r][v], alpha, beta, p + v);
+    } else {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        float* p = C + (size_t)(col0 + v) * ldc + row;
+        p[0] = epi(acc[r][v], alpha, beta, p);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic VALU kernel: any bs, any storage. Thread = one output element per
 // row step; block = (64 columns) x (4 row lanes), grid = (mb, ceil(n/64)).
 // Accumulation order: blocks of the block row in order, k = 0..bs-1 inside.
@@ -2509,7 +2648,7 @@ spmm_status_t cs2_segments(spmm_context* ctx, int mb, int nnzb, int ntiles, cons
 }
 spmm_status_t block_row_order(spmm_context* ctx, int mb, int ntiles, const int* rowptr,
                               const int** order, long slots_per_cu = 12, const int* crp = nullptr,
-                              int m = 0) {
+                              int m = 0, int sub = 0) {
   const int force = order_override();
   *order = nullptr;
   const long waves = (long)mb * ntiles, slots = slots_per_cu * ctx->num_cus;
@@ -2517,7 +2656,7 @@ spmm_status_t block_row_order(spmm_context* ctx, int mb, int ntiles, const int* 
     return SPMM_STATUS_SUCCESS;
   if (spmm_status_t st = spmm::ensure_order_buffer(ctx, mb)) return st;
   hipLaunchKernelGGL(block_row_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, mb, rowptr,
-                     crp, m, ctx->order);
+                     crp, m, sub, ctx->order);
   *order = ctx->order;
   return SPMM_STATUS_SUCCESS;
 }
@@ -2673,6 +2812,28 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
         hipLaunchKernelGGL(seg_fixup_kernel, dim3(nspl, grid.y), dim3(256), 0, ctx->stream, n,
                            spl, pt, alpha, beta, C, ldc);
     }
+  } else if (bs == 64 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 &&
+             aligned(val, 16) && aligned(B, 16) && c16 && !dense_sem) {
+    // bs 64: the bs 32 column stream on the four 32 x 32 sub-blocks of each block
+    // (SUB), one wave per 32-row half of a block row and 128 columns
+    const int mb2 = 2 * mb;
+    const dim3 g2(mb2, (n + 127) / 128);
+    const bool narrow = (size_t)ldb * 128 < (1u << 31);
+    const int* ord = nullptr;
+    if (const spmm_status_t st = block_row_order(ctx, mb2, g2.y, rowptr, &ord, 12, nullptr, 0, 1)) {
+      timing_end(ctx, slot);
+      return st;
+    }
+#define SUB_LAUNCH(CR_, O32_)                                                                    \
+  hipLaunchKernelGGL((bsr32_f32_cs2_kernel<CR_, 32, 6, 3, O32_, true, true, false, true>), g2,    \
+                     dim3(64), 0, ctx->stream, mb2, n, rowptr, colind, val, B, ldb, alpha, beta, \
+                     C, ldc, ord, nullptr, nullptr, nullptr)
+    if (crow) {
+      if (narrow) SUB_LAUNCH(true, true); else SUB_LAUNCH(true, false);
+    } else {
+      if (narrow) SUB_LAUNCH(false, true); else SUB_LAUNCH(false, false);
+    }
+#undef SUB_LAUNCH
   } else if (bs == 32 && vec_ok) {
     const int waves = n <= 32 ? 1 : (n <= 64 ? 2 : 4);
     dim3 grid(mb, (n + 32 * waves - 1) / (32 * waves));
@@ -2694,6 +2855,33 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     SPMM_BSR_DISPATCH(bsr16_f32_mfma_kernel, SPMM_COMMA kBsr16Default, grid, dim3(64 * waves),
                       ctx->stream, rowd, brow, crow, mb, n, rowptr, colind, val, B, ldb, alpha,
                       beta, C, ldc);
+  } else if ((bs == 2 || bs == 4 || bs == 8) && brow && !dense_sem) {
+    // the lane-group VALU kernel: 2 floats per lane when B allows 8-B gathers
+    const bool v2 = n > 64 && n % 2 == 0 && ldb % 2 == 0 && aligned(B, 8);
+    const dim3 grid((mb + 3) / 4, (n + (v2 ? 127 : 63)) / (v2 ? 128 : 64));
+#define SMALL_LAUNCH(BS_, V_)                                                                    \
+  do {                                                                                           \
+    if (rowd && crow)                                                                            \
+      hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, true, true>), grid, dim3(256), 0, ctx->stream, \
+                         mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);               \
+    else if (rowd)                                                                               \
+      hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, true, false>), grid, dim3(256), 0,           \
+                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);  \
+    else if (crow)                                                                               \
+      hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, false, true>), grid, dim3(256), 0,           \
+                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);  \
+    else                                                                                         \
+      hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, false, false>), grid, dim3(256), 0,          \
+                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);  \
+  } while (0)
+    if (bs == 8) {
+      if (v2) SMALL_LAUNCH(8, 2); else SMALL_LAUNCH(8, 1);
+    } else if (bs == 4) {
+      if (v2) SMALL_LAUNCH(4, 2); else SMALL_LAUNCH(4, 1);
+    } else {
+      if (v2) SMALL_LAUNCH(2, 2); else SMALL_LAUNCH(2, 1);
+    }
+#undef SMALL_LAUNCH
   } else {
     dim3 grid(mb, (n + 63) / 64);
     hipLaunchKernelGGL(bsr_generic_kernel<float>, grid, dim3(256), 0, ctx->stream, mb, n, bs,

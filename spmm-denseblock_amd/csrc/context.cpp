@@ -56,6 +56,29 @@ spmm_status_t ensure_order_buffer(spmm_context* ctx, size_t n) {
   return SPMM_STATUS_SUCCESS;
 }
 
+spmm_status_t ensure_tickets(spmm_context* ctx, size_t n) {
+  if (n <= ctx->tickets_cap) return SPMM_STATUS_SUCCESS;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (n <= ctx->tickets_cap) return SPMM_STATUS_SUCCESS;
+  if (ctx->tickets) {
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return from_hip(e);
+    (void)hipFree(ctx->tickets);
+    ctx->tickets = nullptr;
+    ctx->tickets_cap = 0;
+  }
+  const size_t want = n + n / 4 + 1024;
+  hipError_t e = hipMalloc(&ctx->tickets, want * sizeof(int));
+  if (e == hipSuccess) e = hipMemsetAsync(ctx->tickets, 0, want * sizeof(int), ctx->stream);
+  if (e != hipSuccess) {
+    if (ctx->tickets) (void)hipFree(ctx->tickets);
+    ctx->tickets = nullptr;
+    return from_hip(e);
+  }
+  ctx->tickets_cap = want;
+  return SPMM_STATUS_SUCCESS;
+}
+
 int timing_begin(spmm_context* ctx) {
   if (!ctx->timing) return -1;
   const size_t slot = ctx->ev_used;
@@ -141,8 +164,9 @@ spmm_status_t spmm_create(spmm_handle_t* handle) {
 
 spmm_status_t spmm_destroy(spmm_handle_t h) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
-  if (h->ws || h->scratch || h->order) (void)hipStreamSynchronize(h->stream);
+  if (h->ws || h->scratch || h->order || h->tickets) (void)hipStreamSynchronize(h->stream);
   if (h->ws) (void)hipFree(h->ws);
+  if (h->tickets) (void)hipFree(h->tickets);
   if (h->scratch) (void)hipFree(h->scratch);
   if (h->order) (void)hipFree(h->order);
   for (auto e : h->ev_start) (void)hipEventDestroy(e);

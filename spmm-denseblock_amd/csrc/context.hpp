@@ -41,6 +41,11 @@ struct spmm_context {
   // Block-row order of the column-stream BSR kernels (mb ints, grown like ws).
   int* order = nullptr;
   size_t order_cap = 0;
+  // Split-row tickets of the CSR kernels (one int per merge-path slot): zero
+  // between launches (each launch's last arrival resets what it counted), so
+  // they live apart from ws, which other entries overwrite.
+  int* tickets = nullptr;
+  size_t tickets_cap = 0;
 
   // Kernel timing ring.
   bool timing = false;
@@ -59,6 +64,8 @@ spmm_status_t ensure_workspace(spmm_context* ctx, size_t bytes);
 spmm_status_t ensure_scratch(spmm_context* ctx, size_t bytes);
 // The same for the block-row order buffer (at least n ints).
 spmm_status_t ensure_order_buffer(spmm_context* ctx, size_t n);
+// At least n zeroed ticket words (zeroed on the handle's stream when grown).
+spmm_status_t ensure_tickets(spmm_context* ctx, size_t n);
 
 // Record a start/stop event pair around the next main-kernel launch when
 // timing is on. Returns the pair index or -1.
@@ -77,15 +84,17 @@ inline spmm_status_t from_hip(hipError_t e) {
 
 // Kernel launchers (csr_kernels.hip / bsr_kernels.hip). Pointers are device
 // pointers; all shape checks have been done by the API layer.
+// carry_ws: csrmm_carry_bytes of workspace (split-row partials, rewritten by
+// every launch); the split-row tickets come from ensure_tickets.
 spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* rowptr,
                                     const int* colind, const float* val, int base,
                                     const float* B, int ldb, float alpha, float beta, float* C,
-                                    int ldc, float* carry_val, int* carry_row, int nnz_hint,
+                                    int ldc, void* carry_ws, int nnz_hint,
                                     int hot = 0);  // 1: hot-tagged colind; 2: and B below 4 GB
 // spmm_csr_hot_analysis: colind_out = colind with bit 31 set on hot columns
 spmm_status_t launch_csr_hot_analysis(spmm_context* ctx, int k, long long nnz, const int* colind,
                                       int base, long long hot_rows, int* colind_out);
-size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n, int* nwaves_out);
+size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n);
 
 spmm_status_t launch_transpose16(spmm_context* ctx, int rows, int cols, const uint16_t* src,
                                  int ld_src, uint16_t* dst, int ld_dst);

@@ -11,9 +11,10 @@
 //    (rows + nnz) merge path is cut into equal pieces, one per wave64; each
 //    wave finds its start/end coordinates with a 32-ary cooperative search
 //    on rowptr (5 dependent loads for 2.4M rows), walks its nnz range and
-//    emits every row that ends inside it. The one row a wave leaves
-//    unfinished becomes a "carry" that a tiny fix-up kernel adds in wave
-//    order (deterministic, no atomics).
+//    emits every row that ends inside it. A row split over several waves is
+//    finished in the same launch by the last of them to arrive (split_row_*
+//    below: partials in wave order, deterministic, one ticket atomic per
+//    wave and split row).
 //  * One nnz per wave-instruction. All 64 lanes gather the same B row: lane l
 //    owns columns [VEC*l, VEC*l+VEC) of a 64*VEC-wide column tile, so a
 //    gather is one coalesced 256/512/1024-byte global_load_dword{,x2,x4}
@@ -104,6 +105,48 @@ __device__ __forceinline__ float rdlanef(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// Split rows. A row whose nonzeros span merge-path waves w_a .. w_b is
+// finished by the last of those waves to arrive, in the same launch:
+//  * waves w_a .. w_b - 1 end inside the row and leave their partial in their
+//    carry slot; w_b, where the row ends, leaves its partial in its head slot
+//    instead of writing C;
+//  * after its stores have completed (s_waitcnt vmcnt(0)), each of them adds 1
+//    to the row's ticket, tickets[tile * nwaves + w_a] (an agent-scope atomic),
+//    and the wave whose add completes w_b - w_a + 1 arrivals resets the ticket
+//    and writes the row:
+//      C = fma(alpha, ((c_a + c_{a+1}) + ... + c_{b-1}), epi(head))
+//    which is, bit for bit, the two-launch form it replaces (the kernel wrote
+//    epi(head) to C, a fix-up kernel then added alpha * the carries in wave
+//    order).
+// The partials cross workgroups (and XCDs) by MI355X_MICROARCH.md's
+// counter hand-off: sc1 stores and sc1 loads of every handed-off word, each
+// storing wave's vmcnt(0) before its add, the last adder loading only after
+// its add has returned. Tickets are zero between launches (tickets of the
+// handle, never shared with other buffers).
+__device__ __forceinline__ void st_sc1(float* p, float x) {
+  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Adds this wave's arrival to *t (lane 0); true in the wave that completes
+// `count` arrivals, which also resets *t for the next launch.
+__device__ __forceinline__ bool split_row_arrive(int* t, int count, int lane) {
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __builtin_amdgcn_readlane(old, 0);
+  if (old + 1 != count) return false;
+  if (lane == 0) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+// Workspace of the split rows: carry and head slots (kWave * 4 floats each,
+// the widest column tile) for every (column tile, wave).
+struct SplitWs {
+  float* carry;
+  float* head;
+  __host__ __device__ static size_t slot_floats() { return kWave * 4; }
+};
+
 // Merge-path search for two diagonals at once: lanes 0-31 search d0, lanes
 // 32-63 search d1. A[i] = rowptr[i+1]-rp0 (row-end offsets), B[j] = j.
 // Returns (per lane) the number of row ends consumed before the diagonal.
@@ -141,8 +184,8 @@ template <int VEC, bool NT, int HOT = 0>
 __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
     int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, int base, const float* __restrict__ B, int ldb, float alpha,
-    float beta, float* __restrict__ C, int ldc, float* __restrict__ carry_val,
-    int* __restrict__ carry_row, int nwaves) {
+    float beta, float* __restrict__ C, int ldc, SplitWs sws, int* __restrict__ tickets,
+    int nwaves) {
   typedef typename Vec<VEC>::T vec;
   const int lane = threadIdx.x & (kWave - 1);
   const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
@@ -168,6 +211,13 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   const int aoff = rp0 - base;  // array offset of relative nnz 0
   const int J = j1 - j0;
   const int slot = ct * nwaves + w;
+  // the first row this wave finishes began in an earlier wave: its partial goes
+  // to the head slot (split rows, above)
+  const int rs0 = i0 < i1 ? rowptr[i0] - rp0 : 0;
+  const bool split_head = i0 < i1 && rs0 < j0;
+  bool head_pending = split_head;
+  float* const carry_p = sws.carry + (size_t)slot * SplitWs::slot_floats() + lane * VEC;
+  float* const head_p = sws.head + (size_t)slot * SplitWs::slot_floats() + lane * VEC;
 
   // Row ends: lane l holds raw rowptr[rbase+1+l] for 64 rows, reloaded in
   // place when exhausted (one pipeline drain per 64 rows). The load is free
@@ -191,6 +241,15 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   const unsigned ldb4 = 4u * (unsigned)ldb;
 
   auto emit = [&](int row) {
+    if (head_pending) {  // the end of a split row: the raw partial to the head slot
+      head_pending = false;
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) {
+        st_sc1(head_p + c, acc[c]);
+        acc[c] = 0.f;
+      }
+      return;
+    }
     float* cp = Ct + (size_t)row * ldc;
     vec out;
     if (beta == 0.f) {
@@ -334,18 +393,62 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   }
   // Carry: the partial of row i1 accumulated over [max(j0, start(i1)), j1).
   bool has_carry = false;
+  int rs1 = 0;
   if (i1 < m && J > 0) {
-    const int rs1 = rowptr[i1] - rp0;
+    rs1 = rowptr[i1] - rp0;
     has_carry = j1 > rs1;
   }
   if (has_carry) {
-    if (lane == 0) carry_row[slot] = i1;
-    vec out;
 #pragma unroll
-    for (int c = 0; c < VEC; ++c) vset<VEC>(out, c, acc[c]);
-    vstore<VEC>(carry_val + (size_t)slot * (kWave * VEC) + lane * VEC, out);
-  } else if (lane == 0) {
-    carry_row[slot] = -1;
+    for (int c = 0; c < VEC; ++c) st_sc1(carry_p + c, acc[c]);
+  }
+  if (!split_head && !has_carry) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partials are stored
+  // the last arrival of a split row writes it (w_a .. w_b: the row's waves)
+  auto finish = [&](int r, int wa, int wb) {
+    const size_t sf = SplitWs::slot_floats();
+    const float* cw = sws.carry + ((size_t)ct * nwaves + wa) * sf + lane * VEC;
+    float sum[VEC], x[VEC];
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) sum[c] = ld_sc1(cw + c);
+    for (int w2 = wa + 1; w2 < wb; ++w2) {
+      cw += sf;
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) sum[c] = sum[c] + ld_sc1(cw + c);
+    }
+    const float* hw = sws.head + ((size_t)ct * nwaves + wb) * sf + lane * VEC;
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) x[c] = ld_sc1(hw + c);
+    if (!col_ok) return;
+    float* cp = Ct + (size_t)r * ldc;
+    vec out;
+    if (beta == 0.f) {
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) vset<VEC>(out, c, alpha * x[c]);
+    } else {
+      const vec old = vload<VEC>(cp);
+#pragma unroll
+      for (int c = 0; c < VEC; ++c)
+        vset<VEC>(out, c, __builtin_fmaf(beta, vget<VEC>(old, c), alpha * x[c]));
+    }
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) vset<VEC>(out, c, __builtin_fmaf(alpha, sum[c], vget<VEC>(out, c)));
+    if constexpr (NT) {
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) __builtin_nontemporal_store(vget<VEC>(out, c), cp + c);
+    } else {
+      vstore<VEC>(cp, out);
+    }
+  };
+  if (split_head) {
+    const int wa = (int)(((long long)i0 + rs0) / per);
+    if (split_row_arrive(tickets + (size_t)ct * nwaves + wa, w - wa + 1, lane)) finish(i0, wa, w);
+  }
+  if (has_carry) {
+    const int re1 = rowptr[i1 + 1] - rp0;
+    const int wa = (int)(((long long)i1 + rs1) / per), wb = (int)(((long long)i1 + re1) / per);
+    if (split_row_arrive(tickets + (size_t)ct * nwaves + wa, wb - wa + 1, lane))
+      finish(i1, wa, wb);
   }
 }
 
@@ -365,8 +468,8 @@ template <bool NT, int LPG, int PD, bool HOT = false>
 __global__ __launch_bounds__(kWG) void csr_group_kernel(
     int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, int base, const float* __restrict__ B, int ldb, float alpha,
-    float beta, float* __restrict__ C, int ldc, float* __restrict__ carry_val,
-    int* __restrict__ carry_row, int nwaves) {
+    float beta, float* __restrict__ C, int ldc, SplitWs sws, int* __restrict__ tickets,
+    int nwaves) {
   const int lane = threadIdx.x & (kWave - 1);
   const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
   if (w >= nwaves) return;
@@ -389,6 +492,12 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
   const int j1 = (int)(d1 - i1);
   const int aoff = rp0 - base;
   const int slot = w;
+  // split rows (above): column c of a slot is float c (the VEC = 1 layout)
+  const int rs0 = i0 < i1 ? rowptr[i0] - rp0 : 0;
+  const bool split_head = i0 < i1 && rs0 < j0;
+  bool head_pending = split_head;
+  float* const carry_p = sws.carry + (size_t)slot * SplitWs::slot_floats() + col;
+  float* const head_p = sws.head + (size_t)slot * SplitWs::slot_floats() + col;
 
   auto load_rowends = [&](int rb) -> int { return rowptr[min(rb + 1 + lane, m)]; };
   int rbase = i0;
@@ -424,6 +533,15 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
   };
   auto emit = [&](int row) {
     const f32x4 t = fold(acc);
+    if (head_pending) {  // the end of a split row: the summed partial to the head slot
+      head_pending = false;
+      if (grp == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st_sc1(head_p + c, t[c]);
+      }
+      acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
     if (grp == 0 && col_ok) {
       float* cp = C + (size_t)row * ldc + col;
       f32x4 out;
@@ -523,50 +641,44 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
     advance_row();
   }
   bool has_carry = false;
+  int rs1 = 0;
   if (i1 < m && j1 > j0) {
-    const int rs1 = rowptr[i1] - rp0;
+    rs1 = rowptr[i1] - rp0;
     has_carry = j1 > rs1;
   }
   if (has_carry) {
-    if (lane == 0) carry_row[slot] = i1;
     const f32x4 t = fold(acc);
-    if (grp == 0) *reinterpret_cast<f32x4*>(carry_val + (size_t)slot * kWave + col) = t;
-  } else if (lane == 0) {
-    carry_row[slot] = -1;
-  }
-}
-
-// Adds the carries of rows split across waves, summed in wave order. One
-// wave per carry slot; only the first slot of a run of equal rows works.
-template <int VEC>
-__global__ __launch_bounds__(kWG) void csr_carry_fixup_kernel(int n, float alpha,
-                                                              float* __restrict__ C, int ldc,
-                                                              const float* __restrict__ carry_val,
-                                                              const int* __restrict__ carry_row,
-                                                              int nwaves) {
-  typedef typename Vec<VEC>::T vec;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
-  if (w >= nwaves) return;
-  const int ct = blockIdx.y;
-  const int base_slot = ct * nwaves;
-  const int r = carry_row[base_slot + w];
-  if (r < 0) return;
-  if (w > 0 && carry_row[base_slot + w - 1] == r) return;
-  const int col0 = ct * (kWave * VEC) + lane * VEC;
-  vec sum = vload<VEC>(carry_val + (size_t)(base_slot + w) * (kWave * VEC) + lane * VEC);
-  for (int w2 = w + 1; w2 < nwaves && carry_row[base_slot + w2] == r; ++w2) {
-    const vec x = vload<VEC>(carry_val + (size_t)(base_slot + w2) * (kWave * VEC) + lane * VEC);
+    if (grp == 0) {
 #pragma unroll
-    for (int c = 0; c < VEC; ++c) vset<VEC>(sum, c, vget<VEC>(sum, c) + vget<VEC>(x, c));
+      for (int c = 0; c < 4; ++c) st_sc1(carry_p + c, t[c]);
+    }
   }
-  if (col0 < n) {
-    float* cp = C + (size_t)r * ldc + col0;
-    vec cur = vload<VEC>(cp);
-#pragma unroll
-    for (int c = 0; c < VEC; ++c)
-      vset<VEC>(cur, c, __builtin_fmaf(alpha, vget<VEC>(sum, c), vget<VEC>(cur, c)));
-    vstore<VEC>(cp, cur);
+  if (!split_head && !has_carry) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partials are stored
+  // the last arrival writes the row: lane l column l (n <= 64)
+  auto finish = [&](int r, int wa, int wb) {
+    const size_t sf = SplitWs::slot_floats();
+    const float* cw = sws.carry + (size_t)wa * sf + lane;
+    float sum = ld_sc1(cw);
+    for (int w2 = wa + 1; w2 < wb; ++w2) {
+      cw += sf;
+      sum = sum + ld_sc1(cw);
+    }
+    const float x = ld_sc1(sws.head + (size_t)wb * sf + lane);
+    if (lane >= n) return;
+    float* cp = C + (size_t)r * ldc + lane;
+    float out = beta == 0.f ? alpha * x : __builtin_fmaf(beta, *cp, alpha * x);
+    out = __builtin_fmaf(alpha, sum, out);
+    if constexpr (NT) __builtin_nontemporal_store(out, cp); else *cp = out;
+  };
+  if (split_head) {
+    const int wa = (int)(((long long)i0 + rs0) / per);
+    if (split_row_arrive(tickets + wa, w - wa + 1, lane)) finish(i0, wa, w);
+  }
+  if (has_carry) {
+    const int re1 = rowptr[i1 + 1] - rp0;
+    const int wa = (int)(((long long)i1 + rs1) / per), wb = (int)(((long long)i1 + re1) / per);
+    if (split_row_arrive(tickets + wa, wb - wa + 1, lane)) finish(i1, wa, wb);
   }
 }
 
@@ -832,22 +944,20 @@ spmm_status_t launch_csr_hot_analysis(spmm_context* ctx, int k, long long nnz, c
   return from_hip(hipGetLastError());
 }
 
-size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n, int* nwaves_out) {
+size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n) {
   // The grid does not depend on nnz beyond the cap: size it for the cap.
+  // Carry and head slots (kWave * 4 floats) per (column tile, wave).
   const int wpc = ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu : 16;
-  const int nw = ctx->num_cus * wpc;
+  const size_t nw = (size_t)ctx->num_cus * wpc;
   (void)m;
-  const int ntiles_max = (n + 63) / 64;  // VEC = 1 worst case
-  if (nwaves_out) *nwaves_out = nw;
-  const size_t slots = (size_t)nw * ntiles_max;
-  return slots * 64 * sizeof(float) + slots * sizeof(int) + 256;
+  const size_t slots = nw * (size_t)((n + 63) / 64);  // VEC = 1: the most column tiles
+  return 2 * slots * SplitWs::slot_floats() * sizeof(float) + 256;
 }
 
 spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* rowptr,
                                     const int* colind, const float* val, int base,
                                     const float* B, int ldb, float alpha, float beta, float* C,
-                                    int ldc, float* carry_val, int* carry_row, int nnz_hint,
-                                    int hot) {
+                                    int ldc, void* carry_ws, int nnz_hint, int hot) {
   if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   const int vec = pick_vec(n, B, ldb, C, ldc);
   const int tile = kWave * vec;
@@ -855,6 +965,16 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   const int nw = csr_nwaves(ctx, m, nnz_hint);
   dim3 grid((nw + kWavesPerWG - 1) / kWavesPerWG, ntiles);
   dim3 block(kWG);
+  // split rows: carry and head slots in the workspace (sized by csrmm_carry_bytes for
+  // the largest grid), tickets of the handle (zero between launches)
+  const size_t slots_max = (size_t)ctx->num_cus *
+                           (ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu : 16) *
+                           (size_t)((n + 63) / 64);
+  SplitWs sws;
+  sws.carry = static_cast<float*>(carry_ws);
+  sws.head = sws.carry + slots_max * SplitWs::slot_floats();
+  if (spmm_status_t st = ensure_tickets(ctx, (size_t)nw * ntiles)) return st;
+  int* tickets = ctx->tickets;
   const int slot = timing_begin(ctx);
   const bool nt = (ctx->csr_flags & SPMM_CSR_NT_STREAMS) != 0;
   const bool grouped = n <= kGroupMaxK && n % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
@@ -874,16 +994,16 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
 #define SPMM_LAUNCH_GRP_PD(L, PD)                                                              \
   if (hot)                                                                                     \
     hipLaunchKernelGGL((csr_group_kernel<true, L, PD, true>), g8, block, 0, ctx->stream, m, n,  \
-                       rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
-                       carry_row, nw);                                                          \
+                       rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, sws, tickets,    \
+                       nw);                                                                     \
   else if (nt)                                                                                 \
     hipLaunchKernelGGL((csr_group_kernel<true, L, PD>), g8, block, 0, ctx->stream, m, n,        \
-                       rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
-                       carry_row, nw);                                                          \
+                       rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, sws, tickets,    \
+                       nw);                                                                     \
   else                                                                                         \
     hipLaunchKernelGGL((csr_group_kernel<false, L, PD>), g8, block, 0, ctx->stream, m, n,       \
-                       rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
-                       carry_row, nw);
+                       rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, sws, tickets,    \
+                       nw);
     // gathers in flight per wave: 1 at K <= 16, where a gather costs a whole
     // 128-B line and depth is no help; 2 at K = 32 (1.21 vs 1.35 ms on
     // products); 4 at K = 48 / 64 (2.19 / 2.27 ms vs 2.33 / 2.37 for the
@@ -906,19 +1026,14 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
 #undef SPMM_LAUNCH_GRP
 #undef SPMM_LAUNCH_GRP_PD
     timing_end(ctx, slot);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return from_hip(e);
-    hipLaunchKernelGGL(csr_carry_fixup_kernel<1>, g8, block, 0, ctx->stream, n, alpha, C, ldc,
-                       carry_val, carry_row, nw);
     return from_hip(hipGetLastError());
   }
 #define SPMM_LAUNCH_MP(V, N)                                                                   \
   hipLaunchKernelGGL((csr_mergepath_kernel<V, N>), grid, block, 0, ctx->stream, m, n, rowptr, \
-                     colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val, carry_row, nw)
+                     colind, val, base, B, ldb, alpha, beta, C, ldc, sws, tickets, nw)
 #define SPMM_LAUNCH_HOT(V, H)                                                                  \
   hipLaunchKernelGGL((csr_mergepath_kernel<V, true, H>), grid, block, 0, ctx->stream, m, n,    \
-                     rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, carry_val,       \
-                     carry_row, nw)
+                     rowptr, colind, val, base, B, ldb, alpha, beta, C, ldc, sws, tickets, nw)
   if (hot == 2) {
     if (vec == 4) SPMM_LAUNCH_HOT(4, 2); else if (vec == 2) SPMM_LAUNCH_HOT(2, 2); else SPMM_LAUNCH_HOT(1, 2);
   } else if (hot) {
@@ -933,22 +1048,6 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
 #undef SPMM_LAUNCH_MP
 #undef SPMM_LAUNCH_HOT
   timing_end(ctx, slot);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return from_hip(e);
-  switch (vec) {
-    case 4:
-      hipLaunchKernelGGL(csr_carry_fixup_kernel<4>, grid, block, 0, ctx->stream, n, alpha, C, ldc,
-                         carry_val, carry_row, nw);
-      break;
-    case 2:
-      hipLaunchKernelGGL(csr_carry_fixup_kernel<2>, grid, block, 0, ctx->stream, n, alpha, C, ldc,
-                         carry_val, carry_row, nw);
-      break;
-    default:
-      hipLaunchKernelGGL(csr_carry_fixup_kernel<1>, grid, block, 0, ctx->stream, n, alpha, C, ldc,
-                         carry_val, carry_row, nw);
-      break;
-  }
   return from_hip(hipGetLastError());
 }
 

@@ -7,7 +7,8 @@ import ctypes
 import numpy as np
 import pytest
 
-from helpers import (TOL_F16_ACC, TOL_F32, assert_normwise, oracle_bsrmm_f64, oracle_csrmm_f64)
+from helpers import (TOL_F16_ACC, TOL_F32, assert_normwise, oracle_bsrmm_f32, oracle_bsrmm_f64,
+                     oracle_csrmm_f64)
 
 pytestmark = pytest.mark.gpu
 
@@ -685,7 +686,7 @@ def test_dense_block_product_option(oracle, device, bs, dtype, layout):
             fin = ~np.isnan(ref)
             assert_normwise(got[fin], ref[fin], absd[fin], TOL_F32 if dtype == "f32" else
                             TOL_F16_ACC, what)
-        elif bs in (16, 32):  # the column streams / column-masked kernels skip empty columns
+        else:  # the column streams, column-masked and lane-group kernels skip empty columns
             assert np.isfinite(got).all(), what + ": default contract keeps C finite"
 
 
@@ -945,3 +946,77 @@ def test_bsrmm_analysed_f16_matches_column_stream(device):
     ops.bsrmm_analysed_f16(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n, ldb=n, C=C2, ldc=n)
     torch.cuda.synchronize()
     assert torch.equal(C1, C2)
+
+
+@pytest.mark.parametrize("bs", [2, 4, 8])
+@pytest.mark.parametrize("direction", [0, 1])
+@pytest.mark.parametrize("n", [64, 130, 256])
+def test_small_bs_lane_group_bit_exact(oracle, device, bs, direction, n):
+    """bs 2 / 4 / 8 (bsr_small_kernel): every output element is the oracle's
+    sequential fp32 FMA chain (blocks in order, columns in order,
+    oracle_bsrmm_f32 = rocsparse_bsrmm_template<float>'s order) bit for bit,
+    long and empty block rows included; alpha / beta on a second call."""
+    ops = _ops()
+    rng = np.random.default_rng(100 * bs + 10 * direction + n % 7)
+    mb, kb = 37, 300 // bs
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.25, empty_rows=(5,))
+    vb = v.reshape(-1, bs, bs)  # about half the block columns empty (the zero-row gathers)
+    for k in range(vb.shape[0]):
+        dead = rng.random(bs) < 0.5
+        if direction == 0:
+            vb[k][:, dead] = 0.0
+        else:
+            vb[k][dead, :] = 0.0
+    v = vb.reshape(-1)
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B.reshape(-1))
+    C = torch.full((mb * bs, n), float("nan"), device=device)
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=C, ldc=n, direction=direction)
+    torch.cuda.synchronize()
+    want = oracle_bsrmm_f32(oracle, direction, mb, n, bs, rp, ci, v, B, n, 0).reshape(mb * bs, n)
+    got = C.cpu().numpy()
+    assert (got == want).all(), f"bs {bs}: {int((got != want).sum())} elements differ"
+    C0 = rng.uniform(-1, 1, (mb * bs, n)).astype(np.float32)
+    dC = _dev(C0)[0]
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n, alpha=0.5, beta=-2.0,
+              direction=direction)
+    torch.cuda.synchronize()
+    want2 = oracle_bsrmm_f32(oracle, direction, mb, n, bs, rp, ci, v, B, n, 0, 0.5, -2.0, C0,
+                             n, 0).reshape(mb * bs, n)
+    assert (dC.cpu().numpy() == want2).all(), f"bs {bs}: alpha / beta epilogue"
+
+
+@pytest.mark.parametrize("n,oc", [(128, 0), (256, 0), (96, 1)])
+def test_bsr64_matches_bs32_sub_blocks(oracle, device, n, oc):
+    """bs 64 runs the bs 32 column stream on each block's 32 x 32 sub-blocks:
+    C is bit-identical to the bs 32 kernel on the same matrix cut at bs 32
+    (device csr2bsr of the same CSR: its sub-blocks, in block-column order,
+    the all-zero ones dropped, which the stream skips anyway), and within the
+    bar of the f64 oracle."""
+    ops = _ops()
+    rng = np.random.default_rng(640 + n + oc)
+    m = 64 * 41
+    # dense-ish diagonal regions plus one scattered entry per row: fewer than 64
+    # blocks per bs 32 block row, so the bs 32 launch cuts no row into segments
+    rows = []
+    for r in range(m):
+        dense = (r // 32) * 32 + rng.choice(32, 12, replace=False)
+        rows.append(np.unique(np.concatenate([dense, rng.choice(m, 1)])))
+    rp = np.concatenate([[0], np.cumsum([len(x) for x in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    v = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    drp, dci, dv = _dev(rp, ci, v)
+    B = torch.rand((m, n), device=device) * 2 - 1
+    outs = []
+    for bs in (64, 32):
+        brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=m, n=m, bs=bs)
+        mb = m // bs
+        C = torch.full((m, n), float("nan"), device=device) if oc == 0 else \
+            torch.full((n, m), float("nan"), device=device)
+        ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=n, bs=bs, ldb=n, C=C, ldc=n if oc == 0 else m,
+                  order_c=oc)
+        torch.cuda.synchronize()
+        outs.append(C if oc == 0 else C.t())
+    assert torch.equal(outs[0], outs[1]), "bs 64 differs from the bs 32 sub-block stream"
+    ref, absd = oracle_csrmm_f64(oracle, m, n, rp, ci, v, B.cpu().numpy(), n, 0)
+    assert_normwise(outs[0].cpu().numpy(), ref, absd, TOL_F32, f"bs 64 n={n}")

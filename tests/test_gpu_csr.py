@@ -417,3 +417,82 @@ def test_colmajor_forms_match_rowmajor(device, m, K, beta):
         assert torch.equal(dCc.t(), dC)
     else:  # rows split across waves associate beta * C with the carries differently
         assert torch.allclose(dCc.t(), dC, rtol=1e-6, atol=1e-5)
+
+
+def merge_path_model(oracle, rp, ci, v, B, nwaves):
+    """C of the merge-path kernel restated on the host (csr_kernels.hip; alpha
+    1, beta 0): the (rows + nnz) path cut at diagonals w * per, per =
+    ceil((m + nnz) / nwaves); nnz j of row r lies in wave (r + j) // per and
+    the row's end in wave (r + re) // per. A row inside one wave is one
+    sequential fp32 FMA chain (gespmm_csrmm.h:124-129); a row split over waves
+    w_a .. w_b is ((c_a + c_{a+1}) + ... + c_{b-1}) + head, each term the chain
+    over that wave's share, the head (wave w_b's share) possibly empty."""
+    m, K = rp.size - 1, B.shape[1]
+    nnz = int(rp[-1])
+    per = -(-(m + nnz) // nwaves)
+    seg_rp, seg_of = [0], []  # segments: CSR of sub-rows; row -> its segment ids
+    for r in range(m):
+        rs, re = int(rp[r]), int(rp[r + 1])
+        wa, wb = (r + rs) // per, (r + re) // per
+        ids = []
+        for w in range(wa, wb + 1):
+            lo, hi = max(rs, w * per - r), min(re, (w + 1) * per - r)
+            ids.append(len(seg_rp) - 1)
+            seg_rp.append(seg_rp[-1] + max(0, hi - lo))
+        seg_of.append(ids)
+    seg_rp = np.asarray(seg_rp, np.int32)
+    S = oracle_csrmm_f32(oracle, seg_rp.size - 1, K, seg_rp, ci, v, B, K, 0).reshape(-1, K)
+    C = np.empty((m, K), np.float32)
+    for r, ids in enumerate(seg_of):
+        if len(ids) == 1:
+            C[r] = S[ids[0]]
+            continue
+        acc = S[ids[0]].copy()
+        for s in ids[1:-1]:
+            acc = acc + S[s]
+        C[r] = acc + S[ids[-1]]
+    return C
+
+
+@pytest.mark.parametrize("K,opts", [(128, 0), (512, 0), (256, 0), (32, 2), (64, 0)])
+def test_split_rows_bit_exact_model(oracle, device, K, opts):
+    """Every row, split or not, is bit-identical to merge_path_model: the
+    split rows finished in the same launch by their last-arriving wave (split
+    row tickets, csr_kernels.hip) sum their partials in wave order. Power-law
+    rows with hubs that span dozens of waves, empty rows, K at every vector
+    width of the main kernel (K = 32 with SPMM_CSR_SEQUENTIAL_ROWS; K = 64 is
+    the lane-group kernel, whose rows are interleaved chains: checked within
+    the bar)."""
+    from spmm_hip import prep
+    from spmm_hip._lib import CSR_NT_STREAMS
+    ops = _ops()
+    m, nnz = 40000, 600000
+    rp, ci = prep.powerlaw_csr(m, nnz, 15000, 2.1, 11)
+    v = np.random.default_rng(3).uniform(-1, 1, ci.size).astype(np.float32)
+    B = np.random.default_rng(4).uniform(-1, 1, (m, K)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    h = ops.Handle()
+    h.set_csr_options(CSR_NT_STREAMS | opts)
+    C = torch.full((m, K), float("nan"), device=device)
+    ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=C, ldc=K, handle=h)
+    torch.cuda.synchronize()
+    got = C.cpu().numpy()
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    nwaves = min(-(-(m + ci.size) // 512), cus * 16)
+    if K == 64:
+        _check_rowmajor(oracle, rp, ci, v, B, C, "lane-group kernel, split rows")
+        return
+    want = merge_path_model(oracle, rp, ci, v, B, nwaves)
+    per = -(-(m + ci.size) // nwaves)
+    split = np.array([(r + rp[r]) // per != (r + rp[r + 1]) // per for r in range(m)])
+    assert split.sum() > 50, "the case must split many rows"
+    bad = ~(got == want)
+    assert not bad.any(), (f"K={K}: {int(bad.any(axis=1).sum())} rows differ from the merge-path "
+                           f"model ({int(bad[split].any(axis=1).sum())} of {int(split.sum())} "
+                           f"split rows)")
+    # repeated launches: the tickets are back at zero after every launch
+    for _ in range(3):
+        ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=C, ldc=K, handle=h)
+    torch.cuda.synchronize()
+    assert np.array_equal(C.cpu().numpy(), want), "relaunch differs"
+    h.close()

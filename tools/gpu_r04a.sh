@@ -12,7 +12,7 @@ echo "== sc1 repro"
 timeout -k 10 120 python tools/sc1_run.py tools/_sc1/libspmm_hip.so 1 > $O/sc1_form.log 2>&1; rc=$?; cat $O/sc1_form.log | grep '^{'; stop $rc
 timeout -k 10 120 python tools/sc1_run.py tools/_sc1nop/libspmm_hip.so 1 > $O/sc1_nop.log 2>&1; rc=$?; cat $O/sc1_nop.log | grep '^{'; stop $rc
 echo "== new tests"
-timeout -k 10 900 python -u -m pytest tests/test_gpu_scale.py tests/test_gpu_bsr.py tests/test_gpu_configs.py -x -v --timeout 200 --timeout-method thread -k "analysed_bs or nonfinite or dense_block or default_stream or native_multi" > $O/pytest_new.log 2>&1; rc=$?; tail -3 $O/pytest_new.log; stop $rc
+timeout -k 10 900 python -u -m pytest tests/test_gpu_csr.py tests/test_gpu_scale.py tests/test_gpu_bsr.py tests/test_gpu_configs.py -x -v --timeout 200 --timeout-method thread -k "analysed_bs or nonfinite or dense_block or default_stream or native_multi or split_rows" > $O/pytest_new.log 2>&1; rc=$?; tail -3 $O/pytest_new.log; stop $rc
 [ $rc -ne 0 ] && { grep -E "Error|assert" $O/pytest_new.log | head -20; exit $rc; }
 echo "== full gpu suite"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?; tail -2 $O/pytest_gpu.log; stop $rc
