@@ -71,6 +71,13 @@ WORKLOADS = {
                             p_in=0.99, bs=32, K=128, dtype="fp32", analysed=True),
     "products_bsr16_f16_an": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                   p_in=0.97, bs=16, K=512, dtype="fp16", analysed=True),
+    # config 5 on the grouped stream (spmm_bsr16_group_analysis_f16 once, groups of
+    # `grouped` block rows sharing their B-row copies; spmm_bsrmm_grouped_f16 timed)
+    "products_bsr16_f16_grp": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                                   p_in=0.97, bs=16, K=512, dtype="fp16", grouped=4),
+    "products_rcm_bsr16_f16_grp": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                                       p_in=0.97, bs=16, K=512, dtype="fp16", reorder="rcm",
+                                       grouped=4),
     "products_hybrid32": dict(kind="hybrid", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                               p_in=0.97, bs=32, K=128, density="auto"),
     # §8f rank 2 in the loop: scrambled ids -> in-repo RCM -> divide + hybrid
@@ -466,6 +473,17 @@ def cpu_baseline(args, K: int) -> dict:
     res = dict(legs["all_physical_cores"])
     res["protocol"] = ("BASELINE.md §2: OMP_NUM_THREADS = physical cores in this process's "
                        "affinity, OMP_PROC_BIND=close, OMP_PLACES=cores")
+    q = hc.get("cgroup_cpu_quota_cpus")
+    T = hc["physical_cores_in_affinity"]
+    if isinstance(q, (int, float)) and q < T:
+        # the quota, not the core count, is the host's capacity here
+        res["quota_note"] = (
+            f"the process's cgroup grants {q:g} CPUs of time per CFS period across its {T} "
+            f"cores: {T} OpenMP threads run stop-go (all of them stopped whenever the group "
+            f"has spent its quota), so the all-cores figure is a contention measurement and "
+            f"its per-sample spread cannot be brought under 10 % by longer samples (config 1: "
+            f"0.2-0.8 ms calls land anywhere in the stop-go phases); the "
+            f"gpu_share_16_threads leg, within the quota, is the host's usable rate")
     for label, _ in counts[1:]:
         res[label] = legs[label]
     res.update(hc)
@@ -854,7 +872,23 @@ def run_bsr(args, W, world, rank, dev, dist):
     h = ops.Handle()
     fn = ops.bsrmm if dt == "fp32" else ops.bsrmm_f16
     an = bool(W.get("analysed"))
+    gw = int(args.group_rows or W.get("grouped") or 0)
     analysis_ms = None
+    grp = None
+    if gw:
+        if (bs, dt) != (16, "fp16"):
+            raise SystemExit("the grouped stream is bs 16 fp16")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        grp = ops.GroupedBsr16(d_brp, d_bci, d_bv, mb=mb, group_rows=gw, handle=h)
+        torch.cuda.synchronize()
+        analysis_ms = (time.perf_counter() - t0) * 1e3
+        del d_bv
+
+        def fn(rp_, ci_, _v, B_, *, mb, kb, n, bs, ldb, C, ldc, order_b=ops.ORDER_ROW,
+               order_c=ops.ORDER_ROW, handle=None):
+            grp.mm(B_, kb=kb, n=n, ldb=ldb, order_b=order_b, C=C, ldc=ldc, order_c=order_c)
+        d_bv = None
     if an:
         if (bs, dt) not in ((32, "fp32"), (16, "fp16")):
             raise SystemExit("the analysed column streams are bs 32 fp32 and bs 16 fp16")
@@ -943,13 +977,20 @@ def run_bsr(args, W, world, rank, dev, dist):
         mfma_flops = active_cols * 2.0 * bs * K
     else:
         mfma_flops = dense_flops
+    if grp is not None:
+        # one v_mfma_f32_16x16x16_f16 per item, wave and 16 output columns
+        nitems = (grp.bytes - 256) // (64 + gw * 512)
+        mfma_flops = nitems * gw * 2.0 * 16 * 16 * K
     peak = MFMA_PEAK_TFLOPS[dt]
     kbytes = bsr_bytes(mb, nnzb, bs, K, s)
     # Compulsory bytes (the roofline): the block values and the BSR index
     # arrays once per column tile of the kernel, every distinct B row the
     # product touches once, the C write once.
-    # (analysed: the masks and only the nonzero columns' values, column-major)
+    # (analysed: the masks and only the nonzero columns' values, column-major;
+    # grouped: the analysis buffer, item rows and A fragments)
     a_bytes = (4 * nnzb + s * active_cols * bs) if an else s * nnzb * bs * bs
+    if grp is not None:
+        a_bytes = grp.bytes - 4 * (mb + 1) - 4 * nnzb  # the index terms are added below
     comp_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + a_bytes) + s * b_rows * K +
                   4 * mb * bs * K)
     # Upper byte model (round 2's roofline): the same A and indices, the B
@@ -958,7 +999,8 @@ def run_bsr(args, W, world, rank, dev, dist):
     cm_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + a_bytes) + s * active_cols * K +
                 4 * mb * bs * K) if cm else kbytes
     t = kms / 1e3
-    kname = (("bsr32_f32_cs2_kernel" if bs == 32 else
+    kname = ("bsr16_f16_grp_kernel" if grp is not None else
+             ("bsr32_f32_cs2_kernel" if bs == 32 else
               "bsr32_f32_cs2_kernel (bs 64 sub-blocks)" if bs == 64 else
               "bsr16_f16_cs_kernel" if cs16 else "bsr16_cm_kernel") if cm else
              f"bsr_small_kernel<{bs}>" if bs in (2, 4, 8) and dt == "fp32" else
@@ -973,7 +1015,9 @@ def run_bsr(args, W, world, rank, dev, dist):
         data=data,
         config={"workload": f"{args.workload}: " + (f"scrambled ids -> {reorder['method']} -> "
                                                     if reorder else "") +
-                            f"csr2bsr bs={bs} + " + ("analysis + bsrmm_analysed" if an else "bsrmm") +
+                            f"csr2bsr bs={bs} + " + ("analysis + bsrmm_analysed" if an else
+                                                     f"group analysis (W={gw}) + bsrmm_grouped"
+                                                     if grp is not None else "bsrmm") +
                             f" K={K} {dt}", "n": n,
                 "layout_BC": args.bsr_layout,
                 "nnz": nnz, "K": K, "bs": bs, "nnzb": nnzb,
@@ -1009,7 +1053,7 @@ def run_bsr(args, W, world, rank, dev, dist):
                   "full_panel_model_bytes_per_launch": kbytes,
                   "full_panel_model_GBps": round(kbytes / t / 1e9, 1)},
         csr_same_matrix_ms=round(csr_ms, 4), csr2bsr_host_seconds=round(t_conv, 2),
-        analysis_ms=round(analysis_ms, 4) if an else None,
+        analysis_ms=round(analysis_ms, 4) if (an or grp is not None) else None,
         gen_seconds=round(t_gen, 2), reorder=reorder)
     tr = rec["roofline"]["traffic"]
     if tr:
@@ -1018,7 +1062,28 @@ def run_bsr(args, W, world, rank, dev, dist):
         rec["roofline"]["traffic_GBps"] = round(tr / t / 1e9, 1)
         rec["roofline"]["traffic_frac"] = round(tr / t / 1e9 / HBM_PEAK_GBPS, 4)
         rec["roofline"]["traffic_over_compulsory"] = round(tr / comp_bytes, 3)
-    if (not an and args.bsr_layout == "row" and not args.no_analysed_side and
+    if (not an and grp is None and args.bsr_layout == "row" and not args.no_analysed_side and
+            (bs, dt) == (16, "fp16")):
+        # Beside the drop-in line (not `value`): the grouped stream (groups of 4 block
+        # rows sharing their B-row copies, analysis once, timed apart).
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g4 = ops.GroupedBsr16(d_brp, d_bci, d_bv, mb=mb, group_rows=4, handle=h)
+        torch.cuda.synchronize()
+        a_ms = (time.perf_counter() - t0) * 1e3
+        e_g, k_g = timed_loop(lambda: g4.mm(B, kb=mb, n=K, ldb=K, C=C, ldc=K), h, args.steps,
+                              args.warmup, 1, dist)
+        ni = (g4.bytes - 256) // (64 + 4 * 512)
+        rec["grouped_entry"] = {
+            "entry": "spmm_bsr16_group_analysis_f16 (4 block rows per group) once + "
+                     "spmm_bsrmm_grouped_f16 per step",
+            "value": round(2.0 * nnz * K * args.steps / e_g / 1e9, 2), "unit": "GFLOP/s",
+            "ms_per_step": round(e_g / args.steps * 1e3, 4), "kernel_ms": round(k_g, 4),
+            "analysis_ms_first_call": round(a_ms, 3), "items": int(ni),
+            "mfma_executed_TFLOPs": round(ni * 4 * 2.0 * 256 * K / (k_g / 1e3) / 1e12, 2)}
+        g4.close()
+        del g4
+    if (not an and grp is None and args.bsr_layout == "row" and not args.no_analysed_side and
             (bs, dt) in ((32, "fp32"), (16, "fp16"))):
         # Beside the drop-in line (not `value`): the same product on the analysed
         # entry (column masks + column-major A once per matrix, timed apart).
@@ -1185,6 +1250,8 @@ def main() -> None:
     ap.add_argument("--csr-options", type=int, default=None, help="SPMM_CSR_* flags")
     ap.add_argument("--no-hot-side", action="store_true",
                     help="skip the hot-column side measurement of the products_csr line")
+    ap.add_argument("--group-rows", type=int, default=0,
+                    help="bs 16 fp16: run the grouped stream with this many block rows per group")
     ap.add_argument("--no-analysed-side", action="store_true",
                     help="skip the analysed-entry side measurement of the bs 32 / bs 16 fp16 lines")
     ap.add_argument("--chunks", type=int, default=0,

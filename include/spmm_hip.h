@@ -30,6 +30,7 @@
 #ifndef SPMM_HIP_H
 #define SPMM_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -282,6 +283,42 @@ spmm_status_t spmm_bsrmm_analysed_f16(spmm_handle_t handle, int mb, int kb, int 
                                       const uint16_t* valCol, const unsigned* masks,
                                       const uint16_t* B, int ldb, spmm_order_t orderB,
                                       float beta, float* C, int ldc, spmm_order_t orderC);
+
+/* The grouped bs = 16 fp16 stream (an extension, once per matrix like the
+ * analyses above; DESIGN.md §4 "The grouped stream"). groupRows (2, 4 or 8;
+ * 0 = 4) adjacent block rows form a group whose waves share one copy of each
+ * B row the union of their nonzero columns needs: on a reordered graph
+ * neighbouring block rows need mostly the same rows (products stand-in: the
+ * union is 0.43 of the (block row, column) pairs at 4 rows, 0.29 at 8).
+ * Two phases: with buffer == NULL, *bufferBytes receives the size of the
+ * caller-owned device buffer; with a buffer of that size the analysis fills
+ * it. It reads the block columns and column masks on the host, so the call
+ * synchronises the handle's stream. The handle records the buffer's layout:
+ * spmm_bsrmm_grouped_f16 on the same handle takes it (until
+ * spmm_bsr16_group_release or another analysis into the same buffer).
+ * INVALID_VALUE for a bad dir / groupRows, negative sizes, null pointers that
+ * are needed, a row pointer that does not run 0 .. nnzb, or a short buffer. */
+spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction_t dir, int mb,
+                                            int nnzb, int groupRows, const int* bsrRowPtr,
+                                            const int* bsrColInd, const uint16_t* bsrVal,
+                                            void* buffer, size_t* bufferBytes);
+
+/* C(mb*16 x n, fp32) = alpha * A * B(kb*16 x n, fp16) + beta * C on a group
+ * analysis of A (fp32 accumulate), B row- or column-major (staged row-major),
+ * C either order. Same sizes and ld checks as spmm_bsrmm_ex_f16;
+ * INVALID_VALUE for a buffer this handle has no analysis of or another mb;
+ * NOT_SUPPORTED when n % 8 != 0, a row-major ldb % 8 != 0 or B is not 16-B
+ * aligned (spmm_bsrmm_ex_f16 serves those shapes). Non-finite B is GROUPED:
+ * an inf / NaN in B row J*16 + c reaches every row of a group (all its block
+ * rows) when any of its block rows holds a value other than +-0 in that
+ * column; with finite B the product equals spmm_bsrmm_ex_f16's within the
+ * fp32 bar. */
+spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n,
+                                     const void* buffer, float alpha, const uint16_t* B, int ldb,
+                                     spmm_order_t orderB, float beta, float* C, int ldc,
+                                     spmm_order_t orderC);
+/* Forgets the handle's record of a group-analysis buffer (before freeing it). */
+spmm_status_t spmm_bsr16_group_release(spmm_handle_t handle, const void* buffer);
 
 /* fp16 A and B (IEEE binary16 bit patterns), fp32 accumulate and fp32 C.
  * bs = 16 runs on v_mfma_f32_16x16x32_f16 with two blocks per instruction. */

@@ -900,7 +900,7 @@ __global__ __launch_bounds__(256) void bsr16_analysis_kernel(int nnzb, int rowdi
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq)
         msk |= ((b & (0x1111111111111111ull << qq)) != 0ull ? 1u : 0u) << (4 * qq + e);
-      dst[(4 * q + e) * 16 + r] = x[e];
+      if (val_col) dst[(4 * q + e) * 16 + r] = x[e];  // null: masks only (the group analysis)
     }
   } else {
     const unsigned long long b = __builtin_amdgcn_ballot_w64(
@@ -1782,13 +1782,17 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
   u32x2a an0 = {0u, 0u}, an1 = {0u, 0u}, ac0 = {0u, 0u}, ac1 = {0u, 0u};
   int astamp = -64;
+  // (each block's base is a 64-bit scalar address: the column-major copy of a large
+  // matrix passes 4 GB, which a 32-bit lane offset from val cannot reach; RCM-reordered
+  // products, 14.3 M blocks = 7.3 GB, returned wrong values with one)
+  const unsigned aoff_lane = 2u * (unsigned)(16 * r16 + 4 * g);
   auto issue_a_reg = [&](int kr_) {  // blocks k0 + kr_, + 1 (clamped)
-    const unsigned o0 = 2u * (unsigned)(min(k0 + kr_, k1 - 1) * 256 + 16 * r16 + 4 * g);
-    const unsigned o1 = 2u * (unsigned)(min(k0 + kr_ + 1, k1 - 1) * 256 + 16 * r16 + 4 * g);
-    asm volatile("global_load_dwordx2 %0, %2, %4\n\t"
-                 "global_load_dwordx2 %1, %3, %4"
+    const _Float16* b0 = val + (size_t)min(k0 + kr_, k1 - 1) * 256;
+    const _Float16* b1 = val + (size_t)min(k0 + kr_ + 1, k1 - 1) * 256;
+    asm volatile("global_load_dwordx2 %0, %2, %3\n\t"
+                 "global_load_dwordx2 %1, %2, %4"
                  : "=&v"(an0), "=&v"(an1)
-                 : "v"(o0), "v"(o1), "s"(val)
+                 : "v"(aoff_lane), "s"(b0), "s"(b1)
                  : "memory");
     nis += 2;
     astamp = nis;
@@ -2539,6 +2543,241 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// bs = 16 fp16, GROUPED item stream (spmm_bsr16_group_analysis_f16 once per
+// matrix + spmm_bsrmm_grouped_f16). What bounds the column stream above is the
+// B-row gather (40 GB through the texture path per launch on the
+// products stand-in, B 34.7 GB of it for 2.5 GB of distinct rows): every
+// (block row, nonzero column) pair copies its B row, and neighbouring block
+// rows of a reordered graph need mostly the same rows. A workgroup here owns W
+// adjacent block rows (one wave each) and streams the UNION of their nonzero
+// columns (products stand-in: 0.43 of the pairs at W = 4, 0.29 at W = 8):
+//  * an item is 16 union entries (block column J, column c), in (J, c) order;
+//    its 16 B rows are copied ONCE into an LDS stage shared by the W waves
+//    (8 whole-row copies of 1 KB, split over the waves; the stage layout and
+//    the transposed reads are the column stream's FLR ones);
+//  * each wave's A fragment of the item (its block row's values of the 16
+//    entries, zero where its row stores no such column) was built by the
+//    analysis: one 8-B load per lane;
+//  * a ring of P stages: per item every wave waits for its own copies (the
+//    counted ladder), one s_barrier publishes the stage and retires the slot the
+//    next copies overwrite, then 16 transposed reads and 16 MFMAs per wave.
+// Non-finite B: a B row of the item meets the W block rows' A fragments, zeros
+// included, so an inf / NaN in it reaches every row of the group whenever one
+// of its block rows holds a value in that column (the grouped contract,
+// include/spmm_hip.h).
+// ---------------------------------------------------------------------------
+template <int W, int P, bool CROW>
+__global__ __launch_bounds__(64 * W) void bsr16_f16_grp_kernel(
+    int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
+    const unsigned* __restrict__ afrag, const _Float16* __restrict__ B, int ldb, float alpha,
+    float beta, float* __restrict__ C, int ldc) {
+  static_assert(W == 2 || W == 4 || W == 8, "waves per group");
+  static_assert(P >= 2 && P <= 4, "stages");
+  constexpr int COLS = 256, kRowB = 512, kCh = 32, kT = 16, kStage = 16 * kRowB;
+  constexpr int kCpw = 8 / W;  // 1-KB copies per wave per item (8 per item)
+  constexpr int kSw = 2;       // FLR swizzle: chunk c of row R at 16-B slot (c + 2R) & 31
+  __shared__ __attribute__((aligned(16))) char smem[P * kStage];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int g = lane >> 4, r16 = lane & 15;
+  const int grp = blockIdx.x;
+  const int br = grp * W + w;
+  const int jt = blockIdx.y * COLS;
+  const int i0 = item_ptr[grp], i1 = item_ptr[grp + 1];
+  const unsigned lds0 = lds_addr(smem);
+  const size_t ldb2 = (size_t)ldb * 2;
+  const char* const zrow = reinterpret_cast<const char*>(g_zero_row) - 2 * (size_t)jt;
+
+  // this wave's copies: copy cc = w * kCpw + j brings item rows 2 cc (lanes 0-31), 2 cc + 1
+  unsigned boffr[kCpw];
+#pragma unroll
+  for (int j = 0; j < kCpw; ++j) {
+    const int R = 2 * (w * kCpw + j) + (lane >> 5);
+    boffr[j] = 2u * (unsigned)min(jt + 8 * (((lane & 31) - kSw * R) & (kCh - 1)), n - 8);
+  }
+  unsigned tra[kT];
+  {
+    const int R = 4 * g + ((lane >> 2) & 3);
+#pragma unroll
+    for (int t = 0; t < kT; ++t)
+      tra[t] = lds0 + (unsigned)kRowB * R +
+               16u * ((2 * t + ((lane & 3) >> 1) + kSw * R) & (kCh - 1)) + 8u * (lane & 1);
+  }
+
+  f32x4 acc[kT];
+#pragma unroll
+  for (int t = 0; t < kT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int nis = 0;               // vector-memory operations issued by this wave
+  int rrow[kCpw], rstamp = -64;  // row indices of the next item to issue (in flight)
+  typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
+  u32x2a fan[P];             // A fragments in flight (asm-only registers)
+  int stamp[P];
+#pragma unroll
+  for (int s = 0; s < P; ++s) {
+    fan[s] = u32x2a{0u, 0u};
+    stamp[s] = -64;
+  }
+#pragma unroll
+  for (int j = 0; j < kCpw; ++j) rrow[j] = -1;
+  const int ilast = max(i1 - 1, i0);
+  // row indices of item `it` (clamped): lane L of copy j needs rows[it][2 (w kCpw + j) + L / 32]
+  auto load_rows = [&](int it) {
+    const int* src = rows + (size_t)min(it, ilast) * 16;
+#pragma unroll
+    for (int j = 0; j < kCpw; ++j)
+      asm volatile("global_load_dword %0, %1, %2"
+                   : "=&v"(rrow[j])
+                   : "v"(4u * (unsigned)(2 * (w * kCpw + j) + (lane >> 5))), "s"(src)
+                   : "memory");
+    nis += kCpw;
+    rstamp = nis;
+  };
+  // item `it` into stage slot `s`: its row indices landed, its copies and A fragment issued
+  auto issue = [&](int it, int s) {
+    int rw[kCpw];
+    if constexpr (kCpw == 1)
+      asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
+                   : "=&v"(rw[0]) : "s"(nis - rstamp), "v"(rrow[0]) : "scc", "memory");
+    else if constexpr (kCpw == 2)
+      asm volatile(SPMM_VM_LADDER("%2") "v_mov_b32 %0, %3\n\tv_mov_b32 %1, %4"
+                   : "=&v"(rw[0]), "=&v"(rw[1])
+                   : "s"(nis - rstamp), "v"(rrow[0]), "v"(rrow[1]) : "scc", "memory");
+    else
+      asm volatile(SPMM_VM_LADDER("%4")
+                   "v_mov_b32 %0, %5\n\tv_mov_b32 %1, %6\n\tv_mov_b32 %2, %7\n\tv_mov_b32 %3, %8"
+                   : "=&v"(rw[0]), "=&v"(rw[1]), "=&v"(rw[2]), "=&v"(rw[3])
+                   : "s"(nis - rstamp), "v"(rrow[0]), "v"(rrow[1]), "v"(rrow[2]), "v"(rrow[3])
+                   : "scc", "memory");
+    char* const stage = smem + s * kStage;
+#pragma unroll
+    for (int j = 0; j < kCpw; ++j) {
+      const char* be = rw[j] >= 0 ? reinterpret_cast<const char*>(B) + (size_t)rw[j] * ldb2 : zrow;
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(be + boffr[j]),
+                                       (lds_void_t)(stage + 1024 * (w * kCpw + j)), 16, 0, 0);
+    }
+    const unsigned* fsrc = afrag + ((size_t)min(it, ilast) * W + w) * 128;
+    asm volatile("global_load_dwordx2 %0, %1, %2"
+                 : "=&v"(fan[s]) : "v"(8u * (unsigned)lane), "s"(fsrc) : "memory");
+    nis += kCpw + 1;
+    stamp[s] = nis;
+  };
+
+  if (i0 < i1) {
+    load_rows(i0);
+#pragma unroll
+    for (int q = 0; q + 1 < P; ++q) {
+      issue(i0 + q, q);
+      load_rows(i0 + q + 1);
+    }
+    for (int base = i0; base < i1; base += P) {
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        const int it = base + s;
+        if (it >= i1) break;  // uniform over the workgroup: every wave runs the same items
+        // this wave's copies of item `it` and its A fragment landed; then every wave's
+        f16x4 fa;
+        {
+          u32x2a y;
+          asm volatile(SPMM_VM_LADDER("%1") "v_mov_b64 %0, %2"
+                       : "=&v"(y) : "s"(nis - stamp[s]), "v"(fan[s]) : "scc", "memory");
+          fa = __builtin_bit_cast(f16x4, y);
+        }
+        __builtin_amdgcn_s_barrier();
+        // slot (s + P - 1) % P was read by every wave in the previous item: refill it
+        issue(it + P - 1, (s + P - 1) % P);
+        load_rows(it + P);
+        f16x4 fb[16];
+        asm volatile(
+            "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
+              "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
+            : "v"(tra[0]), "v"(tra[1]), "v"(tra[2]), "v"(tra[3]), "v"(tra[4]), "v"(tra[5]),
+              "v"(tra[6]), "v"(tra[7]), "n"(s * kStage)
+            : "memory");
+        asm volatile(
+            "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+            "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(fb[8]), "=&v"(fb[9]), "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]),
+              "=&v"(fb[13]), "=&v"(fb[14]), "=&v"(fb[15])
+            : "v"(tra[8]), "v"(tra[9]), "v"(tra[10]), "v"(tra[11]), "v"(tra[12]), "v"(tra[13]),
+              "v"(tra[14]), "v"(tra[15]), "n"(s * kStage)
+            : "memory");
+#pragma unroll
+        for (int t = 0; t < kT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[t], 0, 0, 0);
+      }
+    }
+  }
+  // nothing in flight past here (the prefetches of clamped items included); the
+  // registers those loads fill stay reserved until this wait (uses after it)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < P; ++s) asm volatile("" : : "v"(fan[s]));
+#pragma unroll
+  for (int j = 0; j < kCpw; ++j) asm volatile("" : : "v"(rrow[j]));
+  if (br >= mb) return;
+#pragma unroll
+  for (int t = 0; t < kT; ++t) {
+    const int j = jt + 16 * t + r16;
+    if (j >= n) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t row = (size_t)br * 16 + 4 * g + e;
+      float* p = CROW ? C + row * ldc + j : C + (size_t)j * ldc + row;
+      *p = epi(acc[t][e], alpha, beta, p);
+    }
+  }
+}
+
+// A fragments of the grouped stream (the device half of the group analysis):
+// one wave per (item, wave of the group); lane (g, r) gets A[r][entries 4g ..
+// 4g + 3] of that wave's block row, src[item][e][w] the block holding entry e
+// (-1: none, zero), entry e's column rows[item][e] & 15 (-1: padding, zero).
+__global__ __launch_bounds__(256) void bsr16_grp_fill_kernel(long long nwork, int W, int rowdir,
+                                                             const int* __restrict__ rows,
+                                                             const int* __restrict__ src,
+                                                             const uint16_t* __restrict__ val,
+                                                             unsigned* __restrict__ afrag) {
+  const int lane = threadIdx.x & 63;
+  const long long wk = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wk >= nwork) return;
+  const long long item = wk / W;
+  const int w = (int)(wk % W);
+  const int g = lane >> 4, r = lane & 15;
+  unsigned short h[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = 4 * g + q;
+    const int row = rows[item * 16 + e];
+    const int k = src[(item * 16 + e) * W + w];
+    h[q] = 0;
+    if (row >= 0 && k >= 0) {
+      const int c = row & 15;
+      h[q] = val[(size_t)k * 256 + (rowdir ? r * 16 + c : c * 16 + r)];
+    }
+  }
+  unsigned* dst = afrag + (size_t)wk * 128 + 2 * lane;
+  dst[0] = (unsigned)h[0] | ((unsigned)h[1] << 16);
+  dst[1] = (unsigned)h[2] | ((unsigned)h[3] << 16);
+}
+
 // Fallback register-fragment kernels (layouts the copy kernels do not cover):
 // bsr32_f32_mfma_kernel / bsr16_*_mfma_kernel variant VAR (launch bounds and
 // prefetch form; the best of the round-1 sweep, DESIGN.md §4 "Variant history").
@@ -2990,6 +3229,42 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
     hipLaunchKernelGGL(bsr_generic_kernel<_Float16>, grid, dim3(256), 0, ctx->stream, mb, n, bs,
                        rowd, rowptr, colind, val, B, ldb, brow, alpha, beta, C, ldc, crow);
   }
+  timing_end(ctx, slot);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_bsr16_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
+                                    const int* rows, const int* src, const uint16_t* val,
+                                    unsigned* afrag) {
+  const long long nwork = nitems * W;
+  if (nwork == 0) return SPMM_STATUS_SUCCESS;
+  hipLaunchKernelGGL(bsr16_grp_fill_kernel, dim3((unsigned)((nwork + 3) / 4)), dim3(256), 0,
+                     ctx->stream, nwork, W, dir == SPMM_DIRECTION_ROW ? 1 : 0, rows, src, val,
+                     afrag);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, int ngroups,
+                                       const int* item_ptr, const int* rows,
+                                       const unsigned* afrag, const uint16_t* B16, int ldb,
+                                       float alpha, float beta, float* C, int ldc, bool crow) {
+  if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  const _Float16* B = reinterpret_cast<const _Float16*>(B16);
+  const int slot = timing_begin(ctx);
+  const dim3 grid(ngroups, (n + 255) / 256);
+#define GRP_LAUNCH(W_)                                                                           \
+  do {                                                                                           \
+    if (crow)                                                                                    \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, 3, true>), grid, dim3(64 * W_), 0,            \
+                         ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc); \
+    else                                                                                         \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, 3, false>), grid, dim3(64 * W_), 0,           \
+                         ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc); \
+  } while (0)
+  if (W == 8) GRP_LAUNCH(8);
+  else if (W == 4) GRP_LAUNCH(4);
+  else GRP_LAUNCH(2);
+#undef GRP_LAUNCH
   timing_end(ctx, slot);
   return from_hip(hipGetLastError());
 }

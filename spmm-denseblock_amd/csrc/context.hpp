@@ -12,6 +12,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -46,6 +47,14 @@ struct spmm_context {
   // they live apart from ws, which other entries overwrite.
   int* tickets = nullptr;
   size_t tickets_cap = 0;
+  // Group analyses made on this handle (spmm_bsr16_group_analysis_f16): buffer ->
+  // its shape, so the grouped product needs no device read to size its grid.
+  struct GroupPlan {
+    int W, mb, ngroups;
+    long long nitems;
+    size_t bytes, rows_off, afrag_off;
+  };
+  std::map<const void*, GroupPlan> group_plans;
 
   // Kernel timing ring.
   bool timing = false;
@@ -133,5 +142,13 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
                                spmm_order_t orderC, const unsigned* masks = nullptr);
 spmm_status_t launch_bsr16_analysis(spmm_context* ctx, spmm_direction_t dir, int nnzb,
                                     const uint16_t* val, unsigned* masks, uint16_t* val_col);
+// the grouped bs 16 stream: A-fragment fill (analysis) and the product
+spmm_status_t launch_bsr16_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
+                                    const int* rows, const int* src, const uint16_t* val,
+                                    unsigned* afrag);
+spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, int ngroups,
+                                       const int* item_ptr, const int* rows,
+                                       const unsigned* afrag, const uint16_t* B16, int ldb,
+                                       float alpha, float beta, float* C, int ldc, bool crow);
 
 }  // namespace spmm

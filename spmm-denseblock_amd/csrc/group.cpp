@@ -1,0 +1,230 @@
+// group.cpp — the group analysis of the grouped bs 16 fp16 stream
+// (spmm_bsr16_group_analysis_f16 / spmm_bsrmm_grouped_f16, include/spmm_hip.h;
+// DESIGN.md §4, "The grouped stream").
+//
+// Once per matrix, like spmm_bsr16_analysis_f16 and cuSPARSE's SpMM preprocess
+// (the reference's rocsparse_bsrmm.h:102-256 has none):
+//  1. the device computes every block's column mask (bsr16_analysis_kernel,
+//     masks only) and the row pointer, block columns and masks come to the host;
+//  2. per group of W adjacent block rows the host merges the W sorted
+//     block-column lists (worker threads over groups) and enumerates the union
+//     of their nonzero columns in (block column J, column c) order, cut into
+//     items of 16 entries (the last one padded with row -1): the B row J*16 + c
+//     of each entry and, per wave w of the group, the block of row w holding
+//     block column J (-1: none);
+//  3. those index arrays go to the device and bsr16_grp_fill_kernel writes each
+//     wave's A fragment of each item into the caller's buffer.
+// The call synchronises the handle's stream (the host merge needs the masks).
+//
+// Buffer layout (caller-owned device memory, bufferBytes from the first call):
+//   [0, 256)                 reserved header
+//   item_ptr[ngroups + 1]    int32, the items of group g are [item_ptr[g], item_ptr[g+1])
+//   rows[nitems][16]         int32, B row of each entry (-1: padding)
+//   afrag[nitems][W][128]    uint32, lane l of wave w: A[l & 15][4 (l >> 4) .. + 3] fp16 x 4
+// The handle records the layout by buffer address (spmm_context::group_plans).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "context.hpp"
+#include "host_util.hpp"
+
+using namespace spmm;
+
+namespace {
+
+constexpr size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct GroupIndex {
+  std::vector<int> item_ptr;  // ngroups + 1
+  std::vector<int> rows;      // nitems * 16
+  std::vector<int> src;       // nitems * 16 * W
+};
+
+// Items of group g: the W rows' blocks merged by block column; for each block
+// column the union of the rows' masks, its set bits in order.
+void build_group(int g, int W, int mb, const int* rp, const int* ci, const unsigned* mk,
+                 std::vector<int>* rows, std::vector<int>* src) {
+  int cur[8], end[8];
+  for (int w = 0; w < W; ++w) {
+    const int br = g * W + w;
+    cur[w] = br < mb ? rp[br] : 0;
+    end[w] = br < mb ? rp[br + 1] : 0;
+  }
+  int e = 0;  // entries emitted so far
+  for (;;) {
+    int J = -1;
+    for (int w = 0; w < W; ++w)
+      if (cur[w] < end[w] && (J < 0 || ci[cur[w]] < J)) J = ci[cur[w]];
+    if (J < 0) break;
+    unsigned u = 0;
+    int kw[8];
+    for (int w = 0; w < W; ++w) {
+      kw[w] = -1;
+      // duplicate block columns in a row (not produced by csr2bsr) are taken in order
+      if (cur[w] < end[w] && ci[cur[w]] == J) {
+        kw[w] = cur[w];
+        u |= mk[cur[w]] & 0xffffu;
+        ++cur[w];
+      }
+    }
+    while (u) {
+      const int c = __builtin_ctz(u);
+      u &= u - 1;
+      rows->push_back(J * 16 + c);
+      for (int w = 0; w < W; ++w) src->push_back(kw[w]);
+      ++e;
+    }
+  }
+  while (e % 16) {  // pad the last item
+    rows->push_back(-1);
+    for (int w = 0; w < W; ++w) src->push_back(-1);
+    ++e;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction_t dir, int mb,
+                                            int nnzb, int groupRows, const int* bsrRowPtr,
+                                            const int* bsrColInd, const uint16_t* bsrVal,
+                                            void* buffer, size_t* bufferBytes) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if ((dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) || mb < 0 || nnzb < 0 ||
+      !bufferBytes)
+    return SPMM_STATUS_INVALID_VALUE;
+  const int W = groupRows == 0 ? 4 : groupRows;
+  if (W != 2 && W != 4 && W != 8) return SPMM_STATUS_INVALID_VALUE;
+  if (mb > 0 && !bsrRowPtr) return SPMM_STATUS_INVALID_VALUE;
+  if (nnzb > 0 && (!bsrColInd || !bsrVal)) return SPMM_STATUS_INVALID_VALUE;
+  const int ngroups = (mb + W - 1) / W;
+  hipStream_t st = handle->stream;
+  // masks on the device (scratch), then row pointer, block columns and masks to the host
+  std::vector<int> rp(mb + 1, 0), ci(nnzb);
+  std::vector<unsigned> mk(nnzb);
+  if (mb > 0) {
+    if (nnzb > 0) {
+      if (spmm_status_t s = ensure_scratch(handle, (size_t)nnzb * 4)) return s;
+      unsigned* dmk = static_cast<unsigned*>(handle->scratch);
+      if (spmm_status_t s = launch_bsr16_analysis(handle, dir, nnzb, bsrVal, dmk, nullptr)) return s;
+      hipError_t e = hipMemcpyAsync(mk.data(), dmk, (size_t)nnzb * 4, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(ci.data(), bsrColInd, (size_t)nnzb * 4, hipMemcpyDeviceToHost, st);
+      if (e != hipSuccess) return from_hip(e);
+    }
+    hipError_t e = hipMemcpyAsync(rp.data(), bsrRowPtr, (size_t)(mb + 1) * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return from_hip(e);
+    if (rp[0] != 0 || rp[mb] != nnzb) return SPMM_STATUS_INVALID_VALUE;
+    for (int i = 0; i < mb; ++i)
+      if (rp[i + 1] < rp[i]) return SPMM_STATUS_INVALID_VALUE;
+  }
+  // per-group items on worker threads, then concatenated in group order
+  std::vector<std::vector<int>> grows(ngroups), gsrc(ngroups);
+  spmm_host::parallel_for(ngroups, [&](int64_t lo, int64_t hi) {
+    for (int64_t g = lo; g < hi; ++g)
+      build_group((int)g, W, mb, rp.data(), ci.data(), mk.data(), &grows[g], &gsrc[g]);
+  });
+  GroupIndex gi;
+  gi.item_ptr.resize(ngroups + 1, 0);
+  for (int g = 0; g < ngroups; ++g) gi.item_ptr[g + 1] = gi.item_ptr[g] + (int)(grows[g].size() / 16);
+  const long long nitems = gi.item_ptr[ngroups];
+  const size_t rows_off = align256(256 + (size_t)(ngroups + 1) * 4);
+  const size_t afrag_off = align256(rows_off + (size_t)nitems * 64);
+  const size_t need = afrag_off + (size_t)nitems * W * 512;
+  if (!buffer) {
+    *bufferBytes = need;
+    return SPMM_STATUS_SUCCESS;
+  }
+  if (*bufferBytes < need) return SPMM_STATUS_INVALID_VALUE;
+  gi.rows.reserve((size_t)nitems * 16);
+  gi.src.reserve((size_t)nitems * 16 * W);
+  for (int g = 0; g < ngroups; ++g) {
+    gi.rows.insert(gi.rows.end(), grows[g].begin(), grows[g].end());
+    gi.src.insert(gi.src.end(), gsrc[g].begin(), gsrc[g].end());
+    std::vector<int>().swap(grows[g]);
+    std::vector<int>().swap(gsrc[g]);
+  }
+  char* buf = static_cast<char*>(buffer);
+  hipError_t e = hipMemsetAsync(buf, 0, 256, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(buf + 256, gi.item_ptr.data(), (size_t)(ngroups + 1) * 4,
+                       hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && nitems)
+    e = hipMemcpyAsync(buf + rows_off, gi.rows.data(), (size_t)nitems * 64, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) return from_hip(e);
+  if (nitems) {
+    // the entry sources go through the scratch buffer (the masks there are consumed)
+    if (spmm_status_t s = ensure_scratch(handle, (size_t)nitems * 16 * W * 4)) return s;
+    int* dsrc = static_cast<int*>(handle->scratch);
+    e = hipMemcpyAsync(dsrc, gi.src.data(), (size_t)nitems * 16 * W * 4, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return from_hip(e);
+    if (spmm_status_t s = launch_bsr16_grp_fill(
+            handle, nitems, W, dir, reinterpret_cast<const int*>(buf + rows_off), dsrc, bsrVal,
+            reinterpret_cast<unsigned*>(buf + afrag_off)))
+      return s;
+  }
+  // the host vectors are freed on return: wait for the copies that read them
+  e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return from_hip(e);
+  std::lock_guard<std::mutex> lk(handle->mu);
+  handle->group_plans[buffer] = spmm_context::GroupPlan{W, mb, ngroups, nitems, need, rows_off,
+                                                        afrag_off};
+  return SPMM_STATUS_SUCCESS;
+}
+
+spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n,
+                                     const void* buffer, float alpha, const uint16_t* B, int ldb,
+                                     spmm_order_t orderB, float beta, float* C, int ldc,
+                                     spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (mb < 0 || kb < 0 || n < 0) return SPMM_STATUS_INVALID_VALUE;
+  if ((orderB != SPMM_ORDER_ROW && orderB != SPMM_ORDER_COL) ||
+      (orderC != SPMM_ORDER_ROW && orderC != SPMM_ORDER_COL))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (mb == 0 || n == 0 || kb == 0) return SPMM_STATUS_SUCCESS;
+  if (!buffer || !B || !C) return SPMM_STATUS_INVALID_VALUE;
+  spmm_context::GroupPlan plan;
+  {
+    std::lock_guard<std::mutex> lk(handle->mu);
+    auto it = handle->group_plans.find(buffer);
+    if (it == handle->group_plans.end()) return SPMM_STATUS_INVALID_VALUE;
+    plan = it->second;
+  }
+  if (plan.mb != mb) return SPMM_STATUS_INVALID_VALUE;
+  const long long K = (long long)kb * 16, M = (long long)mb * 16;
+  if (orderB == SPMM_ORDER_COL ? ldb < K : ldb < n) return SPMM_STATUS_INVALID_VALUE;
+  if (orderC == SPMM_ORDER_COL ? ldc < M : ldc < n) return SPMM_STATUS_INVALID_VALUE;
+  // the stream copies whole 16-B chunks of 256-column B-row pieces
+  if (n < 8 || n % 8 || reinterpret_cast<uintptr_t>(B) % 16) return SPMM_STATUS_NOT_SUPPORTED;
+  const char* buf = static_cast<const char*>(buffer);
+  const uint16_t* Bx = B;
+  int ldbx = ldb;
+  if (orderB == SPMM_ORDER_COL) {  // staged row-major in the workspace, as the column streams
+    if (spmm_status_t s = ensure_workspace(handle, (size_t)K * n * 2)) return s;
+    uint16_t* Bt = static_cast<uint16_t*>(handle->ws);
+    if (spmm_status_t s = launch_transpose16(handle, n, (int)K, B, ldb, Bt, n)) return s;
+    Bx = Bt;
+    ldbx = n;
+  } else if (ldb % 8) {
+    return SPMM_STATUS_NOT_SUPPORTED;
+  }
+  return launch_bsrmm_grouped_f16(
+      handle, plan.W, mb, n, plan.ngroups, reinterpret_cast<const int*>(buf + 256),
+      reinterpret_cast<const int*>(buf + plan.rows_off),
+      reinterpret_cast<const unsigned*>(buf + plan.afrag_off), Bx, ldbx, alpha, beta, C, ldc,
+      orderC == SPMM_ORDER_ROW);
+}
+
+spmm_status_t spmm_bsr16_group_release(spmm_handle_t handle, const void* buffer) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  std::lock_guard<std::mutex> lk(handle->mu);
+  handle->group_plans.erase(buffer);
+  return SPMM_STATUS_SUCCESS;
+}
+
+}  // extern "C"

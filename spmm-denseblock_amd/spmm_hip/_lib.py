@@ -10,7 +10,8 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import c_longlong, POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_uint64, c_void_p
+from ctypes import (c_longlong, POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t,
+                    c_uint64, c_void_p)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(PKG_DIR)
@@ -93,6 +94,11 @@ _PROTOS = {
     "spmm_bsrmm_analysed_f32": (c_int, [_P, c_int, c_int, c_int, c_int, c_float, _P, _P, _P, _P,
                                         _P, c_int, c_int, c_float, _P, c_int, c_int]),
     "spmm_bsr16_analysis_f16": (c_int, [_P, c_int, c_int, _P, _P, _P]),
+    "spmm_bsr16_group_analysis_f16": (c_int, [_P, c_int, c_int, c_int, c_int, _P, _P, _P, _P,
+                                              POINTER(c_size_t)]),
+    "spmm_bsrmm_grouped_f16": (c_int, [_P, c_int, c_int, c_int, _P, c_float, _P, c_int, c_int,
+                                       c_float, _P, c_int, c_int]),
+    "spmm_bsr16_group_release": (c_int, [_P, _P]),
     "spmm_bsrmm_analysed_f16": (c_int, [_P, c_int, c_int, c_int, c_int, c_float, _P, _P, _P, _P,
                                         _P, c_int, c_int, c_float, _P, c_int, c_int]),
     "spmm_gespmm_csrmm_f64": (c_int, [c_int, c_int, _P, _P, _P, _P, _P, _P]),

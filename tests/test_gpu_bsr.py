@@ -1020,3 +1020,62 @@ def test_bsr64_matches_bs32_sub_blocks(oracle, device, n, oc):
     assert torch.equal(outs[0], outs[1]), "bs 64 differs from the bs 32 sub-block stream"
     ref, absd = oracle_csrmm_f64(oracle, m, n, rp, ci, v, B.cpu().numpy(), n, 0)
     assert_normwise(outs[0].cpu().numpy(), ref, absd, TOL_F32, f"bs 64 n={n}")
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+@pytest.mark.parametrize("n,ob,oc,alpha,beta", [(256, 0, 0, 1.0, 0.0), (512, 0, 0, 0.5, -1.0),
+                                                (136, 0, 1, 1.0, 0.0), (264, 1, 0, 2.0, 0.5)])
+def test_bsrmm_grouped_f16(oracle, device, W, n, ob, oc, alpha, beta):
+    """The grouped bs 16 fp16 stream (spmm_bsr16_group_analysis_f16 +
+    spmm_bsrmm_grouped_f16): groups of W block rows sharing the union of their
+    columns, an mb that W does not divide, empty block rows and blocks, empty
+    columns; against the f64 oracle of the same fp16 values, alpha / beta,
+    column-major B (staged) and C."""
+    ops = _ops()
+    rng = np.random.default_rng(16 * W + n + ob)
+    mb, kb = 37, 60
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, 16, 0.3)
+    v16 = v.astype(np.float16)
+    Bd = rng.uniform(-1, 1, (kb * 16, n)).astype(np.float16)
+    B = Bd if ob == 0 else np.ascontiguousarray(Bd.T)
+    m = mb * 16
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    Ch = C0 if oc == 0 else np.ascontiguousarray(C0.T)
+    drp, dci, dv, dB, dC = _dev(rp, ci, v16, B.reshape(-1), Ch.reshape(-1))
+    grp = ops.GroupedBsr16(drp, dci, dv, mb=mb, group_rows=W)
+    grp.mm(dB, kb=kb, n=n, ldb=n if ob == 0 else kb * 16, order_b=ob, C=dC,
+           ldc=n if oc == 0 else m, order_c=oc, alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    got = dC.cpu().numpy().reshape((m, n) if oc == 0 else (n, m))
+    got = got if oc == 0 else got.T
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, 16, rp, ci, v16, Bd, n, 0, half=True)
+    ref = alpha * ref + beta * C0.astype(np.float64)
+    absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+    assert_normwise(got, ref, absd, TOL_F16_ACC, f"grouped W={W} n={n} ob={ob} oc={oc}")
+    grp.close()
+
+
+def test_bsrmm_grouped_f16_checks(device):
+    """A buffer this handle holds no analysis of, or another mb, is
+    INVALID_VALUE; n % 8 != 0 is NOT_SUPPORTED (before any launch)."""
+    from spmm_hip._lib import INVALID_VALUE, NOT_SUPPORTED, SpmmError
+    ops = _ops()
+    rng = np.random.default_rng(3)
+    rp, ci, v = _column_sparse_bsr(rng, 5, 7, 16, 0.5)
+    drp, dci, dv = _dev(rp, ci, v.astype(np.float16))
+    grp = ops.GroupedBsr16(drp, dci, dv, mb=5)
+    B = torch.zeros((7 * 16, 128), dtype=torch.float16, device=device)
+    C = torch.zeros((5 * 16, 128), device=device)
+    grp.mb = 6
+    with pytest.raises(SpmmError) as e:
+        grp.mm(B, kb=7, n=128, ldb=128, C=C, ldc=128)
+    assert e.value.status == INVALID_VALUE
+    grp.mb = 5
+    with pytest.raises(SpmmError) as e:
+        grp.mm(B, kb=7, n=124, ldb=128, C=C, ldc=128)
+    assert e.value.status == NOT_SUPPORTED
+    grp.close()
+    with pytest.raises(SpmmError) as e:  # released: the handle no longer knows the buffer
+        grp.buffer = torch.empty(16, dtype=torch.uint8, device=device)
+        grp.mm(B, kb=7, n=128, ldb=128, C=C, ldc=128)
+    assert e.value.status == INVALID_VALUE

@@ -383,3 +383,37 @@ def test_nonfinite_contract_full_size(device):
         keep = ~want.repeat_interleave(bs)[:n]
         _within(C[:n][keep], Cc[keep], absd[keep], 2 * TOL_F32, f"flags {flags}: finite rows vs CSR")
         h.close()
+
+
+@pytest.mark.parametrize("W,reorder", [(4, False), (8, False), (4, True)])
+def test_grouped_bs16_f16_full_size(oracle, device, W, reorder):
+    """Config 5's product on the grouped stream at full size (products stand-in,
+    K = 512; after RCM too: 14.3 M blocks): sampled rows against the f64 oracle
+    of the same fp16 values and every row against the CSR kernel on the
+    fp16-rounded values."""
+    ops = _ops()
+    rp, ci, n = _graph("products", reorder)
+    K, bs = 512, 16
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float16).astype(np.float32)
+    drp, dci, dv = _dev(rp, ci, v)
+    mb = (n + bs - 1) // bs
+    B16 = (torch.rand((mb * bs, K), device=device) * 2 - 1).half()
+    Bf = B16[:n].float().contiguous()
+    Cc = ops.gespmm_csrmm(drp, dci, dv, Bf)
+    absd = ops.gespmm_csrmm(drp, dci, dv.abs(), Bf.abs())
+    del Bf
+    brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
+    del dci, dv
+    bval16 = bval.half()
+    del bval
+    grp = ops.GroupedBsr16(brp, bci, bval16, mb=mb, group_rows=W)
+    del bval16
+    Cg = torch.empty((mb * bs, K), device=device)
+    grp.mm(B16, kb=mb, n=K, ldb=K, C=Cg, ldc=K)
+    torch.cuda.synchronize()
+    what = f"grouped W={W} bs16 fp16 products{' RCM' if reorder else ''}"
+    rows = _sample_rows(brp.cpu().numpy(), bs, n, 41 + W + reorder)
+    _check_oracle_rows(oracle, Cg, rp, ci, v, B16, rows, TOL_F16_ACC, what)
+    _within(Cg[:n], Cc, absd, 2 * TOL_F16_ACC, what + " vs CSR")
+    assert not bool(Cg[n:].any()), "padding rows of C must be zero"
+    grp.close()
