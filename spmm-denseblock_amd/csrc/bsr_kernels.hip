@@ -2567,13 +2567,14 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 // of its block rows holds a value in that column (the grouped contract,
 // include/spmm_hip.h).
 // ---------------------------------------------------------------------------
-template <int W, int P, bool CROW>
-__global__ __launch_bounds__(64 * W) void bsr16_f16_grp_kernel(
+template <int W, int P, bool CROW, int OCC = 0>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
+void bsr16_f16_grp_kernel(
     int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
     const unsigned* __restrict__ afrag, const _Float16* __restrict__ B, int ldb, float alpha,
     float beta, float* __restrict__ C, int ldc) {
   static_assert(W == 2 || W == 4 || W == 8, "waves per group");
-  static_assert(P >= 2 && P <= 4, "stages");
+  static_assert(P >= 2 && P <= 6, "stages");
   constexpr int COLS = 256, kRowB = 512, kCh = 32, kT = 16, kStage = 16 * kRowB;
   constexpr int kCpw = 8 / W;  // 1-KB copies per wave per item (8 per item)
   constexpr int kSw = 2;       // FLR swizzle: chunk c of row R at 16-B slot (c + 2R) & 31
@@ -3252,19 +3253,44 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   const _Float16* B = reinterpret_cast<const _Float16*>(B16);
   const int slot = timing_begin(ctx);
   const dim3 grid(ngroups, (n + 255) / 256);
-#define GRP_LAUNCH(W_)                                                                           \
+  // stages and occupancy hint: P * 10 + OCC (TUNING builds: SPMM_GRP_VARIANT)
+  int gv = 30;
+#ifdef SPMM_TUNING
+  {
+    static const int env = [] {
+      const char* e = getenv("SPMM_GRP_VARIANT");
+      return e ? atoi(e) : 0;
+    }();
+    if (env == 30 || env == 50 || env == 33 || env == 54 || env == 52) gv = env;
+  }
+#endif
+#define GRP_LAUNCH1(W_, P_, O_)                                                                  \
   do {                                                                                           \
     if (crow)                                                                                    \
-      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, 3, true>), grid, dim3(64 * W_), 0,            \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_>), grid, dim3(64 * W_), 0,       \
                          ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc); \
     else                                                                                         \
-      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, 3, false>), grid, dim3(64 * W_), 0,           \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_>), grid, dim3(64 * W_), 0,      \
                          ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc); \
   } while (0)
+#ifdef SPMM_TUNING
+#define GRP_LAUNCH(W_)                                                                           \
+  do {                                                                                           \
+    if (gv == 50) GRP_LAUNCH1(W_, 5, 0);                                                          \
+    else if (gv == 33) GRP_LAUNCH1(W_, 3, 3);                                                     \
+    else if (gv == 54) GRP_LAUNCH1(W_, 5, 4);                                                     \
+    else if (gv == 52) GRP_LAUNCH1(W_, 5, 2);                                                     \
+    else GRP_LAUNCH1(W_, 3, 0);                                                                   \
+  } while (0)
+#else
+#define GRP_LAUNCH(W_) GRP_LAUNCH1(W_, 3, 0)
+#endif
+  (void)gv;
   if (W == 8) GRP_LAUNCH(8);
   else if (W == 4) GRP_LAUNCH(4);
   else GRP_LAUNCH(2);
 #undef GRP_LAUNCH
+#undef GRP_LAUNCH1
   timing_end(ctx, slot);
   return from_hip(hipGetLastError());
 }
