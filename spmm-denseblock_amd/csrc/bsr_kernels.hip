@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "context.hpp"
 
@@ -2567,6 +2568,12 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 // of its block rows holds a value in that column (the grouped contract,
 // include/spmm_hip.h).
 // ---------------------------------------------------------------------------
+// f(integral_constant<S>) for S = 0, 1, ... while it returns true (static slot indices)
+template <int... S, class F>
+__device__ __forceinline__ void slots_while(std::integer_sequence<int, S...>, F&& f) {
+  (void)(f(std::integral_constant<int, S>{}) && ...);
+}
+
 template <int W, int P, bool CROW, int OCC = 0>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
 void bsr16_f16_grp_kernel(
@@ -2672,11 +2679,9 @@ void bsr16_f16_grp_kernel(
       issue(i0 + q, q);
       load_rows(i0 + q + 1);
     }
-    for (int base = i0; base < i1; base += P) {
-#pragma unroll
-      for (int s = 0; s < P; ++s) {
-        const int it = base + s;
-        if (it >= i1) break;  // uniform over the workgroup: every wave runs the same items
+    // one item in slot s (s a constant: the fan[] / stage indices must be static)
+    auto step = [&](int it, auto sc) {
+      constexpr int s = decltype(sc)::value;
         // this wave's copies of item `it` and its A fragment landed; then every wave's
         f16x4 fa;
         {
@@ -2723,8 +2728,24 @@ void bsr16_f16_grp_kernel(
 #pragma unroll
         for (int t = 0; t < kT; ++t)
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[t], 0, 0, 0);
-      }
-    }
+    };
+    // whole rounds of P items, then the last < P with no edge back into the loop: a
+    // break out of the middle of an unrolled round, merged by the compiler with the
+    // latch, would reach the loop head with a slot's A fragment still in flight in a
+    // register the head is free to reuse (a path the trip count rules out, but the
+    // ISA check, tests/test_isa_waits.py, is path-insensitive and so is the allocator)
+    int base = i0;
+    for (; base + P <= i1; base += P)
+      slots_while(std::make_integer_sequence<int, P>{}, [&](auto sc) {
+        step(base + decltype(sc)::value, sc);
+        return true;
+      });
+    // uniform over the workgroup: every wave runs the same items
+    slots_while(std::make_integer_sequence<int, P>{}, [&](auto sc) {
+      if (base + decltype(sc)::value >= i1) return false;
+      step(base + decltype(sc)::value, sc);
+      return true;
+    });
   }
   // nothing in flight past here (the prefetches of clamped items included); the
   // registers those loads fill stay reserved until this wait (uses after it)
