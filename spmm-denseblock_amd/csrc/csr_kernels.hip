@@ -833,7 +833,15 @@ int csr_nwaves(spmm_context* ctx, int m, long long nnz) {
   const int wpc = ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu : 16;
   const long long cap = (long long)ctx->num_cus * wpc;
   const long long total = nnz >= 0 ? (long long)m + nnz : (long long)m * 32;
-  long long nw = (total + kMinItemsPerWave - 1) / kMinItemsPerWave;
+#ifdef SPMM_TUNING
+  static const int min_items = [] {
+    const char* e = getenv("SPMM_CSR_MIN_ITEMS");  // TUNING builds only
+    return e && atoi(e) > 0 ? atoi(e) : kMinItemsPerWave;
+  }();
+#else
+  constexpr int min_items = kMinItemsPerWave;
+#endif
+  long long nw = (total + min_items - 1) / min_items;
   if (nw < 1) nw = 1;
   if (nw > cap) nw = cap;
   return (int)nw;
