@@ -2579,7 +2579,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OC
 void bsr16_f16_grp_kernel(
     int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
     const unsigned* __restrict__ afrag, const _Float16* __restrict__ B, int ldb, float alpha,
-    float beta, float* __restrict__ C, int ldc) {
+    float beta, float* __restrict__ C, int ldc, int xm) {
   static_assert(W == 2 || W == 4 || W == 8, "waves per group");
   static_assert(P >= 2 && P <= 6, "stages");
   constexpr int COLS = 256, kRowB = 512, kCh = 32, kT = 16, kStage = 16 * kRowB;
@@ -2589,7 +2589,8 @@ void bsr16_f16_grp_kernel(
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int g = lane >> 4, r16 = lane & 15;
-  const int grp = blockIdx.x;
+  // neighbouring groups share B rows: chunks of xm groups per XCD keep them in one L2
+  const int grp = xcd_block_row(blockIdx.x, gridDim.x, xm);
   const int br = grp * W + w;
   const int jt = blockIdx.y * COLS;
   const int i0 = item_ptr[grp], i1 = item_ptr[grp + 1];
@@ -3275,32 +3276,42 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   const int slot = timing_begin(ctx);
   const dim3 grid(ngroups, (n + 255) / 256);
   // stages and occupancy hint: P * 10 + OCC (TUNING builds: SPMM_GRP_VARIANT)
-  int gv = 30;
+  int gv = 30, xm = 0;
 #ifdef SPMM_TUNING
   {
     static const int env = [] {
       const char* e = getenv("SPMM_GRP_VARIANT");
       return e ? atoi(e) : 0;
     }();
-    if (env == 30 || env == 50 || env == 33 || env == 54 || env == 52) gv = env;
+    static const int env_xm = [] {
+      const char* e = getenv("SPMM_GRP_XM");
+      return e ? atoi(e) : -1;
+    }();
+    if (env == 30 || env == 33 || env == 32 || env == 43 || env == 34 || env == 23 || env == 24)
+      gv = env;
+    if (env_xm >= 0) xm = env_xm;
   }
 #endif
 #define GRP_LAUNCH1(W_, P_, O_)                                                                  \
   do {                                                                                           \
     if (crow)                                                                                    \
       hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_>), grid, dim3(64 * W_), 0,       \
-                         ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc); \
+                         ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc, \
+                         xm);                                                                    \
     else                                                                                         \
       hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_>), grid, dim3(64 * W_), 0,      \
-                         ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc); \
+                         ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc, \
+                         xm);                                                                    \
   } while (0)
 #ifdef SPMM_TUNING
 #define GRP_LAUNCH(W_)                                                                           \
   do {                                                                                           \
-    if (gv == 50) GRP_LAUNCH1(W_, 5, 0);                                                          \
-    else if (gv == 33) GRP_LAUNCH1(W_, 3, 3);                                                     \
-    else if (gv == 54) GRP_LAUNCH1(W_, 5, 4);                                                     \
-    else if (gv == 52) GRP_LAUNCH1(W_, 5, 2);                                                     \
+    if (gv == 33) GRP_LAUNCH1(W_, 3, 3);                                                          \
+    else if (gv == 32) GRP_LAUNCH1(W_, 3, 2);                                                     \
+    else if (gv == 43) GRP_LAUNCH1(W_, 4, 3);                                                     \
+    else if (gv == 34) GRP_LAUNCH1(W_, 3, 4);                                                     \
+    else if (gv == 23) GRP_LAUNCH1(W_, 2, 3);                                                     \
+    else if (gv == 24) GRP_LAUNCH1(W_, 2, 4);                                                     \
     else GRP_LAUNCH1(W_, 3, 0);                                                                   \
   } while (0)
 #else
