@@ -45,7 +45,10 @@ constexpr int kWG = kWave * kWavesPerWG;
 constexpr int kU = 8;            // nnz per pipeline group
 constexpr int kR = 4;            // colind/val registers per lane per chunk
 constexpr int kChunk = kWave * kR / kU;  // groups per chunk (32)
-constexpr int kMinItemsPerWave = 512;
+// the merge-path grid's floor on items per wave: below waves_per_cu x CUs waves a small
+// matrix gets more, shorter waves (arxiv stand-in, K = 128: 0.0868 -> 0.0849 ms at 256;
+// 128 ties, profiles/r04d/csr_grid.jsonl)
+constexpr int kMinItemsPerWave = 256;
 constexpr int kGroupMaxK = 64;  // K handled by csr_group_kernel
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));

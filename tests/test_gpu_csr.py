@@ -478,7 +478,7 @@ def test_split_rows_bit_exact_model(oracle, device, K, opts):
     torch.cuda.synchronize()
     got = C.cpu().numpy()
     cus = torch.cuda.get_device_properties(device).multi_processor_count
-    nwaves = min(-(-(m + ci.size) // 512), cus * 16)
+    nwaves = min(-(-(m + ci.size) // 256), cus * 16)  # kMinItemsPerWave, csr_kernels.hip
     if K == 64:
         _check_rowmajor(oracle, rp, ci, v, B, C, "lane-group kernel, split rows")
         return
