@@ -32,8 +32,9 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 6
     dev = torch.device("cuda:0")
     bad = 0
-    # products stand-in (community order): CSR K=128, bs 32 CM4, bs 16 fp16
-    # K=512, hybrid fused (plain and split-bf16), device csr2bsr
+    # products stand-in (community order): CSR K=128, bs 32 column stream and its
+    # analysed form, bs 16 fp16 K=512 (drop-in, analysed, grouped), hybrid fused
+    # (plain and split-bf16), device csr2bsr
     n = 2449029
     rp, ci = prep.community_csr(n, 27.0, 32, 512, 0.97, 1234)
     v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
@@ -87,6 +88,14 @@ def main():
                 return C
             bad += check("bsr16 fp16 K=512 (analysed column stream)", run_an16, reps)
             del masks16, vcol16
+            g = ops.GroupedBsr16(brp, bci, bv16, mb=mb, group_rows=4)
+
+            def run_grp():
+                g.mm(B16, kb=mb, n=K, ldb=K, C=C, ldc=K)
+                return C
+            bad += check("bsr16 fp16 K=512 (grouped stream, 4 block rows)", run_grp, reps)
+            g.close()
+            del g
             del bv16, B16
         del brp, bci, C
         torch.cuda.empty_cache()
@@ -134,6 +143,20 @@ def main():
         ops.hybrid_csrmm(tuple(d[0:3]), tuple(d[3:6]), B, m=n, n=K, k=n, bs=bs, ldb=K, C=C, ldc=K)
         return C
     bad += check("RCM reddit hybrid (fused, longest first)", run, reps)
+    del d, brp, bci, bval
+    # bs 8 (lane-group VALU kernel) and bs 64 (the bs 32 column stream on sub-blocks)
+    for bs2 in (8, 64):
+        mb2 = (n + bs2 - 1) // bs2
+        B2 = torch.rand((mb2 * bs2, K), device=dev) * 2 - 1
+        C2 = torch.empty((mb2 * bs2, K), device=dev)
+        brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs2)
+
+        def run():
+            ops.bsrmm(brp, bci, bval, B2, mb=mb2, kb=mb2, n=K, bs=bs2, ldb=K, C=C2, ldc=K)
+            return C2
+        bad += check(f"RCM reddit bsr{bs2}", run, reps)
+        del brp, bci, bval, B2, C2
+        torch.cuda.empty_cache()
     print(f"total differing elements: {bad}", flush=True)
     sys.exit(1 if bad else 0)
 
