@@ -297,7 +297,8 @@ spmm_status_t spmm_bsrmm_analysed_f16(spmm_handle_t handle, int mb, int kb, int 
  * spmm_bsrmm_grouped_f16 on the same handle takes it (until
  * spmm_bsr16_group_release or another analysis into the same buffer).
  * INVALID_VALUE for a bad dir / groupRows, negative sizes, null pointers that
- * are needed, a row pointer that does not run 0 .. nnzb, or a short buffer. */
+ * are needed, a row pointer that does not run 0 .. nnzb, a negative block
+ * column, or a short buffer; NOT_SUPPORTED past 2^31 - 1 items. */
 spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction_t dir, int mb,
                                             int nnzb, int groupRows, const int* bsrRowPtr,
                                             const int* bsrColInd, const uint16_t* bsrVal,
@@ -306,7 +307,8 @@ spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction
 /* C(mb*16 x n, fp32) = alpha * A * B(kb*16 x n, fp16) + beta * C on a group
  * analysis of A (fp32 accumulate), B row- or column-major (staged row-major),
  * C either order. Same sizes and ld checks as spmm_bsrmm_ex_f16;
- * INVALID_VALUE for a buffer this handle has no analysis of or another mb;
+ * INVALID_VALUE for a buffer this handle has no analysis of, another mb, or a
+ * kb the analysed block columns do not fit (a column >= kb);
  * NOT_SUPPORTED when n % 8 != 0, a row-major ldb % 8 != 0 or B is not 16-B
  * aligned (spmm_bsrmm_ex_f16 serves those shapes). Non-finite B is GROUPED:
  * an inf / NaN in B row J*16 + c reaches every row of a group (all its block

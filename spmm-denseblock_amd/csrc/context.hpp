@@ -53,6 +53,7 @@ struct spmm_context {
     int W, mb, ngroups;
     long long nitems;
     size_t bytes, rows_off, afrag_off;
+    int max_col;  // largest block column (-1: none), checked against kb
   };
   std::map<const void*, GroupPlan> group_plans;
 

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <vector>
 
@@ -43,10 +44,16 @@ struct GroupIndex {
   std::vector<int> src;       // nitems * 16 * W
 };
 
+// block-column range of the matrix (the multiply checks kb against it: a B row
+// past the caller's K would be read out of bounds)
+struct ColRange {
+  int lo = 0, hi = -1;
+};
+
 // Items of group g: the W rows' blocks merged by block column; for each block
 // column the union of the rows' masks, its set bits in order.
 void build_group(int g, int W, int mb, const int* rp, const int* ci, const unsigned* mk,
-                 std::vector<int>* rows, std::vector<int>* src) {
+                 std::vector<int>* rows, std::vector<int>* src, ColRange* cr) {
   int cur[8], end[8];
   for (int w = 0; w < W; ++w) {
     const int br = g * W + w;
@@ -58,7 +65,13 @@ void build_group(int g, int W, int mb, const int* rp, const int* ci, const unsig
     int J = -1;
     for (int w = 0; w < W; ++w)
       if (cur[w] < end[w] && (J < 0 || ci[cur[w]] < J)) J = ci[cur[w]];
-    if (J < 0) break;
+    if (J < 0) {
+      // a negative block column ends the merge above: record it for the caller's check
+      for (int w = 0; w < W; ++w)
+        if (cur[w] < end[w]) cr->lo = std::min(cr->lo, ci[cur[w]]);
+      break;
+    }
+    cr->hi = std::max(cr->hi, J);
     unsigned u = 0;
     int kw[8];
     for (int w = 0; w < W; ++w) {
@@ -125,14 +138,25 @@ spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction
   }
   // per-group items on worker threads, then concatenated in group order
   std::vector<std::vector<int>> grows(ngroups), gsrc(ngroups);
+  std::vector<ColRange> cr(ngroups);
   spmm_host::parallel_for(ngroups, [&](int64_t lo, int64_t hi) {
     for (int64_t g = lo; g < hi; ++g)
-      build_group((int)g, W, mb, rp.data(), ci.data(), mk.data(), &grows[g], &gsrc[g]);
+      build_group((int)g, W, mb, rp.data(), ci.data(), mk.data(), &grows[g], &gsrc[g], &cr[g]);
   });
+  int max_col = -1;
+  for (const ColRange& c : cr) {
+    if (c.lo < 0) return SPMM_STATUS_INVALID_VALUE;  // a negative block column
+    max_col = std::max(max_col, c.hi);
+  }
   GroupIndex gi;
   gi.item_ptr.resize(ngroups + 1, 0);
-  for (int g = 0; g < ngroups; ++g) gi.item_ptr[g + 1] = gi.item_ptr[g] + (int)(grows[g].size() / 16);
-  const long long nitems = gi.item_ptr[ngroups];
+  long long acc = 0;
+  for (int g = 0; g < ngroups; ++g) {
+    acc += (long long)(grows[g].size() / 16);
+    if (acc > INT_MAX) return SPMM_STATUS_NOT_SUPPORTED;  // int32 item pointers
+    gi.item_ptr[g + 1] = (int)acc;
+  }
+  const long long nitems = acc;
   const size_t rows_off = align256(256 + (size_t)(ngroups + 1) * 4);
   const size_t afrag_off = align256(rows_off + (size_t)nitems * 64);
   const size_t need = afrag_off + (size_t)nitems * W * 512;
@@ -173,7 +197,7 @@ spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction
   if (e != hipSuccess) return from_hip(e);
   std::lock_guard<std::mutex> lk(handle->mu);
   handle->group_plans[buffer] = spmm_context::GroupPlan{W, mb, ngroups, nitems, need, rows_off,
-                                                        afrag_off};
+                                                        afrag_off, max_col};
   return SPMM_STATUS_SUCCESS;
 }
 
@@ -195,7 +219,7 @@ spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n
     if (it == handle->group_plans.end()) return SPMM_STATUS_INVALID_VALUE;
     plan = it->second;
   }
-  if (plan.mb != mb) return SPMM_STATUS_INVALID_VALUE;
+  if (plan.mb != mb || plan.max_col >= kb) return SPMM_STATUS_INVALID_VALUE;
   const long long K = (long long)kb * 16, M = (long long)mb * 16;
   if (orderB == SPMM_ORDER_COL ? ldb < K : ldb < n) return SPMM_STATUS_INVALID_VALUE;
   if (orderC == SPMM_ORDER_COL ? ldc < M : ldc < n) return SPMM_STATUS_INVALID_VALUE;

@@ -1056,8 +1056,9 @@ def test_bsrmm_grouped_f16(oracle, device, W, n, ob, oc, alpha, beta):
 
 
 def test_bsrmm_grouped_f16_checks(device):
-    """A buffer this handle holds no analysis of, or another mb, is
-    INVALID_VALUE; n % 8 != 0 is NOT_SUPPORTED (before any launch)."""
+    """A buffer this handle holds no analysis of, another mb, or a kb below
+    an analysed block column is INVALID_VALUE, and so is a negative block
+    column at analysis; n % 8 != 0 is NOT_SUPPORTED (before any launch)."""
     from spmm_hip._lib import INVALID_VALUE, NOT_SUPPORTED, SpmmError
     ops = _ops()
     rng = np.random.default_rng(3)
@@ -1074,7 +1075,16 @@ def test_bsrmm_grouped_f16_checks(device):
     with pytest.raises(SpmmError) as e:
         grp.mm(B, kb=7, n=124, ldb=128, C=C, ldc=128)
     assert e.value.status == NOT_SUPPORTED
+    # a kb the analysed block columns do not fit would read B past its rows
+    with pytest.raises(SpmmError) as e:
+        grp.mm(B, kb=int(ci.max()), n=128, ldb=128, C=C, ldc=128)
+    assert e.value.status == INVALID_VALUE
     grp.close()
+    bad = ci.copy()
+    bad[0] = -1
+    with pytest.raises(SpmmError) as e:  # a negative block column
+        ops.GroupedBsr16(drp, torch.from_numpy(bad).to(device), dv, mb=5)
+    assert e.value.status == INVALID_VALUE
     with pytest.raises(SpmmError) as e:  # released: the handle no longer knows the buffer
         grp.buffer = torch.empty(16, dtype=torch.uint8, device=device)
         grp.mm(B, kb=7, n=128, ldb=128, C=C, ldc=128)
