@@ -164,80 +164,39 @@ def test_column_stream_counts_only_its_copies(bsr_asm, kernel):
         assert msk or n_dma >= (3 if "grp" in kernel else 4), (k, n_dma)
 
 
-def _vregs(ops: str) -> set:
-    out = set()
-    for m in __import__("re").finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", ops):
-        if m.group(3) is not None:
-            out.add(int(m.group(3)))
-        else:
-            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
-    return out
-
-
 @pytest.mark.parametrize("kernel", ["bsr32_f32_cs2_kernel", "bsr16_f16_cs_kernel",
                                     "bsr16_f16_grp_kernel"])
 def test_column_stream_registers_in_flight_are_asm_only(bsr_asm, kernel):
     """bsr32_f32_cs2_kernel loads B rows, block-column chunks and A columns
-    (bsr16_f16_cs_kernel: block-column chunks) with inline asm that does not
-    wait, so hipcc believes their registers hold data at once. They are safe only if nothing but inline asm touches them
-    while the load is in flight: the consume step's asm waits (vmcnt ladder,
-    lgkmcnt(0)) and then copies them out with v_mov. A forward dataflow over
-    the kernel's control-flow graph (union at joins) tracks the registers in
-    flight; any compiler-generated instruction that reads or writes one of
-    them (a copy, a spill, a reuse) fails the test."""
+    (bsr16_f16_cs_kernel: block-column chunks; bsr16_f16_grp_kernel: row indices
+    and A fragments) with inline asm that does not wait, so hipcc believes their
+    registers hold data at once. They are safe only if nothing but inline asm
+    touches them while the load is in flight: the consume step's asm waits
+    (vmcnt ladder, lgkmcnt(0)) and then copies them out with v_mov.
+    tools/isa_vmcnt.py's forward dataflow over the control-flow graph (union at
+    joins) tracks the registers in flight; any compiler-generated instruction
+    that reads or writes one of them (a copy, a spill, a reuse) fails the test,
+    and so does any spill at all in these kernels."""
     funcs = iv.split_functions(bsr_asm)
     cs2 = [k for k in funcs if kernel in k]
     assert len(cs2) >= 2, f"{kernel} instantiations"
     for k in cs2:
-        body = funcs[k]
-        stmt_wait, cur, waits = {}, None, False   # asm line -> its statement waits?
-        lines_of, drains = [], set()
-        for no, line in body:
-            if "#ASMSTART" in line:
-                cur, waits, lines_of = no, False, []
-            elif "#ASMEND" in line:
-                for x in lines_of:
-                    stmt_wait[x] = waits
-                cur = None
-            elif cur is not None:
-                lines_of.append(no)
-                waits |= "s_waitcnt" in line
-                if "vmcnt(0)" in line and "lgkmcnt(0)" in line:
-                    drains.add(no)  # a full wait: nothing in flight after it
-        blocks = iv.build_cfg(body)
-        ins = [None] * len(blocks)
-        ins[0] = frozenset()
-        errs = []
-
-        def transfer(b, state, report):
-            st = set(state)
-            for no, mn, ops in b.insts:
-                regs = _vregs(ops)
-                if no in drains:
-                    st.clear()
-                elif no in stmt_wait:
-                    if mn.startswith(("global_load_dword", "ds_read")) and not stmt_wait[no]:
-                        st |= _vregs(ops.split(",")[0])
-                    elif mn.startswith("v_mov"):
-                        st -= _vregs(ops.partition(",")[2])
-                elif regs & st:
-                    if report:
-                        errs.append((no, mn, ops, sorted(regs & st)))
-            return frozenset(st)
-
-        work = [0]
-        while work:
-            bi = work.pop()
-            out = transfer(blocks[bi], ins[bi], False)
-            for sc in blocks[bi].succ:
-                new = out if ins[sc] is None else ins[sc] | out
-                if new != ins[sc]:
-                    ins[sc] = new
-                    work.append(sc)
-        for bi, b in enumerate(blocks):
-            if ins[bi] is not None:
-                transfer(b, ins[bi], True)
+        errs = iv.inflight_violations(funcs[k])
         assert not errs, f"{k}: compiler touches in-flight registers: {errs[:5]}"
+        assert iv.spills(funcs[k]) == 0, f"{k}: spills"
+
+
+def test_inflight_check_flags_a_spilled_load():
+    """The pattern that faulted a TUNING variant on the GPU (W = 4, P = 3 under
+    a 4-waves occupancy hint): the allocator spilled an A fragment whose asm
+    load was still in flight."""
+    body = [(1, "\t;;#ASMSTART"), (2, "\tglobal_load_dwordx2 v[0:1], v77, s[14:15]"),
+            (3, "\t;;#ASMEND"), (4, "\tscratch_store_dwordx2 off, v[0:1], off offset:4"),
+            (5, "\t;;#ASMSTART"), (6, "\ts_waitcnt vmcnt(0)"), (7, "\tv_mov_b64 v[2:3], v[0:1]"),
+            (8, "\t;;#ASMEND"), (9, "\ts_endpgm")]
+    errs = iv.inflight_violations(body)
+    assert [e[0] for e in errs] == [4], errs
+    assert iv.spills(body) == 1
 
 
 # ---------------------------------------------------------------------------

@@ -21,6 +21,6 @@ print(json.dumps({"W": int(a[0]), "variant": int(a[1]), "xm": int(a[2]),
 PY
   tail -1 $O/grp_sweep.jsonl
 }
-for xm in 0 8 2; do for v in 33 32 43 34; do one 4 $v $xm; done; done
+for xm in 0 8 2; do for v in 33 32 43; do one 4 $v $xm; done; done
 for xm in 0 16; do for v in 33 23 24; do one 2 $v $xm; done; done
-for xm in 0 4; do for v in 34 24; do one 8 $v $xm; done; done
+for xm in 0 4; do for v in 33 24; do one 8 $v $xm; done; done

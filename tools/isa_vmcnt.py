@@ -296,6 +296,100 @@ def audit(text: str, fragments: list[str] | None = None, keep_load: tuple = ("bs
     return out
 
 
+def _vregs(ops: str) -> set:
+    out = set()
+    for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", ops):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def inflight_violations(body: list[tuple[int, str]]) -> list[tuple]:
+    """Compiler-generated instructions that touch a register an inline-asm load
+    still has in flight. An asm load that does not wait leaves hipcc believing
+    its registers hold data at once; they are safe only if nothing but inline asm
+    touches them until the consuming asm (which waits, then copies them out with
+    v_mov). A forward dataflow over the control-flow graph (union at joins)
+    tracks the registers in flight; a full vmcnt(0) lgkmcnt(0) asm wait clears
+    them. -> [(line, mnemonic, operands, registers)] (a copy, a spill, a reuse)."""
+    stmt_wait, cur, waits = {}, None, False   # asm line -> its statement waits?
+    lines_of, drains = [], set()
+    for no, line in body:
+        if "#ASMSTART" in line:
+            cur, waits, lines_of = no, False, []
+        elif "#ASMEND" in line:
+            for x in lines_of:
+                stmt_wait[x] = waits
+            cur = None
+        elif cur is not None:
+            lines_of.append(no)
+            waits |= "s_waitcnt" in line
+            if "vmcnt(0)" in line and "lgkmcnt(0)" in line:
+                drains.add(no)  # a full wait: nothing in flight after it
+    blocks = build_cfg(body)
+    ins = [None] * len(blocks)
+    ins[0] = frozenset()
+    errs = []
+
+    def transfer(b, state, report):
+        st = set(state)
+        for no, mn, ops in b.insts:
+            regs = _vregs(ops)
+            if no in drains:
+                st.clear()
+            elif no in stmt_wait:
+                if mn.startswith(("global_load_dword", "ds_read")) and not stmt_wait[no]:
+                    st |= _vregs(ops.split(",")[0])
+                elif mn.startswith("v_mov"):
+                    st -= _vregs(ops.partition(",")[2])
+            elif regs & st:
+                if report:
+                    errs.append((no, mn, ops, sorted(regs & st)))
+        return frozenset(st)
+
+    work = [0]
+    while work:
+        bi = work.pop()
+        out = transfer(blocks[bi], ins[bi], False)
+        for sc in blocks[bi].succ:
+            new = out if ins[sc] is None else ins[sc] | out
+            if new != ins[sc]:
+                ins[sc] = new
+                work.append(sc)
+    for bi, b in enumerate(blocks):
+        if ins[bi] is not None:
+            transfer(b, ins[bi], True)
+    return errs
+
+
+def spills(body: list[tuple[int, str]]) -> int:
+    return sum(1 for _, line in body if line.strip().startswith("scratch_"))
+
+
+def inflight_audit(text: str, fragments: list[str]) -> dict:
+    """-> {kernel: (spill instructions, in-flight violations)} for the matching kernels:
+    run on a TUNING build's assembly before its variants go to the GPU (a variant
+    whose allocator spills an asm load's registers in flight reads garbage, and a
+    garbage row index is an illegal address)."""
+    return {k: (spills(b), inflight_violations(b)) for k, b in split_functions(text).items()
+            if any(f in k for f in fragments)}
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[1] == "--inflight":
+    txt = open(sys.argv[2]).read()
+    res = inflight_audit(txt, sys.argv[3:] or ["_cs_kernel", "cs2_kernel", "grp_kernel"])
+    bad = 0
+    for k, (sp, errs) in res.items():
+        print(f"{'FAIL' if errs else 'ok  '} spills {sp:3d}  {k[:100]}")
+        for e in errs[:3]:
+            print("      ", e)
+        bad += bool(errs)
+    print(f"{len(res)} kernels, {bad} failing")
+    sys.exit(1 if bad else 0)
+
+
 if __name__ == "__main__":
     txt = open(sys.argv[1]).read()
     res = audit(txt, sys.argv[2:] or None)
