@@ -22,5 +22,6 @@ PY
   tail -1 $O/grp_sweep.jsonl
 }
 for xm in 0 8 2; do for v in 33 32 43; do one 4 $v $xm; done; done
+for xm in 0 8; do one 4 24 $xm; done
 for xm in 0 16; do for v in 33 23 24; do one 2 $v $xm; done; done
 for xm in 0 4; do for v in 33 24; do one 8 $v $xm; done; done
