@@ -2574,7 +2574,7 @@ __device__ __forceinline__ void slots_while(std::integer_sequence<int, S...>, F&
   (void)(f(std::integral_constant<int, S>{}) && ...);
 }
 
-template <int W, int P, bool CROW, int OCC = 0>
+template <int W, int P, bool CROW, int OCC = 0, bool SR = true>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
 void bsr16_f16_grp_kernel(
     int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
@@ -2619,7 +2619,8 @@ void bsr16_f16_grp_kernel(
   for (int t = 0; t < kT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   int nis = 0;               // vector-memory operations issued by this wave
-  int rrow[kCpw], rstamp = -64;  // row indices of the next item to issue (in flight)
+  int rrow[kCpw], rstamp = -64;  // !SR: row indices of the next item to issue (in flight)
+  int ra[kCpw], rb[kCpw];    // SR: the same as scalars (rows 2 cc and 2 cc + 1 of copy cc)
   typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
   u32x2a fan[P];             // A fragments in flight (asm-only registers)
   int stamp[P];
@@ -2629,11 +2630,24 @@ void bsr16_f16_grp_kernel(
     stamp[s] = -64;
   }
 #pragma unroll
-  for (int j = 0; j < kCpw; ++j) rrow[j] = -1;
+  for (int j = 0; j < kCpw; ++j) rrow[j] = ra[j] = rb[j] = -1;
   const int ilast = max(i1 - 1, i0);
-  // row indices of item `it` (clamped): lane L of copy j needs rows[it][2 (w kCpw + j) + L / 32]
+  // row indices of item `it` (clamped): lane L of copy j needs rows[it][2 (w kCpw + j) + L / 32].
+  // SR: scalar loads (lgkmcnt). Vector loads retire in issue order behind the copies
+  // issued before them, so waiting for a vector row load one item ahead also waited for
+  // every copy before it: one item in flight during the MFMAs whatever P was. Scalar
+  // loads keep the P - 1 items of copies in flight (the grouped stream).
   auto load_rows = [&](int it) {
     const int* src = rows + (size_t)min(it, ilast) * 16;
+    if constexpr (SR) {
+      const int* s2 = src + 2 * w * kCpw;
+#pragma unroll
+      for (int j = 0; j < kCpw; ++j) {
+        ra[j] = s2[2 * j];
+        rb[j] = s2[2 * j + 1];
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < kCpw; ++j)
       asm volatile("global_load_dword %0, %1, %2"
@@ -2646,7 +2660,10 @@ void bsr16_f16_grp_kernel(
   // item `it` into stage slot `s`: its row indices landed, its copies and A fragment issued
   auto issue = [&](int it, int s) {
     int rw[kCpw];
-    if constexpr (kCpw == 1)
+    if constexpr (SR) {
+#pragma unroll
+      for (int j = 0; j < kCpw; ++j) rw[j] = (lane >> 5) ? rb[j] : ra[j];
+    } else if constexpr (kCpw == 1)
       asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
                    : "=&v"(rw[0]) : "s"(nis - rstamp), "v"(rrow[0]) : "scc", "memory");
     else if constexpr (kCpw == 2)
@@ -2694,7 +2711,7 @@ void bsr16_f16_grp_kernel(
         __builtin_amdgcn_s_barrier();
         // slot (s + P - 1) % P was read by every wave in the previous item: refill it
         issue(it + P - 1, (s + P - 1) % P);
-        load_rows(it + P);
+        if constexpr (!SR) load_rows(it + P);
         f16x4 fb[16];
         asm volatile(
             "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
@@ -2726,6 +2743,8 @@ void bsr16_f16_grp_kernel(
             : "v"(tra[8]), "v"(tra[9]), "v"(tra[10]), "v"(tra[11]), "v"(tra[12]), "v"(tra[13]),
               "v"(tra[14]), "v"(tra[15]), "n"(s * kStage)
             : "memory");
+        // after the transposed reads: their asm lgkmcnt(0) waits would also wait for it
+        if constexpr (SR) load_rows(it + P);
 #pragma unroll
         for (int t = 0; t < kT; ++t)
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[t], 0, 0, 0);
@@ -3275,8 +3294,9 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   const _Float16* B = reinterpret_cast<const _Float16*>(B16);
   const int slot = timing_begin(ctx);
   const dim3 grid(ngroups, (n + 255) / 256);
-  // stages and occupancy hint: P * 10 + OCC (TUNING builds: SPMM_GRP_VARIANT)
-  int gv = 30, xm = 0;
+  // stages and occupancy hint: P * 10 + OCC, + 100 for vector row-index loads (TUNING builds:
+  // SPMM_GRP_VARIANT; SPMM_GRP_XM groups per XCD chunk)
+  int gv = 33, xm = 0;
 #ifdef SPMM_TUNING
   {
     static const int env = [] {
@@ -3289,34 +3309,47 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
     }();
     // (3, 4) is not offered: at W = 4 the allocator spills the A fragments in flight
     // (tools/isa_vmcnt.py --inflight; it faulted on the GPU)
-    if (env == 30 || env == 33 || env == 32 || env == 43 || env == 23 || env == 24)
-      gv = env;
+    switch (env) {
+      case 30: case 33: case 32: case 42: case 43: case 52: case 53: case 23: case 24:
+      case 130: case 133:
+        gv = env;
+        break;
+      default:
+        break;
+    }
     if (env_xm >= 0) xm = env_xm;
   }
 #endif
-#define GRP_LAUNCH1(W_, P_, O_)                                                                  \
+#define GRP_LAUNCH1(W_, P_, O_, SR_)                                                             \
   do {                                                                                           \
     if (crow)                                                                                    \
-      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_>), grid, dim3(64 * W_), 0,       \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_, SR_>), grid, dim3(64 * W_), 0,  \
                          ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc, \
                          xm);                                                                    \
     else                                                                                         \
-      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_>), grid, dim3(64 * W_), 0,      \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_, SR_>), grid, dim3(64 * W_), 0, \
                          ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc, \
                          xm);                                                                    \
   } while (0)
 #ifdef SPMM_TUNING
 #define GRP_LAUNCH(W_)                                                                           \
   do {                                                                                           \
-    if (gv == 33) GRP_LAUNCH1(W_, 3, 3);                                                          \
-    else if (gv == 32) GRP_LAUNCH1(W_, 3, 2);                                                     \
-    else if (gv == 43) GRP_LAUNCH1(W_, 4, 3);                                                     \
-    else if (gv == 23) GRP_LAUNCH1(W_, 2, 3);                                                     \
-    else if (gv == 24) GRP_LAUNCH1(W_, 2, 4);                                                     \
-    else GRP_LAUNCH1(W_, 3, 0);                                                                   \
+    switch (gv) {                                                                                \
+      case 30: GRP_LAUNCH1(W_, 3, 0, true); break;                                               \
+      case 32: GRP_LAUNCH1(W_, 3, 2, true); break;                                               \
+      case 42: GRP_LAUNCH1(W_, 4, 2, true); break;                                               \
+      case 43: GRP_LAUNCH1(W_, 4, 3, true); break;                                               \
+      case 52: GRP_LAUNCH1(W_, 5, 2, true); break;                                               \
+      case 53: GRP_LAUNCH1(W_, 5, 3, true); break;                                               \
+      case 23: GRP_LAUNCH1(W_, 2, 3, true); break;                                               \
+      case 24: GRP_LAUNCH1(W_, 2, 4, true); break;                                               \
+      case 130: GRP_LAUNCH1(W_, 3, 0, false); break;                                             \
+      case 133: GRP_LAUNCH1(W_, 3, 3, false); break;                                             \
+      default: GRP_LAUNCH1(W_, 3, 3, true); break;                                               \
+    }                                                                                            \
   } while (0)
 #else
-#define GRP_LAUNCH(W_) GRP_LAUNCH1(W_, 3, 0)
+#define GRP_LAUNCH(W_) GRP_LAUNCH1(W_, 3, 3, true)
 #endif
   (void)gv;
   if (W == 8) GRP_LAUNCH(8);

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 4: second A/B of the grouped bs 16 fp16 stream (TUNING build lib_tuning/, copied
 # over lib/ on the box only): block rows per group W x (stages, occupancy hint) x XCD chunk
-# (SPMM_GRP_VARIANT = 10 P + OCC, SPMM_GRP_XM = groups per XCD chunk, 0 = as dispatched).
+# (SPMM_GRP_VARIANT = 10 P + OCC, + 100 for the vector row-index loads; SPMM_GRP_XM = groups
+# per XCD chunk, 0 = as dispatched).
 # Output gpurun_out/r04e/grp_sweep.jsonl.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -21,7 +22,6 @@ print(json.dumps({"W": int(a[0]), "variant": int(a[1]), "xm": int(a[2]),
 PY
   tail -1 $O/grp_sweep.jsonl
 }
-for xm in 0 8 2; do for v in 33 32 43; do one 4 $v $xm; done; done
-for xm in 0 8; do one 4 24 $xm; done
-for xm in 0 16; do for v in 33 23 24; do one 2 $v $xm; done; done
-for xm in 0 4; do for v in 33 24; do one 8 $v $xm; done; done
+for xm in 0 8; do for v in 33 133 43 53 32 42; do one 4 $v $xm; done; done
+for xm in 0 4; do for v in 33 24 43; do one 8 $v $xm; done; done
+for xm in 0 16; do for v in 33 43 53; do one 2 $v $xm; done; done
