@@ -3296,7 +3296,9 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   const dim3 grid(ngroups, (n + 255) / 256);
   // stages and occupancy hint: P * 10 + OCC, + 100 for vector row-index loads (TUNING builds:
   // SPMM_GRP_VARIANT; SPMM_GRP_XM groups per XCD chunk)
-  int gv = 33, xm = 0;
+  // chunks of 32 block rows per XCD, as the drop-in stream (xcd_block_row): neighbouring
+  // groups share B rows in one L2 (W = 4: 3.10 -> 2.87 ms, profiles/r04e/grp_sweep.jsonl)
+  int gv = 33, xm = 32 / W;
 #ifdef SPMM_TUNING
   {
     static const int env = [] {
