@@ -2562,7 +2562,12 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 //    analysis: one 8-B load per lane;
 //  * a ring of P stages: per item every wave waits for its own copies (the
 //    counted ladder), one s_barrier publishes the stage and retires the slot the
-//    next copies overwrite, then 16 transposed reads and 16 MFMAs per wave.
+//    next copies overwrite, then 16 transposed reads and 16 MFMAs per wave;
+//  * an item's row indices come by scalar loads one item ahead (a vector load
+//    would retire behind the copies issued before it and hold the ring to one
+//    item in flight), and groups go to the XCDs in chunks of 32 block rows.
+// Release form: W = 4, P = 3, three waves per SIMD: products stand-in K = 512
+// 2.87 ms against 3.77 for the column stream (profiles/r04e/grp_sweep.jsonl).
 // Non-finite B: a B row of the item meets the W block rows' A fragments, zeros
 // included, so an inf / NaN in it reaches every row of the group whenever one
 // of its block rows holds a value in that column (the grouped contract,
