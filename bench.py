@@ -78,6 +78,12 @@ WORKLOADS = {
     "products_rcm_bsr16_f16_grp": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                        p_in=0.97, bs=16, K=512, dtype="fp16", reorder="rcm",
                                        grouped=4),
+    # configs 3 and north_star's products bs 32 on the grouped bs 32 stream
+    # (spmm_bsr32_group_analysis_f32 once; spmm_bsrmm_grouped_f32 timed)
+    "reddit_bsr32_grp": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
+                             bs=32, K=128, dtype="fp32", grouped=2),
+    "products_bsr32_grp": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
+                               p_in=0.97, bs=32, K=128, dtype="fp32", grouped=2),
     "products_hybrid32": dict(kind="hybrid", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                               p_in=0.97, bs=32, K=128, density="auto"),
     # §8f rank 2 in the loop: scrambled ids -> in-repo RCM -> divide + hybrid
@@ -491,6 +497,7 @@ def cpu_baseline(args, K: int) -> dict:
 
 
 GRAPH = False  # --graph: replay the step as a captured HIP graph (N = 1)
+GRP32_W = 2    # block rows per group of the bs 32 grouped side line (spmm_bsr32_group_analysis_f32)
 
 
 def timed_loop(step, h, steps, warmup, world, dist, raw=False):
@@ -883,11 +890,12 @@ def run_bsr(args, W, world, rank, dev, dist):
     analysis_ms = None
     grp = None
     if gw:
-        if (bs, dt) != (16, "fp16"):
-            raise SystemExit("the grouped stream is bs 16 fp16")
+        if (bs, dt) not in ((16, "fp16"), (32, "fp32")):
+            raise SystemExit("the grouped streams are bs 16 fp16 and bs 32 fp32")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        grp = ops.GroupedBsr16(d_brp, d_bci, d_bv, mb=mb, group_rows=gw, handle=h)
+        Grouped = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
+        grp = Grouped(d_brp, d_bci, d_bv, mb=mb, group_rows=gw, handle=h)
         torch.cuda.synchronize()
         analysis_ms = (time.perf_counter() - t0) * 1e3
         del d_bv
@@ -984,10 +992,12 @@ def run_bsr(args, W, world, rank, dev, dist):
         mfma_flops = active_cols * 2.0 * bs * K
     else:
         mfma_flops = dense_flops
-    if grp is not None:
+    if grp is not None and bs == 16:
         # one v_mfma_f32_16x16x16_f16 per item, wave and 16 output columns
         nitems = (grp.bytes - 256) // (64 + gw * 512)
         mfma_flops = nitems * gw * 2.0 * 16 * 16 * K
+    # (bs 32 grouped: each wave runs the MFMAs of its own nonzero columns, the column
+    # stream's count above)
     peak = MFMA_PEAK_TFLOPS[dt]
     kbytes = bsr_bytes(mb, nnzb, bs, K, s)
     # Compulsory bytes (the roofline): the block values and the BSR index
@@ -1006,7 +1016,7 @@ def run_bsr(args, W, world, rank, dev, dist):
     cm_bytes = (ntiles * (4 * (mb + 1) + 4 * nnzb + a_bytes) + s * active_cols * K +
                 4 * mb * bs * K) if cm else kbytes
     t = kms / 1e3
-    kname = ("bsr16_f16_grp_kernel" if grp is not None else
+    kname = (f"bsr{bs}_{'f16' if bs == 16 else 'f32'}_grp_kernel" if grp is not None else
              ("bsr32_f32_cs2_kernel" if bs == 32 else
               "bsr32_f32_cs2_kernel (bs 64 sub-blocks)" if bs == 64 else
               "bsr16_f16_cs_kernel" if cs16 else "bsr16_cm_kernel") if cm else
@@ -1090,6 +1100,27 @@ def run_bsr(args, W, world, rank, dev, dist):
             "mfma_executed_TFLOPs": round(ni * 4 * 2.0 * 256 * K / (k_g / 1e3) / 1e12, 2)}
         g4.close()
         del g4
+    if (not an and grp is None and args.bsr_layout == "row" and not args.no_analysed_side and
+            (bs, dt) == (32, "fp32") and K % 4 == 0):
+        # Beside the drop-in line (not `value`): the grouped bs 32 stream (groups of 2 block
+        # rows sharing their B-row copies, analysis once, timed apart; C bit-identical)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g2 = ops.GroupedBsr32(d_brp, d_bci, d_bv, mb=mb, group_rows=GRP32_W, handle=h)
+        torch.cuda.synchronize()
+        a_ms = (time.perf_counter() - t0) * 1e3
+        e_g, k_g = timed_loop(lambda: g2.mm(B, kb=mb, n=K, ldb=K, C=C, ldc=K), h, args.steps,
+                              args.warmup, 1, dist)
+        rec["grouped_entry"] = {
+            "entry": f"spmm_bsr32_group_analysis_f32 ({GRP32_W} block rows per group) once + "
+                     "spmm_bsrmm_grouped_f32 per step",
+            "value": round(2.0 * nnz * K * args.steps / e_g / 1e9, 2), "unit": "GFLOP/s",
+            "ms_per_step": round(e_g / args.steps * 1e3, 4), "kernel_ms": round(k_g, 4),
+            "analysis_ms_first_call": round(a_ms, 3),
+            "mfma_executed_TFLOPs": round(mfma_flops / (k_g / 1e3) / 1e12, 2),
+            "mfma_frac": round(mfma_flops / (k_g / 1e3) / 1e12 / peak, 4)}
+        g2.close()
+        del g2
     if (not an and grp is None and args.bsr_layout == "row" and not args.no_analysed_side and
             (bs, dt) in ((32, "fp32"), (16, "fp16"))):
         # Beside the drop-in line (not `value`): the same product on the analysed
@@ -1258,7 +1289,8 @@ def main() -> None:
     ap.add_argument("--no-hot-side", action="store_true",
                     help="skip the hot-column side measurement of the products_csr line")
     ap.add_argument("--group-rows", type=int, default=0,
-                    help="bs 16 fp16: run the grouped stream with this many block rows per group")
+                    help="bs 16 fp16 / bs 32 fp32: run the grouped stream with this many block "
+                         "rows per group")
     ap.add_argument("--no-analysed-side", action="store_true",
                     help="skip the analysed-entry side measurement of the bs 32 / bs 16 fp16 lines")
     ap.add_argument("--chunks", type=int, default=0,

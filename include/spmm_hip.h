@@ -319,7 +319,30 @@ spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n
                                      const void* buffer, float alpha, const uint16_t* B, int ldb,
                                      spmm_order_t orderB, float beta, float* C, int ldc,
                                      spmm_order_t orderC);
-/* Forgets the handle's record of a group-analysis buffer (before freeing it). */
+/* The grouped bs = 32 fp32 stream (an extension, like the bs 16 one above;
+ * DESIGN.md §4 "The grouped bs 32 stream"). groupRows 2 or 4 (0 = 2) adjacent
+ * block rows share one copy of each B row of their union; unlike bs 16 each
+ * block row multiplies only its own nonzero columns (the analysis records them
+ * per item), so C is bit-identical to spmm_bsrmm_ex_f32 /
+ * spmm_bsrmm_analysed_f32 with the same column-granular non-finite contract.
+ * Same two phases, checks and handle record as spmm_bsr16_group_analysis_f16. */
+spmm_status_t spmm_bsr32_group_analysis_f32(spmm_handle_t handle, spmm_direction_t dir, int mb,
+                                            int nnzb, int groupRows, const int* bsrRowPtr,
+                                            const int* bsrColInd, const float* bsrVal,
+                                            void* buffer, size_t* bufferBytes);
+
+/* C(mb*32 x n) = alpha * A * B(kb*32 x n) + beta * C on a bs 32 group analysis of A,
+ * B and C row- or column-major (column-major ones are staged row-major in the
+ * workspace). INVALID_VALUE as spmm_bsrmm_grouped_f16 (a bs 16 analysis is not
+ * taken); NOT_SUPPORTED when n % 4 != 0, a row-major ldb or ldc % 4 != 0, or B or
+ * C is not 16-B aligned (spmm_bsrmm_ex_f32 serves those shapes). */
+spmm_status_t spmm_bsrmm_grouped_f32(spmm_handle_t handle, int mb, int kb, int n,
+                                     const void* buffer, float alpha, const float* B, int ldb,
+                                     spmm_order_t orderB, float beta, float* C, int ldc,
+                                     spmm_order_t orderC);
+
+/* Forgets the handle's record of a group-analysis buffer, bs 16 or bs 32 (before
+ * freeing it). */
 spmm_status_t spmm_bsr16_group_release(spmm_handle_t handle, const void* buffer);
 
 /* fp16 A and B (IEEE binary16 bit patterns), fp32 accumulate and fp32 C.

@@ -853,14 +853,14 @@ __global__ __launch_bounds__(256) void bsr32_analysis_kernel(int nnzb, int rowdi
     f32x4 x[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) x[q] = *reinterpret_cast<const f32x4*>(blk + j * 32 + 16 * h + 4 * q);
-    float* dst = val_col + (size_t)k * 1024;
+    float* dst = val_col ? val_col + (size_t)k * 1024 : nullptr;  // null: masks only
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float v = x[i >> 2][i & 3];
       const unsigned long long b = __builtin_amdgcn_ballot_w64((__float_as_uint(v) & 0x7fffffffu) != 0u);
       msk |= ((unsigned)b != 0u ? 1u : 0u) << i;
       msk |= ((unsigned)(b >> 32) != 0u ? 1u : 0u) << (16 + i);
-      dst[(16 * h + i) * 32 + j] = v;
+      if (val_col) dst[(16 * h + i) * 32 + j] = v;
     }
   } else {
     f32x4 x[4];
@@ -2825,6 +2825,244 @@ __global__ __launch_bounds__(256) void bsr16_grp_fill_kernel(long long nwork, in
   dst[1] = (unsigned)h[2] | ((unsigned)h[3] << 16);
 }
 
+// ---------------------------------------------------------------------------
+// bs = 32 fp32, GROUPED item stream (spmm_bsr32_group_analysis_f32 once per
+// matrix + spmm_bsrmm_grouped_f32; row-major B and C, K tiles of 128). The bs 16
+// grouped stream's idea on the fp32 column stream (bsr32_f32_cs2_kernel): a
+// workgroup owns W = 2 or 4 adjacent block rows, one wave each, and streams the
+// union of their nonzero columns (J, c) in items of 8; an item's 8 B rows (512 B
+// at K = 128) are copied once into an LDS stage shared by the W waves. Unlike
+// bs 16, where one MFMA takes 16 entries whatever rows hold them, a fp32 MFMA
+// here is k = 1 (v_mfma_f32_32x32x1_2b_f32, two per column for 128 outputs),
+// so each wave multiplies only the columns its own block row holds: the
+// analysis stores a per-(item, wave) mask and the MFMAs of the other columns
+// are skipped (wave-uniform branches). A wave's MFMAs are then exactly those of
+// the column streams, in the same (J, c) order, so C is bit-identical to
+// spmm_bsrmm_ex_f32 / spmm_bsrmm_analysed_f32, and the non-finite contract is
+// theirs (column-granular).
+//  * per item and wave: its copies (8 / (2 W) of 1 KB: rows 2 cc and 2 cc + 1),
+//    one 16-B load of its A fragment (rows j, the item's 8 columns; lane (j, h)
+//    columns 4 h .. 4 h + 3, the other four by v_permlane32_swap); row indices
+//    and the mask by scalar loads one ring turn ahead (a vector load would
+//    retire behind the copies issued before it);
+//  * a ring of P stages: counted wait on the wave's own copies and fragment,
+//    one s_barrier, the refill of the slot the previous item freed, 8 ds_read_b64
+//    of the stage (lane (j, h): columns 4 j + 2 h, + 1 of each row), then per
+//    held column two MFMAs.
+// Groups go to the XCDs in chunks of xm groups (neighbouring groups share B rows).
+// ---------------------------------------------------------------------------
+template <int W, int P, int OCC = 0>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
+void bsr32_f32_grp_kernel(
+    int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
+    const unsigned* __restrict__ wmask, const float* __restrict__ afrag,
+    const float* __restrict__ B, int ldb, float alpha, float beta, float* __restrict__ C, int ldc,
+    int xm) {
+  static_assert(W == 2 || W == 4, "waves per group");
+  static_assert(P >= 2 && P <= 6, "stages");
+  constexpr int E = 8, kRowB = 512, kStage = E * kRowB;
+  constexpr int kCpw = E / (2 * W);  // 1-KB copies per wave per item
+  __shared__ __attribute__((aligned(16))) char smem[P * kStage];
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int grp = xcd_block_row(blockIdx.x, gridDim.x, xm);
+  const int br = grp * W + w;
+  const int jt = blockIdx.y * 128;
+  const int i0 = item_ptr[grp], i1 = item_ptr[grp + 1];
+  const unsigned lds0 = lds_addr(smem);
+  const size_t ldb4 = (size_t)ldb * 4;
+  // copy lanes: 16 B at columns jt + 4 (lane & 31) .. + 3 (n % 4 == 0; clamped in bounds)
+  const unsigned boff = 4u * (unsigned)min(jt + 4 * (lane & 31), n - 4);
+  const char* const zrow = reinterpret_cast<const char*>(g_zero_row) - 4 * (size_t)jt;
+  const unsigned rd = lds0 + 16u * (unsigned)j + 8u * (unsigned)h;  // B reads of the stage
+
+  f32x32 u0, u1;
+#pragma unroll
+  for (int e = 0; e < 32; ++e) u0[e] = u1[e] = 0.f;
+
+  int nis = 0;  // vector-memory operations issued by this wave
+  int ra[kCpw], rb[kCpw];  // row indices of the next item to issue (scalars)
+  unsigned msk[P];         // this wave's held columns of the item in each slot (scalars)
+  typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
+  u32x2a fan[P], fbn[P];  // A fragments in flight, columns 4 h, + 1 / 4 h + 2, + 3 (asm only)
+  int stamp[P];
+#pragma unroll
+  for (int s = 0; s < P; ++s) {
+    fan[s] = fbn[s] = u32x2a{0u, 0u};
+    stamp[s] = -64;
+    msk[s] = 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < kCpw; ++q) ra[q] = rb[q] = -1;
+  const int ilast = max(i1 - 1, i0);
+  auto load_rows = [&](int it) {
+    const int* s2 = rows + (size_t)min(it, ilast) * E + 2 * w * kCpw;
+#pragma unroll
+    for (int q = 0; q < kCpw; ++q) {
+      ra[q] = s2[2 * q];
+      rb[q] = s2[2 * q + 1];
+    }
+  };
+  // an item past the group's end holds no columns (its copies are the clamped last item's)
+  auto load_mask = [&](int it) -> unsigned {
+    return it < i1 ? wmask[(size_t)it * W + w] : 0u;
+  };
+  auto issue = [&](int it, int s) {
+    char* const stage = smem + s * kStage;
+#pragma unroll
+    for (int q = 0; q < kCpw; ++q) {
+      const int rw = h ? rb[q] : ra[q];
+      const char* be = rw >= 0 ? reinterpret_cast<const char*>(B) + (size_t)rw * ldb4 : zrow;
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(be + boff),
+                                       (lds_void_t)(stage + 1024 * (w * kCpw + q)), 16, 0, 0);
+    }
+    const float* fsrc = afrag + ((size_t)min(it, ilast) * W + w) * 256;
+    asm volatile("global_load_dwordx2 %0, %2, %3\n\t"
+                 "global_load_dwordx2 %1, %2, %3 offset:8"
+                 : "=&v"(fan[s]), "=&v"(fbn[s])
+                 : "v"(32u * (unsigned)j + 16u * (unsigned)h), "s"(fsrc)
+                 : "memory");
+    nis += kCpw + 2;
+    stamp[s] = nis;
+  };
+
+  if (i0 < i1) {
+    load_rows(i0);
+#pragma unroll
+    for (int q = 0; q + 1 < P; ++q) {
+      msk[q] = load_mask(i0 + q);
+      issue(i0 + q, q);
+      load_rows(i0 + q + 1);
+    }
+    msk[P - 1] = load_mask(i0 + P - 1);
+    auto step = [&](int it, auto sc) {
+      constexpr int s = decltype(sc)::value;
+      unsigned fa[4];
+      {
+        u32x2a y0, y1;
+        asm volatile(SPMM_VM_LADDER("%2") "v_mov_b64 %0, %3\n\tv_mov_b64 %1, %4"
+                     : "=&v"(y0), "=&v"(y1)
+                     : "s"(nis - stamp[s]), "v"(fan[s]), "v"(fbn[s])
+                     : "scc", "memory");
+        fa[0] = y0[0];
+        fa[1] = y0[1];
+        fa[2] = y1[0];
+        fa[3] = y1[1];
+      }
+      __builtin_amdgcn_s_barrier();
+      // slot (s + P - 1) % P was read by every wave in the previous item: refill it
+      issue(it + P - 1, (s + P - 1) % P);
+      f32x2 fb[E];
+      asm volatile(
+          "ds_read_b64 %0, %8 offset:%9\n\t"
+          "ds_read_b64 %1, %8 offset:%10\n\t"
+          "ds_read_b64 %2, %8 offset:%11\n\t"
+          "ds_read_b64 %3, %8 offset:%12\n\t"
+          "ds_read_b64 %4, %8 offset:%13\n\t"
+          "ds_read_b64 %5, %8 offset:%14\n\t"
+          "ds_read_b64 %6, %8 offset:%15\n\t"
+          "ds_read_b64 %7, %8 offset:%16\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]), "=&v"(fb[5]),
+            "=&v"(fb[6]), "=&v"(fb[7])
+          : "v"(rd), "n"(s * kStage), "n"(s * kStage + 512), "n"(s * kStage + 1024),
+            "n"(s * kStage + 1536), "n"(s * kStage + 2048), "n"(s * kStage + 2560),
+            "n"(s * kStage + 3072), "n"(s * kStage + 3584)
+          : "memory");
+      const unsigned m = msk[s];
+      // after the LDS reads: their asm lgkmcnt(0) would also wait for these scalar loads
+      load_rows(it + P);
+      msk[s] = load_mask(it + P);
+      float a[E];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const auto r = __builtin_amdgcn_permlane32_swap(fa[q], fa[q], false, false);
+        a[q] = __uint_as_float(r[0]);
+        a[4 + q] = __uint_as_float(r[1]);
+      }
+#pragma unroll
+      for (int c = 0; c < E; ++c) {
+        if (m & (1u << c)) {
+          u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(a[c], fb[c][0], u0, 0, 0, 0);
+          u1 = __builtin_amdgcn_mfma_f32_32x32x1f32(a[c], fb[c][1], u1, 0, 0, 0);
+        }
+      }
+    };
+    int base = i0;
+    for (; base + P <= i1; base += P)
+      slots_while(std::make_integer_sequence<int, P>{}, [&](auto sc) {
+        step(base + decltype(sc)::value, sc);
+        return true;
+      });
+    // uniform over the workgroup: every wave runs the same items
+    slots_while(std::make_integer_sequence<int, P>{}, [&](auto sc) {
+      if (base + decltype(sc)::value >= i1) return false;
+      step(base + decltype(sc)::value, sc);
+      return true;
+    });
+  }
+  // nothing in flight past here (the prefetches of clamped items included)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : : "memory");
+#pragma unroll
+  for (int s = 0; s < P; ++s) asm volatile("" : : "v"(fan[s]), "v"(fbn[s]));
+  if (br >= mb) return;
+  const int col = jt + 4 * j;
+  if (col >= n) return;
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA -> AGPR read
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const size_t row = (size_t)br * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    f32x4* p = reinterpret_cast<f32x4*>(C + row * ldc + col);
+    f32x4 v;
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\t"
+                 "v_accvgpr_read_b32 %1, %5\n\t"
+                 "v_accvgpr_read_b32 %2, %6\n\t"
+                 "v_accvgpr_read_b32 %3, %7"
+                 : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3])
+                 : "a"(u0[e]), "a"(u1[e]), "a"(u0[16 + e]), "a"(u1[16 + e])
+                 : "memory");
+    if (beta == 0.f) {
+      v *= alpha;
+    } else {
+      const f32x4 c = *p;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
+    }
+    *p = v;
+  }
+}
+
+// A fragments of the grouped bs 32 stream: one wave per (item, wave of the group); lane L
+// writes A[j = L / 2][entries 4 (L & 1) .. + 3] of that wave's block row, src[item][e][w]
+// the block holding entry e (-1: none, zero), entry e's column rows[item][e] & 31 (-1:
+// padding, zero). Layout per (item, wave): [32 rows][8 entries] floats.
+__global__ __launch_bounds__(256) void bsr32_grp_fill_kernel(long long nwork, int W, int rowdir,
+                                                             const int* __restrict__ rows,
+                                                             const int* __restrict__ src,
+                                                             const float* __restrict__ val,
+                                                             float* __restrict__ afrag) {
+  const int lane = threadIdx.x & 63;
+  const long long wk = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wk >= nwork) return;
+  const long long item = wk / W;
+  const int w = (int)(wk % W);
+  const int r = lane >> 1, e0 = 4 * (lane & 1);
+  f32x4 v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = e0 + q;
+    const int row = rows[item * 8 + e];
+    const int k = src[(item * 8 + e) * W + w];
+    v[q] = 0.f;
+    if (row >= 0 && k >= 0) {
+      const int c = row & 31;
+      v[q] = val[(size_t)k * 1024 + (rowdir ? r * 32 + c : c * 32 + r)];
+    }
+  }
+  *reinterpret_cast<f32x4*>(afrag + (size_t)wk * 256 + 8 * r + e0) = v;
+}
+
 // Fallback register-fragment kernels (layouts the copy kernels do not cover):
 // bsr32_f32_mfma_kernel / bsr16_*_mfma_kernel variant VAR (launch bounds and
 // prefetch form; the best of the round-1 sweep, DESIGN.md §4 "Variant history").
@@ -3288,6 +3526,77 @@ spmm_status_t launch_bsr16_grp_fill(spmm_context* ctx, long long nitems, int W, 
   hipLaunchKernelGGL(bsr16_grp_fill_kernel, dim3((unsigned)((nwork + 3) / 4)), dim3(256), 0,
                      ctx->stream, nwork, W, dir == SPMM_DIRECTION_ROW ? 1 : 0, rows, src, val,
                      afrag);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_bsr32_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
+                                    const int* rows, const int* src, const float* val,
+                                    float* afrag) {
+  const long long nwork = nitems * W;
+  if (nwork == 0) return SPMM_STATUS_SUCCESS;
+  hipLaunchKernelGGL(bsr32_grp_fill_kernel, dim3((unsigned)((nwork + 3) / 4)), dim3(256), 0,
+                     ctx->stream, nwork, W, dir == SPMM_DIRECTION_ROW ? 1 : 0, rows, src, val,
+                     afrag);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_bsrmm_grouped_f32(spmm_context* ctx, int W, int mb, int n, int ngroups,
+                                       const int* item_ptr, const int* rows,
+                                       const unsigned* wmask, const float* afrag, const float* B,
+                                       int ldb, float alpha, float beta, float* C, int ldc) {
+  if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
+  const int slot = timing_begin(ctx);
+  const dim3 grid(ngroups, (n + 127) / 128);
+  // stages and occupancy hint P * 10 + OCC (TUNING builds: SPMM_GRP32_VARIANT); chunks of
+  // 32 block rows per XCD (SPMM_GRP_XM)
+  int gv = 33, xm = 32 / W;
+#ifdef SPMM_TUNING
+  {
+    static const int env = [] {
+      const char* e = getenv("SPMM_GRP32_VARIANT");
+      return e ? atoi(e) : 0;
+    }();
+    static const int env_xm = [] {
+      const char* e = getenv("SPMM_GRP_XM");
+      return e ? atoi(e) : -1;
+    }();
+    switch (env) {
+      case 30: case 32: case 33: case 34: case 42: case 43: case 44: case 52: case 53:
+        gv = env;
+        break;
+      default:
+        break;
+    }
+    if (env_xm >= 0) xm = env_xm;
+  }
+#endif
+#define GRP32_LAUNCH1(W_, P_, O_)                                                                \
+  hipLaunchKernelGGL((bsr32_f32_grp_kernel<W_, P_, O_>), grid, dim3(64 * W_), 0, ctx->stream,    \
+                     mb, n, item_ptr, rows, wmask, afrag, B, ldb, alpha, beta, C, ldc, xm)
+#ifdef SPMM_TUNING
+#define GRP32_LAUNCH(W_)                                                                         \
+  do {                                                                                           \
+    switch (gv) {                                                                                \
+      case 30: GRP32_LAUNCH1(W_, 3, 0); break;                                                   \
+      case 32: GRP32_LAUNCH1(W_, 3, 2); break;                                                   \
+      case 34: GRP32_LAUNCH1(W_, 3, 4); break;                                                   \
+      case 42: GRP32_LAUNCH1(W_, 4, 2); break;                                                   \
+      case 43: GRP32_LAUNCH1(W_, 4, 3); break;                                                   \
+      case 44: GRP32_LAUNCH1(W_, 4, 4); break;                                                   \
+      case 52: GRP32_LAUNCH1(W_, 5, 2); break;                                                   \
+      case 53: GRP32_LAUNCH1(W_, 5, 3); break;                                                   \
+      default: GRP32_LAUNCH1(W_, 3, 3); break;                                                   \
+    }                                                                                            \
+  } while (0)
+#else
+#define GRP32_LAUNCH(W_) GRP32_LAUNCH1(W_, 3, 3)
+#endif
+  (void)gv;
+  if (W == 4) GRP32_LAUNCH(4);
+  else GRP32_LAUNCH(2);
+#undef GRP32_LAUNCH
+#undef GRP32_LAUNCH1
+  timing_end(ctx, slot);
   return from_hip(hipGetLastError());
 }
 

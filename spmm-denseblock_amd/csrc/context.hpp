@@ -47,13 +47,16 @@ struct spmm_context {
   // they live apart from ws, which other entries overwrite.
   int* tickets = nullptr;
   size_t tickets_cap = 0;
-  // Group analyses made on this handle (spmm_bsr16_group_analysis_f16): buffer ->
-  // its shape, so the grouped product needs no device read to size its grid.
+  // Group analyses made on this handle (spmm_bsr16_group_analysis_f16 /
+  // spmm_bsr32_group_analysis_f32): buffer -> its shape, so the grouped product needs
+  // no device read to size its grid.
   struct GroupPlan {
     int W, mb, ngroups;
     long long nitems;
     size_t bytes, rows_off, afrag_off;
     int max_col;  // largest block column (-1: none), checked against kb
+    int bs = 16;  // 16: fp16 analysis; 32: fp32 analysis (wmask_off used)
+    size_t wmask_off = 0;
   };
   std::map<const void*, GroupPlan> group_plans;
 
@@ -151,5 +154,13 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
                                        const int* item_ptr, const int* rows,
                                        const unsigned* afrag, const uint16_t* B16, int ldb,
                                        float alpha, float beta, float* C, int ldc, bool crow);
+// the grouped bs 32 stream (row-major B and C)
+spmm_status_t launch_bsr32_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
+                                    const int* rows, const int* src, const float* val,
+                                    float* afrag);
+spmm_status_t launch_bsrmm_grouped_f32(spmm_context* ctx, int W, int mb, int n, int ngroups,
+                                       const int* item_ptr, const int* rows,
+                                       const unsigned* wmask, const float* afrag, const float* B,
+                                       int ldb, float alpha, float beta, float* C, int ldc);
 
 }  // namespace spmm

@@ -1,6 +1,7 @@
-// group.cpp — the group analysis of the grouped bs 16 fp16 stream
-// (spmm_bsr16_group_analysis_f16 / spmm_bsrmm_grouped_f16, include/spmm_hip.h;
-// DESIGN.md §4, "The grouped stream").
+// group.cpp — the group analyses of the grouped streams: bs 16 fp16
+// (spmm_bsr16_group_analysis_f16 / spmm_bsrmm_grouped_f16) and bs 32 fp32
+// (spmm_bsr32_group_analysis_f32 / spmm_bsrmm_grouped_f32), include/spmm_hip.h;
+// DESIGN.md §4, "The grouped stream".
 //
 // Once per matrix, like spmm_bsr16_analysis_f16 and cuSPARSE's SpMM preprocess
 // (the reference's rocsparse_bsrmm.h:102-256 has none):
@@ -9,9 +10,11 @@
 //  2. per group of W adjacent block rows the host merges the W sorted
 //     block-column lists (worker threads over groups) and enumerates the union
 //     of their nonzero columns in (block column J, column c) order, cut into
-//     items of 16 entries (the last one padded with row -1): the B row J*16 + c
-//     of each entry and, per wave w of the group, the block of row w holding
-//     block column J (-1: none);
+//     items of E entries (16 at bs 16, 8 at bs 32; the last one padded with row
+//     -1): the B row J*bs + c of each entry and, per wave w of the group, the
+//     block of row w holding block column J (-1: none; at bs 32 also -1 when
+//     that block's column c is all zeros, and the per-(item, wave) mask of the
+//     entries whose source is a block: the MFMAs that wave runs);
 //  3. those index arrays go to the device and bsr16_grp_fill_kernel writes each
 //     wave's A fragment of each item into the caller's buffer.
 // The call synchronises the handle's stream (the host merge needs the masks).
@@ -19,8 +22,10 @@
 // Buffer layout (caller-owned device memory, bufferBytes from the first call):
 //   [0, 256)                 reserved header
 //   item_ptr[ngroups + 1]    int32, the items of group g are [item_ptr[g], item_ptr[g+1])
-//   rows[nitems][16]         int32, B row of each entry (-1: padding)
-//   afrag[nitems][W][128]    uint32, lane l of wave w: A[l & 15][4 (l >> 4) .. + 3] fp16 x 4
+//   rows[nitems][E]          int32, B row of each entry (-1: padding)
+//   bs 16: afrag[nitems][W][128]  uint32, lane l of wave w: A[l & 15][4 (l >> 4) .. + 3] fp16 x 4
+//   bs 32: wmask[nitems][W]       uint32, bit e: entry e is a column of wave w's block row
+//          afrag[nitems][W][32][8] fp32, A[row][entry] of wave w's block row
 // The handle records the layout by buffer address (spmm_context::group_plans).
 #include <hip/hip_runtime.h>
 
@@ -51,9 +56,12 @@ struct ColRange {
 };
 
 // Items of group g: the W rows' blocks merged by block column; for each block
-// column the union of the rows' masks, its set bits in order.
+// column the union of the rows' masks, its set bits in order. BS 32 (HELD):
+// a wave's source is -1 where its block holds no value in the entry's column.
+template <int BS, int E, bool HELD>
 void build_group(int g, int W, int mb, const int* rp, const int* ci, const unsigned* mk,
                  std::vector<int>* rows, std::vector<int>* src, ColRange* cr) {
+  constexpr unsigned kAll = BS == 32 ? 0xffffffffu : 0xffffu;
   int cur[8], end[8];
   for (int w = 0; w < W; ++w) {
     const int br = g * W + w;
@@ -74,46 +82,47 @@ void build_group(int g, int W, int mb, const int* rp, const int* ci, const unsig
     cr->hi = std::max(cr->hi, J);
     unsigned u = 0;
     int kw[8];
+    unsigned mw[8];
     for (int w = 0; w < W; ++w) {
       kw[w] = -1;
+      mw[w] = 0;
       // duplicate block columns in a row (not produced by csr2bsr) are taken in order
       if (cur[w] < end[w] && ci[cur[w]] == J) {
         kw[w] = cur[w];
-        u |= mk[cur[w]] & 0xffffu;
+        mw[w] = mk[cur[w]] & kAll;
+        u |= mw[w];
         ++cur[w];
       }
     }
     while (u) {
       const int c = __builtin_ctz(u);
       u &= u - 1;
-      rows->push_back(J * 16 + c);
-      for (int w = 0; w < W; ++w) src->push_back(kw[w]);
+      rows->push_back(J * BS + c);
+      for (int w = 0; w < W; ++w)
+        src->push_back(HELD && !((mw[w] >> c) & 1u) ? -1 : kw[w]);
       ++e;
     }
   }
-  while (e % 16) {  // pad the last item
+  while (e % E) {  // pad the last item
     rows->push_back(-1);
     for (int w = 0; w < W; ++w) src->push_back(-1);
     ++e;
   }
 }
 
-}  // namespace
-
-extern "C" {
-
-spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction_t dir, int mb,
-                                            int nnzb, int groupRows, const int* bsrRowPtr,
-                                            const int* bsrColInd, const uint16_t* bsrVal,
-                                            void* buffer, size_t* bufferBytes) {
+// The analysis of either stream: BS 16 (fp16 values, W = 2 / 4 / 8) or 32 (fp32, W = 2 / 4).
+spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir, int mb, int nnzb,
+                             int groupRows, const int* bsrRowPtr, const int* bsrColInd,
+                             const void* bsrVal, void* buffer, size_t* bufferBytes) {
   if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
   if ((dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) || mb < 0 || nnzb < 0 ||
       !bufferBytes)
     return SPMM_STATUS_INVALID_VALUE;
-  const int W = groupRows == 0 ? 4 : groupRows;
-  if (W != 2 && W != 4 && W != 8) return SPMM_STATUS_INVALID_VALUE;
+  const int W = groupRows == 0 ? (BS == 16 ? 4 : 2) : groupRows;
+  if (W != 2 && W != 4 && (BS == 32 || W != 8)) return SPMM_STATUS_INVALID_VALUE;
   if (mb > 0 && !bsrRowPtr) return SPMM_STATUS_INVALID_VALUE;
   if (nnzb > 0 && (!bsrColInd || !bsrVal)) return SPMM_STATUS_INVALID_VALUE;
+  const int E = BS == 16 ? 16 : 8;  // entries per item
   const int ngroups = (mb + W - 1) / W;
   hipStream_t st = handle->stream;
   // masks on the device (scratch), then row pointer, block columns and masks to the host
@@ -123,7 +132,10 @@ spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction
     if (nnzb > 0) {
       if (spmm_status_t s = ensure_scratch(handle, (size_t)nnzb * 4)) return s;
       unsigned* dmk = static_cast<unsigned*>(handle->scratch);
-      if (spmm_status_t s = launch_bsr16_analysis(handle, dir, nnzb, bsrVal, dmk, nullptr)) return s;
+      spmm_status_t s = BS == 16
+          ? launch_bsr16_analysis(handle, dir, nnzb, static_cast<const uint16_t*>(bsrVal), dmk, nullptr)
+          : launch_bsr32_analysis(handle, dir, nnzb, static_cast<const float*>(bsrVal), dmk, nullptr);
+      if (s) return s;
       hipError_t e = hipMemcpyAsync(mk.data(), dmk, (size_t)nnzb * 4, hipMemcpyDeviceToHost, st);
       if (e == hipSuccess)
         e = hipMemcpyAsync(ci.data(), bsrColInd, (size_t)nnzb * 4, hipMemcpyDeviceToHost, st);
@@ -140,8 +152,14 @@ spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction
   std::vector<std::vector<int>> grows(ngroups), gsrc(ngroups);
   std::vector<ColRange> cr(ngroups);
   spmm_host::parallel_for(ngroups, [&](int64_t lo, int64_t hi) {
-    for (int64_t g = lo; g < hi; ++g)
-      build_group((int)g, W, mb, rp.data(), ci.data(), mk.data(), &grows[g], &gsrc[g], &cr[g]);
+    for (int64_t g = lo; g < hi; ++g) {
+      if (BS == 16)
+        build_group<16, 16, false>((int)g, W, mb, rp.data(), ci.data(), mk.data(), &grows[g],
+                                   &gsrc[g], &cr[g]);
+      else
+        build_group<32, 8, true>((int)g, W, mb, rp.data(), ci.data(), mk.data(), &grows[g],
+                                 &gsrc[g], &cr[g]);
+    }
   });
   int max_col = -1;
   for (const ColRange& c : cr) {
@@ -152,26 +170,41 @@ spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction
   gi.item_ptr.resize(ngroups + 1, 0);
   long long acc = 0;
   for (int g = 0; g < ngroups; ++g) {
-    acc += (long long)(grows[g].size() / 16);
+    acc += (long long)(grows[g].size() / E);
     if (acc > INT_MAX) return SPMM_STATUS_NOT_SUPPORTED;  // int32 item pointers
     gi.item_ptr[g + 1] = (int)acc;
   }
   const long long nitems = acc;
   const size_t rows_off = align256(256 + (size_t)(ngroups + 1) * 4);
-  const size_t afrag_off = align256(rows_off + (size_t)nitems * 64);
-  const size_t need = afrag_off + (size_t)nitems * W * 512;
+  const size_t wmask_off = align256(rows_off + (size_t)nitems * E * 4);  // bs 32 only
+  const size_t afrag_off = BS == 16 ? wmask_off : align256(wmask_off + (size_t)nitems * W * 4);
+  const size_t need = afrag_off + (size_t)nitems * W * (BS == 16 ? 512 : 1024);
   if (!buffer) {
     *bufferBytes = need;
     return SPMM_STATUS_SUCCESS;
   }
   if (*bufferBytes < need) return SPMM_STATUS_INVALID_VALUE;
-  gi.rows.reserve((size_t)nitems * 16);
-  gi.src.reserve((size_t)nitems * 16 * W);
+  gi.rows.reserve((size_t)nitems * E);
+  gi.src.reserve((size_t)nitems * E * W);
   for (int g = 0; g < ngroups; ++g) {
     gi.rows.insert(gi.rows.end(), grows[g].begin(), grows[g].end());
     gi.src.insert(gi.src.end(), gsrc[g].begin(), gsrc[g].end());
     std::vector<int>().swap(grows[g]);
     std::vector<int>().swap(gsrc[g]);
+  }
+  // bs 32: per (item, wave) the entries that wave multiplies
+  std::vector<unsigned> wm;
+  if (BS == 32) {
+    wm.assign((size_t)nitems * W, 0u);
+    spmm_host::parallel_for(nitems, [&](int64_t lo, int64_t hi) {
+      for (int64_t it = lo; it < hi; ++it)
+        for (int w = 0; w < W; ++w) {
+          unsigned m = 0;
+          for (int e = 0; e < E; ++e)
+            if (gi.src[((size_t)it * E + e) * W + w] >= 0) m |= 1u << e;
+          wm[(size_t)it * W + w] = m;
+        }
+    });
   }
   char* buf = static_cast<char*>(buffer);
   hipError_t e = hipMemsetAsync(buf, 0, 256, st);
@@ -179,26 +212,66 @@ spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction
     e = hipMemcpyAsync(buf + 256, gi.item_ptr.data(), (size_t)(ngroups + 1) * 4,
                        hipMemcpyHostToDevice, st);
   if (e == hipSuccess && nitems)
-    e = hipMemcpyAsync(buf + rows_off, gi.rows.data(), (size_t)nitems * 64, hipMemcpyHostToDevice, st);
+    e = hipMemcpyAsync(buf + rows_off, gi.rows.data(), (size_t)nitems * E * 4,
+                       hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && nitems && BS == 32)
+    e = hipMemcpyAsync(buf + wmask_off, wm.data(), (size_t)nitems * W * 4, hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return from_hip(e);
   if (nitems) {
     // the entry sources go through the scratch buffer (the masks there are consumed)
-    if (spmm_status_t s = ensure_scratch(handle, (size_t)nitems * 16 * W * 4)) return s;
+    if (spmm_status_t s = ensure_scratch(handle, (size_t)nitems * E * W * 4)) return s;
     int* dsrc = static_cast<int*>(handle->scratch);
-    e = hipMemcpyAsync(dsrc, gi.src.data(), (size_t)nitems * 16 * W * 4, hipMemcpyHostToDevice, st);
+    e = hipMemcpyAsync(dsrc, gi.src.data(), (size_t)nitems * E * W * 4, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return from_hip(e);
-    if (spmm_status_t s = launch_bsr16_grp_fill(
-            handle, nitems, W, dir, reinterpret_cast<const int*>(buf + rows_off), dsrc, bsrVal,
-            reinterpret_cast<unsigned*>(buf + afrag_off)))
-      return s;
+    spmm_status_t s = BS == 16
+        ? launch_bsr16_grp_fill(handle, nitems, W, dir, reinterpret_cast<const int*>(buf + rows_off),
+                                dsrc, static_cast<const uint16_t*>(bsrVal),
+                                reinterpret_cast<unsigned*>(buf + afrag_off))
+        : launch_bsr32_grp_fill(handle, nitems, W, dir, reinterpret_cast<const int*>(buf + rows_off),
+                                dsrc, static_cast<const float*>(bsrVal),
+                                reinterpret_cast<float*>(buf + afrag_off));
+    if (s) return s;
   }
   // the host vectors are freed on return: wait for the copies that read them
   e = hipStreamSynchronize(st);
   if (e != hipSuccess) return from_hip(e);
   std::lock_guard<std::mutex> lk(handle->mu);
-  handle->group_plans[buffer] = spmm_context::GroupPlan{W, mb, ngroups, nitems, need, rows_off,
-                                                        afrag_off, max_col};
+  spmm_context::GroupPlan plan{W, mb, ngroups, nitems, need, rows_off, afrag_off, max_col};
+  plan.bs = BS;
+  plan.wmask_off = wmask_off;
+  handle->group_plans[buffer] = plan;
   return SPMM_STATUS_SUCCESS;
+}
+
+// The plan of `buffer` for a product at block size BS, or an error status.
+spmm_status_t find_plan(spmm_handle_t handle, const void* buffer, int BS, int mb, int kb,
+                        spmm_context::GroupPlan* plan) {
+  std::lock_guard<std::mutex> lk(handle->mu);
+  auto it = handle->group_plans.find(buffer);
+  if (it == handle->group_plans.end() || it->second.bs != BS) return SPMM_STATUS_INVALID_VALUE;
+  *plan = it->second;
+  if (plan->mb != mb || plan->max_col >= kb) return SPMM_STATUS_INVALID_VALUE;
+  return SPMM_STATUS_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction_t dir, int mb,
+                                            int nnzb, int groupRows, const int* bsrRowPtr,
+                                            const int* bsrColInd, const uint16_t* bsrVal,
+                                            void* buffer, size_t* bufferBytes) {
+  return group_analysis(handle, 16, dir, mb, nnzb, groupRows, bsrRowPtr, bsrColInd, bsrVal, buffer,
+                        bufferBytes);
+}
+
+spmm_status_t spmm_bsr32_group_analysis_f32(spmm_handle_t handle, spmm_direction_t dir, int mb,
+                                            int nnzb, int groupRows, const int* bsrRowPtr,
+                                            const int* bsrColInd, const float* bsrVal,
+                                            void* buffer, size_t* bufferBytes) {
+  return group_analysis(handle, 32, dir, mb, nnzb, groupRows, bsrRowPtr, bsrColInd, bsrVal, buffer,
+                        bufferBytes);
 }
 
 spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n,
@@ -213,13 +286,7 @@ spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n
   if (mb == 0 || n == 0 || kb == 0) return SPMM_STATUS_SUCCESS;
   if (!buffer || !B || !C) return SPMM_STATUS_INVALID_VALUE;
   spmm_context::GroupPlan plan;
-  {
-    std::lock_guard<std::mutex> lk(handle->mu);
-    auto it = handle->group_plans.find(buffer);
-    if (it == handle->group_plans.end()) return SPMM_STATUS_INVALID_VALUE;
-    plan = it->second;
-  }
-  if (plan.mb != mb || plan.max_col >= kb) return SPMM_STATUS_INVALID_VALUE;
+  if (spmm_status_t st = find_plan(handle, buffer, 16, mb, kb, &plan)) return st;
   const long long K = (long long)kb * 16, M = (long long)mb * 16;
   if (orderB == SPMM_ORDER_COL ? ldb < K : ldb < n) return SPMM_STATUS_INVALID_VALUE;
   if (orderC == SPMM_ORDER_COL ? ldc < M : ldc < n) return SPMM_STATUS_INVALID_VALUE;
@@ -242,6 +309,59 @@ spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n
       reinterpret_cast<const int*>(buf + plan.rows_off),
       reinterpret_cast<const unsigned*>(buf + plan.afrag_off), Bx, ldbx, alpha, beta, C, ldc,
       orderC == SPMM_ORDER_ROW);
+}
+
+spmm_status_t spmm_bsrmm_grouped_f32(spmm_handle_t handle, int mb, int kb, int n,
+                                     const void* buffer, float alpha, const float* B, int ldb,
+                                     spmm_order_t orderB, float beta, float* C, int ldc,
+                                     spmm_order_t orderC) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (mb < 0 || kb < 0 || n < 0) return SPMM_STATUS_INVALID_VALUE;
+  if ((orderB != SPMM_ORDER_ROW && orderB != SPMM_ORDER_COL) ||
+      (orderC != SPMM_ORDER_ROW && orderC != SPMM_ORDER_COL))
+    return SPMM_STATUS_INVALID_VALUE;
+  if (mb == 0 || n == 0 || kb == 0) return SPMM_STATUS_SUCCESS;
+  if (!buffer || !B || !C) return SPMM_STATUS_INVALID_VALUE;
+  spmm_context::GroupPlan plan;
+  if (spmm_status_t st = find_plan(handle, buffer, 32, mb, kb, &plan)) return st;
+  const long long K = (long long)kb * 32, M = (long long)mb * 32;
+  if (orderB == SPMM_ORDER_COL ? ldb < K : ldb < n) return SPMM_STATUS_INVALID_VALUE;
+  if (orderC == SPMM_ORDER_COL ? ldc < M : ldc < n) return SPMM_STATUS_INVALID_VALUE;
+  // the stream copies 16-B pieces of 128-column B-row tiles and stores 16-B pieces of C rows
+  auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  if (n % 4 || !al16(B) || !al16(C)) return SPMM_STATUS_NOT_SUPPORTED;
+  if ((orderB == SPMM_ORDER_ROW && ldb % 4) || (orderC == SPMM_ORDER_ROW && ldc % 4))
+    return SPMM_STATUS_NOT_SUPPORTED;
+  // column-major B / C are staged row-major in the workspace (B first, then C)
+  const size_t bbytes = orderB == SPMM_ORDER_COL ? (size_t)K * n * 4 : 0;
+  const size_t cbytes = orderC == SPMM_ORDER_COL ? (size_t)M * n * 4 : 0;
+  if (bbytes + cbytes)
+    if (spmm_status_t s = ensure_workspace(handle, bbytes + cbytes)) return s;
+  const float* Bx = B;
+  int ldbx = ldb;
+  if (bbytes) {
+    float* Bt = static_cast<float*>(handle->ws);
+    if (spmm_status_t s = launch_transpose(handle, n, (int)K, B, ldb, Bt, n, 0.f)) return s;
+    Bx = Bt;
+    ldbx = n;
+  }
+  const char* buf = static_cast<const char*>(buffer);
+  float* Cx = C;
+  int ldcx = ldc;
+  float bx = beta;
+  if (cbytes) {  // alpha A B into a row-major tile, then C = tile^T + beta C
+    Cx = reinterpret_cast<float*>(static_cast<char*>(handle->ws) + bbytes);
+    ldcx = n;
+    bx = 0.f;
+  }
+  if (spmm_status_t s = launch_bsrmm_grouped_f32(
+          handle, plan.W, mb, n, plan.ngroups, reinterpret_cast<const int*>(buf + 256),
+          reinterpret_cast<const int*>(buf + plan.rows_off),
+          reinterpret_cast<const unsigned*>(buf + plan.wmask_off),
+          reinterpret_cast<const float*>(buf + plan.afrag_off), Bx, ldbx, alpha, bx, Cx, ldcx))
+    return s;
+  if (cbytes) return launch_transpose(handle, (int)M, n, Cx, ldcx, C, ldc, beta);
+  return SPMM_STATUS_SUCCESS;
 }
 
 spmm_status_t spmm_bsr16_group_release(spmm_handle_t handle, const void* buffer) {

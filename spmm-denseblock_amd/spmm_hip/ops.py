@@ -344,6 +344,47 @@ class GroupedBsr16:
             self.buffer = None
 
 
+class GroupedBsr32:
+    """spmm_bsr32_group_analysis_f32 on a bs = 32 fp32 BSR matrix (once), then
+    .mm(...) = spmm_bsrmm_grouped_f32: groups of group_rows (2 or 4) adjacent
+    block rows sharing their B-row copies, each multiplying only its own
+    nonzero columns (C bit-identical to bsrmm / bsrmm_analysed)."""
+
+    def __init__(self, rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, *,
+                 mb: int, group_rows: int = 2, direction: int = DIRECTION_ROW,
+                 handle: Handle | None = None):
+        from ctypes import c_size_t
+        for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                          (val, torch.float32, "val")):
+            _need(t, dt, nm)
+        self.h = handle or default_handle()
+        self.mb = mb
+        nnzb = colind.numel()
+        size = c_size_t(0)
+        args = (self.h.raw, direction, mb, nnzb, group_rows, _ptr(rowptr), _ptr(colind), _ptr(val))
+        check(lib().spmm_bsr32_group_analysis_f32(*args, None, byref(size)),
+              "spmm_bsr32_group_analysis_f32")
+        self.buffer = torch.empty(max(size.value, 1), dtype=torch.uint8, device=val.device)
+        check(lib().spmm_bsr32_group_analysis_f32(*args, _ptr(self.buffer), byref(size)),
+              "spmm_bsr32_group_analysis_f32")
+        self.bytes = size.value
+
+    def mm(self, B: torch.Tensor, *, kb: int, n: int, ldb: int, C: torch.Tensor, ldc: int,
+           order_b: int = ORDER_ROW, order_c: int = ORDER_ROW, alpha: float = 1.0,
+           beta: float = 0.0) -> torch.Tensor:
+        _need(B, torch.float32, "B")
+        _need(C, torch.float32, "C")
+        check(lib().spmm_bsrmm_grouped_f32(self.h.raw, self.mb, kb, n, _ptr(self.buffer), alpha,
+                                           _ptr(B), ldb, order_b, beta, _ptr(C), ldc, order_c),
+              "spmm_bsrmm_grouped_f32")
+        return C
+
+    def close(self) -> None:
+        if getattr(self, "buffer", None) is not None:
+            lib().spmm_bsr16_group_release(self.h.raw, _ptr(self.buffer))
+            self.buffer = None
+
+
 def bsrmm_f16(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torch.Tensor, *,
               mb: int, kb: int, n: int, bs: int, ldb: int, order_b: int = ORDER_ROW,
               C: torch.Tensor, ldc: int, order_c: int = ORDER_ROW, alpha: float = 1.0,

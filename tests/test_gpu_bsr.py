@@ -1089,3 +1089,85 @@ def test_bsrmm_grouped_f16_checks(device):
         grp.buffer = torch.empty(16, dtype=torch.uint8, device=device)
         grp.mm(B, kb=7, n=128, ldb=128, C=C, ldc=128)
     assert e.value.status == INVALID_VALUE
+
+
+@pytest.mark.parametrize("W", [2, 4])
+@pytest.mark.parametrize("n,ob,oc,alpha,beta,direction",
+                         [(128, 0, 0, 1.0, 0.0, 0), (256, 0, 0, 0.5, -1.0, 0), (64, 0, 0, 1.0, 0.0, 1),
+                          (132, 0, 1, 1.0, 0.0, 0), (260, 1, 0, 2.0, 0.5, 1), (128, 1, 1, 1.0, 1.0, 0)])
+def test_bsrmm_grouped_f32(oracle, device, W, n, ob, oc, alpha, beta, direction):
+    """The grouped bs 32 fp32 stream (spmm_bsr32_group_analysis_f32 +
+    spmm_bsrmm_grouped_f32): groups of W block rows sharing the union of their
+    columns, each multiplying only its own nonzero columns. An mb that W does not
+    divide, empty block rows, explicit zero blocks, single-column blocks, ROW and
+    COLUMN blocks, partial column tiles, alpha / beta, column-major B and C (staged);
+    against the f64 oracle, and bit-identical to spmm_bsrmm_ex_f32 (the same MFMAs
+    in the same order) where both run row-major."""
+    from spmm_hip._lib import DIRECTION_COLUMN, DIRECTION_ROW
+    ops = _ops()
+    rng = np.random.default_rng(32 * W + n + 7 * ob + direction)
+    mb, kb = 37, 60
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, 32, 0.3)
+    vd = v if direction == 0 else np.ascontiguousarray(v.reshape(-1, 32, 32).transpose(0, 2, 1)).reshape(-1)
+    dr = DIRECTION_ROW if direction == 0 else DIRECTION_COLUMN
+    Bd = rng.uniform(-1, 1, (kb * 32, n)).astype(np.float32)
+    B = Bd if ob == 0 else np.ascontiguousarray(Bd.T)
+    m = mb * 32
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    Ch = C0 if oc == 0 else np.ascontiguousarray(C0.T)
+    drp, dci, dv, dB, dC = _dev(rp, ci, vd, B.reshape(-1), Ch.reshape(-1))
+    grp = ops.GroupedBsr32(drp, dci, dv, mb=mb, group_rows=W, direction=dr)
+    grp.mm(dB, kb=kb, n=n, ldb=n if ob == 0 else kb * 32, order_b=ob, C=dC,
+           ldc=n if oc == 0 else m, order_c=oc, alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    got = dC.cpu().numpy().reshape((m, n) if oc == 0 else (n, m))
+    got = got if oc == 0 else got.T
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, 32, rp, ci, v, Bd, n, 0)
+    ref = alpha * ref + beta * C0.astype(np.float64)
+    absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+    assert_normwise(got, ref, absd, TOL_F32, f"grouped bs32 W={W} n={n} ob={ob} oc={oc}")
+    if ob == 0 and oc == 0 and n % 128 == 0:
+        Cd = torch.from_numpy(C0.copy()).to(device)
+        ops.bsrmm(drp, dci, dv, torch.from_numpy(Bd).to(device), mb=mb, kb=kb, n=n, bs=32, ldb=n,
+                  C=Cd, ldc=n, alpha=alpha, beta=beta, direction=dr)
+        torch.cuda.synchronize()
+        assert torch.equal(Cd.cpu(), torch.from_numpy(got)), "grouped bs 32 differs from bsrmm"
+    grp.close()
+
+
+def test_bsrmm_grouped_f32_checks(device):
+    """A bs 16 analysis is not a bs 32 one; another mb, a kb below an analysed
+    block column, a buffer without an analysis are INVALID_VALUE; W = 8 is
+    INVALID_VALUE at bs 32; n % 4 != 0 is NOT_SUPPORTED."""
+    from spmm_hip._lib import INVALID_VALUE, NOT_SUPPORTED, SpmmError
+    ops = _ops()
+    rng = np.random.default_rng(5)
+    rp, ci, v = _column_sparse_bsr(rng, 5, 7, 32, 0.5)
+    drp, dci, dv = _dev(rp, ci, v)
+    grp = ops.GroupedBsr32(drp, dci, dv, mb=5)
+    B = torch.zeros((7 * 32, 128), device=device)
+    C = torch.zeros((5 * 32, 128), device=device)
+    grp.mm(B, kb=7, n=128, ldb=128, C=C, ldc=128)
+    for kw, status in ((dict(kb=7, n=126, ldb=128), NOT_SUPPORTED),
+                       (dict(kb=int(ci.max()), n=128, ldb=128), INVALID_VALUE)):
+        with pytest.raises(SpmmError) as e:
+            grp.mm(B, C=C, ldc=128, **kw)
+        assert e.value.status == status, kw
+    grp.mb = 6
+    with pytest.raises(SpmmError) as e:
+        grp.mm(B, kb=7, n=128, ldb=128, C=C, ldc=128)
+    assert e.value.status == INVALID_VALUE
+    grp.mb = 5
+    grp.close()
+    with pytest.raises(SpmmError) as e:
+        ops.GroupedBsr32(drp, dci, dv, mb=5, group_rows=8)
+    assert e.value.status == INVALID_VALUE
+    # a bs 16 analysis buffer is refused by the bs 32 product
+    rp16, ci16, v16 = _column_sparse_bsr(rng, 5, 7, 16, 0.5)
+    d16 = _dev(rp16, ci16, v16.astype(np.float16))
+    g16 = ops.GroupedBsr16(*d16, mb=5)
+    grp.buffer = g16.buffer
+    with pytest.raises(SpmmError) as e:
+        grp.mm(B, kb=7, n=128, ldb=128, C=C, ldc=128)
+    assert e.value.status == INVALID_VALUE
+    g16.close()
