@@ -417,3 +417,49 @@ def test_grouped_bs16_f16_full_size(oracle, device, W, reorder):
     _within(Cg[:n], Cc, absd, 2 * TOL_F16_ACC, what + " vs CSR")
     assert not bool(Cg[n:].any()), "padding rows of C must be zero"
     grp.close()
+
+
+@pytest.mark.parametrize("kind,reorder,W", [("reddit", False, 2), ("reddit", True, 2),
+                                            ("products", False, 2), ("products", False, 4)])
+def test_grouped_bs32_full_size(oracle, device, kind, reorder, W):
+    """Config 3's bs 32 fp32 product on the grouped bs 32 stream at full size
+    (reddit, RCM reddit, products at 2 and 4 block rows per group): sampled rows
+    against the f64 oracle, every row against the CSR kernel, and C bit-identical
+    to the drop-in column stream wherever that stream runs whole block rows (the
+    segmented outlier rows of RCM reddit sum their partials in another order:
+    there the bar is the oracle's)."""
+    ops = _ops()
+    rp, ci, n = _graph(kind, reorder)
+    K, bs = 128, 32
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
+    drp, dci, dv = _dev(rp, ci, v)
+    mb = (n + bs - 1) // bs
+    B = torch.rand((mb * bs, K), device=device) * 2 - 1
+    Cc = ops.gespmm_csrmm(drp, dci, dv, B[:n].contiguous())
+    absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B[:n].abs().contiguous())
+    brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
+    del dci, dv
+    Cd = torch.empty((mb * bs, K), device=device)
+    ops.bsrmm(brp, bci, bval, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=Cd, ldc=K)
+    grp = ops.GroupedBsr32(brp, bci, bval, mb=mb, group_rows=W)
+    del bval
+    Cg = torch.empty((mb * bs, K), device=device)
+    grp.mm(B, kb=mb, n=K, ldb=K, C=Cg, ldc=K)
+    torch.cuda.synchronize()
+    brp_h = brp.cpu().numpy()
+    seg = _segmented_block_rows(brp_h)
+    what = f"grouped W={W} bs32 {kind}{' RCM' if reorder else ''}"
+    rows = _sample_rows(brp_h, bs, n, 61 + W + 2 * reorder + (kind == "products"), seg)
+    _check_oracle_rows(oracle, Cg, rp, ci, v, B, rows, TOL_F32, what)
+    _within(Cg[:n], Cc, absd, 2 * TOL_F32, what + " vs CSR")
+    assert not bool(Cg[n:].any()), "padding rows of C must be zero"
+    # every segmented block row (seg above holds the shortest and the longest)
+    nbr = np.diff(brp_h)
+    same = torch.ones(mb, dtype=torch.bool)
+    if seg:
+        same[torch.from_numpy(nbr >= nbr[seg[0]])] = False
+    eq = (Cg.view(mb, bs, K) == Cd.view(mb, bs, K)).all(dim=2).all(dim=1).cpu()
+    bad = same & ~eq
+    assert not bool(bad.any()), (f"{what}: {int(bad.sum())} whole block rows differ from the "
+                                 f"drop-in column stream")
+    grp.close()
