@@ -154,6 +154,11 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
                                        const int* item_ptr, const int* rows,
                                        const unsigned* afrag, const uint16_t* B16, int ldb,
                                        float alpha, float beta, float* C, int ldc, bool crow);
+// the group analyses' device merge (grp_build_kernel: PASS 1 counts, PASS 2 writes)
+spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int mb, int ngroups,
+                               const int* rp, const int* ci, const unsigned* mk, int* cnt,
+                               int* maxj, const int* item_ptr, int* rows, int* src,
+                               unsigned* wmask);
 // the grouped bs 32 stream (row-major B and C)
 spmm_status_t launch_bsr32_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
                                     const int* rows, const int* src, const float* val,

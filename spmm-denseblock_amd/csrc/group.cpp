@@ -5,19 +5,21 @@
 //
 // Once per matrix, like spmm_bsr16_analysis_f16 and cuSPARSE's SpMM preprocess
 // (the reference's rocsparse_bsrmm.h:102-256 has none):
-//  1. the device computes every block's column mask (bsr16_analysis_kernel,
-//     masks only) and the row pointer, block columns and masks come to the host;
-//  2. per group of W adjacent block rows the host merges the W sorted
-//     block-column lists (worker threads over groups) and enumerates the union
-//     of their nonzero columns in (block column J, column c) order, cut into
-//     items of E entries (16 at bs 16, 8 at bs 32; the last one padded with row
-//     -1): the B row J*bs + c of each entry and, per wave w of the group, the
-//     block of row w holding block column J (-1: none; at bs 32 also -1 when
-//     that block's column c is all zeros, and the per-(item, wave) mask of the
-//     entries whose source is a block: the MFMAs that wave runs);
-//  3. those index arrays go to the device and bsr16_grp_fill_kernel writes each
-//     wave's A fragment of each item into the caller's buffer.
-// The call synchronises the handle's stream (the host merge needs the masks).
+//  1. the row pointer is checked on the host; the device computes every block's
+//     column mask (bsr16 / bsr32_analysis_kernel, masks only);
+//  2. grp_build_kernel, one thread per group of W adjacent block rows, merges the
+//     W sorted block-column lists and enumerates the union of their nonzero
+//     columns in (block column J, column c) order, cut into items of E entries (16
+//     at bs 16, 8 at bs 32; the last one padded with row -1). PASS 1 counts each
+//     group's items; the host sums them into the item pointers; PASS 2 writes the
+//     B row J*bs + c of each entry and, per wave w of the group, the block of row
+//     w holding block column J (-1: none; at bs 32 also -1 when that block's
+//     column c is all zeros, plus the per-(item, wave) mask of the entries whose
+//     source is a block: the MFMAs that wave runs);
+//  3. the fill kernels write each wave's A fragment of each item into the
+//     caller's buffer.
+// The call synchronises the handle's stream (twice: the row pointer, the counts).
+// Round 4's first form merged on the host: 0.27-0.46 s on the products stand-in.
 //
 // Buffer layout (caller-owned device memory, bufferBytes from the first call):
 //   [0, 256)                 reserved header
@@ -35,7 +37,6 @@
 #include <vector>
 
 #include "context.hpp"
-#include "host_util.hpp"
 
 using namespace spmm;
 
@@ -43,74 +44,11 @@ namespace {
 
 constexpr size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-struct GroupIndex {
-  std::vector<int> item_ptr;  // ngroups + 1
-  std::vector<int> rows;      // nitems * 16
-  std::vector<int> src;       // nitems * 16 * W
-};
-
-// block-column range of the matrix (the multiply checks kb against it: a B row
-// past the caller's K would be read out of bounds)
-struct ColRange {
-  int lo = 0, hi = -1;
-};
-
-// Items of group g: the W rows' blocks merged by block column; for each block
-// column the union of the rows' masks, its set bits in order. BS 32 (HELD):
-// a wave's source is -1 where its block holds no value in the entry's column.
-template <int BS, int E, bool HELD>
-void build_group(int g, int W, int mb, const int* rp, const int* ci, const unsigned* mk,
-                 std::vector<int>* rows, std::vector<int>* src, ColRange* cr) {
-  constexpr unsigned kAll = BS == 32 ? 0xffffffffu : 0xffffu;
-  int cur[8], end[8];
-  for (int w = 0; w < W; ++w) {
-    const int br = g * W + w;
-    cur[w] = br < mb ? rp[br] : 0;
-    end[w] = br < mb ? rp[br + 1] : 0;
-  }
-  int e = 0;  // entries emitted so far
-  for (;;) {
-    int J = -1;
-    for (int w = 0; w < W; ++w)
-      if (cur[w] < end[w] && (J < 0 || ci[cur[w]] < J)) J = ci[cur[w]];
-    if (J < 0) {
-      // a negative block column ends the merge above: record it for the caller's check
-      for (int w = 0; w < W; ++w)
-        if (cur[w] < end[w]) cr->lo = std::min(cr->lo, ci[cur[w]]);
-      break;
-    }
-    cr->hi = std::max(cr->hi, J);
-    unsigned u = 0;
-    int kw[8];
-    unsigned mw[8];
-    for (int w = 0; w < W; ++w) {
-      kw[w] = -1;
-      mw[w] = 0;
-      // duplicate block columns in a row (not produced by csr2bsr) are taken in order
-      if (cur[w] < end[w] && ci[cur[w]] == J) {
-        kw[w] = cur[w];
-        mw[w] = mk[cur[w]] & kAll;
-        u |= mw[w];
-        ++cur[w];
-      }
-    }
-    while (u) {
-      const int c = __builtin_ctz(u);
-      u &= u - 1;
-      rows->push_back(J * BS + c);
-      for (int w = 0; w < W; ++w)
-        src->push_back(HELD && !((mw[w] >> c) & 1u) ? -1 : kw[w]);
-      ++e;
-    }
-  }
-  while (e % E) {  // pad the last item
-    rows->push_back(-1);
-    for (int w = 0; w < W; ++w) src->push_back(-1);
-    ++e;
-  }
-}
-
 // The analysis of either stream: BS 16 (fp16 values, W = 2 / 4 / 8) or 32 (fp32, W = 2 / 4).
+// Everything runs on the device but the item pointers' prefix sum: masks
+// (bsr16 / bsr32_analysis_kernel, masks only), the per-group merge counting items
+// (grp_build_kernel PASS 1), the prefix sum on the host (one int per group), the
+// merge writing entries (PASS 2), the A fragments (the fill kernels).
 spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir, int mb, int nnzb,
                              int groupRows, const int* bsrRowPtr, const int* bsrColInd,
                              const void* bsrVal, void* buffer, size_t* bufferBytes) {
@@ -125,54 +63,48 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
   const int E = BS == 16 ? 16 : 8;  // entries per item
   const int ngroups = (mb + W - 1) / W;
   hipStream_t st = handle->stream;
-  // masks on the device (scratch), then row pointer, block columns and masks to the host
-  std::vector<int> rp(mb + 1, 0), ci(nnzb);
-  std::vector<unsigned> mk(nnzb);
+  // scratch: masks [nnzb], per-group item counts and largest block columns [2 ngroups]
+  const size_t mk_bytes = ((size_t)nnzb * 4 + 255) & ~size_t(255);
+  if (spmm_status_t s = ensure_scratch(handle, mk_bytes + (size_t)ngroups * 8 + 8)) return s;
+  unsigned* dmk = static_cast<unsigned*>(handle->scratch);
+  int* dcnt = reinterpret_cast<int*>(static_cast<char*>(handle->scratch) + mk_bytes);
+  int* dmaxj = dcnt + ngroups;
+  std::vector<int> cnt(ngroups), maxj(ngroups);
   if (mb > 0) {
-    if (nnzb > 0) {
-      if (spmm_status_t s = ensure_scratch(handle, (size_t)nnzb * 4)) return s;
-      unsigned* dmk = static_cast<unsigned*>(handle->scratch);
-      spmm_status_t s = BS == 16
-          ? launch_bsr16_analysis(handle, dir, nnzb, static_cast<const uint16_t*>(bsrVal), dmk, nullptr)
-          : launch_bsr32_analysis(handle, dir, nnzb, static_cast<const float*>(bsrVal), dmk, nullptr);
-      if (s) return s;
-      hipError_t e = hipMemcpyAsync(mk.data(), dmk, (size_t)nnzb * 4, hipMemcpyDeviceToHost, st);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(ci.data(), bsrColInd, (size_t)nnzb * 4, hipMemcpyDeviceToHost, st);
-      if (e != hipSuccess) return from_hip(e);
-    }
-    hipError_t e = hipMemcpyAsync(rp.data(), bsrRowPtr, (size_t)(mb + 1) * 4, hipMemcpyDeviceToHost, st);
+    // the row pointer is checked on the host before any kernel indexes the block columns
+    // with it (0 .. nnzb, never decreasing)
+    std::vector<int> rp(mb + 1);
+    hipError_t e = hipMemcpyAsync(rp.data(), bsrRowPtr, (size_t)(mb + 1) * 4,
+                                  hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return from_hip(e);
     if (rp[0] != 0 || rp[mb] != nnzb) return SPMM_STATUS_INVALID_VALUE;
     for (int i = 0; i < mb; ++i)
       if (rp[i + 1] < rp[i]) return SPMM_STATUS_INVALID_VALUE;
-  }
-  // per-group items on worker threads, then concatenated in group order
-  std::vector<std::vector<int>> grows(ngroups), gsrc(ngroups);
-  std::vector<ColRange> cr(ngroups);
-  spmm_host::parallel_for(ngroups, [&](int64_t lo, int64_t hi) {
-    for (int64_t g = lo; g < hi; ++g) {
-      if (BS == 16)
-        build_group<16, 16, false>((int)g, W, mb, rp.data(), ci.data(), mk.data(), &grows[g],
-                                   &gsrc[g], &cr[g]);
-      else
-        build_group<32, 8, true>((int)g, W, mb, rp.data(), ci.data(), mk.data(), &grows[g],
-                                 &gsrc[g], &cr[g]);
+    if (nnzb > 0) {
+      spmm_status_t s = BS == 16
+          ? launch_bsr16_analysis(handle, dir, nnzb, static_cast<const uint16_t*>(bsrVal), dmk, nullptr)
+          : launch_bsr32_analysis(handle, dir, nnzb, static_cast<const float*>(bsrVal), dmk, nullptr);
+      if (s) return s;
     }
-  });
-  int max_col = -1;
-  for (const ColRange& c : cr) {
-    if (c.lo < 0) return SPMM_STATUS_INVALID_VALUE;  // a negative block column
-    max_col = std::max(max_col, c.hi);
+    if (spmm_status_t s = launch_grp_build(handle, W, BS, false, mb, ngroups, bsrRowPtr, bsrColInd,
+                                           dmk, dcnt, dmaxj, nullptr, nullptr, nullptr, nullptr))
+      return s;
+    e = hipMemcpyAsync(cnt.data(), dcnt, (size_t)ngroups * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(maxj.data(), dmaxj, (size_t)ngroups * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return from_hip(e);
   }
-  GroupIndex gi;
-  gi.item_ptr.resize(ngroups + 1, 0);
+  int max_col = -1;
+  std::vector<int> item_ptr(ngroups + 1, 0);
   long long acc = 0;
   for (int g = 0; g < ngroups; ++g) {
-    acc += (long long)(grows[g].size() / E);
+    if (maxj[g] == INT_MIN) return SPMM_STATUS_INVALID_VALUE;  // a negative block column
+    max_col = std::max(max_col, maxj[g]);
+    acc += cnt[g];
     if (acc > INT_MAX) return SPMM_STATUS_NOT_SUPPORTED;  // int32 item pointers
-    gi.item_ptr[g + 1] = (int)acc;
+    item_ptr[g + 1] = (int)acc;
   }
   const long long nitems = acc;
   const size_t rows_off = align256(256 + (size_t)(ngroups + 1) * 4);
@@ -184,55 +116,32 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
     return SPMM_STATUS_SUCCESS;
   }
   if (*bufferBytes < need) return SPMM_STATUS_INVALID_VALUE;
-  gi.rows.reserve((size_t)nitems * E);
-  gi.src.reserve((size_t)nitems * E * W);
-  for (int g = 0; g < ngroups; ++g) {
-    gi.rows.insert(gi.rows.end(), grows[g].begin(), grows[g].end());
-    gi.src.insert(gi.src.end(), gsrc[g].begin(), gsrc[g].end());
-    std::vector<int>().swap(grows[g]);
-    std::vector<int>().swap(gsrc[g]);
-  }
-  // bs 32: per (item, wave) the entries that wave multiplies
-  std::vector<unsigned> wm;
-  if (BS == 32) {
-    wm.assign((size_t)nitems * W, 0u);
-    spmm_host::parallel_for(nitems, [&](int64_t lo, int64_t hi) {
-      for (int64_t it = lo; it < hi; ++it)
-        for (int w = 0; w < W; ++w) {
-          unsigned m = 0;
-          for (int e = 0; e < E; ++e)
-            if (gi.src[((size_t)it * E + e) * W + w] >= 0) m |= 1u << e;
-          wm[(size_t)it * W + w] = m;
-        }
-    });
-  }
   char* buf = static_cast<char*>(buffer);
   hipError_t e = hipMemsetAsync(buf, 0, 256, st);
   if (e == hipSuccess)
-    e = hipMemcpyAsync(buf + 256, gi.item_ptr.data(), (size_t)(ngroups + 1) * 4,
-                       hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && nitems)
-    e = hipMemcpyAsync(buf + rows_off, gi.rows.data(), (size_t)nitems * E * 4,
-                       hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && nitems && BS == 32)
-    e = hipMemcpyAsync(buf + wmask_off, wm.data(), (size_t)nitems * W * 4, hipMemcpyHostToDevice, st);
+    e = hipMemcpyAsync(buf + 256, item_ptr.data(), (size_t)(ngroups + 1) * 4, hipMemcpyHostToDevice,
+                       st);
   if (e != hipSuccess) return from_hip(e);
   if (nitems) {
-    // the entry sources go through the scratch buffer (the masks there are consumed)
-    if (spmm_status_t s = ensure_scratch(handle, (size_t)nitems * E * W * 4)) return s;
-    int* dsrc = static_cast<int*>(handle->scratch);
-    e = hipMemcpyAsync(dsrc, gi.src.data(), (size_t)nitems * E * W * 4, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return from_hip(e);
+    // the entry sources in the workspace (the masks stay in the scratch buffer)
+    if (spmm_status_t s = ensure_workspace(handle, (size_t)nitems * E * W * 4)) return s;
+    int* dsrc = static_cast<int*>(handle->ws);
+    int* drows = reinterpret_cast<int*>(buf + rows_off);
+    if (spmm_status_t s = launch_grp_build(handle, W, BS, true, mb, ngroups, bsrRowPtr, bsrColInd,
+                                           dmk, nullptr, nullptr,
+                                           reinterpret_cast<const int*>(buf + 256), drows, dsrc,
+                                           reinterpret_cast<unsigned*>(buf + wmask_off)))
+      return s;
     spmm_status_t s = BS == 16
-        ? launch_bsr16_grp_fill(handle, nitems, W, dir, reinterpret_cast<const int*>(buf + rows_off),
-                                dsrc, static_cast<const uint16_t*>(bsrVal),
+        ? launch_bsr16_grp_fill(handle, nitems, W, dir, drows, dsrc,
+                                static_cast<const uint16_t*>(bsrVal),
                                 reinterpret_cast<unsigned*>(buf + afrag_off))
-        : launch_bsr32_grp_fill(handle, nitems, W, dir, reinterpret_cast<const int*>(buf + rows_off),
-                                dsrc, static_cast<const float*>(bsrVal),
+        : launch_bsr32_grp_fill(handle, nitems, W, dir, drows, dsrc,
+                                static_cast<const float*>(bsrVal),
                                 reinterpret_cast<float*>(buf + afrag_off));
     if (s) return s;
   }
-  // the host vectors are freed on return: wait for the copies that read them
+  // the host item pointers are freed on return: wait for the copy that reads them
   e = hipStreamSynchronize(st);
   if (e != hipSuccess) return from_hip(e);
   std::lock_guard<std::mutex> lk(handle->mu);
