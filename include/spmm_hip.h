@@ -292,8 +292,9 @@ spmm_status_t spmm_bsrmm_analysed_f16(spmm_handle_t handle, int mb, int kb, int 
  * union is 0.43 of the (block row, column) pairs at 4 rows, 0.29 at 8).
  * Two phases: with buffer == NULL, *bufferBytes receives the size of the
  * caller-owned device buffer; with a buffer of that size the analysis fills
- * it. It reads the block columns and column masks on the host, so the call
- * synchronises the handle's stream. The handle records the buffer's layout:
+ * it. It checks the row pointer on the host and sums the groups' item counts
+ * there, so the call synchronises the handle's stream. The handle records the
+ * buffer's layout:
  * spmm_bsrmm_grouped_f16 on the same handle takes it (until
  * spmm_bsr16_group_release or another analysis into the same buffer).
  * INVALID_VALUE for a bad dir / groupRows, negative sizes, null pointers that
