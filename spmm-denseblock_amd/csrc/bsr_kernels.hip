@@ -2851,7 +2851,7 @@ __global__ __launch_bounds__(256) void bsr16_grp_fill_kernel(long long nwork, in
 //    held column two MFMAs.
 // Groups go to the XCDs in chunks of xm groups (neighbouring groups share B rows).
 // ---------------------------------------------------------------------------
-template <int W, int P, int OCC = 0>
+template <int W, int P, int OCC = 0, bool NOMFMA = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
 void bsr32_f32_grp_kernel(
     int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
@@ -2981,11 +2981,15 @@ void bsr32_f32_grp_kernel(
         a[q] = __uint_as_float(r[0]);
         a[4 + q] = __uint_as_float(r[1]);
       }
+      if constexpr (NOMFMA) {  // TUNING diagnostic only (wrong results): the stream without MFMAs
+        asm volatile("" : : "v"(a[0]), "v"(a[4]), "v"(fb[0]), "v"(fb[7]), "s"(m));
+      } else {
 #pragma unroll
-      for (int c = 0; c < E; ++c) {
-        if (m & (1u << c)) {
-          u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(a[c], fb[c][0], u0, 0, 0, 0);
-          u1 = __builtin_amdgcn_mfma_f32_32x32x1f32(a[c], fb[c][1], u1, 0, 0, 0);
+        for (int c = 0; c < E; ++c) {
+          if (m & (1u << c)) {
+            u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(a[c], fb[c][0], u0, 0, 0, 0);
+            u1 = __builtin_amdgcn_mfma_f32_32x32x1f32(a[c], fb[c][1], u1, 0, 0, 0);
+          }
         }
       }
     };
@@ -3697,7 +3701,7 @@ spmm_status_t launch_bsrmm_grouped_f32(spmm_context* ctx, int W, int mb, int n, 
       return e ? atoi(e) : -1;
     }();
     switch (env) {
-      case 30: case 32: case 33: case 34: case 42: case 43: case 44: case 52: case 53:
+      case 30: case 32: case 33: case 34: case 42: case 43: case 44: case 52: case 53: case 933:
         gv = env;
         break;
       default:
@@ -3721,6 +3725,11 @@ spmm_status_t launch_bsrmm_grouped_f32(spmm_context* ctx, int W, int mb, int n, 
       case 44: GRP32_LAUNCH1(W_, 4, 4); break;                                                   \
       case 52: GRP32_LAUNCH1(W_, 5, 2); break;                                                   \
       case 53: GRP32_LAUNCH1(W_, 5, 3); break;                                                   \
+      case 933:  /* diagnostic: no MFMAs (wrong results) */                                    \
+        hipLaunchKernelGGL((bsr32_f32_grp_kernel<W_, 3, 3, true>), grid, dim3(64 * W_), 0,       \
+                           ctx->stream, mb, n, item_ptr, rows, wmask, afrag, B, ldb, alpha, beta, \
+                           C, ldc, xm);                                                          \
+        break;                                                                                   \
       default: GRP32_LAUNCH1(W_, 3, 3); break;                                                   \
     }                                                                                            \
   } while (0)
