@@ -4,7 +4,8 @@
 # trace, every workload line, counter bytes of the plain and hot CSR kernels (the bench's
 # traffic and hot-line counter bytes), determinism. Output in gpurun_out/final_r04/ (+
 # gpurun_out/pmcb/). PHASE selects a (suite, smoke, bench, trace), b (workload lines),
-# c (counter bytes, determinism). A GPU fault, abort or time limit (rc >= 124) stops it.
+# k (kernel traces of workload lines), c (counter bytes, determinism). A GPU fault, abort or
+# time limit (rc >= 124) stops it.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd); export TMPDIR=/tmp
@@ -22,12 +23,16 @@ echo "== kernel trace"
 fi
 if [[ $PH == *b* ]]; then
 : > $O/workloads.jsonl
-for w in ${WLS:-arxiv_csr products_csr_k256 products_csr_hot reddit_bsr32 products_bsr32 products_bsr16_f16 products_bsr16_f16_grp products_rcm_bsr16_f16_grp reddit_bsr8 reddit_bsr64 reddit_hybrid32 products_hybrid32}; do
+for w in ${WLS:-arxiv_csr products_csr_k256 products_csr_hot reddit_bsr32 products_bsr32 reddit_bsr32_grp products_bsr32_grp products_bsr16_f16 products_bsr16_f16_grp products_rcm_bsr16_f16_grp reddit_bsr8 reddit_bsr64 reddit_hybrid32 products_hybrid32}; do
   timeout -k 10 300 python bench.py --workload $w --steps 20 --warmup 5 --no-cpu-baseline > $O/bw.log 2>&1; rc=$?; stop $rc
   [ $rc -eq 0 ] || { tail -5 $O/bw.log; continue; }
   grep '^{' $O/bw.log >> $O/workloads.jsonl
   grep '^{' $O/bw.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); f=r['roofline']; print('$w', r['ms_per_step'], f.get('kernel_ms'), 'frac', f.get('frac'), 'mfma', f.get('mfma_frac'))"
 done
+fi
+if [[ $PH == *k* ]]; then
+echo "== kernel traces of the workload lines"
+WLS="arxiv_csr reddit_bsr32_grp products_bsr16_f16_grp reddit_bsr8 reddit_bsr64" KT_TAG=_r04 bash tools/profile_kt.sh; stop $?
 fi
 if [[ $PH == *c* ]]; then
 echo "== counter bytes, plain and hot CSR"
