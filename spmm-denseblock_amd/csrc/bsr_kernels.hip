@@ -2851,7 +2851,7 @@ __global__ __launch_bounds__(256) void bsr16_grp_fill_kernel(long long nwork, in
 //    held column two MFMAs.
 // Groups go to the XCDs in chunks of xm groups (neighbouring groups share B rows).
 // ---------------------------------------------------------------------------
-template <int W, int P, int OCC = 0, bool NOMFMA = false, bool K2 = false>
+template <int W, int P, int OCC = 0, bool NOMFMA = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
 void bsr32_f32_grp_kernel(
     int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
@@ -2880,14 +2880,6 @@ void bsr32_f32_grp_kernel(
   f32x32 u0, u1;
 #pragma unroll
   for (int e = 0; e < 32; ++e) u0[e] = u1[e] = 0.f;
-  // K2 (TUNING A/B only: not bit-identical to the column stream): v_mfma_f32_32x32x2_f32 on
-  // column pairs (q, q + 4), four independent 32 x 32 output blocks instead of two chains
-  f32x16 c4[4];
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) c4[cb][e] = 0.f;
-  const unsigned rdk = lds0 + (unsigned)h * 2048u + 4u * (unsigned)j;
 
   int nis = 0;  // vector-memory operations issued by this wave
   int ra[kCpw], rb[kCpw];  // row indices of the next item to issue (scalars)
@@ -2961,46 +2953,6 @@ void bsr32_f32_grp_kernel(
       __builtin_amdgcn_s_barrier();
       // slot (s + P - 1) % P was read by every wave in the previous item: refill it
       issue(it + P - 1, (s + P - 1) % P);
-      if constexpr (K2) {
-        float bk[16];  // bk[4 q + cb]: row (h ? 4 + q : q), column 32 cb + j
-        asm volatile(
-            "ds_read_b32 %0, %16 offset:%17\n\tds_read_b32 %1, %16 offset:%18\n\t"
-            "ds_read_b32 %2, %16 offset:%19\n\tds_read_b32 %3, %16 offset:%20\n\t"
-            "ds_read_b32 %4, %16 offset:%21\n\tds_read_b32 %5, %16 offset:%22\n\t"
-            "ds_read_b32 %6, %16 offset:%23\n\tds_read_b32 %7, %16 offset:%24\n\t"
-            "ds_read_b32 %8, %16 offset:%25\n\tds_read_b32 %9, %16 offset:%26\n\t"
-            "ds_read_b32 %10, %16 offset:%27\n\tds_read_b32 %11, %16 offset:%28\n\t"
-            "ds_read_b32 %12, %16 offset:%29\n\tds_read_b32 %13, %16 offset:%30\n\t"
-            "ds_read_b32 %14, %16 offset:%31\n\tds_read_b32 %15, %16 offset:%32\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(bk[0]), "=&v"(bk[1]), "=&v"(bk[2]), "=&v"(bk[3]), "=&v"(bk[4]), "=&v"(bk[5]),
-              "=&v"(bk[6]), "=&v"(bk[7]), "=&v"(bk[8]), "=&v"(bk[9]), "=&v"(bk[10]),
-              "=&v"(bk[11]), "=&v"(bk[12]), "=&v"(bk[13]), "=&v"(bk[14]), "=&v"(bk[15])
-            : "v"(rdk), "n"(s * kStage), "n"(s * kStage + 128), "n"(s * kStage + 256),
-              "n"(s * kStage + 384), "n"(s * kStage + 512), "n"(s * kStage + 640),
-              "n"(s * kStage + 768), "n"(s * kStage + 896), "n"(s * kStage + 1024),
-              "n"(s * kStage + 1152), "n"(s * kStage + 1280), "n"(s * kStage + 1408),
-              "n"(s * kStage + 1536), "n"(s * kStage + 1664), "n"(s * kStage + 1792),
-              "n"(s * kStage + 1920)
-            : "memory");
-        const unsigned m = msk[s];
-        load_rows(it + P);
-        msk[s] = load_mask(it + P);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const unsigned m0 = (m >> q) & 1u, m1 = (m >> (4 + q)) & 1u;
-          if (m0 | m1) {
-            // an unheld column of the pair multiplies zero A by zero B (no inf * 0)
-            const bool keep = h ? m1 != 0u : m0 != 0u;
-            const float av = __uint_as_float(fa[q]);
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb)
-              c4[cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, keep ? bk[4 * q + cb] : 0.f, c4[cb],
-                                                            0, 0, 0);
-          }
-        }
-        return;
-      }
       f32x2 fb[E];
       asm volatile(
           "ds_read_b64 %0, %8 offset:%9\n\t"
@@ -3055,29 +3007,10 @@ void bsr32_f32_grp_kernel(
     });
   }
   // nothing in flight past here (the prefetches of clamped items included)
-  if constexpr (K2)
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(c4[0]), "+a"(c4[1]), "+a"(c4[2]), "+a"(c4[3])
-                 : : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : : "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : : "memory");
 #pragma unroll
   for (int s = 0; s < P; ++s) asm volatile("" : : "v"(fan[s]), "v"(fbn[s]));
   if (br >= mb) return;
-  if constexpr (K2) {
-    // 32 x 32 output block cb: lane (j, h) holds column 32 cb + j, rows 4 h + (i & 3) + 8 (i >> 2)
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int cc = jt + 32 * cb + j;
-      if (cc >= n) continue;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const size_t row = (size_t)br * 32 + 4 * h + (i & 3) + 8 * (i >> 2);
-        float* p = C + row * ldc + cc;
-        *p = epi(c4[cb][i], alpha, beta, p);
-      }
-    }
-    return;
-  }
   const int col = jt + 4 * j;
   if (col >= n) return;
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA -> AGPR read
@@ -3769,7 +3702,6 @@ spmm_status_t launch_bsrmm_grouped_f32(spmm_context* ctx, int W, int mb, int n, 
     }();
     switch (env) {
       case 30: case 32: case 33: case 34: case 42: case 43: case 44: case 52: case 53: case 933:
-      case 1033: case 1034:
         gv = env;
         break;
       default:
@@ -3793,16 +3725,6 @@ spmm_status_t launch_bsrmm_grouped_f32(spmm_context* ctx, int W, int mb, int n, 
       case 44: GRP32_LAUNCH1(W_, 4, 4); break;                                                   \
       case 52: GRP32_LAUNCH1(W_, 5, 2); break;                                                   \
       case 53: GRP32_LAUNCH1(W_, 5, 3); break;                                                   \
-      case 1033:  /* k = 2 MFMAs on column pairs (not bit-identical) */                        \
-        hipLaunchKernelGGL((bsr32_f32_grp_kernel<W_, 3, 3, false, true>), grid, dim3(64 * W_), 0, \
-                           ctx->stream, mb, n, item_ptr, rows, wmask, afrag, B, ldb, alpha, beta, \
-                           C, ldc, xm);                                                          \
-        break;                                                                                   \
-      case 1034:                                                                                 \
-        hipLaunchKernelGGL((bsr32_f32_grp_kernel<W_, 3, 4, false, true>), grid, dim3(64 * W_), 0, \
-                           ctx->stream, mb, n, item_ptr, rows, wmask, afrag, B, ldb, alpha, beta, \
-                           C, ldc, xm);                                                          \
-        break;                                                                                   \
       case 933:  /* diagnostic: no MFMAs (wrong results) */                                    \
         hipLaunchKernelGGL((bsr32_f32_grp_kernel<W_, 3, 3, true>), grid, dim3(64 * W_), 0,       \
                            ctx->stream, mb, n, item_ptr, rows, wmask, afrag, B, ldb, alpha, beta, \
