@@ -343,7 +343,9 @@ spmm_status_t spmm_bsrmm_grouped_f32(spmm_handle_t handle, int mb, int kb, int n
                                      spmm_order_t orderC);
 
 /* Forgets the handle's record of a group-analysis buffer, bs 16 or bs 32 (before
- * freeing it). */
+ * freeing it). spmm_bsr_group_release is the same call under a block-size-neutral
+ * name; spmm_bsr16_group_release stays for the bs 16 stream's first users. */
+spmm_status_t spmm_bsr_group_release(spmm_handle_t handle, const void* buffer);
 spmm_status_t spmm_bsr16_group_release(spmm_handle_t handle, const void* buffer);
 
 /* fp16 A and B (IEEE binary16 bit patterns), fp32 accumulate and fp32 C.

@@ -280,4 +280,8 @@ spmm_status_t spmm_bsr16_group_release(spmm_handle_t handle, const void* buffer)
   return SPMM_STATUS_SUCCESS;
 }
 
+spmm_status_t spmm_bsr_group_release(spmm_handle_t handle, const void* buffer) {
+  return spmm_bsr16_group_release(handle, buffer);
+}
+
 }  // extern "C"

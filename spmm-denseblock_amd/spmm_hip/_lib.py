@@ -99,6 +99,7 @@ _PROTOS = {
     "spmm_bsrmm_grouped_f16": (c_int, [_P, c_int, c_int, c_int, _P, c_float, _P, c_int, c_int,
                                        c_float, _P, c_int, c_int]),
     "spmm_bsr16_group_release": (c_int, [_P, _P]),
+    "spmm_bsr_group_release": (c_int, [_P, _P]),
     "spmm_bsr32_group_analysis_f32": (c_int, [_P, c_int, c_int, c_int, c_int, _P, _P, _P, _P,
                                               POINTER(c_size_t)]),
     "spmm_bsrmm_grouped_f32": (c_int, [_P, c_int, c_int, c_int, _P, c_float, _P, c_int, c_int,

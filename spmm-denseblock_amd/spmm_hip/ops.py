@@ -381,7 +381,7 @@ class GroupedBsr32:
 
     def close(self) -> None:
         if getattr(self, "buffer", None) is not None:
-            lib().spmm_bsr16_group_release(self.h.raw, _ptr(self.buffer))
+            lib().spmm_bsr_group_release(self.h.raw, _ptr(self.buffer))
             self.buffer = None
 
 
