@@ -1171,3 +1171,41 @@ def test_bsrmm_grouped_f32_checks(device):
         grp.mm(B, kb=7, n=128, ldb=128, C=C, ldc=128)
     assert e.value.status == INVALID_VALUE
     g16.close()
+
+
+def test_grouped_streams_random_shapes(oracle, device):
+    """Both grouped streams over random small shapes: mb from 1 (a single, partial
+    group) to 45, every W, block rows with no blocks, n at and around the tile
+    widths, beta != 0; against the f64 oracle (bs 32 also bit-identical to
+    spmm_bsrmm_ex_f32 where both run row-major)."""
+    ops = _ops()
+    rng = np.random.default_rng(2024)
+    for case in range(16):
+        bs = 16 if case % 2 == 0 else 32
+        W = int(rng.choice([2, 4, 8] if bs == 16 else [2, 4]))
+        mb = int(rng.integers(1, 46))
+        kb = int(rng.integers(1, 50))
+        n = int(rng.choice([8, 16, 120, 256, 264]) if bs == 16 else rng.choice([4, 64, 128, 132, 256]))
+        rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, float(rng.uniform(0.05, 0.6)))
+        half = bs == 16
+        vv = v.astype(np.float16) if half else v
+        Bd = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float16 if half else np.float32)
+        C0 = rng.uniform(-1, 1, (mb * bs, n)).astype(np.float32)
+        drp, dci, dv, dB, dC = _dev(rp, ci, vv, Bd.reshape(-1), C0.reshape(-1))
+        G = ops.GroupedBsr16 if half else ops.GroupedBsr32
+        grp = G(drp, dci, dv, mb=mb, group_rows=W)
+        grp.mm(dB, kb=kb, n=n, ldb=n, C=dC, ldc=n, alpha=1.5, beta=0.5)
+        torch.cuda.synchronize()
+        got = dC.cpu().numpy().reshape(mb * bs, n)
+        ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, vv, Bd, n, 0, half=half)
+        ref = 1.5 * ref + 0.5 * C0.astype(np.float64)
+        absd = 1.5 * absd + 0.5 * np.abs(C0.astype(np.float64))
+        what = f"case {case}: bs {bs} W {W} mb {mb} kb {kb} n {n}"
+        assert_normwise(got, ref, absd, TOL_F16_ACC if half else TOL_F32, what)
+        if not half:
+            Cd = torch.from_numpy(C0.copy()).to(device)
+            ops.bsrmm(drp, dci, dv, torch.from_numpy(Bd).to(device), mb=mb, kb=kb, n=n, bs=32,
+                      ldb=n, C=Cd, ldc=n, alpha=1.5, beta=0.5)
+            torch.cuda.synchronize()
+            assert torch.equal(Cd.cpu(), torch.from_numpy(got)), what + ": differs from bsrmm"
+        grp.close()
