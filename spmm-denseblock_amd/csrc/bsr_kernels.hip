@@ -2579,7 +2579,7 @@ __device__ __forceinline__ void slots_while(std::integer_sequence<int, S...>, F&
   (void)(f(std::integral_constant<int, S>{}) && ...);
 }
 
-template <int W, int P, bool CROW, int OCC = 0, bool SR = true>
+template <int W, int P, bool CROW, int OCC = 0, int IPB = 1>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
 void bsr16_f16_grp_kernel(
     int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
@@ -2623,11 +2623,11 @@ void bsr16_f16_grp_kernel(
 #pragma unroll
   for (int t = 0; t < kT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int nis = 0;               // vector-memory operations issued by this wave
-  int rrow[kCpw], rstamp = -64;  // !SR: row indices of the next item to issue (in flight)
-  int ra[kCpw], rb[kCpw];    // SR: the same as scalars (rows 2 cc and 2 cc + 1 of copy cc)
+  int nis = 0;  // vector-memory operations issued by this wave
+  // row indices of the next IPB items to issue (scalars; rows 2 cc and 2 cc + 1 of copy cc)
+  int ra[IPB][kCpw], rb[IPB][kCpw];
   typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
-  u32x2a fan[P];             // A fragments in flight (asm-only registers)
+  u32x2a fan[P];  // A fragments in flight (asm-only registers)
   int stamp[P];
 #pragma unroll
   for (int s = 0; s < P; ++s) {
@@ -2635,56 +2635,33 @@ void bsr16_f16_grp_kernel(
     stamp[s] = -64;
   }
 #pragma unroll
-  for (int j = 0; j < kCpw; ++j) rrow[j] = ra[j] = rb[j] = -1;
+  for (int i = 0; i < IPB; ++i)
+#pragma unroll
+    for (int j = 0; j < kCpw; ++j) ra[i][j] = rb[i][j] = -1;
   const int ilast = max(i1 - 1, i0);
-  // row indices of item `it` (clamped): lane L of copy j needs rows[it][2 (w kCpw + j) + L / 32].
-  // SR: scalar loads (lgkmcnt). Vector loads retire in issue order behind the copies
-  // issued before them, so waiting for a vector row load one item ahead also waited for
-  // every copy before it: one item in flight during the MFMAs whatever P was. Scalar
-  // loads keep the P - 1 items of copies in flight (the grouped stream).
+  // row indices of items it .. it + IPB - 1 (clamped) by scalar loads (lgkmcnt): lane L of
+  // copy j needs rows[it][2 (w kCpw + j) + L / 32]. Vector loads retire in issue order
+  // behind the copies issued before them, so waiting for a vector row load one item ahead
+  // also waited for every copy before it: one item in flight during the MFMAs whatever P
+  // was (the grouped stream).
   auto load_rows = [&](int it) {
-    const int* src = rows + (size_t)min(it, ilast) * 16;
-    if constexpr (SR) {
-      const int* s2 = src + 2 * w * kCpw;
+#pragma unroll
+    for (int i = 0; i < IPB; ++i) {
+      const int* s2 = rows + (size_t)min(it + i, ilast) * 16 + 2 * w * kCpw;
 #pragma unroll
       for (int j = 0; j < kCpw; ++j) {
-        ra[j] = s2[2 * j];
-        rb[j] = s2[2 * j + 1];
+        ra[i][j] = s2[2 * j];
+        rb[i][j] = s2[2 * j + 1];
       }
-      return;
     }
-#pragma unroll
-    for (int j = 0; j < kCpw; ++j)
-      asm volatile("global_load_dword %0, %1, %2"
-                   : "=&v"(rrow[j])
-                   : "v"(4u * (unsigned)(2 * (w * kCpw + j) + (lane >> 5))), "s"(src)
-                   : "memory");
-    nis += kCpw;
-    rstamp = nis;
   };
-  // item `it` into stage slot `s`: its row indices landed, its copies and A fragment issued
-  auto issue = [&](int it, int s) {
-    int rw[kCpw];
-    if constexpr (SR) {
-#pragma unroll
-      for (int j = 0; j < kCpw; ++j) rw[j] = (lane >> 5) ? rb[j] : ra[j];
-    } else if constexpr (kCpw == 1)
-      asm volatile(SPMM_VM_LADDER("%1") "v_mov_b32 %0, %2"
-                   : "=&v"(rw[0]) : "s"(nis - rstamp), "v"(rrow[0]) : "scc", "memory");
-    else if constexpr (kCpw == 2)
-      asm volatile(SPMM_VM_LADDER("%2") "v_mov_b32 %0, %3\n\tv_mov_b32 %1, %4"
-                   : "=&v"(rw[0]), "=&v"(rw[1])
-                   : "s"(nis - rstamp), "v"(rrow[0]), "v"(rrow[1]) : "scc", "memory");
-    else
-      asm volatile(SPMM_VM_LADDER("%4")
-                   "v_mov_b32 %0, %5\n\tv_mov_b32 %1, %6\n\tv_mov_b32 %2, %7\n\tv_mov_b32 %3, %8"
-                   : "=&v"(rw[0]), "=&v"(rw[1]), "=&v"(rw[2]), "=&v"(rw[3])
-                   : "s"(nis - rstamp), "v"(rrow[0]), "v"(rrow[1]), "v"(rrow[2]), "v"(rrow[3])
-                   : "scc", "memory");
+  // item `it` (rows ra / rb [i]) into stage slot `s`: its copies and A fragment issued
+  auto issue = [&](int it, int s, int i) {
     char* const stage = smem + s * kStage;
 #pragma unroll
     for (int j = 0; j < kCpw; ++j) {
-      const char* be = rw[j] >= 0 ? reinterpret_cast<const char*>(B) + (size_t)rw[j] * ldb2 : zrow;
+      const int rw = (lane >> 5) ? rb[i][j] : ra[i][j];
+      const char* be = rw >= 0 ? reinterpret_cast<const char*>(B) + (size_t)rw * ldb2 : zrow;
       __builtin_amdgcn_global_load_lds((gbl_void_t)(be + boffr[j]),
                                        (lds_void_t)(stage + 1024 * (w * kCpw + j)), 16, 0, 0);
     }
@@ -2694,65 +2671,86 @@ void bsr16_f16_grp_kernel(
     nis += kCpw + 1;
     stamp[s] = nis;
   };
+  // the 16 transposed reads of slot s and the item's 16 MFMAs
+  auto mfma_item = [&](f16x4 fa, auto sc) {
+    constexpr int s = decltype(sc)::value;
+    f16x4 fb[16];
+    asm volatile(
+        "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]), "=&v"(fb[5]),
+          "=&v"(fb[6]), "=&v"(fb[7])
+        : "v"(tra[0]), "v"(tra[1]), "v"(tra[2]), "v"(tra[3]), "v"(tra[4]), "v"(tra[5]),
+          "v"(tra[6]), "v"(tra[7]), "n"(s * kStage)
+        : "memory");
+    asm volatile(
+        "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+        "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(fb[8]), "=&v"(fb[9]), "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]),
+          "=&v"(fb[13]), "=&v"(fb[14]), "=&v"(fb[15])
+        : "v"(tra[8]), "v"(tra[9]), "v"(tra[10]), "v"(tra[11]), "v"(tra[12]), "v"(tra[13]),
+          "v"(tra[14]), "v"(tra[15]), "n"(s * kStage)
+        : "memory");
+#pragma unroll
+    for (int t = 0; t < kT; ++t)
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[t], 0, 0, 0);
+  };
 
   if (i0 < i1) {
-    load_rows(i0);
+    static_assert(P % IPB == 0 && P >= 2 * IPB, "whole barrier groups in the ring");
+    // prologue: items i0 .. i0 + P - IPB - 1 in flight, the rows of the next IPB loaded
 #pragma unroll
-    for (int q = 0; q + 1 < P; ++q) {
-      issue(i0 + q, q);
-      load_rows(i0 + q + 1);
+    for (int q = 0; q + IPB < P; q += IPB) {
+      load_rows(i0 + q);
+#pragma unroll
+      for (int i = 0; i < IPB; ++i) issue(i0 + q + i, q + i, i);
     }
-    // one item in slot s (s a constant: the fan[] / stage indices must be static)
+    load_rows(i0 + P - IPB);
+    // IPB items in slots S IPB .. S IPB + IPB - 1 (static: the fan[] / stage indices)
     auto step = [&](int it, auto sc) {
-      constexpr int s = decltype(sc)::value;
-        // this wave's copies of item `it` and its A fragment landed; then every wave's
-        f16x4 fa;
-        {
-          u32x2a y;
-          asm volatile(SPMM_VM_LADDER("%1") "v_mov_b64 %0, %2"
-                       : "=&v"(y) : "s"(nis - stamp[s]), "v"(fan[s]) : "scc", "memory");
-          fa = __builtin_bit_cast(f16x4, y);
-        }
-        __builtin_amdgcn_s_barrier();
-        // slot (s + P - 1) % P was read by every wave in the previous item: refill it
-        issue(it + P - 1, (s + P - 1) % P);
-        if constexpr (!SR) load_rows(it + P);
-        f16x4 fb[16];
-        asm volatile(
-            "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]),
-              "=&v"(fb[5]), "=&v"(fb[6]), "=&v"(fb[7])
-            : "v"(tra[0]), "v"(tra[1]), "v"(tra[2]), "v"(tra[3]), "v"(tra[4]), "v"(tra[5]),
-              "v"(tra[6]), "v"(tra[7]), "n"(s * kStage)
-            : "memory");
-        asm volatile(
-            "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
-            "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(fb[8]), "=&v"(fb[9]), "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]),
-              "=&v"(fb[13]), "=&v"(fb[14]), "=&v"(fb[15])
-            : "v"(tra[8]), "v"(tra[9]), "v"(tra[10]), "v"(tra[11]), "v"(tra[12]), "v"(tra[13]),
-              "v"(tra[14]), "v"(tra[15]), "n"(s * kStage)
-            : "memory");
-        // after the transposed reads: their asm lgkmcnt(0) waits would also wait for it
-        if constexpr (SR) load_rows(it + P);
+      constexpr int S = decltype(sc)::value;
+      constexpr int s0 = S * IPB;
+      // this wave's copies and A fragments of the IPB items landed (in issue order: the
+      // last slot's count covers the others); then every wave's, at the barrier
+      f16x4 fa[IPB];
+      if constexpr (IPB == 1) {
+        u32x2a y;
+        asm volatile(SPMM_VM_LADDER("%1") "v_mov_b64 %0, %2"
+                     : "=&v"(y) : "s"(nis - stamp[s0]), "v"(fan[s0]) : "scc", "memory");
+        fa[0] = __builtin_bit_cast(f16x4, y);
+      } else {
+        u32x2a y0, y1;
+        asm volatile(SPMM_VM_LADDER("%2") "v_mov_b64 %0, %3\n\tv_mov_b64 %1, %4"
+                     : "=&v"(y0), "=&v"(y1)
+                     : "s"(nis - stamp[s0 + 1]), "v"(fan[s0]), "v"(fan[s0 + 1])
+                     : "scc", "memory");
+        fa[0] = __builtin_bit_cast(f16x4, y0);
+        fa[1] = __builtin_bit_cast(f16x4, y1);
+      }
+      __builtin_amdgcn_s_barrier();
+      // the IPB slots before s0 were read by every wave in the previous step: refill them
 #pragma unroll
-        for (int t = 0; t < kT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[t], 0, 0, 0);
+      for (int i = 0; i < IPB; ++i) issue(it + P - IPB + i, (s0 + P - IPB + i) % P, i);
+      mfma_item(fa[0], std::integral_constant<int, s0>{});
+      // after the first transposed reads: their asm lgkmcnt(0) would also wait for these
+      load_rows(it + P);
+      if constexpr (IPB == 2) {
+        if (it + 1 < i1) mfma_item(fa[1], std::integral_constant<int, s0 + 1>{});
+      }
     };
     // whole rounds of P items, then the last < P with no edge back into the loop: a
     // break out of the middle of an unrolled round, merged by the compiler with the
@@ -2761,14 +2759,14 @@ void bsr16_f16_grp_kernel(
     // ISA check, tests/test_isa_waits.py, is path-insensitive and so is the allocator)
     int base = i0;
     for (; base + P <= i1; base += P)
-      slots_while(std::make_integer_sequence<int, P>{}, [&](auto sc) {
-        step(base + decltype(sc)::value, sc);
+      slots_while(std::make_integer_sequence<int, P / IPB>{}, [&](auto sc) {
+        step(base + IPB * decltype(sc)::value, sc);
         return true;
       });
     // uniform over the workgroup: every wave runs the same items
-    slots_while(std::make_integer_sequence<int, P>{}, [&](auto sc) {
-      if (base + decltype(sc)::value >= i1) return false;
-      step(base + decltype(sc)::value, sc);
+    slots_while(std::make_integer_sequence<int, P / IPB>{}, [&](auto sc) {
+      if (base + IPB * decltype(sc)::value >= i1) return false;
+      step(base + IPB * decltype(sc)::value, sc);
       return true;
     });
   }
@@ -2777,8 +2775,6 @@ void bsr16_f16_grp_kernel(
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int s = 0; s < P; ++s) asm volatile("" : : "v"(fan[s]));
-#pragma unroll
-  for (int j = 0; j < kCpw; ++j) asm volatile("" : : "v"(rrow[j]));
   if (br >= mb) return;
 #pragma unroll
   for (int t = 0; t < kT; ++t) {
@@ -3753,7 +3749,7 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   const _Float16* B = reinterpret_cast<const _Float16*>(B16);
   const int slot = timing_begin(ctx);
   const dim3 grid(ngroups, (n + 255) / 256);
-  // stages and occupancy hint: P * 10 + OCC, + 100 for vector row-index loads (TUNING builds:
+  // stages and occupancy hint: P * 10 + OCC, + 200 for two items per barrier (TUNING builds:
   // SPMM_GRP_VARIANT; SPMM_GRP_XM groups per XCD chunk)
   // chunks of 32 block rows per XCD, as the drop-in stream (xcd_block_row): neighbouring
   // groups share B rows in one L2 (W = 4: 3.10 -> 2.87 ms, profiles/r04e/grp_sweep.jsonl)
@@ -3768,11 +3764,11 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
       const char* e = getenv("SPMM_GRP_XM");
       return e ? atoi(e) : -1;
     }();
-    // (3, 4) is not offered: at W = 4 the allocator spills the A fragments in flight
-    // (tools/isa_vmcnt.py --inflight; it faulted on the GPU)
+    // (3, 4) and (4, 4) with two items per barrier are not offered: at W = 4 the allocator
+    // spills the A fragments in flight (tools/isa_vmcnt.py --inflight; the first faulted)
     switch (env) {
       case 30: case 33: case 32: case 42: case 43: case 52: case 53: case 23: case 24:
-      case 130: case 133:
+      case 243: case 262: case 263:
         gv = env;
         break;
       default:
@@ -3781,36 +3777,37 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
     if (env_xm >= 0) xm = env_xm;
   }
 #endif
-#define GRP_LAUNCH1(W_, P_, O_, SR_)                                                             \
+#define GRP_LAUNCH1(W_, P_, O_, IPB_)                                                            \
   do {                                                                                           \
     if (crow)                                                                                    \
-      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_, SR_>), grid, dim3(64 * W_), 0,  \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_, IPB_>), grid, dim3(64 * W_), 0, \
                          ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc, \
                          xm);                                                                    \
     else                                                                                         \
-      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_, SR_>), grid, dim3(64 * W_), 0, \
-                         ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc, \
-                         xm);                                                                    \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_, IPB_>), grid, dim3(64 * W_),   \
+                         0, ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C,   \
+                         ldc, xm);                                                               \
   } while (0)
 #ifdef SPMM_TUNING
 #define GRP_LAUNCH(W_)                                                                           \
   do {                                                                                           \
     switch (gv) {                                                                                \
-      case 30: GRP_LAUNCH1(W_, 3, 0, true); break;                                               \
-      case 32: GRP_LAUNCH1(W_, 3, 2, true); break;                                               \
-      case 42: GRP_LAUNCH1(W_, 4, 2, true); break;                                               \
-      case 43: GRP_LAUNCH1(W_, 4, 3, true); break;                                               \
-      case 52: GRP_LAUNCH1(W_, 5, 2, true); break;                                               \
-      case 53: GRP_LAUNCH1(W_, 5, 3, true); break;                                               \
-      case 23: GRP_LAUNCH1(W_, 2, 3, true); break;                                               \
-      case 24: GRP_LAUNCH1(W_, 2, 4, true); break;                                               \
-      case 130: GRP_LAUNCH1(W_, 3, 0, false); break;                                             \
-      case 133: GRP_LAUNCH1(W_, 3, 3, false); break;                                             \
-      default: GRP_LAUNCH1(W_, 3, 3, true); break;                                               \
+      case 30: GRP_LAUNCH1(W_, 3, 0, 1); break;                                                  \
+      case 32: GRP_LAUNCH1(W_, 3, 2, 1); break;                                                  \
+      case 42: GRP_LAUNCH1(W_, 4, 2, 1); break;                                                  \
+      case 43: GRP_LAUNCH1(W_, 4, 3, 1); break;                                                  \
+      case 52: GRP_LAUNCH1(W_, 5, 2, 1); break;                                                  \
+      case 53: GRP_LAUNCH1(W_, 5, 3, 1); break;                                                  \
+      case 23: GRP_LAUNCH1(W_, 2, 3, 1); break;                                                  \
+      case 24: GRP_LAUNCH1(W_, 2, 4, 1); break;                                                  \
+      case 243: GRP_LAUNCH1(W_, 4, 3, 2); break;  /* two items per barrier */                    \
+      case 262: GRP_LAUNCH1(W_, 6, 2, 2); break;                                                 \
+      case 263: GRP_LAUNCH1(W_, 6, 3, 2); break;                                                 \
+      default: GRP_LAUNCH1(W_, 3, 3, 1); break;                                                  \
     }                                                                                            \
   } while (0)
 #else
-#define GRP_LAUNCH(W_) GRP_LAUNCH1(W_, 3, 3, true)
+#define GRP_LAUNCH(W_) GRP_LAUNCH1(W_, 3, 3, 1)
 #endif
   (void)gv;
   if (W == 8) GRP_LAUNCH(8);
