@@ -2584,7 +2584,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OC
 void bsr16_f16_grp_kernel(
     int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
     const unsigned* __restrict__ afrag, const _Float16* __restrict__ B, int ldb, float alpha,
-    float beta, float* __restrict__ C, int ldc, int xm) {
+    float beta, float* __restrict__ C, int ldc, int xm, int ngroups, int ntt) {
   static_assert(W == 2 || W == 4 || W == 8, "waves per group");
   static_assert(P >= 2 && P <= 6, "stages");
   constexpr int COLS = 256, kRowB = 512, kCh = 32, kT = 16, kStage = 16 * kRowB;
@@ -2594,10 +2594,23 @@ void bsr16_f16_grp_kernel(
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int g = lane >> 4, r16 = lane & 15;
-  // neighbouring groups share B rows: chunks of xm groups per XCD keep them in one L2
-  const int grp = xcd_block_row(blockIdx.x, gridDim.x, xm);
+  // neighbouring groups share B rows: chunks of xm groups per XCD keep them in one L2.
+  // ntt > 0 (tiles together): a 1-D grid of 8 ceil(ngroups / 8) ntt workgroups in which
+  // the ntt column tiles of a group are consecutive on one XCD (dispatch puts workgroup L on
+  // XCD L % 8), so the later tiles read the group's A fragments from that L2
+  int grp, tile;
+  if (ntt > 0) {
+    const int L = blockIdx.x, x = L & 7, i = L >> 3;
+    const int b = x + 8 * (i / ntt);
+    if (b >= ngroups) return;  // the grid's padding (whole workgroup)
+    grp = xcd_block_row(b, ngroups, xm);
+    tile = i % ntt;
+  } else {
+    grp = xcd_block_row(blockIdx.x, gridDim.x, xm);
+    tile = blockIdx.y;
+  }
   const int br = grp * W + w;
-  const int jt = blockIdx.y * COLS;
+  const int jt = tile * COLS;
   const int i0 = item_ptr[grp], i1 = item_ptr[grp + 1];
   const unsigned lds0 = lds_addr(smem);
   const size_t ldb2 = (size_t)ldb * 2;
@@ -3748,14 +3761,19 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   const _Float16* B = reinterpret_cast<const _Float16*>(B16);
   const int slot = timing_begin(ctx);
-  const dim3 grid(ngroups, (n + 255) / 256);
+  const int ntiles = (n + 255) / 256;
   // stages and occupancy hint: P * 10 + OCC, + 200 for two items per barrier (TUNING builds:
   // SPMM_GRP_VARIANT; SPMM_GRP_XM groups per XCD chunk)
   // chunks of 32 block rows per XCD, as the drop-in stream (xcd_block_row): neighbouring
   // groups share B rows in one L2 (W = 4: 3.10 -> 2.87 ms, profiles/r04e/grp_sweep.jsonl)
-  int gv = 33, xm = 32 / W;
+  int gv = 33, xm = 32 / W, tt = 0;
 #ifdef SPMM_TUNING
   {
+    static const int env_tt = [] {
+      const char* e = getenv("SPMM_GRP_TT");
+      return e ? atoi(e) : -1;
+    }();
+    if (env_tt >= 0) tt = env_tt;
     static const int env = [] {
       const char* e = getenv("SPMM_GRP_VARIANT");
       return e ? atoi(e) : 0;
@@ -3777,16 +3795,19 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
     if (env_xm >= 0) xm = env_xm;
   }
 #endif
+  const int ntt = tt && ntiles > 1 ? ntiles : 0;
+  const dim3 grid = ntt ? dim3((unsigned)(8 * ((ngroups + 7) / 8) * ntt), 1)
+                        : dim3((unsigned)ngroups, (unsigned)ntiles);
 #define GRP_LAUNCH1(W_, P_, O_, IPB_)                                                            \
   do {                                                                                           \
     if (crow)                                                                                    \
       hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_, IPB_>), grid, dim3(64 * W_), 0, \
                          ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc, \
-                         xm);                                                                    \
+                         xm, ngroups, ntt);                                                      \
     else                                                                                         \
       hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_, IPB_>), grid, dim3(64 * W_),   \
                          0, ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C,   \
-                         ldc, xm);                                                               \
+                         ldc, xm, ngroups, ntt);                                                 \
   } while (0)
 #ifdef SPMM_TUNING
 #define GRP_LAUNCH(W_)                                                                           \
