@@ -3766,7 +3766,10 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   // SPMM_GRP_VARIANT; SPMM_GRP_XM groups per XCD chunk)
   // chunks of 32 block rows per XCD, as the drop-in stream (xcd_block_row): neighbouring
   // groups share B rows in one L2 (W = 4: 3.10 -> 2.87 ms, profiles/r04e/grp_sweep.jsonl)
-  int gv = 33, xm = 32 / W, tt = 0;
+  // tiles together (ntt): a group's column tiles consecutive on one XCD, the later ones
+  // reading the A fragments from L2: products stand-in 2.83 -> 2.62 ms, RCM 6.73 -> 6.38
+  // (profiles/r04n/lines.jsonl)
+  int gv = 33, xm = 32 / W, tt = 1;
 #ifdef SPMM_TUNING
   {
     static const int env_tt = [] {
