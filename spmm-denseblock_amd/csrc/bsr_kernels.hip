@@ -2565,9 +2565,12 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 //    next copies overwrite, then 16 transposed reads and 16 MFMAs per wave;
 //  * an item's row indices come by scalar loads one item ahead (a vector load
 //    would retire behind the copies issued before it and hold the ring to one
-//    item in flight), and groups go to the XCDs in chunks of 32 block rows.
-// Release form: W = 4, P = 3, three waves per SIMD: products stand-in K = 512
-// 2.87 ms against 3.77 for the column stream (profiles/r04e/grp_sweep.jsonl).
+//    item in flight), and groups go to the XCDs in chunks of 32 block rows,
+//    the column tiles of a group consecutive on one XCD (the later tiles read
+//    the A fragments from L2).
+// Release form: W = 4, P = 3, three waves per SIMD, one item per barrier:
+// products stand-in K = 512 2.44-2.62 ms against 3.77 for the column stream
+// (profiles/r04n/, profiles/r04o/).
 // Non-finite B: a B row of the item meets the W block rows' A fragments, zeros
 // included, so an inf / NaN in it reaches every row of the group whenever one
 // of its block rows holds a value in that column (the grouped contract,
