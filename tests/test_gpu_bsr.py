@@ -1209,3 +1209,27 @@ def test_grouped_streams_random_shapes(oracle, device):
             torch.cuda.synchronize()
             assert torch.equal(Cd.cpu(), torch.from_numpy(got)), what + ": differs from bsrmm"
         grp.close()
+
+
+@pytest.mark.parametrize("bs", [16, 32])
+def test_grouped_streams_empty_matrix(device, bs):
+    """A matrix with block rows but no blocks: the analysis makes no items and the product
+    leaves C = beta C (the padding of every group empty); mb = 0 is a quick success."""
+    ops = _ops()
+    mb, kb, n = 7, 5, 128
+    rp = np.zeros(mb + 1, np.int32)
+    ci = np.zeros(0, np.int32)
+    v = np.zeros(0, np.float16 if bs == 16 else np.float32)
+    drp, dci = torch.from_numpy(rp).to(device), torch.from_numpy(ci).to(device)
+    dv = torch.from_numpy(v).to(device)
+    G = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
+    grp = G(drp, dci, dv, mb=mb)
+    B = torch.ones((kb * bs, n), dtype=torch.float16 if bs == 16 else torch.float32, device=device)
+    C = torch.full((mb * bs, n), 2.0, device=device)
+    grp.mm(B, kb=kb, n=n, ldb=n, C=C, ldc=n, alpha=1.0, beta=0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(C, torch.full_like(C, 1.0))
+    grp.close()
+    g0 = G(torch.zeros(1, dtype=torch.int32, device=device), dci, dv, mb=0)
+    g0.mm(B, kb=kb, n=n, ldb=n, C=C, ldc=n)
+    g0.close()
