@@ -72,6 +72,14 @@ def main():
                 return C
             bad += check("bsr32 fp32 K=128 (analysed column stream)", run_an, reps)
             del masks, vcol
+            g32 = ops.GroupedBsr32(brp, bci, bval, mb=mb, group_rows=2)
+
+            def run_g32():
+                g32.mm(B, kb=mb, n=K, ldb=K, C=C, ldc=K)
+                return C
+            bad += check("bsr32 fp32 K=128 (grouped stream, 2 block rows)", run_g32, reps)
+            g32.close()
+            del g32
         else:
             bv16, B16 = bval.half(), B.half()
             del bval, B
