@@ -1706,7 +1706,7 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const _Float16* __restrict__ val, const _Float16* __restrict__ B, int ldb, float alpha,
     float beta, float* __restrict__ C, int ldc, const int* __restrict__ order,
-    const unsigned* __restrict__ masks = nullptr) {
+    const unsigned* __restrict__ masks = nullptr, int ntt = 0) {
   // COLS: output columns per wave (the launcher uses 256). 512 makes a stage row one whole
   // 1-KB B row and serves all 512 columns with one A copy and one walk per block row; 128
   // quarters the stage. Both pass the parity subset and lose on the products stand-in, K =
@@ -1737,8 +1737,17 @@ __global__ __launch_bounds__(64) void bsr16_f16_cs_kernel(
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int lane = threadIdx.x;
   const int g = lane >> 4, r16 = lane & 15, h = lane >> 5;
-  const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
-  const int jt = blockIdx.y * COLS;
+  // ntt > 0 (tiles together; TUNING A/B): a 1-D grid in which the ntt column tiles of a
+  // block row are consecutive on one XCD (the grouped stream's mapping)
+  int bslot = blockIdx.x, tile = blockIdx.y;
+  if (ntt > 0) {
+    const int L = blockIdx.x, i = L >> 3;
+    bslot = (L & 7) + 8 * (i / ntt);
+    if (bslot >= mb) return;  // the grid's padding
+    tile = i % ntt;
+  }
+  const int br = order ? order[bslot] : xcd_block_row(bslot, mb, 32);
+  const int jt = tile * COLS;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const unsigned lds0 = lds_addr(smem);
   const unsigned abuf = lds0 + kAbuf;
@@ -3503,16 +3512,26 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
         timing_end(ctx, slot);
         return st;
       }
+#ifdef SPMM_TUNING
+      static const int env_tt = [] {
+        const char* e = getenv("SPMM_CS16_TT");  // TUNING builds only
+        return e ? atoi(e) : 0;
+      }();
+      const int ntt = env_tt && gc.y > 1 ? (int)gc.y : 0;
+#else
+      constexpr int ntt = 0;
+#endif
+      const dim3 gg = ntt ? dim3((unsigned)(8 * ((mb + 7) / 8) * ntt), 1) : gc;
 #define CS16_LAUNCH(...)                                                                         \
   do {                                                                                           \
     if (crow)                                                                                    \
-      hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, 2, 4, 0, 48, __VA_ARGS__>), gc, dim3(64), 0, \
+      hipLaunchKernelGGL((bsr16_f16_cs_kernel<true, 2, 4, 0, 48, __VA_ARGS__>), gg, dim3(64), 0, \
                          ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
-                         ord, masks);                                                            \
+                         ord, masks, ntt);                                                       \
     else                                                                                         \
-      hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, 2, 4, 0, 48, __VA_ARGS__>), gc, dim3(64),   \
+      hipLaunchKernelGGL((bsr16_f16_cs_kernel<false, 2, 4, 0, 48, __VA_ARGS__>), gg, dim3(64),   \
                          0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C,     \
-                         ldc, ord, masks);                                                       \
+                         ldc, ord, masks, ntt);                                                  \
   } while (0)
       if (msk) CS16_LAUNCH(true, true, 256, true);
       else if (lv == kBsr16F16Cs) CS16_LAUNCH(true, true);
