@@ -2591,7 +2591,7 @@ __device__ __forceinline__ void slots_while(std::integer_sequence<int, S...>, F&
   (void)(f(std::integral_constant<int, S>{}) && ...);
 }
 
-template <int W, int P, bool CROW, int OCC = 0, int IPB = 1>
+template <int W, int P, bool CROW, int OCC = 0, int IPB = 1, bool AL = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
 void bsr16_f16_grp_kernel(
     int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
@@ -2602,7 +2602,11 @@ void bsr16_f16_grp_kernel(
   constexpr int COLS = 256, kRowB = 512, kCh = 32, kT = 16, kStage = 16 * kRowB;
   constexpr int kCpw = 8 / W;  // 1-KB copies per wave per item (8 per item)
   constexpr int kSw = 2;       // FLR swizzle: chunk c of row R at 16-B slot (c + 2R) & 31
-  __shared__ __attribute__((aligned(16))) char smem[P * kStage];
+  // AL (TUNING A/B): the W waves' A fragments of an item come by LDS-DMA beside its B rows
+  // (1 KB per copy: two waves' fragments), W / 2 copies per item instead of W 8-B loads
+  static_assert(!AL || IPB == 1, "fragments through LDS: one item per barrier");
+  constexpr int kSlot = kStage + (AL ? W * 512 : 0);  // bytes per ring slot
+  __shared__ __attribute__((aligned(16))) char smem[P * kSlot];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int g = lane >> 4, r16 = lane & 15;
@@ -2682,7 +2686,7 @@ void bsr16_f16_grp_kernel(
   };
   // item `it` (rows ra / rb [i]) into stage slot `s`: its copies and A fragment issued
   auto issue = [&](int it, int s, int i) {
-    char* const stage = smem + s * kStage;
+    char* const stage = smem + s * kSlot;
 #pragma unroll
     for (int j = 0; j < kCpw; ++j) {
       const int rw = (lane >> 5) ? rb[i][j] : ra[i][j];
@@ -2690,10 +2694,21 @@ void bsr16_f16_grp_kernel(
       __builtin_amdgcn_global_load_lds((gbl_void_t)(be + boffr[j]),
                                        (lds_void_t)(stage + 1024 * (w * kCpw + j)), 16, 0, 0);
     }
-    const unsigned* fsrc = afrag + ((size_t)min(it, ilast) * W + w) * 128;
-    asm volatile("global_load_dwordx2 %0, %1, %2"
-                 : "=&v"(fan[s]) : "v"(8u * (unsigned)lane), "s"(fsrc) : "memory");
-    nis += kCpw + 1;
+    if constexpr (AL) {
+      // waves 0 .. W / 2 - 1: the fragments of waves 2 w and 2 w + 1 (lanes 0-31 / 32-63)
+      if (w < W / 2) {
+        const unsigned* fsrc = afrag + ((size_t)min(it, ilast) * W + 2 * w) * 128 + 4 * lane;
+        __builtin_amdgcn_global_load_lds((gbl_void_t)fsrc,
+                                         (lds_void_t)(stage + kStage + 1024 * w), 16, 0, 0);
+        nis += 1;
+      }
+      nis += kCpw;
+    } else {
+      const unsigned* fsrc = afrag + ((size_t)min(it, ilast) * W + w) * 128;
+      asm volatile("global_load_dwordx2 %0, %1, %2"
+                   : "=&v"(fan[s]) : "v"(8u * (unsigned)lane), "s"(fsrc) : "memory");
+      nis += kCpw + 1;
+    }
     stamp[s] = nis;
   };
   // the 16 transposed reads of slot s and the item's 16 MFMAs
@@ -2713,7 +2728,7 @@ void bsr16_f16_grp_kernel(
         : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]), "=&v"(fb[4]), "=&v"(fb[5]),
           "=&v"(fb[6]), "=&v"(fb[7])
         : "v"(tra[0]), "v"(tra[1]), "v"(tra[2]), "v"(tra[3]), "v"(tra[4]), "v"(tra[5]),
-          "v"(tra[6]), "v"(tra[7]), "n"(s * kStage)
+          "v"(tra[6]), "v"(tra[7]), "n"(s * kSlot)
         : "memory");
     asm volatile(
         "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
@@ -2728,7 +2743,7 @@ void bsr16_f16_grp_kernel(
         : "=&v"(fb[8]), "=&v"(fb[9]), "=&v"(fb[10]), "=&v"(fb[11]), "=&v"(fb[12]),
           "=&v"(fb[13]), "=&v"(fb[14]), "=&v"(fb[15])
         : "v"(tra[8]), "v"(tra[9]), "v"(tra[10]), "v"(tra[11]), "v"(tra[12]), "v"(tra[13]),
-          "v"(tra[14]), "v"(tra[15]), "n"(s * kStage)
+          "v"(tra[14]), "v"(tra[15]), "n"(s * kSlot)
         : "memory");
 #pragma unroll
     for (int t = 0; t < kT; ++t)
@@ -2752,7 +2767,9 @@ void bsr16_f16_grp_kernel(
       // this wave's copies and A fragments of the IPB items landed (in issue order: the
       // last slot's count covers the others); then every wave's, at the barrier
       f16x4 fa[IPB];
-      if constexpr (IPB == 1) {
+      if constexpr (AL) {
+        asm volatile(SPMM_VM_LADDER("%0") : : "s"(nis - stamp[s0]) : "scc", "memory");
+      } else if constexpr (IPB == 1) {
         u32x2a y;
         asm volatile(SPMM_VM_LADDER("%1") "v_mov_b64 %0, %2"
                      : "=&v"(y) : "s"(nis - stamp[s0]), "v"(fan[s0]) : "scc", "memory");
@@ -2767,6 +2784,15 @@ void bsr16_f16_grp_kernel(
         fa[1] = __builtin_bit_cast(f16x4, y1);
       }
       __builtin_amdgcn_s_barrier();
+      if constexpr (AL) {  // this wave's fragment of the item, from the slot's fragment area
+        u32x2a y;
+        asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(y)
+                     : "v"(lds0 + (unsigned)kStage + 512u * (unsigned)w + 8u * (unsigned)lane),
+                       "n"(s0 * kSlot)
+                     : "memory");
+        fa[0] = __builtin_bit_cast(f16x4, y);
+      }
       // the IPB slots before s0 were read by every wave in the previous step: refill them
 #pragma unroll
       for (int i = 0; i < IPB; ++i) issue(it + P - IPB + i, (s0 + P - IPB + i) % P, i);
@@ -3811,7 +3837,7 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
     // spills the A fragments in flight (tools/isa_vmcnt.py --inflight; the first faulted)
     switch (env) {
       case 30: case 33: case 32: case 42: case 43: case 52: case 53: case 23: case 24:
-      case 243: case 262: case 263:
+      case 243: case 262: case 263: case 1033: case 1043:
         gv = env;
         break;
       default:
@@ -3823,17 +3849,18 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   const int ntt = tt && ntiles > 1 ? ntiles : 0;
   const dim3 grid = ntt ? dim3((unsigned)(8 * ((ngroups + 7) / 8) * ntt), 1)
                         : dim3((unsigned)ngroups, (unsigned)ntiles);
-#define GRP_LAUNCH1(W_, P_, O_, IPB_)                                                            \
+#define GRP_LAUNCH2(W_, P_, O_, IPB_, AL_)                                                       \
   do {                                                                                           \
     if (crow)                                                                                    \
-      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_, IPB_>), grid, dim3(64 * W_), 0, \
-                         ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C, ldc, \
-                         xm, ngroups, ntt);                                                      \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_, IPB_, AL_>), grid,               \
+                         dim3(64 * W_), 0, ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb,     \
+                         alpha, beta, C, ldc, xm, ngroups, ntt);                                 \
     else                                                                                         \
-      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_, IPB_>), grid, dim3(64 * W_),   \
-                         0, ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb, alpha, beta, C,   \
-                         ldc, xm, ngroups, ntt);                                                 \
+      hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_, IPB_, AL_>), grid,              \
+                         dim3(64 * W_), 0, ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb,     \
+                         alpha, beta, C, ldc, xm, ngroups, ntt);                                 \
   } while (0)
+#define GRP_LAUNCH1(W_, P_, O_, IPB_) GRP_LAUNCH2(W_, P_, O_, IPB_, false)
 #ifdef SPMM_TUNING
 #define GRP_LAUNCH(W_)                                                                           \
   do {                                                                                           \
@@ -3849,6 +3876,8 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
       case 243: GRP_LAUNCH1(W_, 4, 3, 2); break;  /* two items per barrier */                    \
       case 262: GRP_LAUNCH1(W_, 6, 2, 2); break;                                                 \
       case 263: GRP_LAUNCH1(W_, 6, 3, 2); break;                                                 \
+      case 1033: GRP_LAUNCH2(W_, 3, 3, 1, true); break;  /* fragments through LDS */             \
+      case 1043: GRP_LAUNCH2(W_, 4, 3, 1, true); break;                                          \
       default: GRP_LAUNCH1(W_, 3, 3, 1); break;                                                  \
     }                                                                                            \
   } while (0)
@@ -3861,6 +3890,7 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   else GRP_LAUNCH(2);
 #undef GRP_LAUNCH
 #undef GRP_LAUNCH1
+#undef GRP_LAUNCH2
   timing_end(ctx, slot);
   return from_hip(hipGetLastError());
 }
