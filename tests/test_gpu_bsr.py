@@ -1233,3 +1233,41 @@ def test_grouped_streams_empty_matrix(device, bs):
     g0 = G(torch.zeros(1, dtype=torch.int32, device=device), dci, dv, mb=0)
     g0.mm(B, kb=kb, n=n, ldb=n, C=C, ldc=n)
     g0.close()
+
+
+@pytest.mark.parametrize("bs,W", [(16, 2), (16, 4), (16, 8), (32, 2), (32, 4)])
+def test_group_analysis_layout(device, bs, W):
+    """The device group analysis against a numpy restatement of the grouping: per group of
+    W block rows, the union of their blocks' nonzero columns in (block column, column)
+    order, cut into items of 16 (bs 16) or 8 (bs 32) entries, the last padded with -1. The
+    buffer's item pointers and entry rows must be exactly that (include/spmm_hip.h layout:
+    256-B header, item_ptr[ngroups + 1], rows[nitems][E] at the next 256-B boundary)."""
+    ops = _ops()
+    rng = np.random.default_rng(100 * bs + W)
+    mb, kb = 29, 40
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.35)
+    E = 16 if bs == 16 else 8
+    vb = v.reshape(-1, bs, bs)  # ROW blocks: [block][row][column]
+    nz_cols = [np.nonzero((np.abs(vb[k]) > 0).any(axis=0))[0] for k in range(vb.shape[0])]
+    ngroups = (mb + W - 1) // W
+    want_ptr, want_rows = [0], []
+    for g in range(ngroups):
+        ent = set()
+        for br in range(g * W, min(mb, g * W + W)):
+            for k in range(rp[br], rp[br + 1]):
+                ent.update(int(ci[k]) * bs + int(c) for c in nz_cols[k])
+        ent = sorted(ent)
+        ent += [-1] * (-len(ent) % E)
+        want_rows += ent
+        want_ptr.append(want_ptr[-1] + len(ent) // E)
+    vv = v.astype(np.float16) if bs == 16 else v
+    drp, dci, dv = _dev(rp, ci, vv)
+    G = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
+    grp = G(drp, dci, dv, mb=mb, group_rows=W)
+    buf = grp.buffer.cpu().numpy()
+    ptr = buf[256:256 + 4 * (ngroups + 1)].view(np.int32)
+    assert np.array_equal(ptr, np.array(want_ptr, np.int32)), "item pointers"
+    rows_off = (256 + 4 * (ngroups + 1) + 255) // 256 * 256
+    got_rows = buf[rows_off:rows_off + 4 * len(want_rows)].view(np.int32)
+    assert np.array_equal(got_rows, np.array(want_rows, np.int32)), "entry rows"
+    grp.close()
