@@ -1247,7 +1247,8 @@ def test_group_analysis_layout(device, bs, W):
     mb, kb = 29, 40
     rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.35)
     E = 16 if bs == 16 else 8
-    vb = v.reshape(-1, bs, bs)  # ROW blocks: [block][row][column]
+    vv = v.astype(np.float16) if bs == 16 else v
+    vb = vv.astype(np.float32).reshape(-1, bs, bs)  # ROW blocks: [block][row][column]
     nz_cols = [np.nonzero((np.abs(vb[k]) > 0).any(axis=0))[0] for k in range(vb.shape[0])]
     ngroups = (mb + W - 1) // W
     want_ptr, want_rows = [0], []
@@ -1260,7 +1261,6 @@ def test_group_analysis_layout(device, bs, W):
         ent += [-1] * (-len(ent) % E)
         want_rows += ent
         want_ptr.append(want_ptr[-1] + len(ent) // E)
-    vv = v.astype(np.float16) if bs == 16 else v
     drp, dci, dv = _dev(rp, ci, vv)
     G = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
     grp = G(drp, dci, dv, mb=mb, group_rows=W)
