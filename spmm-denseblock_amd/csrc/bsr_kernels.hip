@@ -878,38 +878,53 @@ __global__ __launch_bounds__(256) void bsr32_analysis_kernel(int nnzb, int rowdi
   if (lane == 0) masks[k] = msk;
 }
 
-// The same analysis for bs = 16 fp16 (spmm_bsr16_analysis_f16): one wave per block
-// (512 B), lane L holding 4 halves. ROW: lane (r = L / 4, q = L % 4) holds row r,
-// columns 4q .. 4q + 3, and writes them to the column-major copy; COLUMN: lane L
-// holds column L / 4, rows 4 (L % 4) .. + 3.
+// The same analysis for bs = 16 fp16 (spmm_bsr16_analysis_f16): one wave per
+// kAna16Bpw consecutive blocks (512 B each; the loads of all of them issued before
+// the first wait: one block per wave left the kernel latency-bound), lane L holding
+// 4 halves of each. ROW: lane (r = L / 4, q = L % 4) holds row r, columns 4q ..
+// 4q + 3, and writes them to the column-major copy; COLUMN: lane L holds column
+// L / 4, rows 4 (L % 4) .. + 3.
+constexpr int kAna16Bpw = 4;
+
 __global__ __launch_bounds__(256) void bsr16_analysis_kernel(int nnzb, int rowdir,
                                                              const uint16_t* __restrict__ val,
                                                              unsigned* __restrict__ masks,
                                                              uint16_t* __restrict__ val_col) {
   const int lane = threadIdx.x & 63;
-  const long long k = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (k >= nnzb) return;
+  const long long k0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kAna16Bpw;
+  if (k0 >= nnzb) return;
   typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
-  const u16x4 x = *reinterpret_cast<const u16x4*>(val + (size_t)k * 256 + 4 * lane);
-  unsigned msk = 0;
-  if (rowdir) {
-    const int r = lane >> 2, q = lane & 3;
-    uint16_t* dst = val_col + (size_t)k * 256;
+  u16x4 xs[kAna16Bpw];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const unsigned long long b = __builtin_amdgcn_ballot_w64((x[e] & 0x7fffu) != 0u);
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq)
-        msk |= ((b & (0x1111111111111111ull << qq)) != 0ull ? 1u : 0u) << (4 * qq + e);
-      if (val_col) dst[(4 * q + e) * 16 + r] = x[e];  // null: masks only (the group analysis)
-    }
-  } else {
-    const unsigned long long b = __builtin_amdgcn_ballot_w64(
-        ((x[0] | x[1] | x[2] | x[3]) & 0x7fffu) != 0u);
-#pragma unroll
-    for (int c = 0; c < 16; ++c) msk |= (((b >> (4 * c)) & 15ull) != 0ull ? 1u : 0u) << c;
+  for (int f = 0; f < kAna16Bpw; ++f) {
+    const long long k = min(k0 + f, (long long)nnzb - 1);  // past the end: loaded, not used
+    xs[f] = *reinterpret_cast<const u16x4*>(val + (size_t)k * 256 + 4 * lane);
   }
-  if (lane == 0) masks[k] = msk;
+#pragma unroll
+  for (int f = 0; f < kAna16Bpw; ++f) {
+    const long long k = k0 + f;
+    if (k >= nnzb) break;
+    const u16x4 x = xs[f];
+    unsigned msk = 0;
+    if (rowdir) {
+      const int r = lane >> 2, q = lane & 3;
+      uint16_t* dst = val_col + (size_t)k * 256;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const unsigned long long b = __builtin_amdgcn_ballot_w64((x[e] & 0x7fffu) != 0u);
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          msk |= ((b & (0x1111111111111111ull << qq)) != 0ull ? 1u : 0u) << (4 * qq + e);
+        if (val_col) dst[(4 * q + e) * 16 + r] = x[e];  // null: masks only (the group analysis)
+      }
+    } else {
+      const unsigned long long b = __builtin_amdgcn_ballot_w64(
+          ((x[0] | x[1] | x[2] | x[3]) & 0x7fffu) != 0u);
+#pragma unroll
+      for (int c = 0; c < 16; ++c) msk |= (((b >> (4 * c)) & 15ull) != 0ull ? 1u : 0u) << c;
+    }
+    if (lane == 0) masks[k] = msk;
+  }
 }
 
 // Longest-first block-row order for the one-wave-per-block-row kernels (the
@@ -3314,8 +3329,10 @@ spmm_status_t launch_bsr32_analysis(spmm_context* ctx, spmm_direction_t dir, int
 spmm_status_t launch_bsr16_analysis(spmm_context* ctx, spmm_direction_t dir, int nnzb,
                                     const uint16_t* val, unsigned* masks, uint16_t* val_col) {
   if (nnzb == 0) return SPMM_STATUS_SUCCESS;
-  hipLaunchKernelGGL(bsr16_analysis_kernel, dim3((nnzb + 3) / 4), dim3(256), 0, ctx->stream, nnzb,
-                     dir == SPMM_DIRECTION_ROW ? 1 : 0, val, masks, val_col);
+  const long long per_block = 4 * kAna16Bpw;  // 4 waves, kAna16Bpw blocks each
+  hipLaunchKernelGGL(bsr16_analysis_kernel, dim3((unsigned)((nnzb + per_block - 1) / per_block)),
+                     dim3(256), 0, ctx->stream, nnzb, dir == SPMM_DIRECTION_ROW ? 1 : 0, val,
+                     masks, val_col);
   return from_hip(hipGetLastError());
 }
 
