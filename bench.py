@@ -653,7 +653,6 @@ def run_csr(args, W, world, rank, dev, dist):
     g = torch.Generator(device=dev)
     g.manual_seed(1234)
     B = torch.rand((n, K), device=dev, generator=g) * 2 - 1
-    mr = shard.max_rows
     h = ops.Handle()
     if args.waves_per_cu:
         h.set_csr_waves_per_cu(args.waves_per_cu)
@@ -662,6 +661,8 @@ def run_csr(args, W, world, rank, dev, dist):
     nch = args.chunks or (4 if world > 1 else 1)
     if nch > 1 and not dist.is_initialized():
         raise SystemExit("--chunks > 1 at N = 1 needs a torch.distributed launcher")
+    if (world > 1 or nch > 1) and args.csr_layout == "col":
+        raise SystemExit("--csr-layout col is a 1-GPU, one-chunk form")
     hot = bool(W.get("hot"))
     analysis_ms = None
     if hot:
@@ -676,25 +677,27 @@ def run_csr(args, W, world, rank, dev, dist):
             ts.append(time.perf_counter() - t0)
         analysis_ms = min(ts) * 1e3
         hot_share = float((d_tag < 0).float().mean())
-    if nch > 1:
-        # the all-gather of chunk c overlaps the compute of chunk c + 1
-        out = torch.empty((nch, world, sdist.chunk_rows(shard, nch), K), device=dev)
+    if world > 1 or nch > 1:
+        # C is the contiguous n x K matrix on every rank: the kernel writes
+        # this rank's rows in place, and the exchange of chunk c (batched
+        # isend / irecv of exact row shards, RCCL p2p over xGMI) overlaps the
+        # compute of chunk c + 1
+        C_full = torch.empty((n, K), device=dev)
 
         def compute_chunk(r0, r1, dest):
             ops.csrmm(d_rp[r0:r1 + 1], d_ci, d_v, B, m=r1 - r0, n=K, k=n, ldb=K, C=dest,
                       ldc=K, handle=h)
 
         def step():
-            sdist.chunked_spmm(shard, out, compute_chunk, nch, compact=False)
+            sdist.chunked_spmm(shard, C_full, compute_chunk, nch)
 
         def exchange_only():
-            works = [dist.all_gather_into_tensor(out[c].view(-1, K), out[c, rank], async_op=True)
-                     for c in range(nch)]
+            works = []
+            for c in range(nch):
+                works += sdist.exchange_chunk(C_full, shard, c, nch)
             for w in works:
                 w.wait()
     elif args.csr_layout == "col":
-        if world > 1:
-            raise SystemExit("--csr-layout col is a 1-GPU form")
         # cusparseScsrmm's layout (run_csrmm.cu:135-137): B and C column-major
         Bc = B.t().contiguous()
         Cc = torch.empty((K, n), device=dev)
@@ -703,8 +706,7 @@ def run_csr(args, W, world, rank, dev, dist):
             ops.csrmm(d_rp, d_ci, d_v, Bc, m=n, n=K, k=n, ldb=n, order_b=ops.ORDER_COL, C=Cc,
                       ldc=n, order_c=ops.ORDER_COL, handle=h)
     else:
-        out = torch.empty((world * mr, K), device=dev)
-        C_slot = out[rank * mr: rank * mr + shard.rows]
+        C_slot = torch.empty((n, K), device=dev)
         product, ci_step = ops.csrmm, d_ci
         if hot:
             product, ci_step = ops.csrmm_hot, d_tag
@@ -712,11 +714,6 @@ def run_csr(args, W, world, rank, dev, dist):
         def step():
             product(d_rp, ci_step, d_v, B, m=shard.rows, n=K, k=n, ldb=K, C=C_slot, ldc=K,
                     handle=h)
-            if world > 1:
-                sdist.gather(out, shard, compact=False)
-
-        def exchange_only():
-            sdist.gather(out, shard, compact=False)
 
     elapsed, kt = timed_loop(step, h, args.steps, args.warmup, world, dist, raw=True)
     # kernel time per step (all chunks of a step; one launch when unchunked)
@@ -758,8 +755,10 @@ def run_csr(args, W, world, rank, dev, dist):
         data=("synthetic (Chung-Lu power-law digraph with the dataset's n / nnz / max degree, "
               "U(-1,1) values and B; OGB data not reachable offline)"),
         config={"workload": f"{args.workload}: csr_spmm K={K}" +
-                (f" row-partitioned over {world} ranks (nnz-balanced) + chunked RCCL all-gather "
-                 f"of C in the step (BASELINE config 4), strong scaling" if world > 1 else ""),
+                (f" row-partitioned over {world} ranks (nnz-balanced) + chunked RCCL exchange of "
+                 f"C's row shards in the step (BASELINE config 4's all-gather: exact shards, "
+                 f"batched p2p over xGMI, into the contiguous n x K C on every rank), strong "
+                 f"scaling" if world > 1 else ""),
                 "n": n, "nnz": nnz, "K": K, "max_deg": int(np.diff(rp).max()),
                 "parallelism": f"rows{world}" if world > 1 else "single",
                 "exchange_chunks": nch, "hip_graph": bool(GRAPH and world == 1),
@@ -810,9 +809,10 @@ def run_csr(args, W, world, rank, dev, dist):
                                       "analysis_ms apart; spmm_csrmm_hot_f32 per step)")
     if dist.is_initialized() and nch > 1 or world > 1:
         # compute and collective reported separately (a world-1
-        # torch.distributed launch with --chunks > 1 rehearses it through RCCL).
+        # torch.distributed launch with --chunks > 1 rehearses it through RCCL:
+        # no peer, so nothing moves).
         #  kernel_ms (roofline): this rank's kernels per step, max over ranks;
-        #  allgather_ms: the step's all-gathers alone (no compute), max over ranks;
+        #  exchange_ms: the step's exchanges alone (no compute), max over ranks;
         #  collective_ms_exposed: step minus the slowest rank's kernel time, the
         #    part of the collective the overlap did not hide.
         for _ in range(2):
@@ -827,11 +827,14 @@ def run_csr(args, W, world, rank, dev, dist):
         ag = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64,
                           device=dev)
         dist.all_reduce(ag, op=dist.ReduceOp.MAX)
-        recv = (world - 1) * (out.numel() // world) * 4
-        rec["allgather_ms"] = round(float(ag[0]), 4)
-        rec["allgather_bytes_received_per_rank"] = int(recv)
-        rec["allgather_bytes_per_rank_buffer"] = int(out.numel() * 4)
-        rec["allgather_GBps_per_rank"] = round(recv / (float(ag[0]) / 1e3) / 1e9, 1)
+        recv = (n - shard.rows) * K * 4
+        rec["exchange"] = ("all-gather of exact row shards: per chunk one batch of isend / irecv "
+                           "pairs (RCCL p2p, one per peer and direction) straight into the "
+                           "contiguous n x K C of every rank; no padding, no compaction")
+        rec["exchange_ms"] = round(float(ag[0]), 4)
+        rec["exchange_bytes_received_rank0"] = int(recv)
+        rec["exchange_GBps_rank0"] = (round(recv / (float(ag[0]) / 1e3) / 1e9, 1)
+                                      if recv else None)
         rec["collective_ms_exposed"] = round(rec["ms_per_step"] - kms_max, 4)
         rec["rows_per_rank"] = [int(b) for b in np.diff(shard.bounds)]
         rec["nnz_per_rank"] = [int(rp[b1] - rp[b0]) for b0, b1 in
@@ -1266,6 +1269,37 @@ def run_hybrid(args, W, world, rank, dev, dist):
     return rec, None
 
 
+def launch_argv(argv: list[str], n: int, port: int) -> list[str]:
+    """The one-process-per-GPU launch of this same command line: the driver's
+    own form (torch.distributed.run, one node, n ranks, rendezvous on
+    127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: start the N
+    ranks as a CHILD torch.distributed.run (never an exec: nothing here has
+    touched the GPU, and the ranks initialise it themselves), relay its
+    output (rank 0's JSON line is the only stdout line) and return its exit
+    code. Fewer than N visible devices: an error on stderr, no JSON line,
+    exit 2 (a line whose n_gpus differs from --gpus is never printed)."""
+    import socket
+    import torch
+    have = torch.cuda.device_count()  # counts devices without initialising HIP
+    if have < n:
+        print(f"bench.py: --gpus {n} but {have} GPU(s) visible; no measurement", file=sys.stderr,
+              flush=True)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(launch_argv(argv, n, port), env=env).returncode
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1323,14 +1357,21 @@ def main() -> None:
         cpu_baseline_child(args)
         return
 
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and args.gpus != world:
+    if args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if local >= torch.cuda.device_count():
+        raise SystemExit(f"LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if "WORLD_SIZE" in os.environ:

@@ -12,16 +12,17 @@
  * Partitioning (host, spmm_csr_partition_rows in spmm_hip.h): contiguous row
  * ranges of A balanced on nnz + rows, part p = rows [bounds[p], bounds[p+1]).
  * B is replicated (2.5 GB for products at K = 256 against 288 GB of HBM per
- * GPU). Each device computes its rows into its slot of a padded output and
- * the slots are exchanged with in-place ncclAllGather over xGMI, so every
- * device ends up holding all of C.
+ * GPU). Each device computes its rows straight into the same rows of its own
+ * C, and the rows are exchanged over xGMI with grouped ncclSend / ncclRecv
+ * (an all-gather of exact, uneven shards: every peer pair on its own link),
+ * so every device ends up holding all of C.
  *
- * Output layout on every device: chunk-major [chunks][ngpu][slotRows][ldc]
- * floats, slotRows = spmm_multi_slot_rows(...). Chunk c of part p holds the
- * part's local rows [c*slotRows, min((c+1)*slotRows, rows_p)); rows past a
- * part's end in its slot are left as they were (padding). chunks = 1 gives
- * the plain [ngpu][maxRows][ldc] form. With chunks > 1 the all-gather of
- * chunk c (collective stream) runs while chunk c+1 is computed.
+ * Output layout on every device: the m x n row-major C itself, leading
+ * dimension ldc. Part p's local rows are cut into chunks of chunkRows =
+ * spmm_multi_slot_rows(...) rows; with chunks > 1 the exchange of chunk c
+ * (collective stream) runs while chunk c+1 is computed. The exchange moves
+ * whole rows of ldc floats (the last row of a chunk n), so columns n..ldc-1
+ * of another part's rows take that part's values.
  *
  * Numerics: each device runs the 1-GPU kernel on its rows, so with
  * ngpu = 1 and chunks = 1 the result is bit-identical to spmm_csrmm_ex_f32 on
@@ -54,7 +55,7 @@ int spmm_multi_size(spmm_multi_t ctx);
  * legacy null (default) stream; streams == NULL means no ordering. That
  * call first makes part p's compute stream wait for the work already queued
  * on streams[p] (the producers of B, the CSR arrays and C), and at the end
- * makes streams[p] wait for part p's last all-gather, so work queued on
+ * makes streams[p] wait for part p's last exchange, so work queued on
  * streams[p] afterwards sees all of C. The call then forgets the streams
  * (set them again before every call that needs the ordering), so no handle
  * is kept past the call it was given for. */
@@ -63,7 +64,8 @@ spmm_status_t spmm_multi_set_user_streams(spmm_multi_t ctx, void* const* streams
  * p are complete once this stream is). */
 spmm_status_t spmm_multi_get_stream(spmm_multi_t ctx, int part, void** stream);
 
-/* Rows per output slot for a partition: ceil(max_p rows_p / chunks). */
+/* Rows per chunk for a partition: ceil(max_p rows_p / chunks) (the same on
+ * every part; a short part's trailing chunks are empty). */
 int spmm_multi_slot_rows(int ngpu, const int* bounds, int chunks);
 
 /* C = A(m x k, csr) * B(k x n), A row-partitioned by `bounds` (host,
@@ -74,7 +76,7 @@ int spmm_multi_slot_rows(int ngpu, const int* bounds, int chunks);
  *     arrays uploaded to device p works);
  *   partNnz[p]: host, rowPtr[p][rows_p] - rowPtr[p][0] (sizes the grid);
  *   B[p]: device p's replica of B, row-major, ldb >= n;
- *   C[p]: device p's output, layout above, ldc >= n.
+ *   C[p]: device p's m x n output, row-major, ldc >= n.
  * Asynchronous on the parts' streams; spmm_multi_synchronize waits. Status
  * behaviour of spmm_csrmm_ex_f32 for bad sizes / pointers. */
 spmm_status_t spmm_csr_f32_multi(spmm_multi_t ctx, int m, int n, int k, const int* bounds,
@@ -87,7 +89,7 @@ spmm_status_t spmm_multi_synchronize(spmm_multi_t ctx);
 /* Per-part timing of the last spmm_csr_f32_multi call (events on the
  * streams, recorded when enabled): compute_ms[p] = first kernel start to last
  * kernel end on device p, total_ms[p] = first kernel start to the end of
- * the last all-gather on device p. Synchronises. */
+ * the last exchange on device p. Synchronises. */
 spmm_status_t spmm_multi_set_timing(spmm_multi_t ctx, int enable);
 spmm_status_t spmm_multi_get_times(spmm_multi_t ctx, float* compute_ms, float* total_ms);
 

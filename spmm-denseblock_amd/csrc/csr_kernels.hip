@@ -142,12 +142,14 @@ __device__ __forceinline__ bool split_row_arrive(int* t, int count, int lane) {
   if (lane == 0) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
-// Workspace of the split rows: carry and head slots (kWave * 4 floats each,
-// the widest column tile) for every (column tile, wave).
+// Workspace of the split rows: carry and head slots for every (column tile,
+// wave), `stride` floats each: the launch's column-tile width (kWave * VEC;
+// kWave for the K <= 64 group kernel). The host sizes each of the two arrays
+// for the widest grid at that width (csrmm_carry_bytes).
 struct SplitWs {
   float* carry;
   float* head;
-  __host__ __device__ static size_t slot_floats() { return kWave * 4; }
+  int stride;
 };
 
 // Merge-path search for two diagonals at once: lanes 0-31 search d0, lanes
@@ -219,8 +221,8 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   const int rs0 = i0 < i1 ? rowptr[i0] - rp0 : 0;
   const bool split_head = i0 < i1 && rs0 < j0;
   bool head_pending = split_head;
-  float* const carry_p = sws.carry + (size_t)slot * SplitWs::slot_floats() + lane * VEC;
-  float* const head_p = sws.head + (size_t)slot * SplitWs::slot_floats() + lane * VEC;
+  float* const carry_p = sws.carry + (size_t)slot * sws.stride + lane * VEC;
+  float* const head_p = sws.head + (size_t)slot * sws.stride + lane * VEC;
 
   // Row ends: lane l holds raw rowptr[rbase+1+l] for 64 rows, reloaded in
   // place when exhausted (one pipeline drain per 64 rows). The load is free
@@ -409,7 +411,7 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partials are stored
   // the last arrival of a split row writes it (w_a .. w_b: the row's waves)
   auto finish = [&](int r, int wa, int wb) {
-    const size_t sf = SplitWs::slot_floats();
+    const size_t sf = sws.stride;
     const float* cw = sws.carry + ((size_t)ct * nwaves + wa) * sf + lane * VEC;
     float sum[VEC], x[VEC];
 #pragma unroll
@@ -499,8 +501,8 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
   const int rs0 = i0 < i1 ? rowptr[i0] - rp0 : 0;
   const bool split_head = i0 < i1 && rs0 < j0;
   bool head_pending = split_head;
-  float* const carry_p = sws.carry + (size_t)slot * SplitWs::slot_floats() + col;
-  float* const head_p = sws.head + (size_t)slot * SplitWs::slot_floats() + col;
+  float* const carry_p = sws.carry + (size_t)slot * sws.stride + col;
+  float* const head_p = sws.head + (size_t)slot * sws.stride + col;
 
   auto load_rowends = [&](int rb) -> int { return rowptr[min(rb + 1 + lane, m)]; };
   int rbase = i0;
@@ -660,7 +662,7 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partials are stored
   // the last arrival writes the row: lane l column l (n <= 64)
   auto finish = [&](int r, int wa, int wb) {
-    const size_t sf = SplitWs::slot_floats();
+    const size_t sf = sws.stride;
     const float* cw = sws.carry + (size_t)wa * sf + lane;
     float sum = ld_sc1(cw);
     for (int w2 = wa + 1; w2 < wb; ++w2) {
@@ -955,14 +957,22 @@ spmm_status_t launch_csr_hot_analysis(spmm_context* ctx, int k, long long nnz, c
   return from_hip(hipGetLastError());
 }
 
-size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n) {
-  // The grid does not depend on nnz beyond the cap: size it for the cap.
-  // Carry and head slots (kWave * 4 floats) per (column tile, wave).
+namespace {
+// Floats of ONE of the two split-row arrays (carry, head): a slot of tile
+// floats per (column tile, wave) at the capped wave count. The tiles of any
+// VEC cover at most roundup(n, 256) columns (tile = 64 * VEC, VEC <= 4), and
+// the group kernel's single tile of kWave floats is within that too, so one
+// size serves every launch of this n.
+size_t split_array_floats(spmm_context* ctx, int n) {
   const int wpc = ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu : 16;
-  const size_t nw = (size_t)ctx->num_cus * wpc;
-  (void)m;
-  const size_t slots = nw * (size_t)((n + 63) / 64);  // VEC = 1: the most column tiles
-  return 2 * slots * SplitWs::slot_floats() * sizeof(float) + 256;
+  const size_t nw = (size_t)ctx->num_cus * wpc;  // the grid's cap (csr_nwaves)
+  return nw * (((size_t)n + 255) & ~(size_t)255);
+}
+}  // namespace
+
+size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n) {
+  (void)m;  // the grid does not depend on m or nnz beyond the cap: size it for the cap
+  return 2 * split_array_floats(ctx, n) * sizeof(float) + 256;
 }
 
 spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* rowptr,
@@ -978,12 +988,10 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   dim3 block(kWG);
   // split rows: carry and head slots in the workspace (sized by csrmm_carry_bytes for
   // the largest grid), tickets of the handle (zero between launches)
-  const size_t slots_max = (size_t)ctx->num_cus *
-                           (ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu : 16) *
-                           (size_t)((n + 63) / 64);
   SplitWs sws;
   sws.carry = static_cast<float*>(carry_ws);
-  sws.head = sws.carry + slots_max * SplitWs::slot_floats();
+  sws.head = sws.carry + split_array_floats(ctx, n);
+  sws.stride = tile;
   if (spmm_status_t st = ensure_tickets(ctx, (size_t)nw * ntiles)) return st;
   int* tickets = ctx->tickets;
   const int slot = timing_begin(ctx);
@@ -993,6 +1001,7 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
                       reinterpret_cast<uintptr_t>(C) % 16 == 0 &&
                       (ctx->csr_flags & SPMM_CSR_SEQUENTIAL_ROWS) == 0;
   if (grouped) {
+    sws.stride = kWave;  // one column tile: lane l owns column l (n <= 64)
     dim3 g8((nw + kWavesPerWG - 1) / kWavesPerWG, 1);
 #ifdef SPMM_TUNING
     static const int pd_env = [] {

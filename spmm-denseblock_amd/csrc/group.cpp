@@ -60,6 +60,10 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
   if (W != 2 && W != 4 && (BS == 32 || W != 8)) return SPMM_STATUS_INVALID_VALUE;
   if (mb > 0 && !bsrRowPtr) return SPMM_STATUS_INVALID_VALUE;
   if (nnzb > 0 && (!bsrColInd || !bsrVal)) return SPMM_STATUS_INVALID_VALUE;
+  // the mask and fill kernels read the values as f32x4 (BS 32) / u16x4 (BS 16)
+  // vectors, as spmm_bsr32_analysis_f32 / spmm_bsr16_analysis_f16 require
+  if (nnzb > 0 && reinterpret_cast<uintptr_t>(bsrVal) % (BS == 32 ? 16 : 8) != 0)
+    return SPMM_STATUS_INVALID_VALUE;
   const int E = BS == 16 ? 16 : 8;  // entries per item
   const int ngroups = (mb + W - 1) / W;
   hipStream_t st = handle->stream;

@@ -2,13 +2,16 @@
 // (include/spmm_multi.h).
 //
 // Per call and chunk c: every device p computes its chunk-c rows with the
-// 1-GPU merge-path kernel into its slot of the chunk-major output on its
+// 1-GPU merge-path kernel straight into their rows of its own m x n C on its
 // compute stream, records an event, and its collective stream waits on that
-// event and runs the in-place ncclAllGather of chunk c (one ncclGroup over all
-// devices, so one host thread can drive every rank). Chunk c+1's kernel is
-// queued on the compute stream right away and overlaps chunk c's exchange.
-// At the end each compute stream waits for its collective stream, so a
-// caller that synchronises the compute stream sees all of C.
+// event and runs the exchange of chunk c: one ncclGroup in which every device
+// ncclSends its chunk-c rows to each peer and ncclRecvs each peer's chunk-c
+// rows into the same rows of its C (an all-gather of exact, uneven shards;
+// xGMI is point-to-point, so every peer pair has its own link and all of them
+// carry data at once). Chunk c+1's kernel is queued on the compute stream
+// right away and overlaps chunk c's exchange. At the end each compute stream
+// waits for its collective stream, so a caller that synchronises the compute
+// stream sees all of C.
 //
 // RCCL is resolved at run time (dlopen of librccl.so.1 on the first
 // spmm_multi_create): the single-GPU entry points of libspmm_hip.so never
@@ -59,7 +62,8 @@ struct Rccl {
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
-  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
   bool ok = false;
 };
 
@@ -75,8 +79,9 @@ const Rccl& rccl() {
     r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
     r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
     r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
-    r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
-    r.ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.all_gather;
+    r.send = reinterpret_cast<decltype(r.send)>(dlsym(h, "ncclSend"));
+    r.recv = reinterpret_cast<decltype(r.recv)>(dlsym(h, "ncclRecv"));
+    r.ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.send && r.recv;
   });
   return r;
 }
@@ -216,8 +221,17 @@ spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int*
   for (int p = 0; p < P; ++p)
     if (!rowPtr[p] || !C[p] || (k > 0 && !B[p]) || (partNnz[p] > 0 && (!colInd[p] || !val[p])))
       return SPMM_STATUS_INVALID_VALUE;
-  const int cr = spmm_multi_slot_rows(P, bounds, chunks);
-  const size_t slot = (size_t)cr * ldc;  // floats per (chunk, part) slot
+  const int cr = spmm_multi_slot_rows(P, bounds, chunks);  // rows per chunk
+  // part q's chunk ch: local rows [lo, hi), global rows bounds[q] + [lo, hi)
+  auto chunk = [&](int q, int ch, int& lo, int& hi) {
+    const int rows = bounds[q + 1] - bounds[q];
+    lo = std::min(ch * cr, rows);
+    hi = std::min(lo + cr, rows);
+  };
+  // rows r0..r1 of a row-major C with leading dimension ldc as one span: whole
+  // rows of ldc floats, the last one n (the padding columns between the
+  // exchanged rows travel with them)
+  auto span = [&](int r0, int r1) { return (size_t)(r1 - r0 - 1) * ldc + n; };
   DeviceGuard guard;
   for (int p = 0; p < P; ++p) {
     auto& ev = c->chunk_done[p];
@@ -241,34 +255,43 @@ spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int*
       SPMM_TRY_HIP(hipSetDevice(c->dev[p]));
       if (ch == 0 && c->timing) SPMM_TRY_HIP(hipEventRecord(c->t0[p], c->compute[p]));
       const int rows = bounds[p + 1] - bounds[p];
-      const int r0 = std::min(ch * cr, rows), r1 = std::min(r0 + cr, rows);
+      int r0, r1;
+      chunk(p, ch, r0, r1);
       if (r1 > r0) {
         // nnz hint: the part's average share (grid sizing only)
         const int nnz = (int)((long long)partNnz[p] * (r1 - r0) / std::max(rows, 1));
         spmm_status_t st = spmm_csrmm_ex_f32(
             c->handle[p], r1 - r0, n, k, nnz, 1.f, rowPtr[p] + r0, colInd[p], val[p],
             SPMM_INDEX_BASE_ZERO, B[p], ldb, SPMM_ORDER_ROW, 0.f,
-            C[p] + ((size_t)ch * P + p) * slot, ldc, SPMM_ORDER_ROW);
+            C[p] + (size_t)(bounds[p] + r0) * ldc, ldc, SPMM_ORDER_ROW);
         if (st != SPMM_STATUS_SUCCESS) return st;
       }
       if (ch == chunks - 1 && c->timing) SPMM_TRY_HIP(hipEventRecord(c->t_comp[p], c->compute[p]));
       SPMM_TRY_HIP(hipEventRecord(c->chunk_done[p][ch], c->compute[p]));
       SPMM_TRY_HIP(hipStreamWaitEvent(c->coll[p], c->chunk_done[p][ch], 0));
     }
-    // in-place all-gather of chunk ch, on one device too (a one-rank RCCL
-    // communicator: the same call, stream and event chain as at P > 1)
-    {
-      const Rccl& R = rccl();
-      spmm_status_t st = from_nccl(R.group_start());
-      for (int p = 0; p < P && st == SPMM_STATUS_SUCCESS; ++p) {
-        float* base = C[p] + (size_t)ch * P * slot;
-        st = from_nccl(R.all_gather(base + (size_t)p * slot, base, slot, ncclFloat, c->comm[p],
-                                    c->coll[p]));
+    if (P == 1) continue;  // one part: nothing to exchange
+    // exchange of chunk ch: every (p, q) pair once in each direction, one group
+    const Rccl& R = rccl();
+    spmm_status_t st = from_nccl(R.group_start());
+    for (int p = 0; p < P && st == SPMM_STATUS_SUCCESS; ++p) {
+      int m0, m1;
+      chunk(p, ch, m0, m1);
+      for (int q = 0; q < P && st == SPMM_STATUS_SUCCESS; ++q) {
+        if (q == p) continue;
+        if (m1 > m0)
+          st = from_nccl(R.send(C[p] + (size_t)(bounds[p] + m0) * ldc, span(m0, m1), ncclFloat, q,
+                                c->comm[p], c->coll[p]));
+        int q0, q1;
+        chunk(q, ch, q0, q1);
+        if (st == SPMM_STATUS_SUCCESS && q1 > q0)
+          st = from_nccl(R.recv(C[p] + (size_t)(bounds[q] + q0) * ldc, span(q0, q1), ncclFloat, q,
+                                c->comm[p], c->coll[p]));
       }
-      const spmm_status_t st2 = from_nccl(R.group_end());
-      if (st != SPMM_STATUS_SUCCESS) return st;
-      if (st2 != SPMM_STATUS_SUCCESS) return st2;
     }
+    const spmm_status_t st2 = from_nccl(R.group_end());
+    if (st != SPMM_STATUS_SUCCESS) return st;
+    if (st2 != SPMM_STATUS_SUCCESS) return st2;
   }
   for (int p = 0; p < P; ++p) {
     SPMM_TRY_HIP(hipSetDevice(c->dev[p]));

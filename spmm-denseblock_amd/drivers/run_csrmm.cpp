@@ -8,9 +8,10 @@
 // B layout, col-major C) — all served by libspmm_hip.so.
 // --gpus N (impl gespmm; not in the reference, which is single-GPU): the rows
 // are cut into N nnz-balanced shards (spmm_csr_partition_rows), one per GPU
-// of this process, B replicated, and C assembled on every GPU by the in-place
-// RCCL all-gather of spmm_csr_f32_multi (include/spmm_multi.h), C chunks
-// overlapping the next chunk's compute. Every mode ends with a checksum of C.
+// of this process, B replicated, and C assembled on every GPU by the RCCL
+// exchange of spmm_csr_f32_multi (include/spmm_multi.h: grouped send / recv
+// of exact row shards into each GPU's n x dim C), C chunks overlapping the
+// next chunk's compute. Every mode ends with a checksum of C.
 #include <cassert>
 #include <chrono>
 #include <iostream>
@@ -35,7 +36,7 @@ static int run_multi(int ngpu, int chunks, const std::vector<int>& rp, const std
   std::vector<int> bounds(ngpu + 1);
   HANDLE_SPMM_ERROR(spmm_csr_partition_rows(n, rp.data(), ngpu, bounds.data()));
   const int slot = spmm_multi_slot_rows(ngpu, bounds.data(), chunks);
-  printf("multi-GPU: ngpu=%d chunks=%d slot_rows=%d rows/part:", ngpu, chunks, slot);
+  printf("multi-GPU: ngpu=%d chunks=%d chunk_rows=%d rows/part:", ngpu, chunks, slot);
   for (int p = 0; p < ngpu; ++p) printf(" %d", bounds[p + 1] - bounds[p]);
   printf("\n");
   DeviceArena mem;
@@ -43,7 +44,7 @@ static int run_multi(int ngpu, int chunks, const std::vector<int>& rp, const std
   std::vector<const float*> dv(ngpu), dB(ngpu);
   std::vector<float*> dC(ngpu);
   std::vector<int> part_nnz(ngpu);
-  const size_t cfloats = (size_t)chunks * ngpu * slot * dim;
+  const size_t cfloats = (size_t)n * dim;
   for (int p = 0; p < ngpu; ++p) {
     HANDLE_ERROR(hipSetDevice(p));
     const int r0 = bounds[p], r1 = bounds[p + 1], j0 = rp[r0], j1 = rp[r1];
@@ -79,7 +80,7 @@ static int run_multi(int ngpu, int chunks, const std::vector<int>& rp, const std
       cm = std::max(cm, comp[p]);
       tm = std::max(tm, tot[p]);
     }
-    printf("csrmm cost time:  %3.10f ms  (max over GPUs: compute %.4f ms, compute + all-gather "
+    printf("csrmm cost time:  %3.10f ms  (max over GPUs: compute %.4f ms, compute + exchange "
            "%.4f ms)\n", t, cm, tm);
     total += t;
     comp_max += cm;
@@ -87,21 +88,13 @@ static int run_multi(int ngpu, int chunks, const std::vector<int>& rp, const std
   }
   const float avg = total / epoch;
   printf("average csrmm cost time: %3.10f ms\n", avg);
-  printf("average per-GPU compute %.4f ms, compute + all-gather %.4f ms\n", comp_max / epoch,
+  printf("average per-GPU compute %.4f ms, compute + exchange %.4f ms\n", comp_max / epoch,
          tot_max / epoch);
   printf("GFLOP/s (2*nnz*dim/t): %6.3f\n", 2.0 * (double)rp[n] * dim / (avg * 1e6));
-  // C on GPU 0 (every GPU holds all of it): chunk-major slots -> rows
-  std::vector<float> buf(cfloats), z((size_t)n * dim);
-  HANDLE_ERROR(hipSetDevice(0));
-  HANDLE_ERROR(hipMemcpy(buf.data(), dC[0], cfloats * sizeof(float), hipMemcpyDeviceToHost));
-  for (int p = 0; p < ngpu; ++p) {
-    const int rows = bounds[p + 1] - bounds[p];
-    for (int r = 0; r < rows; ++r) {
-      const int c = r / slot, rr = r % slot;
-      const float* src = buf.data() + (((size_t)c * ngpu + p) * slot + rr) * dim;
-      std::copy(src, src + dim, z.begin() + (size_t)(bounds[p] + r) * dim);
-    }
-  }
+  // C on the last GPU (every GPU holds all of it, row-major n x dim)
+  std::vector<float> z(cfloats);
+  HANDLE_ERROR(hipSetDevice(ngpu - 1));
+  HANDLE_ERROR(hipMemcpy(z.data(), dC[ngpu - 1], cfloats * sizeof(float), hipMemcpyDeviceToHost));
   print_checksum(z, n, dim);
   dump_result(z);
   spmm_multi_destroy(ctx);

@@ -3,24 +3,24 @@
 One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm).
 Every rank holds the full dense B (replicated: 2.5 GB for products at K=256,
 far under 288 GB), owns a contiguous nnz-balanced row range of A, computes
-its rows of C with the HIP kernel, and the ranks exchange C with ONE
-all-gather over xGMI. Output rows are independent: a row that no merge-path
+its rows of C with the HIP kernel, and the ranks exchange their rows of C
+over xGMI. Output rows are independent: a row that no merge-path
 wave splits is bit-identical to the 1-GPU result; a split row's carries are
 associated by where the wave boundaries fall (within the fp32 bar).
 
-Shards have unequal row counts; the all-gather runs on a padded
-[world, max_rows, K] buffer whose rank-r slot is written in place by the
-kernel (no staging copy). ``gather(..., compact=True)`` returns the dense
-[m, K] matrix (one extra device copy); the padded buffer plus ``bounds`` is
-the zero-copy form.
+Shards have unequal row counts. C is the caller's contiguous [m, K] matrix
+on every rank: the kernel writes this rank's rows in place, and the exchange
+(an all-gather with exact, uneven shards) moves every rank's rows straight
+into the same rows of every peer's C — no padding, no staging copy, no
+compaction after it. xGMI is point-to-point (7 links per GPU), so the exchange
+is one batch of isend / irecv pairs, one per peer and direction, all links
+busy at once (``exchange_chunk``).
 
 ``chunked_spmm`` overlaps the exchange with the compute: each rank's rows are
-cut into ``nchunks`` pieces, and piece c's all-gather (RCCL on its own
-stream, ``async_op``) runs while piece c+1 is computed. The buffer is
-chunk-major, [nchunks, world, rows_per_chunk, K], so every piece's gather is
-one contiguous in-place all-gather.
+cut into ``nchunks`` pieces, and piece c's exchange (RCCL on its own stream)
+runs while piece c+1 is computed.
 
-``stacked_block`` is the weak-scaling form (bench.py's default at N > 1):
+``stacked_block`` is the weak-scaling form (bench.py --scaling weak):
 every rank owns a products-size row block of a world-times larger graph, B
 replicated, and C stays row-sharded where the kernel wrote it — no
 collective on the data path, per-GPU work fixed as N grows.
@@ -87,34 +87,6 @@ def stacked_block(n: int, nnz: int, max_deg: int, rank: int, world: int, seed: i
     return rp, cj.astype(np.int32)
 
 
-def gather(local_out, shard: Shard, group=None, compact: bool = True):
-    """All-gather the rank slots of a padded [world*max_rows, K] buffer.
-    `local_out` must be the padded buffer itself (this rank's rows already in
-    its slot); returns the dense [m, K] C if compact, else the buffer."""
-    import torch
-    import torch.distributed as dist
-    mr = shard.max_rows
-    K = local_out.shape[1]
-    slot = local_out[shard.rank * mr:(shard.rank + 1) * mr]
-    dist.all_gather_into_tensor(local_out, slot, group=group)
-    if not compact:
-        return local_out
-    parts = [local_out[r * mr:r * mr + int(shard.bounds[r + 1] - shard.bounds[r])]
-             for r in range(shard.world)]
-    return torch.cat(parts, 0) if parts else local_out.new_zeros((0, K))
-
-
-def partitioned_spmm(shard: Shard, B, out, compute: Callable, group=None, compact: bool = True):
-    """C = A @ B across ranks: compute(rowptr, colind, val, B, C_slot) fills
-    this rank's rows into its slot of `out` ([world*max_rows, K]), then one
-    all-gather. `compute` is the HIP op in production (ops.gespmm_csrmm);
-    the CPU tests inject the oracle."""
-    mr = shard.max_rows
-    slot = out[shard.rank * mr:shard.rank * mr + shard.rows]
-    compute(shard, B, slot)
-    return gather(out, shard, group=group, compact=compact)
-
-
 def chunk_rows(shard: Shard, nchunks: int) -> int:
     """Rows per chunk (same on every rank: derived from the shared bounds)."""
     return max(1, -(-shard.max_rows // nchunks))
@@ -128,33 +100,77 @@ def chunk_range(shard: Shard, rank: int, c: int, nchunks: int) -> tuple[int, int
     return r0, min(r0 + cr, rows)
 
 
-def chunked_spmm(shard: Shard, out, compute_chunk: Callable, nchunks: int, group=None,
-                 compact: bool = True):
-    """C = A @ B across ranks with the all-gather of chunk c overlapping the
-    compute of chunk c+1. `out` is [nchunks, world, chunk_rows, K];
-    compute_chunk(r0, r1, dest) writes local rows [r0, r1) into dest (a
-    [r1-r0, K] view of this rank's slot of chunk c). Returns the dense [m, K]
-    C if compact, else `out`."""
-    import torch
+def _rows_of(C, shard: Shard, rank: int, c: int, nchunks: int):
+    """The global rows of rank's chunk c as a contiguous view of C (None if
+    the chunk is empty)."""
+    r0, r1 = chunk_range(shard, rank, c, nchunks)
+    if r1 <= r0:
+        return None
+    g0 = int(shard.bounds[rank])
+    return C[g0 + r0:g0 + r1]
+
+
+def exchange_chunk(C, shard: Shard, c: int, nchunks: int, group=None) -> list:
+    """Start the exchange of chunk c: this rank's chunk-c rows go to every peer
+    and every peer's chunk-c rows land in place in C (an all-gather with
+    uneven, exact shards). xGMI is point-to-point, so each rank sends its
+    rows straight to each peer over that peer's link and receives the peers'
+    rows the same way: one batch of isend / irecv pairs (one ncclGroup on
+    RCCL), every link busy at once. Both sides derive the chunk ranges from
+    the shared bounds, so an empty chunk is skipped on both. Returns the
+    requests (empty at world 1: nothing to move)."""
     import torch.distributed as dist
-    nch, world, cr, K = out.shape
-    assert nch == nchunks and world == shard.world and cr == chunk_rows(shard, nchunks)
+    ops = []
+    mine = _rows_of(C, shard, shard.rank, c, nchunks)
+    for q in range(shard.world):
+        if q == shard.rank:
+            continue
+        if mine is not None:
+            ops.append(dist.P2POp(dist.isend, mine, q, group=group))
+        theirs = _rows_of(C, shard, q, c, nchunks)
+        if theirs is not None:
+            ops.append(dist.P2POp(dist.irecv, theirs, q, group=group))
+    return dist.batch_isend_irecv(ops) if ops else []
+
+
+def _check_out(C, shard: Shard) -> None:
+    m = int(shard.bounds[-1])
+    if C.dim() != 2 or C.shape[0] != m or not C.is_contiguous():
+        raise ValueError(f"C must be the contiguous [{m}, K] output, got {tuple(C.shape)}")
+
+
+def gather(C, shard: Shard, group=None):
+    """Complete C on every rank: this rank's rows [row0, row1) are already in
+    place; the other ranks' rows arrive in place (exchange_chunk, one chunk).
+    Returns C."""
+    _check_out(C, shard)
+    for w in exchange_chunk(C, shard, 0, 1, group):
+        w.wait()
+    return C
+
+
+def partitioned_spmm(shard: Shard, B, C, compute: Callable, group=None):
+    """C = A @ B across ranks: compute(shard, B, rows) fills this rank's rows
+    (a [rows, K] view of the [m, K] C), then the exchange. `compute` is the
+    HIP op in production (ops.csrmm); the CPU tests inject the oracle."""
+    _check_out(C, shard)
+    compute(shard, B, C[shard.row0:shard.row1])
+    return gather(C, shard, group=group)
+
+
+def chunked_spmm(shard: Shard, C, compute_chunk: Callable, nchunks: int, group=None):
+    """C = A @ B across ranks with the exchange of chunk c overlapping the
+    compute of chunk c+1. C is the contiguous [m, K] output on every rank;
+    compute_chunk(r0, r1, dest) writes local rows [r0, r1) into dest (their
+    [r1-r0, K] view of C). Returns C, complete on every rank."""
+    _check_out(C, shard)
     works = []
     for c in range(nchunks):
-        r0, r1 = chunk_range(shard, shard.rank, c, nchunks)
-        if r1 > r0:
-            compute_chunk(r0, r1, out[c, shard.rank, :r1 - r0])
-        works.append(dist.all_gather_into_tensor(out[c].view(world * cr, K),
-                                                 out[c, shard.rank], group=group,
-                                                 async_op=True))
+        dest = _rows_of(C, shard, shard.rank, c, nchunks)
+        if dest is not None:
+            r0, r1 = chunk_range(shard, shard.rank, c, nchunks)
+            compute_chunk(r0, r1, dest)
+        works += exchange_chunk(C, shard, c, nchunks, group)
     for w in works:
         w.wait()
-    if not compact:
-        return out
-    parts = []
-    for r in range(world):
-        for c in range(nchunks):
-            r0, r1 = chunk_range(shard, r, c, nchunks)
-            if r1 > r0:
-                parts.append(out[c, r, :r1 - r0])
-    return torch.cat(parts, 0) if parts else out.new_zeros((0, K))
+    return C

@@ -303,86 +303,99 @@ def bsrmm_analysed_f16(rowptr: torch.Tensor, colind: torch.Tensor, val_col: torc
     return C
 
 
-class GroupedBsr16:
-    """spmm_bsr16_group_analysis_f16 on a bs = 16 fp16 BSR matrix (once), then
-    .mm(...) = spmm_bsrmm_grouped_f16: the grouped stream, groups of
-    group_rows adjacent block rows sharing their B-row copies. The analysis
-    buffer is a torch uint8 tensor owned by this object."""
+class _Grouped:
+    """The analysis buffer of a grouped stream (a torch uint8 tensor owned by
+    this object) and the plan the handle keeps for it: released by close(),
+    by leaving a `with` block, or when the object is collected (a plan keyed
+    by a freed address would otherwise outlive its buffer)."""
+
+    BS, VT, ANALYSIS, PRODUCT, RELEASE = 0, None, "", "", ""
 
     def __init__(self, rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, *,
-                 mb: int, group_rows: int = 4, direction: int = DIRECTION_ROW,
+                 mb: int, group_rows: int, direction: int = DIRECTION_ROW,
                  handle: Handle | None = None):
         from ctypes import c_size_t
+        self.buffer = None
         for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
-                          (val, torch.float16, "val")):
+                          (val, self.VT, "val")):
             _need(t, dt, nm)
+        nnzb = colind.numel()
+        if mb < 0 or rowptr.numel() < mb + 1:
+            raise ValueError(f"{type(self).__name__}: rowptr has {rowptr.numel()} entries, "
+                             f"needs mb + 1 = {mb + 1}")
+        if val.numel() < nnzb * self.BS * self.BS:
+            raise ValueError(f"{type(self).__name__}: val has {val.numel()} entries, needs "
+                             f"nnzb * {self.BS * self.BS} = {nnzb * self.BS * self.BS}")
         self.h = handle or default_handle()
         self.mb = mb
-        nnzb = colind.numel()
         size = c_size_t(0)
         args = (self.h.raw, direction, mb, nnzb, group_rows, _ptr(rowptr), _ptr(colind), _ptr(val))
-        check(lib().spmm_bsr16_group_analysis_f16(*args, None, byref(size)),
-              "spmm_bsr16_group_analysis_f16")
-        self.buffer = torch.empty(max(size.value, 1), dtype=torch.uint8, device=val.device)
-        check(lib().spmm_bsr16_group_analysis_f16(*args, _ptr(self.buffer), byref(size)),
-              "spmm_bsr16_group_analysis_f16")
+        fn = getattr(lib(), self.ANALYSIS)
+        check(fn(*args, None, byref(size)), self.ANALYSIS)
+        buf = torch.empty(max(size.value, 1), dtype=torch.uint8, device=val.device)
+        check(fn(*args, _ptr(buf), byref(size)), self.ANALYSIS)
+        self.buffer = buf
         self.bytes = size.value
 
     def mm(self, B: torch.Tensor, *, kb: int, n: int, ldb: int, C: torch.Tensor, ldc: int,
            order_b: int = ORDER_ROW, order_c: int = ORDER_ROW, alpha: float = 1.0,
            beta: float = 0.0) -> torch.Tensor:
-        _need(B, torch.float16, "B")
+        if self.buffer is None:
+            raise ValueError(f"{type(self).__name__}: closed")
+        _need(B, self.VT, "B")
         _need(C, torch.float32, "C")
-        check(lib().spmm_bsrmm_grouped_f16(self.h.raw, self.mb, kb, n, _ptr(self.buffer), alpha,
+        check(getattr(lib(), self.PRODUCT)(self.h.raw, self.mb, kb, n, _ptr(self.buffer), alpha,
                                            _ptr(B), ldb, order_b, beta, _ptr(C), ldc, order_c),
-              "spmm_bsrmm_grouped_f16")
+              self.PRODUCT)
         return C
 
     def close(self) -> None:
         if getattr(self, "buffer", None) is not None:
-            lib().spmm_bsr16_group_release(self.h.raw, _ptr(self.buffer))
+            getattr(lib(), self.RELEASE)(self.h.raw, _ptr(self.buffer))
             self.buffer = None
 
+    def __enter__(self):
+        return self
 
-class GroupedBsr32:
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class GroupedBsr16(_Grouped):
+    """spmm_bsr16_group_analysis_f16 on a bs = 16 fp16 BSR matrix (once), then
+    .mm(...) = spmm_bsrmm_grouped_f16: the grouped stream, groups of
+    group_rows adjacent block rows sharing their B-row copies."""
+
+    BS, VT = 16, torch.float16
+    ANALYSIS, PRODUCT = "spmm_bsr16_group_analysis_f16", "spmm_bsrmm_grouped_f16"
+    RELEASE = "spmm_bsr16_group_release"
+
+    def __init__(self, rowptr, colind, val, *, mb: int, group_rows: int = 4,
+                 direction: int = DIRECTION_ROW, handle: Handle | None = None):
+        super().__init__(rowptr, colind, val, mb=mb, group_rows=group_rows, direction=direction,
+                         handle=handle)
+
+
+class GroupedBsr32(_Grouped):
     """spmm_bsr32_group_analysis_f32 on a bs = 32 fp32 BSR matrix (once), then
     .mm(...) = spmm_bsrmm_grouped_f32: groups of group_rows (2 or 4) adjacent
     block rows sharing their B-row copies, each multiplying only its own
     nonzero columns (C bit-identical to bsrmm / bsrmm_analysed)."""
 
-    def __init__(self, rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, *,
-                 mb: int, group_rows: int = 2, direction: int = DIRECTION_ROW,
-                 handle: Handle | None = None):
-        from ctypes import c_size_t
-        for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
-                          (val, torch.float32, "val")):
-            _need(t, dt, nm)
-        self.h = handle or default_handle()
-        self.mb = mb
-        nnzb = colind.numel()
-        size = c_size_t(0)
-        args = (self.h.raw, direction, mb, nnzb, group_rows, _ptr(rowptr), _ptr(colind), _ptr(val))
-        check(lib().spmm_bsr32_group_analysis_f32(*args, None, byref(size)),
-              "spmm_bsr32_group_analysis_f32")
-        self.buffer = torch.empty(max(size.value, 1), dtype=torch.uint8, device=val.device)
-        check(lib().spmm_bsr32_group_analysis_f32(*args, _ptr(self.buffer), byref(size)),
-              "spmm_bsr32_group_analysis_f32")
-        self.bytes = size.value
+    BS, VT = 32, torch.float32
+    ANALYSIS, PRODUCT = "spmm_bsr32_group_analysis_f32", "spmm_bsrmm_grouped_f32"
+    RELEASE = "spmm_bsr_group_release"
 
-    def mm(self, B: torch.Tensor, *, kb: int, n: int, ldb: int, C: torch.Tensor, ldc: int,
-           order_b: int = ORDER_ROW, order_c: int = ORDER_ROW, alpha: float = 1.0,
-           beta: float = 0.0) -> torch.Tensor:
-        _need(B, torch.float32, "B")
-        _need(C, torch.float32, "C")
-        check(lib().spmm_bsrmm_grouped_f32(self.h.raw, self.mb, kb, n, _ptr(self.buffer), alpha,
-                                           _ptr(B), ldb, order_b, beta, _ptr(C), ldc, order_c),
-              "spmm_bsrmm_grouped_f32")
-        return C
-
-    def close(self) -> None:
-        if getattr(self, "buffer", None) is not None:
-            lib().spmm_bsr_group_release(self.h.raw, _ptr(self.buffer))
-            self.buffer = None
+    def __init__(self, rowptr, colind, val, *, mb: int, group_rows: int = 2,
+                 direction: int = DIRECTION_ROW, handle: Handle | None = None):
+        super().__init__(rowptr, colind, val, mb=mb, group_rows=group_rows, direction=direction,
+                         handle=handle)
 
 
 def bsrmm_f16(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, B: torch.Tensor, *,
@@ -508,7 +521,8 @@ def coo2csr(coo_row: torch.Tensor, m: int, base: int = 0,
 class MultiGPU:
     """spmm_multi_t (include/spmm_multi.h): one host thread drives the row
     shards of a CSR x dense product on several GPUs, RCCL communicators from
-    ncclCommInitAll, in-place all-gather of the padded output."""
+    ncclCommInitAll; every device's rows go straight into the same rows of
+    every device's m x n C (grouped ncclSend / ncclRecv of exact shards)."""
 
     def __init__(self, devices: list[int]):
         self._c = c_void_p()
@@ -518,6 +532,7 @@ class MultiGPU:
 
     @staticmethod
     def slot_rows(bounds, chunks: int = 1) -> int:
+        """Rows per chunk (spmm_multi_slot_rows)."""
         b = (c_int * len(bounds))(*[int(x) for x in bounds])
         return lib().spmm_multi_slot_rows(len(bounds) - 1, b, chunks)
 
@@ -525,7 +540,8 @@ class MultiGPU:
               ldc: int, chunks: int = 1) -> None:
         """parts[p] = (rowptr, colind, val) tensors on device p (rowptr of the
         part's rows, indexing colind / val directly); Bs[p] B replicas; Cs[p]
-        the [chunks * world * slot_rows, ldc] outputs (include/spmm_multi.h).
+        the m x n row-major outputs with leading dimension ldc, one per device,
+        each complete after the call (include/spmm_multi.h).
         Ordered against each device's current torch stream: the kernels start
         after the work already queued there, and work queued there afterwards
         sees all of C (spmm_multi_set_user_streams)."""
@@ -534,8 +550,9 @@ class MultiGPU:
             raise ValueError(f"MultiGPU.csrmm: {P} parts expected")
         if chunks < 1 or ldc < n or ldb < n:
             raise ValueError("MultiGPU.csrmm: chunks >= 1, ldb >= n and ldc >= n")
-        slot = self.slot_rows(bounds, chunks)
-        need_c = chunks * P * slot * ldc
+        if int(bounds[0]) != 0 or int(bounds[-1]) != m:
+            raise ValueError(f"MultiGPU.csrmm: bounds must run from 0 to m = {m}")
+        need_c = (m - 1) * ldc + n if m > 0 else 0
         for p in range(P):
             rp, ci, v = parts[p]
             for t, dt, nm in ((rp, torch.int32, "rowptr"), (ci, torch.int32, "colind"),
@@ -549,8 +566,8 @@ class MultiGPU:
             if rp.numel() < rows + 1:
                 raise ValueError(f"part {p}: rowptr has {rp.numel()} entries, needs {rows + 1}")
             if Cs[p].numel() < need_c:
-                raise ValueError(f"part {p}: C has {Cs[p].numel()} floats, the chunk-major "
-                                 f"output needs chunks * world * slot_rows * ldc = {need_c}")
+                raise ValueError(f"part {p}: C has {Cs[p].numel()} floats, the m x n output "
+                                 f"with ldc {ldc} needs {need_c}")
             if k > 0 and Bs[p].numel() < (k - 1) * ldb + n:
                 raise ValueError(f"part {p}: B has {Bs[p].numel()} floats, needs "
                                  f"{(k - 1) * ldb + n}")

@@ -1,4 +1,4 @@
-"""bench.py helpers that need no GPU: the BSR workloads' PMC traffic lookup
+"""bench.py helpers that need no GPU: the --gpus N launch path, the BSR workloads' PMC traffic lookup
 (profiles/r03_pmc_bytes/bytes.jsonl), the CSR roofline rule,
 the CPU-baseline timing helpers and the reorder-in-the-loop graph builder
  on a small community graph."""
@@ -107,3 +107,32 @@ def test_community_graph_reorder_record():
     assert rec2 is None and "community-ordered" in data2
     # the reordered graph is a relabelling of the same graph: same degree multiset
     assert np.array_equal(np.sort(np.diff(rp)), np.sort(np.diff(rp2)))
+
+
+def test_gpus_n_without_launcher_starts_ranks_or_fails():
+    """`bench.py --gpus N` (N > 1) with no torch.distributed launcher starts N
+    ranks as a child torch.distributed.run of the same command line (the
+    driver's form, rendezvous on 127.0.0.1); with fewer than N GPUs visible
+    (this container has none) it exits 2 with no JSON line, so no line ever
+    reports n_gpus != --gpus."""
+    import subprocess
+    b = _bench()
+    argv = b.launch_argv(["--gpus", "8", "--steps", "3"], 8, 29577)
+    assert argv[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in argv and "--nnodes=1" in argv
+    assert argv[argv.index("--master-addr") + 1] == "127.0.0.1"
+    assert argv[argv.index("--master-port") + 1] == "29577"
+    assert argv[-4:] == ["--gpus", "8", "--steps", "3"]
+    assert argv[-5] == os.path.join(ROOT, "bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "--gpus 2 but 0 GPU(s) visible" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    # under a launcher, --gpus must equal WORLD_SIZE (before any GPU call)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"],
+                       env=dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "--gpus 1 but WORLD_SIZE=2" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -1,5 +1,6 @@
 """Multi-rank plumbing of the row-partitioned path on CPU with
-gloo, world_size 2 and 3: nnz-balanced sharding, padded all-gather, and the
+gloo, world_size 2 and 3: nnz-balanced sharding, the exact-shard exchange
+into the contiguous [m, K] C (batched isend / irecv, chunked), and the
 gathered C equal to the single-process result bit for bit. The per-shard
 compute is injected (the oracle, test infrastructure) — on the GPU box the
 same code runs the HIP kernel with RCCL."""
@@ -40,15 +41,20 @@ def _worker(rank, world, port, q):
         B = np.random.default_rng(2).uniform(-1, 1, (n, K)).astype(np.float32)
         sh = sdist.make_shard(rp, ci, val, rank, world)
 
-        def compute(shard, Bt, slot):
+        def compute(shard, Bt, rows):
             c = oracle_csrmm_f32(L, shard.rows, K, shard.rowptr, shard.colind, shard.val,
                                  Bt.numpy(), K, 0)
-            slot.copy_(torch.from_numpy(c.reshape(shard.rows, K)))
+            rows.copy_(torch.from_numpy(c.reshape(shard.rows, K)))
 
-        out = torch.zeros((world * sh.max_rows, K))
-        C = sdist.partitioned_spmm(sh, torch.from_numpy(B), out, compute, compact=True)
+        out = torch.full((n, K), float("nan"))
+        C = sdist.partitioned_spmm(sh, torch.from_numpy(B), out, compute)
         full = oracle_csrmm_f32(L, n, K, rp, ci, val, B, K, 0).reshape(n, K)
-        ok = bool(np.array_equal(C.numpy(), full))
+        ok = bool(np.array_equal(C.numpy(), full)) and C.data_ptr() == out.data_ptr()
+        try:  # a padded or short C is refused before anything moves
+            sdist.gather(torch.zeros((n + 1, K)), sh)
+            ok = False
+        except ValueError:
+            pass
 
         # chunked exchange: chunk c's all-gather in flight while c+1 computes
         def compute_chunk(r0, r1, dest):
@@ -58,9 +64,13 @@ def _worker(rank, world, port, q):
                                  B, K, 0)
             dest.copy_(torch.from_numpy(c.reshape(r1 - r0, K)))
 
-        for nch in (1, 3, 7):
-            buf = torch.full((nch, world, sdist.chunk_rows(sh, nch), K), float("nan"))
-            Cc = sdist.chunked_spmm(sh, buf, compute_chunk, nch, compact=True)
+        # 64 chunks: the ranks' row counts differ (nnz-balanced bounds), so the
+        # shorter ranks' trailing chunks are empty (skipped on both sides)
+        assert any(sdist.chunk_range(sh, r, 63, 64)[0] == sdist.chunk_range(sh, r, 63, 64)[1]
+                   for r in range(world))
+        for nch in (1, 3, 7, 64):
+            buf = torch.full((n, K), float("nan"))
+            Cc = sdist.chunked_spmm(sh, buf, compute_chunk, nch)
             ok = ok and bool(np.array_equal(Cc.numpy(), full))
         q.put((rank, ok, sh.bounds.tolist(), int(sh.colind.size)))
     finally:

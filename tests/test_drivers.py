@@ -127,7 +127,7 @@ def test_run_csrmm_multi_gpu_cli(tmp_path, chunks):
     _run(["run_csrmm", "pl", 64, "gespmm", 0], tmp_path, env={"SPMM_DRIVER_DUMP": one})
     out = _run(["run_csrmm", "pl", 64, "gespmm", 0, "--gpus", 1, "--chunks", chunks], tmp_path,
                env={"SPMM_DRIVER_DUMP": multi})
-    assert f"multi-GPU: ngpu=1 chunks={chunks}" in out and "compute + all-gather" in out
+    assert f"multi-GPU: ngpu=1 chunks={chunks}" in out and "compute + exchange" in out
     assert out.rstrip().endswith("end")
     prep.rng_seed(1234)
     B = prep.random_dense_matrix(20000, 64)

@@ -129,16 +129,13 @@ def test_config4_products_k256_row_shards(oracle, device, products_k256):
     assert_normwise(Cw.cpu().numpy()[rows], ref, rabs, TOL_F32, "products K=256 whole matrix")
     for world in (2, 4, 8):
         shards = [sdist.make_shard(rp, ci, v, r, world) for r in range(world)]
-        mr = shards[0].max_rows
-        # the padded buffer the in-place all-gather exchanges: rank r's rows
-        # in slot r, written there by the kernel
-        out = torch.full((world * mr, K), float("nan"), device=device)
+        # the contiguous C the exchange fills: rank r's rows written in place
+        # by the kernel, at their global rows
+        C = torch.full((n, K), float("nan"), device=device)
         for sh in shards:
             srp, sci, sv = _dev(sh.rowptr, sh.colind, sh.val)
-            ops.csrmm(srp, sci, sv, B, m=sh.rows, n=K, k=n, ldb=K,
-                      C=out[sh.rank * mr: sh.rank * mr + sh.rows], ldc=K)
+            ops.csrmm(srp, sci, sv, B, m=sh.rows, n=K, k=n, ldb=K, C=C[sh.row0:sh.row1], ldc=K)
         torch.cuda.synchronize()
-        C = torch.cat([out[r * mr: r * mr + shards[r].rows] for r in range(world)])
         assert C.shape == Cw.shape
         err = (C - Cw).abs()
         assert bool((err <= 2 * TOL_F32 * absd + 1e-30).all()), f"world {world} vs whole matrix"
@@ -149,11 +146,11 @@ def test_config4_products_k256_row_shards(oracle, device, products_k256):
 @pytest.mark.parametrize("chunks", [1, 4])
 def test_config4_native_multi_entry(oracle, device, products_k256, chunks):
     """spmm_csr_f32_multi (include/spmm_multi.h) over ncclCommInitAll on this
-    box's one GPU: every chunk goes through the in-place ncclAllGather of a
-    one-rank communicator and its event chain, as at P > 1. One chunk is the
-    same kernel on the same rows as the whole-matrix call (bit-identical);
-    four chunks overlap the exchange with the compute and agree within the
-    fp32 bar."""
+    box's one GPU: the chunks' kernels write straight into the n x K C and
+    run the per-chunk event chain of P > 1 (a one-part call has no peer to
+    exchange with). One chunk is the same kernel on the same rows as the
+    whole-matrix call (bit-identical); four chunks agree within the fp32
+    bar. The output is C itself: nothing past row n is written."""
     from spmm_hip import ops, prep
     rp, ci, v, K = products_k256
     n = rp.size - 1
@@ -165,15 +162,15 @@ def test_config4_native_multi_entry(oracle, device, products_k256, chunks):
     ops.csrmm(drp, dci, dv, B, n=K, k=n, ldb=K, C=Cw, ldc=K)
     mg = ops.MultiGPU([device.index or 0])
     bounds = prep.partition_rows(rp, 1)
-    slot = ops.MultiGPU.slot_rows(bounds, chunks)
-    Cm = torch.empty((chunks * slot, K), device=device)
+    Cm = torch.full((n + 1, K), float("nan"), device=device)
     mg.set_timing(True)
-    mg.csrmm(bounds, [(drp, dci, dv)], [ci.size], [B], [Cm], m=n, n=K, k=n, ldb=K, ldc=K,
+    mg.csrmm(bounds, [(drp, dci, dv)], [ci.size], [B], [Cm[:n]], m=n, n=K, k=n, ldb=K, ldc=K,
              chunks=chunks)
     mg.synchronize()
     comp, tot = mg.times()
     assert 0 < comp[0] <= tot[0]
     torch.cuda.synchronize()
+    assert bool(torch.isnan(Cm[n]).all())
     got = Cm[:n]
     if chunks == 1:
         assert torch.equal(got, Cw)
@@ -184,17 +181,17 @@ def test_config4_native_multi_entry(oracle, device, products_k256, chunks):
 
 
 def test_config4_native_multi_checks_outputs(device):
-    """MultiGPU.csrmm refuses a C shorter than the chunk-major output and a
-    tensor on another device before anything is launched (the kernel and the
-    in-place all-gather would write past a short C)."""
+    """MultiGPU.csrmm refuses a C shorter than m x n (ldc) and a tensor on
+    another device before anything is launched (the kernel and the exchange
+    would write past a short C)."""
     from spmm_hip import ops
     mg = ops.MultiGPU([device.index or 0])
     rp = torch.tensor([0, 1, 2], dtype=torch.int32, device=device)
     ci = torch.tensor([0, 1], dtype=torch.int32, device=device)
     v = torch.ones(2, device=device)
     B = torch.ones((2, 8), device=device)
-    short = torch.empty((3, 8), device=device)  # 4 chunks x 1 slot row x 8 needed = 32
-    with pytest.raises(ValueError, match="chunk-major"):
+    short = torch.empty((1, 8), device=device)  # m x n = 2 x 8 needed
+    with pytest.raises(ValueError, match="m x n output"):
         mg.csrmm([0, 2], [(rp, ci, v)], [2], [B], [short], m=2, n=8, k=2, ldb=8, ldc=8,
                  chunks=4)
     with pytest.raises(ValueError, match="HIP device"):
@@ -220,7 +217,7 @@ def test_config4_native_multi_orders_against_default_stream(device):
     ci = (torch.arange(2 * m, dtype=torch.int32, device=device) * 7) % m
     v = torch.ones(2 * m, device=device)
     B = torch.zeros((m, K), device=device)
-    C = torch.zeros((2 * m, K), device=device)  # 2 chunks x 1 part x m / 2 rows
+    C = torch.zeros((m, K), device=device)
     mg = ops.MultiGPU([device.index or 0])
     torch.cuda.synchronize()
     for rep in range(2):  # the ordering holds on every call, not only the first
@@ -234,11 +231,11 @@ def test_config4_native_multi_orders_against_default_stream(device):
 
 
 def test_config4_torch_distributed_world1(tmp_path):
-    """bench.py's N > 1 exchange path through RCCL on this one GPU: a fresh
-    child process initialises torch.distributed (nccl backend) at world 1
-    before any GPU call, then the in-place all-gather (chunks = 1, bit-identical
-    to the whole-matrix kernel) and chunked_spmm with 4 async all-gathers
-    overlapping the next chunk's kernel (within the fp32 bar)."""
+    """bench.py's N > 1 path through RCCL on this one GPU: a fresh child
+    process initialises torch.distributed (nccl backend) at world 1 before any
+    GPU call, then partitioned_spmm (chunks = 1, bit-identical to the
+    whole-matrix kernel) and chunked_spmm with 4 chunks (within the fp32 bar),
+    both into the contiguous n x K C, and a max-over-ranks all_reduce."""
     import subprocess
     import sys
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29541", RANK="0",
@@ -252,4 +249,4 @@ def test_config4_torch_distributed_world1(tmp_path):
     assert res["backend"] == "nccl" and res["world"] == 1
     assert res["chunks1_bit_identical"]
     assert res["chunks4_within_bar"] and res["chunks4_no_nan"], res
-    assert res["allgather_ms"] > 0
+    assert res["exchange_requests_world1"] == 0 and res["allreduce_max_ok"]

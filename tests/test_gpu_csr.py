@@ -419,14 +419,23 @@ def test_colmajor_forms_match_rowmajor(device, m, K, beta):
         assert torch.allclose(dCc.t(), dC, rtol=1e-6, atol=1e-5)
 
 
-def merge_path_model(oracle, rp, ci, v, B, nwaves):
-    """C of the merge-path kernel restated on the host (csr_kernels.hip; alpha
-    1, beta 0): the (rows + nnz) path cut at diagonals w * per, per =
+def merge_path_model(oracle, rp, ci, v, B, nwaves, alpha=1.0, beta=0.0, C0=None):
+    """C of the merge-path kernel restated on the host (csr_kernels.hip): the
+    (rows + nnz) path cut at diagonals w * per, per =
     ceil((m + nnz) / nwaves); nnz j of row r lies in wave (r + j) // per and
     the row's end in wave (r + re) // per. A row inside one wave is one
     sequential fp32 FMA chain (gespmm_csrmm.h:124-129); a row split over waves
     w_a .. w_b is ((c_a + c_{a+1}) + ... + c_{b-1}) + head, each term the chain
-    over that wave's share, the head (wave w_b's share) possibly empty."""
+    over that wave's share, the head (wave w_b's share) possibly empty.
+    Epilogue (alpha, beta, the old C0): an unsplit row is fma(beta, old,
+    alpha * acc) (alpha * acc at beta 0); a split row's last arrival writes
+    fma(alpha, sum, e), e = fma(beta, old, alpha * head) (alpha * head at beta
+    0). Restated in float32 numpy, so alpha and beta must be powers of two
+    (every product exact: each fma is one rounding of an exact sum, as
+    numpy's add)."""
+    for x in (alpha, beta):
+        assert x == 0 or float(np.log2(abs(x))).is_integer(), "alpha / beta: powers of two"
+    a32, b32 = np.float32(alpha), np.float32(beta)
     m, K = rp.size - 1, B.shape[1]
     nnz = int(rp[-1])
     per = -(-(m + nnz) // nwaves)
@@ -443,26 +452,35 @@ def merge_path_model(oracle, rp, ci, v, B, nwaves):
     seg_rp = np.asarray(seg_rp, np.int32)
     S = oracle_csrmm_f32(oracle, seg_rp.size - 1, K, seg_rp, ci, v, B, K, 0).reshape(-1, K)
     C = np.empty((m, K), np.float32)
+
+    def epi(x, r):
+        return a32 * x if beta == 0.0 else b32 * C0[r] + a32 * x
+
     for r, ids in enumerate(seg_of):
         if len(ids) == 1:
-            C[r] = S[ids[0]]
+            C[r] = epi(S[ids[0]], r)
             continue
         acc = S[ids[0]].copy()
         for s in ids[1:-1]:
             acc = acc + S[s]
-        C[r] = acc + S[ids[-1]]
+        C[r] = a32 * acc + epi(S[ids[-1]], r)
     return C
 
 
-@pytest.mark.parametrize("K,opts", [(128, 0), (512, 0), (256, 0), (32, 2), (64, 0)])
-def test_split_rows_bit_exact_model(oracle, device, K, opts):
+@pytest.mark.parametrize("K,opts,alpha,beta", [
+    (128, 0, 1.0, 0.0), (512, 0, 1.0, 0.0), (256, 0, 1.0, 0.0), (32, 2, 1.0, 0.0),
+    (64, 0, 1.0, 0.0), (128, 0, 2.0, 0.5), (512, 0, -0.5, 2.0), (256, 0, 0.25, -1.0),
+    (32, 2, 2.0, -0.5), (64, 0, -2.0, 0.5), (64, 0, 0.7, -1.3), (128, 0, 0.7, -1.3)])
+def test_split_rows_bit_exact_model(oracle, device, K, opts, alpha, beta):
     """Every row, split or not, is bit-identical to merge_path_model: the
     split rows finished in the same launch by their last-arriving wave (split
     row tickets, csr_kernels.hip) sum their partials in wave order. Power-law
     rows with hubs that span dozens of waves, empty rows, K at every vector
     width of the main kernel (K = 32 with SPMM_CSR_SEQUENTIAL_ROWS; K = 64 is
     the lane-group kernel, whose rows are interleaved chains: checked within
-    the bar)."""
+    the bar). alpha != 1 and beta != 0 (a finite C0 read by the finishing
+    wave): bit-exact for powers of two, within the bar against the f64
+    oracle of alpha A B + beta C0 for any other pair."""
     from spmm_hip import prep
     from spmm_hip._lib import CSR_NT_STREAMS
     ops = _ops()
@@ -470,19 +488,26 @@ def test_split_rows_bit_exact_model(oracle, device, K, opts):
     rp, ci = prep.powerlaw_csr(m, nnz, 15000, 2.1, 11)
     v = np.random.default_rng(3).uniform(-1, 1, ci.size).astype(np.float32)
     B = np.random.default_rng(4).uniform(-1, 1, (m, K)).astype(np.float32)
+    C0 = np.random.default_rng(5).uniform(-1, 1, (m, K)).astype(np.float32)
     drp, dci, dv, dB = _dev(rp, ci, v, B)
     h = ops.Handle()
     h.set_csr_options(CSR_NT_STREAMS | opts)
-    C = torch.full((m, K), float("nan"), device=device)
-    ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=C, ldc=K, handle=h)
+    init = (lambda: torch.from_numpy(C0).to(device)) if beta != 0.0 else \
+        (lambda: torch.full((m, K), float("nan"), device=device))
+    C = init()
+    ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=C, ldc=K, alpha=alpha, beta=beta, handle=h)
     torch.cuda.synchronize()
     got = C.cpu().numpy()
     cus = torch.cuda.get_device_properties(device).multi_processor_count
     nwaves = min(-(-(m + ci.size) // 256), cus * 16)  # kMinItemsPerWave, csr_kernels.hip
-    if K == 64:
-        _check_rowmajor(oracle, rp, ci, v, B, C, "lane-group kernel, split rows")
+    pow2 = all(x == 0 or float(np.log2(abs(x))).is_integer() for x in (alpha, beta))
+    if K == 64 or not pow2:
+        ref, absd = oracle_csrmm_f64(oracle, m, K, rp, ci, v, B, K, 0)
+        ref = alpha * ref + beta * C0.astype(np.float64)
+        absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+        assert_normwise(got, ref, absd, TOL_F32, f"K={K} alpha={alpha} beta={beta}, split rows")
         return
-    want = merge_path_model(oracle, rp, ci, v, B, nwaves)
+    want = merge_path_model(oracle, rp, ci, v, B, nwaves, alpha, beta, C0)
     per = -(-(m + ci.size) // nwaves)
     split = np.array([(r + rp[r]) // per != (r + rp[r + 1]) // per for r in range(m)])
     assert split.sum() > 50, "the case must split many rows"
@@ -492,7 +517,9 @@ def test_split_rows_bit_exact_model(oracle, device, K, opts):
                            f"split rows)")
     # repeated launches: the tickets are back at zero after every launch
     for _ in range(3):
-        ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=C, ldc=K, handle=h)
+        C = init()
+        ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=C, ldc=K, alpha=alpha, beta=beta,
+                  handle=h)
     torch.cuda.synchronize()
     assert np.array_equal(C.cpu().numpy(), want), "relaunch differs"
     h.close()
