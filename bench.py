@@ -863,6 +863,36 @@ def run_csr(args, W, world, rank, dev, dist):
     return rec, (rp, ci, K)
 
 
+def _timed_analysis(make):
+    """A group analysis timed twice (host wall clock to the end of its work on the
+    stream): the first call on the handle (it loads the analysis kernels and grows
+    the handle's buffers), then a second on a fresh object, the once-per-matrix
+    cost of a warm process. Returns (the second object, first ms, repeat ms)."""
+    import torch
+    ts, obj = [], None
+    for _ in range(2):
+        if obj is not None:
+            obj.close()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        obj = make()
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return obj, ts[0], ts[1]
+
+
+def _epoch_loop(analysis_ms: float, grouped_ms: float, dropin_ms: float, epochs: int = 10):
+    """run_csrmm.cu:120-159's loop of 10 products on one matrix: the grouped
+    entry pays its analysis once, the drop-in stream nothing."""
+    g = analysis_ms + epochs * grouped_ms
+    d = epochs * dropin_ms
+    return {"epoch_loop": {"epochs": epochs, "grouped_with_analysis_ms": round(g, 3),
+                           "drop_in_ms": round(d, 3), "grouped_wins": bool(g < d),
+                           "note": "run_csrmm.cu:120-159's epoch loop; analysis_ms_repeat + "
+                                   "epochs x grouped ms_per_step against epochs x the drop-in "
+                                   "line's ms_per_step"}}
+
+
 def run_bsr(args, W, world, rank, dev, dist):
     import torch
     from spmm_hip import ops, prep
@@ -890,17 +920,14 @@ def run_bsr(args, W, world, rank, dev, dist):
     fn = ops.bsrmm if dt == "fp32" else ops.bsrmm_f16
     an = bool(W.get("analysed"))
     gw = int(args.group_rows or W.get("grouped") or 0)
-    analysis_ms = None
+    analysis_ms = analysis_first_ms = None
     grp = None
     if gw:
         if (bs, dt) not in ((16, "fp16"), (32, "fp32")):
             raise SystemExit("the grouped streams are bs 16 fp16 and bs 32 fp32")
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
         Grouped = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
-        grp = Grouped(d_brp, d_bci, d_bv, mb=mb, group_rows=gw, handle=h)
-        torch.cuda.synchronize()
-        analysis_ms = (time.perf_counter() - t0) * 1e3
+        grp, analysis_first_ms, analysis_ms = _timed_analysis(
+            lambda: Grouped(d_brp, d_bci, d_bv, mb=mb, group_rows=gw, handle=h))
         del d_bv
 
         def fn(rp_, ci_, _v, B_, *, mb, kb, n, bs, ldb, C, ldc, order_b=ops.ORDER_ROW,
@@ -1074,6 +1101,7 @@ def run_bsr(args, W, world, rank, dev, dist):
                   "full_panel_model_GBps": round(kbytes / t / 1e9, 1)},
         csr_same_matrix_ms=round(csr_ms, 4), csr2bsr_host_seconds=round(t_conv, 2),
         analysis_ms=round(analysis_ms, 4) if (an or grp is not None) else None,
+        analysis_ms_first_call=(round(analysis_first_ms, 4) if grp is not None else None),
         gen_seconds=round(t_gen, 2), reorder=reorder)
     tr = rec["roofline"]["traffic"]
     if tr:
@@ -1086,11 +1114,8 @@ def run_bsr(args, W, world, rank, dev, dist):
             (bs, dt) == (16, "fp16")):
         # Beside the drop-in line (not `value`): the grouped stream (groups of 4 block
         # rows sharing their B-row copies, analysis once, timed apart).
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        g4 = ops.GroupedBsr16(d_brp, d_bci, d_bv, mb=mb, group_rows=4, handle=h)
-        torch.cuda.synchronize()
-        a_ms = (time.perf_counter() - t0) * 1e3
+        g4, a_ms, a_rep = _timed_analysis(lambda: ops.GroupedBsr16(d_brp, d_bci, d_bv, mb=mb,
+                                                                   group_rows=4, handle=h))
         e_g, k_g = timed_loop(lambda: g4.mm(B, kb=mb, n=K, ldb=K, C=C, ldc=K), h, args.steps,
                               args.warmup, 1, dist)
         ni = (g4.bytes - 256) // (64 + 4 * 512)
@@ -1099,19 +1124,18 @@ def run_bsr(args, W, world, rank, dev, dist):
                      "spmm_bsrmm_grouped_f16 per step",
             "value": round(2.0 * nnz * K * args.steps / e_g / 1e9, 2), "unit": "GFLOP/s",
             "ms_per_step": round(e_g / args.steps * 1e3, 4), "kernel_ms": round(k_g, 4),
-            "analysis_ms_first_call": round(a_ms, 3), "items": int(ni),
-            "mfma_executed_TFLOPs": round(ni * 4 * 2.0 * 256 * K / (k_g / 1e3) / 1e12, 2)}
+            "analysis_ms_first_call": round(a_ms, 3), "analysis_ms_repeat": round(a_rep, 3),
+            "items": int(ni),
+            "mfma_executed_TFLOPs": round(ni * 4 * 2.0 * 256 * K / (k_g / 1e3) / 1e12, 2),
+            **_epoch_loop(a_rep, e_g / args.steps * 1e3, elapsed / args.steps * 1e3)}
         g4.close()
         del g4
     if (not an and grp is None and args.bsr_layout == "row" and not args.no_analysed_side and
             (bs, dt) == (32, "fp32") and K % 4 == 0):
         # Beside the drop-in line (not `value`): the grouped bs 32 stream (groups of 2 block
         # rows sharing their B-row copies, analysis once, timed apart; C bit-identical)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        g2 = ops.GroupedBsr32(d_brp, d_bci, d_bv, mb=mb, group_rows=GRP32_W, handle=h)
-        torch.cuda.synchronize()
-        a_ms = (time.perf_counter() - t0) * 1e3
+        g2, a_ms, a_rep = _timed_analysis(lambda: ops.GroupedBsr32(d_brp, d_bci, d_bv, mb=mb,
+                                                                   group_rows=GRP32_W, handle=h))
         e_g, k_g = timed_loop(lambda: g2.mm(B, kb=mb, n=K, ldb=K, C=C, ldc=K), h, args.steps,
                               args.warmup, 1, dist)
         rec["grouped_entry"] = {
@@ -1119,9 +1143,10 @@ def run_bsr(args, W, world, rank, dev, dist):
                      "spmm_bsrmm_grouped_f32 per step",
             "value": round(2.0 * nnz * K * args.steps / e_g / 1e9, 2), "unit": "GFLOP/s",
             "ms_per_step": round(e_g / args.steps * 1e3, 4), "kernel_ms": round(k_g, 4),
-            "analysis_ms_first_call": round(a_ms, 3),
+            "analysis_ms_first_call": round(a_ms, 3), "analysis_ms_repeat": round(a_rep, 3),
             "mfma_executed_TFLOPs": round(mfma_flops / (k_g / 1e3) / 1e12, 2),
-            "mfma_frac": round(mfma_flops / (k_g / 1e3) / 1e12 / peak, 4)}
+            "mfma_frac": round(mfma_flops / (k_g / 1e3) / 1e12 / peak, 4),
+            **_epoch_loop(a_rep, e_g / args.steps * 1e3, elapsed / args.steps * 1e3)}
         g2.close()
         del g2
     if (not an and grp is None and args.bsr_layout == "row" and not args.no_analysed_side and

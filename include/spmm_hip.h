@@ -290,11 +290,18 @@ spmm_status_t spmm_bsrmm_analysed_f16(spmm_handle_t handle, int mb, int kb, int 
  * B row the union of their nonzero columns needs: on a reordered graph
  * neighbouring block rows need mostly the same rows (products stand-in: the
  * union is 0.43 of the (block row, column) pairs at 4 rows, 0.29 at 8).
- * Two phases: with buffer == NULL, *bufferBytes receives the size of the
- * caller-owned device buffer; with a buffer of that size the analysis fills
- * it. It checks the row pointer on the host and sums the groups' item counts
- * there, so the call synchronises the handle's stream. The handle records the
- * buffer's layout:
+ * Two phases: with buffer == NULL (the size query), *bufferBytes receives the
+ * size of the caller-owned device buffer; with a buffer of that size the
+ * analysis fills it. Everything runs on the device: the size query checks the
+ * row pointer, counts and sums the groups' items there and synchronises the
+ * handle's stream once (16 bytes come back for the size); the filling call
+ * with the same arguments starts from the size query's device results, kept
+ * on the handle, and only launches kernels and async copies (no
+ * synchronisation, no host data: it can be captured in a HIP graph once the
+ * handle's workspace has grown to the matrix). The arrays must not change
+ * between the two calls (as between cuSPARSE's bufferSize and preprocess);
+ * a filling call without a size query of the same arguments runs one first.
+ * The handle records the buffer's layout:
  * spmm_bsrmm_grouped_f16 on the same handle takes it (until
  * spmm_bsr16_group_release or another analysis into the same buffer).
  * INVALID_VALUE for a bad dir / groupRows, negative sizes, null pointers that

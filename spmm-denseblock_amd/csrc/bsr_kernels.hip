@@ -3648,7 +3648,7 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
 // is all zeros) and, at BS 32, the per-(item, wave) masks of held entries.
 // ---------------------------------------------------------------------------
 template <int W, int BS, bool PASS2>
-__global__ __launch_bounds__(256) void grp_build_kernel(int mb, int ngroups,
+__global__ __launch_bounds__(256) void grp_build_kernel(int mb, int nnzb, int ngroups,
                                                         const int* __restrict__ rp,
                                                         const int* __restrict__ ci,
                                                         const unsigned* __restrict__ mk,
@@ -3662,14 +3662,20 @@ __global__ __launch_bounds__(256) void grp_build_kernel(int mb, int ngroups,
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= ngroups) return;
   int cur[W], end[W];
-  bool bad = false;
+  // the row pointer is checked here, before it indexes the block columns: within
+  // [0, nnzb], never decreasing, rp[0] = 0 and rp[mb] = nnzb (a group with a bad
+  // row walks nothing and reports INT_MIN)
+  bool bad = (g == 0 && rp[0] != 0) || (g == ngroups - 1 && rp[mb] != nnzb);
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     const int br = g * W + w;
     cur[w] = br < mb ? rp[br] : 0;
     end[w] = br < mb ? rp[br + 1] : 0;
-    bad |= end[w] < cur[w];
-    if (end[w] < cur[w]) end[w] = cur[w];
+    bad |= end[w] < cur[w] || cur[w] < 0 || end[w] > nnzb;
+  }
+  if (bad) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) end[w] = cur[w] = 0;
   }
   long long e = 0;  // entries so far
   int hi = -1;
@@ -3745,9 +3751,9 @@ __global__ __launch_bounds__(256) void grp_build_kernel(int mb, int ngroups,
   }
 }
 
-spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int mb, int ngroups,
-                               const int* rp, const int* ci, const unsigned* mk, int* cnt,
-                               int* maxj, const int* item_ptr, int* rows, int* src,
+spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int mb, int nnzb,
+                               int ngroups, const int* rp, const int* ci, const unsigned* mk,
+                               int* cnt, int* maxj, const int* item_ptr, int* rows, int* src,
                                unsigned* wmask) {
   if (ngroups == 0) return SPMM_STATUS_SUCCESS;
   const dim3 grid((ngroups + 255) / 256);
@@ -3755,10 +3761,10 @@ spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int
   do {                                                                                           \
     if (pass2)                                                                                   \
       hipLaunchKernelGGL((grp_build_kernel<W_, BS_, true>), grid, dim3(256), 0, ctx->stream, mb, \
-                         ngroups, rp, ci, mk, cnt, maxj, item_ptr, rows, src, wmask);             \
+                         nnzb, ngroups, rp, ci, mk, cnt, maxj, item_ptr, rows, src, wmask);       \
     else                                                                                         \
       hipLaunchKernelGGL((grp_build_kernel<W_, BS_, false>), grid, dim3(256), 0, ctx->stream,    \
-                         mb, ngroups, rp, ci, mk, cnt, maxj, item_ptr, rows, src, wmask);        \
+                         mb, nnzb, ngroups, rp, ci, mk, cnt, maxj, item_ptr, rows, src, wmask);  \
   } while (0)
   if (BS == 16) {
     if (W == 8) GRP_BUILD(8, 16);
@@ -3769,6 +3775,41 @@ spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int
     else GRP_BUILD(2, 32);
   }
 #undef GRP_BUILD
+  return from_hip(hipGetLastError());
+}
+
+// One workgroup: stats[0] = max maxj (-1 when n = 0), stats[1] = any INT_MIN.
+__global__ __launch_bounds__(1024) void grp_stats_kernel(const int* __restrict__ maxj, int n,
+                                                         int* __restrict__ stats) {
+  __shared__ int smax[16], sbad[16];
+  int hi = -1, bad = 0;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const int x = maxj[i];
+    bad |= x == INT_MIN;
+    hi = max(hi, x);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    hi = max(hi, __shfl_xor(hi, o));
+    bad |= __shfl_xor(bad, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    smax[threadIdx.x >> 6] = hi;
+    sbad[threadIdx.x >> 6] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; ++w) {
+      hi = max(hi, smax[w]);
+      bad |= sbad[w];
+    }
+    stats[0] = hi;
+    stats[1] = bad;
+  }
+}
+
+spmm_status_t launch_grp_stats(spmm_context* ctx, const int* maxj, int n, int* stats) {
+  hipLaunchKernelGGL(grp_stats_kernel, dim3(1), dim3(1024), 0, ctx->stream, maxj, n, stats);
   return from_hip(hipGetLastError());
 }
 

@@ -35,6 +35,10 @@ spmm_status_t ensure_scratch(spmm_context* ctx, size_t bytes) {
   return grow_buffer(ctx, ctx->scratch, ctx->scratch_bytes, bytes);
 }
 
+spmm_status_t ensure_group_pending(spmm_context* ctx, size_t bytes) {
+  return grow_buffer(ctx, ctx->grp_pend, ctx->grp_pend_bytes, bytes);
+}
+
 spmm_status_t ensure_order_buffer(spmm_context* ctx, size_t n) {
   if (n <= ctx->order_cap) return SPMM_STATUS_SUCCESS;
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -164,8 +168,10 @@ spmm_status_t spmm_create(spmm_handle_t* handle) {
 
 spmm_status_t spmm_destroy(spmm_handle_t h) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
-  if (h->ws || h->scratch || h->order || h->tickets) (void)hipStreamSynchronize(h->stream);
+  if (h->ws || h->scratch || h->order || h->tickets || h->grp_pend)
+    (void)hipStreamSynchronize(h->stream);
   if (h->ws) (void)hipFree(h->ws);
+  if (h->grp_pend) (void)hipFree(h->grp_pend);
   if (h->tickets) (void)hipFree(h->tickets);
   if (h->scratch) (void)hipFree(h->scratch);
   if (h->order) (void)hipFree(h->order);

@@ -59,6 +59,22 @@ struct spmm_context {
     size_t wmask_off = 0;
   };
   std::map<const void*, GroupPlan> group_plans;
+  // The size query of a group analysis (buffer == NULL) leaves its device results
+  // (column masks, item pointers) in grp_pend for the filling call with the same
+  // arguments, which then needs neither those kernels again nor any host round trip
+  // (group.cpp). Cleared by that call and by a size query of other arguments.
+  struct GroupPending {
+    bool valid = false;
+    int bs = 0, W = 0, dir = 0, mb = 0, nnzb = 0;
+    const void *rp = nullptr, *ci = nullptr, *val = nullptr;
+    long long nitems = 0;
+    int max_col = -1;
+    size_t need = 0, rows_off = 0, wmask_off = 0, afrag_off = 0;
+    size_t ptr_off = 0;  // offset of the item pointers in grp_pend (masks at 0)
+  };
+  GroupPending grp_pending;
+  void* grp_pend = nullptr;
+  size_t grp_pend_bytes = 0;
 
   // Kernel timing ring.
   bool timing = false;
@@ -77,6 +93,8 @@ spmm_status_t ensure_workspace(spmm_context* ctx, size_t bytes);
 spmm_status_t ensure_scratch(spmm_context* ctx, size_t bytes);
 // The same for the block-row order buffer (at least n ints).
 spmm_status_t ensure_order_buffer(spmm_context* ctx, size_t n);
+// The same for the pending group analysis (grp_pend).
+spmm_status_t ensure_group_pending(spmm_context* ctx, size_t bytes);
 // At least n zeroed ticket words (zeroed on the handle's stream when grown).
 spmm_status_t ensure_tickets(spmm_context* ctx, size_t n);
 
@@ -154,11 +172,18 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
                                        const int* item_ptr, const int* rows,
                                        const unsigned* afrag, const uint16_t* B16, int ldb,
                                        float alpha, float beta, float* C, int ldc, bool crow);
-// the group analyses' device merge (grp_build_kernel: PASS 1 counts, PASS 2 writes)
-spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int mb, int ngroups,
-                               const int* rp, const int* ci, const unsigned* mk, int* cnt,
-                               int* maxj, const int* item_ptr, int* rows, int* src,
+// the group analyses' device merge (grp_build_kernel: PASS 1 checks the row pointer
+// and counts, PASS 2 writes)
+spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int mb, int nnzb,
+                               int ngroups, const int* rp, const int* ci, const unsigned* mk,
+                               int* cnt, int* maxj, const int* item_ptr, int* rows, int* src,
                                unsigned* wmask);
+// stats[0] = max over maxj[0..n), stats[1] = 1 if any maxj is INT_MIN (pass 1's "bad")
+spmm_status_t launch_grp_stats(spmm_context* ctx, const int* maxj, int n, int* stats);
+// exclusive scan of count[0..n) into out[0..n] (out[0] = 0) and *total (one workgroup,
+// convert_kernels.hip)
+spmm_status_t launch_scan_counts(spmm_context* ctx, const int* count, int n, int* out,
+                                 long long* total);
 // the grouped bs 32 stream (row-major B and C)
 spmm_status_t launch_bsr32_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
                                     const int* rows, const int* src, const float* val,

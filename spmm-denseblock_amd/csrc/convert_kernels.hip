@@ -194,6 +194,16 @@ __global__ __launch_bounds__(256) void coo2csr_kernel(const int* __restrict__ co
 
 }  // namespace
 
+namespace spmm {
+
+spmm_status_t launch_scan_counts(spmm_context* ctx, const int* count, int n, int* out,
+                                 long long* total) {
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, count, n, 0, out, total);
+  return from_hip(hipGetLastError());
+}
+
+}  // namespace spmm
+
 extern "C" {
 
 spmm_status_t spmm_xcoo2csr(spmm_handle_t handle, const int* cooRowInd, int nnz, int m,

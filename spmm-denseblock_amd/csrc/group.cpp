@@ -4,22 +4,29 @@
 // DESIGN.md §4, "The grouped stream".
 //
 // Once per matrix, like spmm_bsr16_analysis_f16 and cuSPARSE's SpMM preprocess
-// (the reference's rocsparse_bsrmm.h:102-256 has none):
-//  1. the row pointer is checked on the host; the device computes every block's
-//     column mask (bsr16 / bsr32_analysis_kernel, masks only);
-//  2. grp_build_kernel, one thread per group of W adjacent block rows, merges the
-//     W sorted block-column lists and enumerates the union of their nonzero
-//     columns in (block column J, column c) order, cut into items of E entries (16
-//     at bs 16, 8 at bs 32; the last one padded with row -1). PASS 1 counts each
-//     group's items; the host sums them into the item pointers; PASS 2 writes the
-//     B row J*bs + c of each entry and, per wave w of the group, the block of row
-//     w holding block column J (-1: none; at bs 32 also -1 when that block's
-//     column c is all zeros, plus the per-(item, wave) mask of the entries whose
-//     source is a block: the MFMAs that wave runs);
-//  3. the fill kernels write each wave's A fragment of each item into the
-//     caller's buffer.
-// The call synchronises the handle's stream (twice: the row pointer, the counts).
-// Round 4's first form merged on the host: 0.27-0.46 s on the products stand-in.
+// (the reference's rocsparse_bsrmm.h:102-256 has none), as two calls:
+//  size query (buffer == NULL):
+//  1. the device computes every block's column mask (bsr16 / bsr32_analysis_kernel,
+//     masks only);
+//  2. grp_build_kernel PASS 1, one thread per group of W adjacent block rows, checks
+//     the group's row pointer entries, merges the W sorted block-column lists and
+//     counts the items of the union of their nonzero columns in (block column J,
+//     column c) order, cut into items of E entries (16 at bs 16, 8 at bs 32; the
+//     last one padded with row -1);
+//  3. a one-workgroup scan sums the counts into the item pointers, a reduction
+//     finds the largest block column and any bad group; 16 bytes come back to the
+//     host (the analysis's one synchronisation) and size the buffer;
+//  filling call (the caller's buffer, same arguments):
+//  4. PASS 2 writes the B row J*bs + c of each entry and, per wave w of the group,
+//     the block of row w holding block column J (-1: none; at bs 32 also -1 when
+//     that block's column c is all zeros, plus the per-(item, wave) mask of the
+//     entries whose source is a block: the MFMAs that wave runs);
+//  5. the fill kernels write each wave's A fragment of each item.
+// The filling call reuses the size query's device results (handle->grp_pending):
+// the arrays must not change between the two calls, as between cuSPARSE's
+// bufferSize and preprocess calls. It launches kernels and async copies only.
+// Round 4's first form merged on the host (0.27-0.46 s on the products stand-in),
+// and its second ran the masks and PASS 1 again behind two synchronisations.
 //
 // Buffer layout (caller-owned device memory, bufferBytes from the first call):
 //   [0, 256)                 reserved header
@@ -45,10 +52,17 @@ namespace {
 constexpr size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // The analysis of either stream: BS 16 (fp16 values, W = 2 / 4 / 8) or 32 (fp32, W = 2 / 4).
-// Everything runs on the device but the item pointers' prefix sum: masks
+// Everything runs on the device. The size query (buffer == NULL): the column masks
 // (bsr16 / bsr32_analysis_kernel, masks only), the per-group merge counting items
-// (grp_build_kernel PASS 1), the prefix sum on the host (one int per group), the
-// merge writing entries (PASS 2), the A fragments (the fill kernels).
+// (grp_build_kernel PASS 1, which also checks the row pointer), the item pointers'
+// scan and the stats (largest block column, bad rows); one 16-B copy to the host
+// and the only synchronisation of the analysis, for the size the caller must
+// allocate. The results stay on the handle (grp_pending). The filling call
+// (buffer != NULL) with the same arguments starts from them: the header and the
+// item pointers into the buffer, the merge writing entries (PASS 2), the A
+// fragments (the fill kernels); it neither synchronises nor reads anything on the
+// host, so it can be captured in a graph. A filling call without that size query
+// runs it first.
 spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir, int mb, int nnzb,
                              int groupRows, const int* bsrRowPtr, const int* bsrColInd,
                              const void* bsrVal, void* buffer, size_t* bufferBytes) {
@@ -67,91 +81,109 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
   const int E = BS == 16 ? 16 : 8;  // entries per item
   const int ngroups = (mb + W - 1) / W;
   hipStream_t st = handle->stream;
-  // scratch: masks [nnzb], per-group item counts and largest block columns [2 ngroups]
-  const size_t mk_bytes = ((size_t)nnzb * 4 + 255) & ~size_t(255);
-  if (spmm_status_t s = ensure_scratch(handle, mk_bytes + (size_t)ngroups * 8 + 8)) return s;
-  unsigned* dmk = static_cast<unsigned*>(handle->scratch);
-  int* dcnt = reinterpret_cast<int*>(static_cast<char*>(handle->scratch) + mk_bytes);
-  int* dmaxj = dcnt + ngroups;
-  std::vector<int> cnt(ngroups), maxj(ngroups);
-  if (mb > 0) {
-    // the row pointer is checked on the host before any kernel indexes the block columns
-    // with it (0 .. nnzb, never decreasing)
-    std::vector<int> rp(mb + 1);
-    hipError_t e = hipMemcpyAsync(rp.data(), bsrRowPtr, (size_t)(mb + 1) * 4,
-                                  hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+  auto& pend = handle->grp_pending;
+  const bool same = pend.valid && pend.bs == BS && pend.W == W && pend.dir == (int)dir &&
+                    pend.mb == mb && pend.nnzb == nnzb && pend.rp == bsrRowPtr &&
+                    pend.ci == bsrColInd && pend.val == bsrVal;
+  if (!same) {
+    // the size query: masks [nnzb], item pointers [ngroups + 1] and the stats in grp_pend,
+    // per-group counts and largest block columns [2 ngroups] in the scratch
+    pend.valid = false;
+    const size_t mk_bytes = align256((size_t)nnzb * 4);
+    const size_t ptr_off = mk_bytes;
+    const size_t stat_off = align256(ptr_off + (size_t)(ngroups + 1) * 4);
+    if (spmm_status_t s = ensure_group_pending(handle, stat_off + 256)) return s;
+    if (spmm_status_t s = ensure_scratch(handle, (size_t)ngroups * 8 + 8)) return s;
+    char* pb = static_cast<char*>(handle->grp_pend);
+    unsigned* dmk = reinterpret_cast<unsigned*>(pb);
+    int* dptr = reinterpret_cast<int*>(pb + ptr_off);
+    long long* dtot = reinterpret_cast<long long*>(pb + stat_off);
+    int* dstat = reinterpret_cast<int*>(pb + stat_off + 8);
+    int* dcnt = static_cast<int*>(handle->scratch);
+    int* dmaxj = dcnt + ngroups;
+    hipError_t e = hipMemsetAsync(pb + stat_off, 0, 16, st);
     if (e != hipSuccess) return from_hip(e);
-    if (rp[0] != 0 || rp[mb] != nnzb) return SPMM_STATUS_INVALID_VALUE;
-    for (int i = 0; i < mb; ++i)
-      if (rp[i + 1] < rp[i]) return SPMM_STATUS_INVALID_VALUE;
-    if (nnzb > 0) {
+    if (nnzb > 0 && mb > 0) {
       spmm_status_t s = BS == 16
           ? launch_bsr16_analysis(handle, dir, nnzb, static_cast<const uint16_t*>(bsrVal), dmk, nullptr)
           : launch_bsr32_analysis(handle, dir, nnzb, static_cast<const float*>(bsrVal), dmk, nullptr);
       if (s) return s;
     }
-    if (spmm_status_t s = launch_grp_build(handle, W, BS, false, mb, ngroups, bsrRowPtr, bsrColInd,
-                                           dmk, dcnt, dmaxj, nullptr, nullptr, nullptr, nullptr))
-      return s;
-    e = hipMemcpyAsync(cnt.data(), dcnt, (size_t)ngroups * 4, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(maxj.data(), dmaxj, (size_t)ngroups * 4, hipMemcpyDeviceToHost, st);
+    if (mb > 0) {
+      if (spmm_status_t s = launch_grp_build(handle, W, BS, false, mb, nnzb, ngroups, bsrRowPtr,
+                                             bsrColInd, dmk, dcnt, dmaxj, nullptr, nullptr, nullptr,
+                                             nullptr))
+        return s;
+      if (spmm_status_t s = launch_scan_counts(handle, dcnt, ngroups, dptr, dtot)) return s;
+      if (spmm_status_t s = launch_grp_stats(handle, dmaxj, ngroups, dstat)) return s;
+    } else {
+      e = hipMemsetAsync(dptr, 0, 4, st);
+      if (e != hipSuccess) return from_hip(e);
+      e = hipMemsetAsync(dstat, 0xff, 4, st);  // max_col -1
+      if (e != hipSuccess) return from_hip(e);
+    }
+    struct { long long total; int max_col, bad; } host{};
+    e = hipMemcpyAsync(&host, dtot, 16, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return from_hip(e);
+    if (host.bad) return SPMM_STATUS_INVALID_VALUE;  // a bad row pointer or negative block column
+    if (host.total > INT_MAX) return SPMM_STATUS_NOT_SUPPORTED;  // int32 item pointers
+    const long long nitems = host.total;
+    pend.rows_off = align256(256 + (size_t)(ngroups + 1) * 4);
+    pend.wmask_off = align256(pend.rows_off + (size_t)nitems * E * 4);  // bs 32 only
+    pend.afrag_off = BS == 16 ? pend.wmask_off : align256(pend.wmask_off + (size_t)nitems * W * 4);
+    pend.need = pend.afrag_off + (size_t)nitems * W * (BS == 16 ? 512 : 1024);
+    pend.nitems = nitems;
+    pend.max_col = host.max_col;
+    pend.ptr_off = ptr_off;
+    pend.bs = BS;
+    pend.W = W;
+    pend.dir = (int)dir;
+    pend.mb = mb;
+    pend.nnzb = nnzb;
+    pend.rp = bsrRowPtr;
+    pend.ci = bsrColInd;
+    pend.val = bsrVal;
+    pend.valid = true;
   }
-  int max_col = -1;
-  std::vector<int> item_ptr(ngroups + 1, 0);
-  long long acc = 0;
-  for (int g = 0; g < ngroups; ++g) {
-    if (maxj[g] == INT_MIN) return SPMM_STATUS_INVALID_VALUE;  // a negative block column
-    max_col = std::max(max_col, maxj[g]);
-    acc += cnt[g];
-    if (acc > INT_MAX) return SPMM_STATUS_NOT_SUPPORTED;  // int32 item pointers
-    item_ptr[g + 1] = (int)acc;
-  }
-  const long long nitems = acc;
-  const size_t rows_off = align256(256 + (size_t)(ngroups + 1) * 4);
-  const size_t wmask_off = align256(rows_off + (size_t)nitems * E * 4);  // bs 32 only
-  const size_t afrag_off = BS == 16 ? wmask_off : align256(wmask_off + (size_t)nitems * W * 4);
-  const size_t need = afrag_off + (size_t)nitems * W * (BS == 16 ? 512 : 1024);
   if (!buffer) {
-    *bufferBytes = need;
+    *bufferBytes = pend.need;
     return SPMM_STATUS_SUCCESS;
   }
-  if (*bufferBytes < need) return SPMM_STATUS_INVALID_VALUE;
+  if (*bufferBytes < pend.need) return SPMM_STATUS_INVALID_VALUE;
+  pend.valid = false;  // consumed: another analysis starts from its own size query
+  const long long nitems = pend.nitems;
   char* buf = static_cast<char*>(buffer);
+  const char* pb = static_cast<const char*>(handle->grp_pend);
   hipError_t e = hipMemsetAsync(buf, 0, 256, st);
   if (e == hipSuccess)
-    e = hipMemcpyAsync(buf + 256, item_ptr.data(), (size_t)(ngroups + 1) * 4, hipMemcpyHostToDevice,
-                       st);
+    e = hipMemcpyAsync(buf + 256, pb + pend.ptr_off, (size_t)(ngroups + 1) * 4,
+                       hipMemcpyDeviceToDevice, st);
   if (e != hipSuccess) return from_hip(e);
   if (nitems) {
-    // the entry sources in the workspace (the masks stay in the scratch buffer)
+    // the entry sources in the workspace (the masks stay in grp_pend)
     if (spmm_status_t s = ensure_workspace(handle, (size_t)nitems * E * W * 4)) return s;
     int* dsrc = static_cast<int*>(handle->ws);
-    int* drows = reinterpret_cast<int*>(buf + rows_off);
-    if (spmm_status_t s = launch_grp_build(handle, W, BS, true, mb, ngroups, bsrRowPtr, bsrColInd,
-                                           dmk, nullptr, nullptr,
-                                           reinterpret_cast<const int*>(buf + 256), drows, dsrc,
-                                           reinterpret_cast<unsigned*>(buf + wmask_off)))
+    int* drows = reinterpret_cast<int*>(buf + pend.rows_off);
+    if (spmm_status_t s = launch_grp_build(handle, W, BS, true, mb, nnzb, ngroups, bsrRowPtr,
+                                           bsrColInd, reinterpret_cast<const unsigned*>(pb), nullptr,
+                                           nullptr, reinterpret_cast<const int*>(buf + 256), drows,
+                                           dsrc, reinterpret_cast<unsigned*>(buf + pend.wmask_off)))
       return s;
     spmm_status_t s = BS == 16
         ? launch_bsr16_grp_fill(handle, nitems, W, dir, drows, dsrc,
                                 static_cast<const uint16_t*>(bsrVal),
-                                reinterpret_cast<unsigned*>(buf + afrag_off))
+                                reinterpret_cast<unsigned*>(buf + pend.afrag_off))
         : launch_bsr32_grp_fill(handle, nitems, W, dir, drows, dsrc,
                                 static_cast<const float*>(bsrVal),
-                                reinterpret_cast<float*>(buf + afrag_off));
+                                reinterpret_cast<float*>(buf + pend.afrag_off));
     if (s) return s;
   }
-  // the host item pointers are freed on return: wait for the copy that reads them
-  e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return from_hip(e);
   std::lock_guard<std::mutex> lk(handle->mu);
-  spmm_context::GroupPlan plan{W, mb, ngroups, nitems, need, rows_off, afrag_off, max_col};
+  spmm_context::GroupPlan plan{W, mb, ngroups, nitems, pend.need, pend.rows_off, pend.afrag_off,
+                               pend.max_col};
   plan.bs = BS;
-  plan.wmask_off = wmask_off;
+  plan.wmask_off = pend.wmask_off;
   handle->group_plans[buffer] = plan;
   return SPMM_STATUS_SUCCESS;
 }

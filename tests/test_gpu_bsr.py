@@ -1055,6 +1055,82 @@ def test_bsrmm_grouped_f16(oracle, device, W, n, ob, oc, alpha, beta):
     grp.close()
 
 
+def grouped_nonfinite_block_rows(rp, ci, v, bs, W, mb, bad_rows):
+    """The GROUPED non-finite contract of spmm_bsrmm_grouped_f16
+    (include/spmm_hip.h), predicted from the pattern on the host: a non-finite
+    B row J * bs + c reaches every row of every block row of group G (block
+    rows W G .. W G + W - 1) when any block row of G stores block column J
+    with a value other than +-0 in its column c (that makes (J, c) an entry of
+    the group's union, and each block row's fragment meets it, zeros
+    included); no other row. v: [nnzb, bs, bs] row-major block values.
+    Returns a bool per block row."""
+    held = np.zeros(mb, bool)
+    blk_row = np.repeat(np.arange(mb), np.diff(rp))
+    for b in bad_rows:
+        J, c = divmod(int(b), bs)
+        k = np.nonzero(ci == J)[0]
+        k = k[(v[k, :, c] != 0).any(axis=1)]
+        held[blk_row[k]] = True
+    grp = held.reshape(-1, W).any(axis=1) if mb % W == 0 else \
+        np.pad(held, (0, -mb % W)).reshape(-1, W).any(axis=1)
+    return np.repeat(grp, W)[:mb]
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+@pytest.mark.parametrize("bad", ["nan", "inf"])
+def test_bsrmm_grouped_f16_nonfinite_contract(device, W, bad):
+    """An inf / NaN in B through the grouped stream: exactly the block rows
+    grouped_nonfinite_block_rows predicts are non-finite in every element
+    (the whole group, the rows whose own blocks hold no value in that column
+    included), every other element finite and within the bar of the same
+    product on B with those rows zeroed. The column-sparse generator makes
+    explicit all-zero blocks and single-column blocks, so the groups that
+    store the block column only with a zero column stay finite."""
+    ops = _ops()
+    rng = np.random.default_rng(7 * W + (bad == "inf"))
+    mb, kb, n = 37, 60, 256
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, 16, 0.3)
+    v16 = v.astype(np.float16)
+    B = rng.uniform(-1, 1, (kb * 16, n)).astype(np.float16)
+    # bad rows: a column some block holds a value in, one whose blocks hold it only as
+    # zeros (if the pattern has one), and one no block stores
+    vb = v16.astype(np.float32).reshape(-1, 16, 16)
+    col_nz = np.zeros((kb, 16), bool)
+    col_st = np.zeros(kb, bool)
+    col_st[ci] = True
+    for k, J in enumerate(ci):
+        col_nz[J] |= (vb[k] != 0).any(axis=0)
+    held = np.argwhere(col_nz)
+    zero_only = np.argwhere(~col_nz & col_st[:, None])
+    unstored = np.nonzero(~col_st)[0]
+    bad_rows = [int(held[len(held) // 2][0]) * 16 + int(held[len(held) // 2][1])]
+    if len(zero_only):
+        bad_rows.append(int(zero_only[0][0]) * 16 + int(zero_only[0][1]))
+    if len(unstored):
+        bad_rows.append(int(unstored[0]) * 16 + 5)
+    want = grouped_nonfinite_block_rows(rp, ci, vb, 16, W, mb, bad_rows)
+    assert 0 < want.sum() < mb, "the case must hit some groups and spare others"
+    B0 = B.copy()
+    B0[bad_rows] = 0
+    B[bad_rows] = np.float16(np.nan if bad == "nan" else np.inf)
+    drp, dci, dv = _dev(rp, ci, v16)
+    grp = ops.GroupedBsr16(drp, dci, dv, mb=mb, group_rows=W)
+    outs = []
+    for Bx in (B, B0):
+        C = torch.zeros((mb * 16, n), device=device)
+        grp.mm(torch.from_numpy(Bx).to(device), kb=kb, n=n, ldb=n, C=C, ldc=n)
+        outs.append(C)
+    torch.cuda.synchronize()
+    grp.close()
+    bad_el = ~torch.isfinite(outs[0]).view(mb, 16 * n)
+    w = torch.from_numpy(want).to(device)
+    assert torch.equal(bad_el.any(dim=1), w) and torch.equal(bad_el.all(dim=1), w), (
+        f"W={W} {bad}: non-finite block rows {int(bad_el.any(dim=1).sum())} "
+        f"(whole: {int(bad_el.all(dim=1).sum())}), expected {int(want.sum())}")
+    keep = ~w.repeat_interleave(16)
+    assert torch.equal(outs[0][keep], outs[1][keep]), "finite rows differ from the zeroed-B run"
+
+
 def test_bsrmm_grouped_f16_checks(device):
     """A buffer this handle holds no analysis of, another mb, or a kb below
     an analysed block column is INVALID_VALUE, and so is a negative block
@@ -1271,3 +1347,107 @@ def test_group_analysis_layout(device, bs, W):
     got_rows = buf[rows_off:rows_off + 4 * len(want_rows)].view(np.int32)
     assert np.array_equal(got_rows, np.array(want_rows, np.int32)), "entry rows"
     grp.close()
+
+
+@pytest.mark.parametrize("bs", [16, 32])
+def test_group_analysis_row_pointer_checked_on_device(device, bs):
+    """The group analysis checks the row pointer on the device (grp_build_kernel
+    PASS 1) before it indexes the block columns: rp[0] != 0, a decreasing entry,
+    an entry past nnzb and rp[mb] != nnzb are each INVALID_VALUE from the size
+    query, with no fault; the same handle then analyses a good matrix."""
+    from spmm_hip._lib import INVALID_VALUE, SpmmError
+    ops = _ops()
+    rng = np.random.default_rng(9 + bs)
+    mb, kb = 23, 30
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.3)
+    vv = v.astype(np.float16) if bs == 16 else v
+    G = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
+    nnzb = int(rp[-1])
+    bads = []
+    for fix in ("first", "decrease", "past", "last"):
+        b = rp.copy()
+        if fix == "first":
+            b[0] = 1
+        elif fix == "decrease":
+            b[mb // 2] = b[mb // 2 + 1] + 1
+        elif fix == "past":
+            b[mb // 2] = nnzb + 1000
+        else:
+            b[mb] = nnzb - 1
+        bads.append(b)
+    h = ops.Handle()
+    for b in bads:
+        drp, dci, dv = _dev(b, ci, vv)
+        with pytest.raises(SpmmError) as e:
+            G(drp, dci, dv, mb=mb, handle=h)
+        assert e.value.status == INVALID_VALUE
+    drp, dci, dv = _dev(rp, ci, vv)
+    G(drp, dci, dv, mb=mb, handle=h).close()
+    torch.cuda.synchronize()
+    h.close()
+
+
+@pytest.mark.parametrize("bs", [16, 32])
+def test_group_analysis_fill_is_graph_capturable(device, bs):
+    """The filling call of the group analysis only launches kernels and async
+    copies: after an eager analysis has grown the handle's buffers, a size query
+    (eager) followed by the filling call CAPTURED in a HIP graph and replayed
+    writes the same buffer, byte for byte, as the eager analysis, and the
+    grouped product on it equals the eager one. A filling call after a size
+    query of other arguments (another matrix) still analyses its own matrix."""
+    from ctypes import byref, c_size_t, c_void_p
+    from spmm_hip._lib import lib
+    ops = _ops()
+    rng = np.random.default_rng(77 + bs)
+    mb, kb, n = 41, 50, 128
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.3)
+    vv = v.astype(np.float16) if bs == 16 else v
+    drp, dci, dv = _dev(rp, ci, vv)
+    G = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
+    fn = lib().spmm_bsr16_group_analysis_f16 if bs == 16 else lib().spmm_bsr32_group_analysis_f32
+    W = 4 if bs == 16 else 2
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        h = ops.Handle(s)
+        ref = G(drp, dci, dv, mb=mb, group_rows=W, handle=h)  # eager: grows the buffers
+        size = c_size_t(0)
+        args = (h.raw, 0, mb, int(ci.size), W, c_void_p(drp.data_ptr()), c_void_p(dci.data_ptr()),
+                c_void_p(dv.data_ptr()))
+        assert fn(*args, None, byref(size)) == 0 and size.value == ref.bytes
+        buf = torch.zeros(size.value, dtype=torch.uint8, device=device)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            h.set_stream(s)
+            st = fn(*args, c_void_p(buf.data_ptr()), byref(size))
+        assert st == 0
+        g.replay()
+        s.synchronize()
+        assert torch.equal(buf, ref.buffer[:size.value]), "captured fill differs from the eager one"
+        # the product on the captured buffer (recorded on the handle at capture)
+        vt = torch.float16 if bs == 16 else torch.float32
+        B = (torch.rand((kb * bs, n), device=device) * 2 - 1).to(vt)
+        C1 = torch.zeros((mb * bs, n), device=device)
+        C2 = torch.zeros((mb * bs, n), device=device)
+        ref.mm(B, kb=kb, n=n, ldb=n, C=C1, ldc=n)
+        pfn = lib().spmm_bsrmm_grouped_f16 if bs == 16 else lib().spmm_bsrmm_grouped_f32
+        assert pfn(h.raw, mb, kb, n, c_void_p(buf.data_ptr()), 1.0, c_void_p(B.data_ptr()), n, 0,
+                   0.0, c_void_p(C2.data_ptr()), n, 0) == 0
+        s.synchronize()
+        assert torch.equal(C1, C2)
+        # a size query of another matrix, then the filling call of this one
+        rp2, ci2, v2 = _column_sparse_bsr(rng, 9, 12, bs, 0.5)
+        v2 = v2.astype(np.float16) if bs == 16 else v2
+        e_rp, e_ci, e_v = _dev(rp2, ci2, v2)
+        other = (h.raw, 0, 9, int(ci2.size), W, c_void_p(e_rp.data_ptr()),
+                 c_void_p(e_ci.data_ptr()), c_void_p(e_v.data_ptr()))
+        assert fn(*other, None, byref(c_size_t(0))) == 0
+        buf2 = torch.zeros(ref.bytes, dtype=torch.uint8, device=device)
+        size = c_size_t(ref.bytes)
+        assert fn(*args, c_void_p(buf2.data_ptr()), byref(size)) == 0
+        s.synchronize()
+        assert torch.equal(buf2, ref.buffer[:ref.bytes])
+    ref.close()
+    for b in (buf, buf2):
+        lib().spmm_bsr_group_release(h.raw, c_void_p(b.data_ptr()))
+    h.close()
