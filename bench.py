@@ -109,10 +109,14 @@ WORKLOADS = {
     "products_rcm_bsr32": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                p_in=0.97, bs=32, K=128, dtype="fp32", reorder="rcm"),
     # the block sizes benchmark.py:3-19 sweeps besides 16 / 32, on the reddit
-    # stand-in: bs 8 (lane-group VALU kernel) and bs 64 (the bs 32 column stream
-    # on 32 x 32 sub-blocks)
+    # stand-in: bs 2 / 4 / 8 (lane-group VALU kernel) and bs 64 (the bs 32 column
+    # stream on 32 x 32 sub-blocks)
     "reddit_bsr8": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
                         bs=8, K=128, dtype="fp32"),
+    "reddit_bsr4": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
+                        bs=4, K=128, dtype="fp32"),
+    "reddit_bsr2": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
+                        bs=2, K=128, dtype="fp32"),
     "reddit_bsr64": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
                          bs=64, K=128, dtype="fp32"),
     # §8f next row: dense-block + CSR remainder (divide.cu) on the reddit stand-in

@@ -2417,22 +2417,30 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f16_mf
 // bs = 2 / 4 / 8, fp32, row-major B: a lane-group VALU kernel
 // (rocsparse_bsrmm.h:227-252 sends bs <= 8 to its large-blockdim kernel;
 // rocsparse_bsrmm_impl.h:315-389). A bs x bs block feeds too few rows per B row
-// for an MFMA tile (8 of 32), and the product is bound by the B-row gathers
-// (4 flop per gathered byte at bs 8), so the VALU does the FMAs at a small
-// fraction of its rate. One wave per (block row, 64 * VEC columns), four
-// independent waves per workgroup. Per block:
-//  * A: lane l < bs^2 holds element l of the block (one coalesced load), its
-//    column mask is one ballot, and a(r, c) comes to the FMAs by v_readlane;
+// for an MFMA tile (8 of 32), and fp32 MFMA has the packed VALU FMA's peak
+// anyway, so the VALU does the FMAs (v_pk_fma_f32: two output columns per
+// lane and instruction). One wave per (block row, 64 * VEC columns), four
+// waves per workgroup; the workgroups go to the XCDs in chunks of XM (32 block
+// rows), so the waves of neighbouring block rows, which gather mostly the same
+// B rows on a reordered graph, meet in one L2. Per block:
+//  * A: lane l < bs^2 holds element l (one coalesced load); its column mask
+//    is one ballot; the lanes then park it in this wave's LDS ring slot, from
+//    which every lane reads the values back as uniform-address ds_read_b128
+//    (broadcast): a(r, c) reaches v_pk_fma_f32 as a VGPR with no per-value
+//    v_readlane (round 4's form spent one VALU issue per value on them, as
+//    many as on the FMAs);
 //  * B: one gather per block column: the 64 lanes read VEC floats each of row
 //    bc * bs + c (a whole 256 / 512-B row piece); a column whose values are all
-//    +-0 reads the L2-resident zero row instead, so every block issues the same
-//    bs gathers and the compiler's counted waits hold across the pipeline
-//    (the column-granular contract of include/spmm_hip.h);
+//    +-0 reads the L2-resident zero row instead and its FMAs are skipped (a
+//    wave-uniform branch), so every block issues the same bs gathers and the
+//    compiler's counted waits hold across the pipeline (the column-granular
+//    contract of include/spmm_hip.h);
 //  * pipeline: a ring of R = 4 block slots, A loaded two blocks ahead and the
 //    B gathers one block ahead of the FMAs (unrolled R times: static
-//    registers, no branch around a load).
+//    registers and LDS slots, no branch around a load).
 // Each output element is one sequential fp32 FMA chain, blocks in order and
-// columns in order inside a block: the oracle's bsrmm order bit for bit.
+// columns in order inside a block: the oracle's bsrmm order bit for bit (a
+// skipped empty column adds nothing but the sign of a zero).
 // ---------------------------------------------------------------------------
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
@@ -2440,63 +2448,109 @@ template <int BS, int VEC, bool ROWD, bool CROW>
 __global__ __launch_bounds__(256) void bsr_small_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
-    float* __restrict__ C, int ldc) {
+    float* __restrict__ C, int ldc, int xm) {
   static_assert(BS == 2 || BS == 4 || BS == 8, "bs 2 / 4 / 8");
   static_assert(VEC == 1 || VEC == 2, "VEC 1 / 2");
   constexpr int E = BS * BS;
   constexpr int R = 4;  // ring slots: A of block k + 2, B of block k + 1, FMAs of block k
   typedef typename std::conditional<VEC == 2, f32x2v, float>::type vec;
+  // [wave][slot][element] as (a, a) pairs: a read lands as a v_pk_fma_f32 operand pair
+  __shared__ __attribute__((aligned(16))) f32x2v lds_a[4][R][64];
   const int lane = threadIdx.x & 63;
-  const int br = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int wv = threadIdx.x >> 6;
+  const int wg = xcd_block_row(blockIdx.x, gridDim.x, xm);
+  const int br = __builtin_amdgcn_readfirstlane(wg * 4 + wv);
   if (br >= mb) return;
   const int col0 = blockIdx.y * 64 * VEC + lane * VEC;
   const bool col_ok = col0 < n;
   const int col_ld = col_ok ? col0 : 0;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const int kl = k1 - 1;
-  const float* const zrow = g_zero_row + lane * VEC;
+  f32x2v* const slots = &lds_a[wv][0][0];
 
-  float acc[BS][VEC];
+  vec acc[BS];
 #pragma unroll
-  for (int r = 0; r < BS; ++r)
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) acc[r][v] = 0.f;
+  for (int r = 0; r < BS; ++r) acc[r] = vec{};
 
-  float av[R];      // A of a block: lane l < E holds element l
-  int bcol[R];      // its block column
-  vec x[R][BS];     // its B rows (zero row for empty columns)
+  float av[R];          // A of a block: lane l < E holds element l
+  int bcol[R];          // its block column
+  unsigned cmask[R];    // its nonzero columns (bit c)
+  vec x[R][BS];         // its B rows (zero row for empty columns)
   auto load_a = [&](int k, int s) {
     const int kk = min(k, kl);
     av[s] = val[(size_t)kk * E + (lane < E ? lane : 0)];
     bcol[s] = colind[kk];
   };
+  // the zero row as seen from this tile's first column (uniform: the per-lane
+  // offset is added at the load, like a B row's)
+  const float* const zbase = g_zero_row - (size_t)blockIdx.y * 64 * VEC;
+  const int boff = 4 * col_ld;
   auto load_b = [&](int s) {
     const unsigned long long bits =
         __builtin_amdgcn_ballot_w64(lane < E && (__float_as_uint(av[s]) & 0x7fffffffu) != 0u);
-    const float* base = B + (size_t)bcol[s] * BS * ldb + col_ld;
+    slots[s * 64 + lane] = f32x2v{av[s], av[s]};  // the block's values for the broadcast reads
+    const float* base = B + (size_t)bcol[s] * BS * ldb;  // uniform
+    unsigned cm = 0;
 #pragma unroll
     for (int c = 0; c < BS; ++c) {
       unsigned long long colbits = 0;
 #pragma unroll
       for (int r = 0; r < BS; ++r) colbits |= 1ull << (ROWD ? r * BS + c : c * BS + r);
-      const float* p = (bits & colbits) ? base + (size_t)c * ldb : zrow;
-      x[s][c] = *reinterpret_cast<const vec*>(p);
+      const bool nz = (bits & colbits) != 0;
+      cm |= nz ? 1u << c : 0u;
+      const float* rowp = nz ? base + (size_t)c * ldb : zbase;  // uniform select
+      // a buffer load from a per-row resource: the row address stays in SGPRs and
+      // the lane's byte offset is one loop-invariant VGPR (no 64-bit VALU address)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(rowp), 0, 0x7fffffff, 0x00020000);
+      if constexpr (VEC == 2)
+        x[s][c] = __builtin_bit_cast(vec, __builtin_amdgcn_raw_buffer_load_b64(rs, boff, 0, 0));
+      else
+        x[s][c] = __builtin_bit_cast(vec, __builtin_amdgcn_raw_buffer_load_b32(rs, boff, 0, 0));
+    }
+    cmask[s] = cm;
+  };
+  // a(r, c) of slot s for r = 0 .. BS-1 and the columns c0 .. c0 + NC - 1: uniform
+  // ds_read_b128 broadcasts (every lane reads the same 16 B: two (a, a) pairs)
+  auto fma_cols = [&](int s, auto c0c, auto ncc) {
+    constexpr int c0 = decltype(c0c)::value, NC = decltype(ncc)::value;
+    f32x2v a[BS][NC];
+    const float4* sl = reinterpret_cast<const float4*>(&lds_a[wv][s][0]);
+    auto pair = [&](int e, f32x2v& lo, f32x2v& hi) {  // elements e, e + 1 (e even)
+      const float4 q = sl[e / 2];
+      lo = f32x2v{q.x, q.y};
+      hi = f32x2v{q.z, q.w};
+    };
+    if constexpr (ROWD) {  // row r: elements r * BS + c0 .. + NC - 1
+#pragma unroll
+      for (int r = 0; r < BS; ++r)
+#pragma unroll
+        for (int c = 0; c < NC; c += 2) pair(r * BS + c0 + c, a[r][c], a[r][c + 1]);
+    } else {  // column c: elements c * BS .. + BS - 1
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int r = 0; r < BS; r += 2) pair((c0 + c) * BS + r, a[r][c], a[r + 1][c]);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (!(cmask[s] & (1u << (c0 + c)))) continue;  // wave-uniform: an empty column
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        if constexpr (VEC == 1)
+          acc[r] = __builtin_fmaf(a[r][c][0], x[s][c0 + c], acc[r]);
+        else
+          acc[r] = __builtin_elementwise_fma(a[r][c], x[s][c0 + c], acc[r]);
+      }
     }
   };
   auto fma_block = [&](int s) {
-#pragma unroll
-    for (int c = 0; c < BS; ++c) {
-#pragma unroll
-      for (int r = 0; r < BS; ++r) {
-        const float a = __int_as_float(
-            __builtin_amdgcn_readlane(__float_as_int(av[s]), ROWD ? r * BS + c : c * BS + r));
-        if constexpr (VEC == 1) {
-          acc[r][0] = __builtin_fmaf(a, x[s][c], acc[r][0]);
-        } else {
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) acc[r][v] = __builtin_fmaf(a, x[s][c][v], acc[r][v]);
-        }
-      }
+    // four columns at a time keep the broadcast values of one step in 4 BS VGPRs
+    if constexpr (BS == 8) {
+      fma_cols(s, std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+      fma_cols(s, std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{});
+    } else {
+      fma_cols(s, std::integral_constant<int, 0>{}, std::integral_constant<int, BS>{});
     }
   };
 
@@ -2520,15 +2574,22 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
   for (int r = 0; r < BS; ++r) {
     const size_t row = (size_t)br * BS + r;
     if (!col_ok) break;
+    float o[VEC];
+    if constexpr (VEC == 1) {
+      o[0] = acc[r];
+    } else {
+      o[0] = acc[r][0];
+      o[1] = acc[r][1];
+    }
     if constexpr (CROW) {
       float* p = C + row * ldc + col0;
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) p[v] = epi(acc[r][v], alpha, beta, p + v);
+      for (int v = 0; v < VEC; ++v) p[v] = epi(o[v], alpha, beta, p + v);
     } else {
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
         float* p = C + (size_t)(col0 + v) * ldc + row;
-        p[0] = epi(acc[r][v], alpha, beta, p);
+        p[0] = epi(o[v], alpha, beta, p);
       }
     }
   }
@@ -3491,20 +3552,29 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // the lane-group VALU kernel: 2 floats per lane when B allows 8-B gathers
     const bool v2 = n > 64 && n % 2 == 0 && ldb % 2 == 0 && aligned(B, 8);
     const dim3 grid((mb + 3) / 4, (n + (v2 ? 127 : 63)) / (v2 ? 128 : 64));
+    // XCD chunks of 8 workgroups (32 block rows; TUNING builds: SPMM_SMALL_XM)
+#ifdef SPMM_TUNING
+    static const int xm = [] {
+      const char* e = getenv("SPMM_SMALL_XM");
+      return e ? atoi(e) : 8;
+    }();
+#else
+    constexpr int xm = 8;
+#endif
 #define SMALL_LAUNCH(BS_, V_)                                                                    \
   do {                                                                                           \
     if (rowd && crow)                                                                            \
       hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, true, true>), grid, dim3(256), 0, ctx->stream, \
-                         mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);               \
+                         mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm);           \
     else if (rowd)                                                                               \
       hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, true, false>), grid, dim3(256), 0,           \
-                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);  \
+                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm); \
     else if (crow)                                                                               \
       hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, false, true>), grid, dim3(256), 0,           \
-                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);  \
+                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm); \
     else                                                                                         \
       hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, false, false>), grid, dim3(256), 0,          \
-                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);  \
+                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm); \
   } while (0)
     if (bs == 8) {
       if (v2) SMALL_LAUNCH(8, 2); else SMALL_LAUNCH(8, 1);
