@@ -15,7 +15,7 @@ with `s_nop 1` in its own string).
 Round 3 met it: a build whose bs 32 column-stream epilogue stored C with an
 inline-asm `global_store_dwordx4 ... sc1` (write-through) returned 4.8e-42
 (the bit pattern of a small integer: the next row's address arithmetic) for
-0.8 % of C (profiles/r03_sc1_store_tests.log). tools/sc1_store_repro.py
+0.8 % of C (profiles/r03_sc1_store_tests.log). tools/history/sc1_store_repro.py
 rebuilds that form and this audit names the instruction that overwrote the
 data registers.
 

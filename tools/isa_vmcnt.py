@@ -12,7 +12,7 @@ was a B copy of the row's last block. A counted wait is only as right as the
 instruction stream it counts, so this module checks the stream the compiler
 emitted (check_kernel: what a stage hand-off wait keeps in flight and what it
 retires; loop_drains: vmcnt(0) waits inside a copy loop that drain the
-prefetch). tools/vmcnt_order.hip measured the ordering rule itself on the
+prefetch). tools/history/vmcnt_order.hip measured the ordering rule itself on the
 GPU: a younger VGPR load never retired ahead of an older LDS-DMA copy, nor the
 reverse (profiles/r02_vmcnt_order.jsonl).
 
