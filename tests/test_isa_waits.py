@@ -261,3 +261,58 @@ def test_store_hazard_checker_flags_the_pattern():
     assert len(hz) == 2, hz
     assert "v_accvgpr_read_b32 v2" in hz[0] and "inline asm" in hz[0]
     assert "v_add_u32_e32 v12" in hz[1]
+
+
+CSR_ASM = os.path.join(PKG, "build", "csr_kernels-hip-amdgcn-amd-amdhsa-gfx950.s")
+
+
+def _functions(asm: str, pattern: str) -> dict[str, list[str]]:
+    """Instruction lines (labels and comments dropped) of every function whose
+    mangled name matches `pattern`."""
+    out = {}
+    for m in re.finditer(r"^(_Z[^:\s]*(?:" + pattern + r")[^:\s]*):[^\n]*$", asm, re.M):
+        body = asm[m.end():asm.index(".Lfunc_end", m.end())]
+        out[m.group(1)] = [ln.strip() for ln in body.splitlines()
+                           if ln.strip() and not ln.strip().startswith((";", "."))
+                           and not ln.strip().endswith(":")]
+    return out
+
+
+def test_split_row_handoff_order_in_shipped_csr_code():
+    """The split-row hand-off of the CSR kernels (csr_kernels.hip, split rows) is
+    relaxed agent-scope atomics ordered by hand, not by the memory model
+    (ADVICE round 4): a wave's partial stores, then s_waitcnt vmcnt(0), then
+    its ticket add; the last arriver waits for the add's return before it
+    loads the others' partials, with sc1 loads. This pins that order in the
+    shipped assembly, path-insensitively (linear order within each function):
+      * before the first ticket add, a vmcnt(0) with no vector store after it;
+      * after every ticket add, a vmcnt(0) before the next vector load;
+      * the partials are read with sc1 loads after the first add, and the
+        ticket reset is an sc1 store.
+    A compiler that moved a partial store past the wait, or a load above the
+    add's return, fails here."""
+    if not os.path.exists(CSR_ASM):
+        subprocess.run(["make", "-C", PKG, "lib"], check=True, capture_output=True)
+    with open(CSR_ASM) as f:
+        asm = f.read()
+    fns = _functions(asm, "csr_mergepath_kernel|csr_group_kernel")
+    assert len(fns) >= 6, f"only {len(fns)} CSR kernel instantiations found"
+    is_store = re.compile(r"^(global|buffer)_store")
+    is_load = re.compile(r"^(global|buffer)_load")
+    for name, ins in fns.items():
+        atoms = [i for i, x in enumerate(ins) if x.startswith("global_atomic_add")]
+        assert atoms, f"{name}: no ticket add"
+        a0 = atoms[0]
+        waits = [i for i in range(a0) if re.match(r"s_waitcnt vmcnt\(0\)", ins[i])]
+        assert waits, f"{name}: no vmcnt(0) before the first ticket add"
+        between = [ins[i] for i in range(waits[-1] + 1, a0) if is_store.match(ins[i])]
+        assert not between, f"{name}: stores between the wait and the ticket add: {between}"
+        for a in atoms:
+            for i in range(a + 1, len(ins)):
+                if re.match(r"s_waitcnt vmcnt\(0\)", ins[i]):
+                    break
+                assert not is_load.match(ins[i]), (
+                    f"{name}: {ins[i]!r} before the ticket add's return is waited for")
+        after = ins[a0:]
+        assert any(is_load.match(x) and " sc1" in x for x in after), f"{name}: no sc1 load"
+        assert any(is_store.match(x) and " sc1" in x for x in after), f"{name}: no sc1 store"
