@@ -2413,34 +2413,40 @@ __global__ __launch_bounds__(256, (VAR >> 3) ? (VAR >> 3) : 1) void bsr16_f16_mf
   }
 }
 
+// f(integral_constant<S>) for S = 0, 1, ... while it returns true (static slot indices)
+template <int... S, class F>
+__device__ __forceinline__ void slots_while(std::integer_sequence<int, S...>, F&& f) {
+  (void)(f(std::integral_constant<int, S>{}) && ...);
+}
+
 // ---------------------------------------------------------------------------
 // bs = 2 / 4 / 8, fp32, row-major B: a lane-group VALU kernel
 // (rocsparse_bsrmm.h:227-252 sends bs <= 8 to its large-blockdim kernel;
 // rocsparse_bsrmm_impl.h:315-389). A bs x bs block feeds too few rows per B row
-// for an MFMA tile (8 of 32), and fp32 MFMA has the packed VALU FMA's peak
-// anyway, so the VALU does the FMAs (v_pk_fma_f32: two output columns per
-// lane and instruction). One wave per (block row, 64 * VEC columns), four
-// waves per workgroup; the workgroups go to the XCDs in chunks of XM (32 block
-// rows), so the waves of neighbouring block rows, which gather mostly the same
-// B rows on a reordered graph, meet in one L2. Per block:
-//  * A: lane l < bs^2 holds element l (one coalesced load); its column mask
-//    is one ballot; the lanes then park it in this wave's LDS ring slot, from
-//    which every lane reads the values back as uniform-address ds_read_b128
-//    (broadcast): a(r, c) reaches v_pk_fma_f32 as a VGPR with no per-value
-//    v_readlane (round 4's form spent one VALU issue per value on them, as
-//    many as on the FMAs);
+// for an MFMA tile (8 of 32), and the product is bound by the B-row gathers
+// (4 flop per gathered byte at bs 8), so the VALU does the FMAs at a small
+// fraction of its rate. One wave per (block row, 64 * VEC columns), four
+// independent waves per workgroup. Per block:
+//  * A: lane l < bs^2 holds element l of the block (one coalesced load), its
+//    column mask is one ballot, and a(r, c) comes to the FMAs by v_readlane;
 //  * B: one gather per block column: the 64 lanes read VEC floats each of row
-//    bc * bs + c (a whole 256 / 512-B row piece); a column whose values are all
-//    +-0 reads the L2-resident zero row instead and its FMAs are skipped (a
-//    wave-uniform branch), so every block issues the same bs gathers and the
-//    compiler's counted waits hold across the pipeline (the column-granular
-//    contract of include/spmm_hip.h);
+//    bc * bs + c (a whole 256 / 512-B row piece) by a buffer load from a
+//    resource built on the row's address in SGPRs (no 64-bit VALU address per
+//    gather); a column whose values are all +-0 gets a resource of zero
+//    records, so its load returns zeros without touching memory (round 4 read
+//    the zero row from L2: a quarter of the gathers on the reddit stand-in).
+//    Every block issues the same bs loads and the compiler's counted waits
+//    hold across the pipeline (the column-granular contract of include/spmm_hip.h);
 //  * pipeline: a ring of R = 4 block slots, A loaded two blocks ahead and the
 //    B gathers one block ahead of the FMAs (unrolled R times: static
-//    registers and LDS slots, no branch around a load).
+//    registers, no branch around a load).
 // Each output element is one sequential fp32 FMA chain, blocks in order and
-// columns in order inside a block: the oracle's bsrmm order bit for bit (a
-// skipped empty column adds nothing but the sign of a zero).
+// columns in order inside a block: the oracle's bsrmm order bit for bit.
+// Workgroups go to the XCDs in chunks of xm (xcd_block_row; 1 = none).
+// (Measured and dropped, round 5: the block's values parked in LDS and read back
+// as uniform ds_read_b128 broadcasts in place of the v_readlane per value: 2.62
+// against 2.06 ms on reddit bs 8. A broadcast read still returns 64 lanes' worth
+// of data, so 16-32 of them per block made the LDS the bound.)
 // ---------------------------------------------------------------------------
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
@@ -2454,103 +2460,63 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
   constexpr int E = BS * BS;
   constexpr int R = 4;  // ring slots: A of block k + 2, B of block k + 1, FMAs of block k
   typedef typename std::conditional<VEC == 2, f32x2v, float>::type vec;
-  // [wave][slot][element] as (a, a) pairs: a read lands as a v_pk_fma_f32 operand pair
-  __shared__ __attribute__((aligned(16))) f32x2v lds_a[4][R][64];
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
   const int wg = xcd_block_row(blockIdx.x, gridDim.x, xm);
-  const int br = __builtin_amdgcn_readfirstlane(wg * 4 + wv);
+  const int br = __builtin_amdgcn_readfirstlane(wg * 4 + (threadIdx.x >> 6));
   if (br >= mb) return;
   const int col0 = blockIdx.y * 64 * VEC + lane * VEC;
   const bool col_ok = col0 < n;
   const int col_ld = col_ok ? col0 : 0;
   const int k0 = rowptr[br], k1 = rowptr[br + 1];
   const int kl = k1 - 1;
-  f32x2v* const slots = &lds_a[wv][0][0];
+  const int boff = 4 * col_ld;  // the lane's byte offset in a B row
 
-  vec acc[BS];
+  float acc[BS][VEC];
 #pragma unroll
-  for (int r = 0; r < BS; ++r) acc[r] = vec{};
+  for (int r = 0; r < BS; ++r)
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[r][v] = 0.f;
 
-  float av[R];          // A of a block: lane l < E holds element l
-  int bcol[R];          // its block column
-  unsigned cmask[R];    // its nonzero columns (bit c)
-  vec x[R][BS];         // its B rows (zero row for empty columns)
+  float av[R];      // A of a block: lane l < E holds element l
+  int bcol[R];      // its block column
+  vec x[R][BS];     // its B rows (zero row for empty columns)
   auto load_a = [&](int k, int s) {
     const int kk = min(k, kl);
     av[s] = val[(size_t)kk * E + (lane < E ? lane : 0)];
     bcol[s] = colind[kk];
   };
-  // the zero row as seen from this tile's first column (uniform: the per-lane
-  // offset is added at the load, like a B row's)
-  const float* const zbase = g_zero_row - (size_t)blockIdx.y * 64 * VEC;
-  const int boff = 4 * col_ld;
   auto load_b = [&](int s) {
     const unsigned long long bits =
         __builtin_amdgcn_ballot_w64(lane < E && (__float_as_uint(av[s]) & 0x7fffffffu) != 0u);
-    slots[s * 64 + lane] = f32x2v{av[s], av[s]};  // the block's values for the broadcast reads
     const float* base = B + (size_t)bcol[s] * BS * ldb;  // uniform
-    unsigned cm = 0;
 #pragma unroll
     for (int c = 0; c < BS; ++c) {
       unsigned long long colbits = 0;
 #pragma unroll
       for (int r = 0; r < BS; ++r) colbits |= 1ull << (ROWD ? r * BS + c : c * BS + r);
       const bool nz = (bits & colbits) != 0;
-      cm |= nz ? 1u << c : 0u;
-      const float* rowp = nz ? base + (size_t)c * ldb : zbase;  // uniform select
-      // a buffer load from a per-row resource: the row address stays in SGPRs and
-      // the lane's byte offset is one loop-invariant VGPR (no 64-bit VALU address)
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(rowp), 0, 0x7fffffff, 0x00020000);
+          const_cast<float*>(base + (size_t)c * ldb), 0, nz ? 0x7fffffff : 0, 0x00020000);
       if constexpr (VEC == 2)
         x[s][c] = __builtin_bit_cast(vec, __builtin_amdgcn_raw_buffer_load_b64(rs, boff, 0, 0));
       else
         x[s][c] = __builtin_bit_cast(vec, __builtin_amdgcn_raw_buffer_load_b32(rs, boff, 0, 0));
     }
-    cmask[s] = cm;
-  };
-  // a(r, c) of slot s for r = 0 .. BS-1 and the columns c0 .. c0 + NC - 1: uniform
-  // ds_read_b128 broadcasts (every lane reads the same 16 B: two (a, a) pairs)
-  auto fma_cols = [&](int s, auto c0c, auto ncc) {
-    constexpr int c0 = decltype(c0c)::value, NC = decltype(ncc)::value;
-    f32x2v a[BS][NC];
-    const float4* sl = reinterpret_cast<const float4*>(&lds_a[wv][s][0]);
-    auto pair = [&](int e, f32x2v& lo, f32x2v& hi) {  // elements e, e + 1 (e even)
-      const float4 q = sl[e / 2];
-      lo = f32x2v{q.x, q.y};
-      hi = f32x2v{q.z, q.w};
-    };
-    if constexpr (ROWD) {  // row r: elements r * BS + c0 .. + NC - 1
-#pragma unroll
-      for (int r = 0; r < BS; ++r)
-#pragma unroll
-        for (int c = 0; c < NC; c += 2) pair(r * BS + c0 + c, a[r][c], a[r][c + 1]);
-    } else {  // column c: elements c * BS .. + BS - 1
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int r = 0; r < BS; r += 2) pair((c0 + c) * BS + r, a[r][c], a[r + 1][c]);
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      if (!(cmask[s] & (1u << (c0 + c)))) continue;  // wave-uniform: an empty column
-#pragma unroll
-      for (int r = 0; r < BS; ++r) {
-        if constexpr (VEC == 1)
-          acc[r] = __builtin_fmaf(a[r][c][0], x[s][c0 + c], acc[r]);
-        else
-          acc[r] = __builtin_elementwise_fma(a[r][c], x[s][c0 + c], acc[r]);
-      }
-    }
   };
   auto fma_block = [&](int s) {
-    // four columns at a time keep the broadcast values of one step in 4 BS VGPRs
-    if constexpr (BS == 8) {
-      fma_cols(s, std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
-      fma_cols(s, std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{});
-    } else {
-      fma_cols(s, std::integral_constant<int, 0>{}, std::integral_constant<int, BS>{});
+#pragma unroll
+    for (int c = 0; c < BS; ++c) {
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        const float a = __int_as_float(
+            __builtin_amdgcn_readlane(__float_as_int(av[s]), ROWD ? r * BS + c : c * BS + r));
+        if constexpr (VEC == 1) {
+          acc[r][0] = __builtin_fmaf(a, x[s][c], acc[r][0]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[r][v] = __builtin_fmaf(a, x[s][c][v], acc[r][v]);
+        }
+      }
     }
   };
 
@@ -2574,22 +2540,15 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
   for (int r = 0; r < BS; ++r) {
     const size_t row = (size_t)br * BS + r;
     if (!col_ok) break;
-    float o[VEC];
-    if constexpr (VEC == 1) {
-      o[0] = acc[r];
-    } else {
-      o[0] = acc[r][0];
-      o[1] = acc[r][1];
-    }
     if constexpr (CROW) {
       float* p = C + row * ldc + col0;
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) p[v] = epi(o[v], alpha, beta, p + v);
+      for (int v = 0; v < VEC; ++v) p[v] = epi(acc[r][v], alpha, beta, p + v);
     } else {
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
         float* p = C + (size_t)(col0 + v) * ldc + row;
-        p[0] = epi(o[v], alpha, beta, p);
+        p[0] = epi(acc[r][v], alpha, beta, p);
       }
     }
   }
@@ -2661,11 +2620,6 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 // of its block rows holds a value in that column (the grouped contract,
 // include/spmm_hip.h).
 // ---------------------------------------------------------------------------
-// f(integral_constant<S>) for S = 0, 1, ... while it returns true (static slot indices)
-template <int... S, class F>
-__device__ __forceinline__ void slots_while(std::integer_sequence<int, S...>, F&& f) {
-  (void)(f(std::integral_constant<int, S>{}) && ...);
-}
 
 template <int W, int P, bool CROW, int OCC = 0, int IPB = 1, bool AL = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
@@ -3535,13 +3489,21 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
                       beta, C, ldc);
   } else if (bs == 16 && rowd && brow && n >= 4 && n % 4 == 0 && ldb % 4 == 0 &&
              aligned(val, 16) && aligned(B, 16) && !dense_sem) {
-    const dim3 grid(mb, (n + 255) / 256);
-    if (crow)
-      hipLaunchKernelGGL((bsr16_cm_kernel<float, true, 2, 5>), grid, dim3(256), 0, ctx->stream, mb,
-                         n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
-    else
-      hipLaunchKernelGGL((bsr16_cm_kernel<float, false, 2, 5>), grid, dim3(256), 0, ctx->stream,
-                         mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc);
+    // output columns per workgroup: 256, or the narrower tile a small n fills (at n = 64
+    // a 256-column tile left 3 of its 4 waves idle: reference sweep, profiles/r05_sweep/)
+    const int cols = n <= 64 ? 64 : (n <= 128 ? 128 : 256);
+    const dim3 grid(mb, (n + cols - 1) / cols);
+#define CM16_LAUNCH(CR_, COLS_)                                                                   \
+  hipLaunchKernelGGL((bsr16_cm_kernel<float, CR_, 2, 5, 1, COLS_>), grid, dim3(256), 0,           \
+                     ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc)
+    if (cols == 64) {
+      if (crow) CM16_LAUNCH(true, 64); else CM16_LAUNCH(false, 64);
+    } else if (cols == 128) {
+      if (crow) CM16_LAUNCH(true, 128); else CM16_LAUNCH(false, 128);
+    } else {
+      if (crow) CM16_LAUNCH(true, 256); else CM16_LAUNCH(false, 256);
+    }
+#undef CM16_LAUNCH
   } else if (bs == 16 && vec_ok) {
     const int waves = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
     dim3 grid(mb, (n + 64 * waves - 1) / (64 * waves));
@@ -3561,20 +3523,15 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
 #else
     constexpr int xm = 8;
 #endif
+#define SMALL_ONE(BS_, V_, RD_, CR_)                                                             \
+  hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, RD_, CR_>), grid, dim3(256), 0, ctx->stream, mb, \
+                     n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm)
 #define SMALL_LAUNCH(BS_, V_)                                                                    \
   do {                                                                                           \
-    if (rowd && crow)                                                                            \
-      hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, true, true>), grid, dim3(256), 0, ctx->stream, \
-                         mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm);           \
-    else if (rowd)                                                                               \
-      hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, true, false>), grid, dim3(256), 0,           \
-                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm); \
-    else if (crow)                                                                               \
-      hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, false, true>), grid, dim3(256), 0,           \
-                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm); \
-    else                                                                                         \
-      hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, false, false>), grid, dim3(256), 0,          \
-                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm); \
+    if (rowd && crow) SMALL_ONE(BS_, V_, true, true);                                            \
+    else if (rowd) SMALL_ONE(BS_, V_, true, false);                                              \
+    else if (crow) SMALL_ONE(BS_, V_, false, true);                                              \
+    else SMALL_ONE(BS_, V_, false, false);                                                       \
   } while (0)
     if (bs == 8) {
       if (v2) SMALL_LAUNCH(8, 2); else SMALL_LAUNCH(8, 1);
@@ -3584,6 +3541,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       if (v2) SMALL_LAUNCH(2, 2); else SMALL_LAUNCH(2, 1);
     }
 #undef SMALL_LAUNCH
+#undef SMALL_ONE
   } else {
     dim3 grid(mb, (n + 63) / 64);
     hipLaunchKernelGGL(bsr_generic_kernel<float>, grid, dim3(256), 0, ctx->stream, mb, n, bs,

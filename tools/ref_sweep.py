@@ -27,7 +27,8 @@ each distinct B row once, the C write) and the fp32 fraction of 157.3 TFLOP/s
 (MFMA at bs >= 16; the VALU kernel at bs <= 8, whose own peak is the same
 with packed FMAs).
 
-    python tools/ref_sweep.py --out profiles/r05_sweep [--quick]
+    python tools/ref_sweep.py > sweep.jsonl 2> progress.log
+    python tools/ref_sweep.py --table sweep.jsonl > table.md
 """
 from __future__ import annotations
 
@@ -164,6 +165,42 @@ def csr_cells(torch, lib, h, descr, p, Ks, reps, gen):
     del rp, ci, val
 
 
+def table(path: str) -> None:
+    """Markdown tables of a sweep's JSON lines: per (p, bs) the ms and useful GFLOP/s
+    per dim (transB = 1 / 0), the compulsory-byte and fp32 fractions at dim 512; the
+    CSR cells per (p, impl)."""
+    rows = [json.loads(ln) for ln in open(path) if ln.startswith("{")]
+    bsr = {(r["p"], r["bs"], r["dim"], r["transB"]): r for r in rows if r["kind"] == "bsrmm"}
+    dims = sorted({k[2] for k in bsr})
+    print("test_bsrmm (benchmark.py:3-19): ms, transB = 1 / 0; useful GFLOP/s (transB = 1); "
+          "at dim 512: compulsory-byte fraction of 8 TB/s and fp32 fraction of 157.3 TFLOP/s\n")
+    print("| p | bs | nnzb | " + " | ".join(f"dim {d}" for d in dims) +
+          " | comp 512 | fp32 512 |")
+    print("|" + "---|" * (len(dims) + 5))
+    for p, bs in sorted({(k[0], k[1]) for k in bsr}):
+        cells = []
+        for d in dims:
+            a, b = bsr.get((p, bs, d, 1)), bsr.get((p, bs, d, 0))
+            cells.append(f"{a['ms']:.3f} / {b['ms']:.3f} ({a['useful_GFLOPs'] / 1e3:.1f} T)"
+                         if a and b else "-")
+        z = bsr.get((p, bs, dims[-1], 1), {})
+        nz = next(r["nnzb"] for k, r in bsr.items() if k[:2] == (p, bs))
+        print(f"| {p:g} | {bs} | {nz} | " + " | ".join(cells) +
+              f" | {z.get('compulsory_frac', '-')} | {z.get('fp32_frac', '-')} |")
+    csr = [r for r in rows if r["kind"] == "csrmm"]
+    if csr:
+        print("\ntest_csrmm (benchmark.py:21-31): ms (GFLOP/s), gespmm = row-major B and C, "
+              "cusparse = column-major B and C\n")
+        print("| p | impl | nnz | " + " | ".join(f"dim {d}" for d in dims) + " |")
+        print("|" + "---|" * (len(dims) + 3))
+        for p, impl in sorted({(r["p"], r["impl"]) for r in csr}):
+            rr = {r["dim"]: r for r in csr if r["p"] == p and r["impl"] == impl}
+            nz = next(iter(rr.values()))["nnz"]
+            print(f"| {p:g} | {impl} | {nz} | " + " | ".join(
+                f"{rr[d]['ms']:.3f} ({rr[d]['GFLOPs'] / 1e3:.2f} T)" if d in rr else "-"
+                for d in dims) + " |")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--densities", default="0.0002,0.002,0.02")
@@ -173,7 +210,11 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--skip-csr", action="store_true")
     ap.add_argument("--skip-bsr", action="store_true")
+    ap.add_argument("--table", default=None, help="print the markdown tables of a sweep JSONL")
     args = ap.parse_args()
+    if args.table:
+        table(args.table)
+        return
     import torch
     from spmm_hip import ops
     from spmm_hip._lib import lib
