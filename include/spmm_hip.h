@@ -364,6 +364,28 @@ spmm_status_t spmm_bsrmm_ex_f16(spmm_handle_t handle, spmm_direction_t dir, int 
                                 spmm_order_t orderB, float beta, float* C, int ldc,
                                 spmm_order_t orderC);
 
+/* Re-blocking to bs 32 on the device (an extension; DESIGN.md §4, "Small blocks
+ * re-blocked to 32"): the same matrix in 32 x 32 blocks, so a bs = 2 / 4 / 8 / 16
+ * product can run on the bs 32 MFMA streams (spmm_bsr32_analysis_f32 +
+ * spmm_bsrmm_analysed_f32, or the group analysis) instead of the VALU kernel.
+ * A block (I, J) of blockDim lands in block (I / R, J / R), R = 32 / blockDim, at
+ * sub-block (I % R, J % R); the rest of each 32 x 32 block is zero. dir is kept
+ * (ROW blocks stay ROW). mb32 = ceil(mb / R) block rows; the product then needs
+ * B with ceil(kb / R) * 32 rows and C with mb32 * 32 rows (the extra rows are
+ * zero columns / rows of A). cusparseXcsr2bsrNnz / Scsr2bsr's two calls: the
+ * first fills bsrRowPtr32[mb32 + 1] and *nnzb32HostPtr (it synchronises the
+ * handle's stream), the second bsrColInd32[nnzb32] and bsrVal32[nnzb32 * 1024]
+ * (zero-filled first; no synchronisation). Block columns must be sorted per
+ * block row; a negative one is INVALID_VALUE. */
+spmm_status_t spmm_xbsr_reblock32_nnzb(spmm_handle_t handle, spmm_direction_t dir, int mb,
+                                       int nnzb, int blockDim, const int* bsrRowPtr,
+                                       const int* bsrColInd, int* bsrRowPtr32,
+                                       int* nnzb32HostPtr);
+spmm_status_t spmm_sbsr_reblock32(spmm_handle_t handle, spmm_direction_t dir, int mb, int nnzb,
+                                  int blockDim, const int* bsrRowPtr, const int* bsrColInd,
+                                  const float* bsrVal, const int* bsrRowPtr32, int nnzb32,
+                                  int* bsrColInd32, float* bsrVal32);
+
 /* ------------------------------------------------------------------------ */
 /* Preprocessing on the HOST (all pointers are host pointers)                  */
 /* ------------------------------------------------------------------------ */

@@ -18,6 +18,7 @@
 // its block row's entries with coalesced stores.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 
 #include "context.hpp"
@@ -192,6 +193,90 @@ __global__ __launch_bounds__(256) void coo2csr_kernel(const int* __restrict__ co
   csr_rowptr[r] = lo + base;
 }
 
+// Re-blocking to bs 32 (spmm_xbsr_reblock32_nnzb / spmm_sbsr_reblock32): a small
+// block (bs = 2 / 4 / 8 / 16, R = 32 / bs of them per side of a 32 x 32 block) of
+// block row I and block column J lies inside the 32 x 32 block (I / R, J / R), at
+// sub-block (I % R, J % R). One wave per 32-row block row merges its R block rows'
+// sorted block-column lists on J / R (lane r < R holds block row I32 * R + r's
+// cursor): PASS 1 counts the distinct J / R, PASS 2 writes them and, per small
+// block, its 32 x 32 block and the element offset of its sub-block there.
+template <bool FILL>
+__global__ __launch_bounds__(kWG) void reblock32_kernel(int mb, int R, int shift,
+                                                        const int* __restrict__ rowptr,
+                                                        const int* __restrict__ colind,
+                                                        int* __restrict__ count,
+                                                        const int* __restrict__ rowptr32,
+                                                        int* __restrict__ colind32,
+                                                        int* __restrict__ map_k,
+                                                        int* __restrict__ map_off, int bs,
+                                                        int rowdir, int* __restrict__ bad) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int mb32 = (mb + R - 1) / R;
+  const int br = blockIdx.x * (kWG / kWave) + (threadIdx.x >> 6);
+  if (br >= mb32) return;
+  const int I = br * R + lane;
+  int ptr = 0, end = 0;
+  if (lane < R && I < mb) {
+    ptr = rowptr[I];
+    end = rowptr[I + 1];
+  }
+  int flag = 0;
+  auto head = [&]() -> int {
+    while (ptr < end) {
+      const int J = colind[ptr];
+      if (J >= 0) return J >> shift;
+      flag = 1;  // a negative block column: skipped and reported
+      ++ptr;
+    }
+    return INT_MAX;
+  };
+  int hd = head();
+  int k = FILL ? rowptr32[br] : 0;
+  int t = 0;
+  while (true) {
+    const int mn = wave_min(hd);
+    if (mn == INT_MAX) break;
+    if (FILL && lane == 0) colind32[k] = mn;
+    if (hd == mn) {
+      while (ptr < end) {
+        const int J = colind[ptr];
+        if (J < 0) {
+          flag = 1;
+          ++ptr;
+          continue;
+        }
+        if ((J >> shift) != mn) break;
+        if constexpr (FILL) {
+          const int sc = (J & (R - 1)) * bs, sr = lane * bs;  // sub-block column / row
+          map_k[ptr] = k;
+          map_off[ptr] = rowdir ? sr * 32 + sc : sc * 32 + sr;
+        }
+        ++ptr;
+      }
+      hd = head();
+    }
+    ++k;
+    ++t;
+  }
+  if (!FILL && lane == 0) count[br] = t;
+  if (flag) *bad = 1;
+}
+
+// Element e of small block b to its place in the zero-filled bs 32 values (ROW: e =
+// row * bs + col, COLUMN: e = col * bs + row; both land at off + (e / bs) * 32 + e % bs).
+__global__ __launch_bounds__(256) void reblock32_values_kernel(long long total, int bs, int bs2,
+                                                               const float* __restrict__ val,
+                                                               const int* __restrict__ map_k,
+                                                               const int* __restrict__ map_off,
+                                                               float* __restrict__ val32) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total;
+       i += (long long)gridDim.x * 256) {
+    const long long b = i / bs2;
+    const int e = (int)(i - b * bs2);
+    val32[(size_t)map_k[b] * 1024 + map_off[b] + (e / bs) * 32 + e % bs] = val[i];
+  }
+}
+
 }  // namespace
 
 namespace spmm {
@@ -316,6 +401,79 @@ spmm_status_t spmm_sbsr2csr_dev(spmm_handle_t handle, spmm_direction_t dir, int 
     hipLaunchKernelGGL((bsr2csr_kernel<false>), grid, dim3(kWG), 0, ctx->stream, mb, blockDim,
                        bsrRowPtr, bsrColInd, bsrVal, (int)descrA->base, (int)descrC->base,
                        csrRowPtr, csrColInd, csrVal);
+  return spmm::from_hip(hipGetLastError());
+}
+
+spmm_status_t spmm_xbsr_reblock32_nnzb(spmm_handle_t handle, spmm_direction_t dir, int mb,
+                                       int nnzb, int blockDim, const int* bsrRowPtr,
+                                       const int* bsrColInd, int* bsrRowPtr32,
+                                       int* nnzb32HostPtr) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if ((dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) || mb < 0 || nnzb < 0 ||
+      !nnzb32HostPtr)
+    return SPMM_STATUS_INVALID_VALUE;
+  if (blockDim != 2 && blockDim != 4 && blockDim != 8 && blockDim != 16 && blockDim != 32)
+    return SPMM_STATUS_INVALID_VALUE;
+  if (!bsrRowPtr32 || (mb > 0 && !bsrRowPtr) || (nnzb > 0 && !bsrColInd))
+    return SPMM_STATUS_INVALID_VALUE;
+  spmm_context* ctx = handle;
+  const int R = 32 / blockDim, shift = __builtin_ctz(R);
+  const int mb32 = (mb + R - 1) / R;
+  const size_t need = 32 + (((size_t)mb32 * 4 + 255) & ~(size_t)255);
+  if (spmm_status_t st = spmm::ensure_workspace(ctx, need); st != SPMM_STATUS_SUCCESS) return st;
+  char* ws = static_cast<char*>(ctx->ws);
+  long long* total = reinterpret_cast<long long*>(ws);
+  int* bad = reinterpret_cast<int*>(ws + 8);
+  int* count = reinterpret_cast<int*>(ws + 32);
+  if (hipMemsetAsync(ws, 0, 32, ctx->stream) != hipSuccess) return SPMM_STATUS_EXECUTION_FAILED;
+  if (mb32 > 0)
+    hipLaunchKernelGGL(reblock32_kernel<false>, dim3((mb32 + 3) / 4), dim3(kWG), 0, ctx->stream,
+                       mb, R, shift, bsrRowPtr, bsrColInd, count, nullptr, nullptr, nullptr,
+                       nullptr, blockDim, dir == SPMM_DIRECTION_ROW ? 1 : 0, bad);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, count, mb32, 0,
+                     bsrRowPtr32, total);
+  long long host[2] = {0, 0};
+  if (hipMemcpyAsync(host, ws, 16, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess)
+    return SPMM_STATUS_EXECUTION_FAILED;
+  if ((int)(host[1] & 0xffffffff) != 0) return SPMM_STATUS_INVALID_VALUE;  // negative column
+  if (host[0] > INT32_MAX) return SPMM_STATUS_NOT_SUPPORTED;
+  *nnzb32HostPtr = (int)host[0];
+  return spmm::from_hip(hipGetLastError());
+}
+
+spmm_status_t spmm_sbsr_reblock32(spmm_handle_t handle, spmm_direction_t dir, int mb, int nnzb,
+                                  int blockDim, const int* bsrRowPtr, const int* bsrColInd,
+                                  const float* bsrVal, const int* bsrRowPtr32, int nnzb32,
+                                  int* bsrColInd32, float* bsrVal32) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if ((dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) || mb < 0 || nnzb < 0 ||
+      nnzb32 < 0)
+    return SPMM_STATUS_INVALID_VALUE;
+  if (blockDim != 2 && blockDim != 4 && blockDim != 8 && blockDim != 16 && blockDim != 32)
+    return SPMM_STATUS_INVALID_VALUE;
+  if (!bsrRowPtr32 || (mb > 0 && !bsrRowPtr) || (nnzb > 0 && (!bsrColInd || !bsrVal)) ||
+      (nnzb32 > 0 && (!bsrColInd32 || !bsrVal32)))
+    return SPMM_STATUS_INVALID_VALUE;
+  spmm_context* ctx = handle;
+  const int R = 32 / blockDim, shift = __builtin_ctz(R);
+  const int mb32 = (mb + R - 1) / R;
+  if (hipMemsetAsync(bsrVal32, 0, (size_t)nnzb32 * 1024 * sizeof(float), ctx->stream) != hipSuccess)
+    return SPMM_STATUS_EXECUTION_FAILED;
+  if (nnzb == 0 || mb32 == 0) return SPMM_STATUS_SUCCESS;
+  const size_t need = 32 + (size_t)nnzb * 8;
+  if (spmm_status_t st = spmm::ensure_workspace(ctx, need); st != SPMM_STATUS_SUCCESS) return st;
+  char* ws = static_cast<char*>(ctx->ws);
+  int* bad = reinterpret_cast<int*>(ws);
+  int* map_k = reinterpret_cast<int*>(ws + 32);
+  int* map_off = map_k + nnzb;
+  hipLaunchKernelGGL(reblock32_kernel<true>, dim3((mb32 + 3) / 4), dim3(kWG), 0, ctx->stream, mb,
+                     R, shift, bsrRowPtr, bsrColInd, nullptr, bsrRowPtr32, bsrColInd32, map_k,
+                     map_off, blockDim, dir == SPMM_DIRECTION_ROW ? 1 : 0, bad);
+  const long long total = (long long)nnzb * blockDim * blockDim;
+  const long long blocks = std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(reblock32_values_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
+                     total, blockDim, blockDim * blockDim, bsrVal, map_k, map_off, bsrVal32);
   return spmm::from_hip(hipGetLastError());
 }
 

@@ -124,6 +124,9 @@ _PROTOS = {
     "spmm_divide_nnz": (c_int, [c_int, _P, _P, c_int, c_float, _P, _P, _PI, _PI]),
     "spmm_sdivide": (c_int, [c_int, _P, _P, _P, c_int, c_float, _P, _P, _P, _P, _P, _P]),
     "spmm_xcsr2bsr_nnz_dev": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, _PI]),
+    "spmm_xbsr_reblock32_nnzb": (c_int, [_P, c_int, c_int, c_int, c_int, _P, _P, _P, _PI]),
+    "spmm_sbsr_reblock32": (c_int, [_P, c_int, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P,
+                                    _P]),
     "spmm_scsr2bsr_dev": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P,
                                   _P]),
     "spmm_sbsr2csr_dev": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P,

@@ -486,6 +486,35 @@ def csr2bsr(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, *, m:
     return brp, bci, bval
 
 
+def bsr_reblock32(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, *, mb: int,
+                  bs: int, direction: int = DIRECTION_ROW, handle: Handle | None = None):
+    """The same BSR matrix in 32 x 32 blocks (spmm_xbsr_reblock32_nnzb +
+    spmm_sbsr_reblock32): a bs = 2 / 4 / 8 / 16 matrix onto the bs 32 MFMA streams.
+    Returns (rowptr32, colind32, val32) with ceil(mb * bs / 32) block rows."""
+    for t, dt, nm in ((rowptr, torch.int32, "rowptr"), (colind, torch.int32, "colind"),
+                      (val, torch.float32, "val")):
+        _need(t, dt, nm)
+    nnzb = colind.numel()
+    if rowptr.numel() < mb + 1 or val.numel() < nnzb * bs * bs:
+        raise ValueError("bsr_reblock32: rowptr needs mb + 1 entries, val nnzb * bs^2")
+    h = handle or default_handle()
+    R = 32 // bs if bs in (2, 4, 8, 16, 32) else 0
+    if not R:
+        raise ValueError("bsr_reblock32: bs must divide 32")
+    mb32 = (mb + R - 1) // R
+    rp32 = torch.empty(mb32 + 1, dtype=torch.int32, device=val.device)
+    nnzb32 = c_int(0)
+    check(lib().spmm_xbsr_reblock32_nnzb(h.raw, direction, mb, nnzb, bs, _ptr(rowptr),
+                                         _ptr(colind), _ptr(rp32), byref(nnzb32)),
+          "spmm_xbsr_reblock32_nnzb")
+    ci32 = torch.empty(max(nnzb32.value, 1), dtype=torch.int32, device=val.device)
+    v32 = torch.empty(max(nnzb32.value, 1) * 1024, dtype=torch.float32, device=val.device)
+    check(lib().spmm_sbsr_reblock32(h.raw, direction, mb, nnzb, bs, _ptr(rowptr), _ptr(colind),
+                                    _ptr(val), _ptr(rp32), nnzb32.value, _ptr(ci32), _ptr(v32)),
+          "spmm_sbsr_reblock32")
+    return rp32, ci32[:nnzb32.value], v32[:nnzb32.value * 1024]
+
+
 def bsr2csr(rowptr: torch.Tensor, colind: torch.Tensor, val: torch.Tensor, *, mb: int, nb: int,
             bs: int, direction: int = DIRECTION_ROW, base: int = 0,
             handle: Handle | None = None):

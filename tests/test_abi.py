@@ -104,7 +104,7 @@ def test_release_build_reads_no_environment():
     data = open(_lib.LIB_PATH, "rb").read()
     for var in (b"SPMM_BSR_VARIANT", b"SPMM_BSR_ORDER", b"SPMM_CSR_GROUP_PD", b"SPMM_GRP_VARIANT",
                 b"SPMM_CSR_MIN_ITEMS", b"SPMM_GRP32_VARIANT", b"SPMM_GRP_XM", b"SPMM_GRP_TT",
-                b"SPMM_CS16_TT"):
+                b"SPMM_CS16_TT", b"SPMM_SMALL_XM"):
         assert var not in data, var
     assert L.spmm_set_bsr_options(None, 1) == 1
     assert L.spmm_get_version() == 100

@@ -1451,3 +1451,93 @@ def test_group_analysis_fill_is_graph_capturable(device, bs):
     for b in (buf, buf2):
         lib().spmm_bsr_group_release(h.raw, c_void_p(b.data_ptr()))
     h.close()
+
+
+def _reblock32_numpy(rp, ci, v, bs, mb, direction):
+    """Host restatement of spmm_xbsr_reblock32_nnzb + spmm_sbsr_reblock32: block
+    (I, J) of size bs into block (I // R, J // R) of size 32 at sub-block
+    (I % R, J % R), R = 32 // bs, the rest zero; direction kept."""
+    R = 32 // bs
+    mb32 = -(-mb // R)
+    vb = v.reshape(-1, bs, bs)
+    rows32, vals = [], {}
+    for I32 in range(mb32):
+        cols = set()
+        for I in range(I32 * R, min(mb, I32 * R + R)):
+            for k in range(rp[I], rp[I + 1]):
+                J = int(ci[k])
+                cols.add(J // R)
+                blk = vals.setdefault((I32, J // R), np.zeros((32, 32), np.float32))
+                r0, c0 = (I % R) * bs, (J % R) * bs
+                if direction == 0:
+                    blk[r0:r0 + bs, c0:c0 + bs] = vb[k]
+                else:  # COLUMN blocks: stored transposed, and so is the 32 x 32 block
+                    blk[c0:c0 + bs, r0:r0 + bs] = vb[k]
+        rows32.append(sorted(cols))
+    rp32 = np.concatenate([[0], np.cumsum([len(c) for c in rows32])]).astype(np.int32)
+    ci32 = np.array([c for cs in rows32 for c in cs], np.int32)
+    v32 = np.stack([vals[(I32, c)] for I32, cs in enumerate(rows32) for c in cs]) \
+        if ci32.size else np.zeros((0, 32, 32), np.float32)
+    return rp32, ci32, v32.reshape(-1)
+
+
+@pytest.mark.parametrize("bs", [2, 4, 8, 16])
+@pytest.mark.parametrize("direction", [0, 1])
+def test_bsr_reblock32_exact_and_product(oracle, device, bs, direction):
+    """spmm_xbsr_reblock32_nnzb + spmm_sbsr_reblock32 against the host
+    restatement, bit for bit (row pointer, block columns, every value and
+    zero), for ROW and COLUMN blocks, an mb the ratio R = 32 / bs does not
+    divide and an empty block row; then the bs 32 analysed stream on the
+    re-blocked matrix against the f64 oracle of the ORIGINAL matrix."""
+    from spmm_hip._lib import DIRECTION_COLUMN, DIRECTION_ROW
+    ops = _ops()
+    rng = np.random.default_rng(40 + bs + 7 * direction)
+    R = 32 // bs
+    mb, kb = 5 * R + 3, 4 * R + 1
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.15, empty_rows=(2,))
+    dr = DIRECTION_ROW if direction == 0 else DIRECTION_COLUMN
+    drp, dci, dv = _dev(rp, ci, v)
+    rp32, ci32, v32 = ops.bsr_reblock32(drp, dci, dv, mb=mb, bs=bs, direction=dr)
+    torch.cuda.synchronize()
+    wrp, wci, wv = _reblock32_numpy(rp, ci, v, bs, mb, direction)
+    assert np.array_equal(rp32.cpu().numpy(), wrp)
+    assert np.array_equal(ci32.cpu().numpy(), wci)
+    assert np.array_equal(v32.cpu().numpy(), wv), "values placed differently"
+    mb32, kb32 = -(-mb // R), -(-kb // R)
+    n = 128
+    Bh = np.zeros((kb32 * 32, n), np.float32)
+    Bh[:kb * bs] = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    if direction == 0:
+        masks, vcol = ops.bsr32_analysis(v32, nnzb=int(ci32.numel()))
+        C = torch.zeros((mb32 * 32, n), device=device)
+        ops.bsrmm_analysed(rp32, ci32, vcol, masks, torch.from_numpy(Bh).to(device), mb=mb32,
+                           kb=kb32, n=n, ldb=n, C=C, ldc=n)
+    else:
+        C = torch.zeros((mb32 * 32, n), device=device)
+        ops.bsrmm(rp32, ci32, v32, torch.from_numpy(Bh).to(device), mb=mb32, kb=kb32, n=n, bs=32,
+                  ldb=n, C=C, ldc=n, direction=dr)
+    torch.cuda.synchronize()
+    ref, absd = oracle_bsrmm_f64(oracle, direction, mb, n, bs, rp, ci, v, Bh[:kb * bs], n, 0)
+    got = C.cpu().numpy()
+    assert_normwise(got[:mb * bs], ref, absd, TOL_F32, f"reblocked bs {bs} dir {direction}")
+    assert not got[mb * bs:].any(), "rows past mb * bs must stay zero"
+
+
+def test_bsr_reblock32_matches_csr2bsr32_full_size(device):
+    """At full size (the reddit stand-in): csr2bsr at bs 8 then re-blocking to
+    32 is, bit for bit, csr2bsr at bs 32 of the same CSR (the same blocks, the
+    same values, the same explicit zeros)."""
+    from spmm_hip import prep
+    ops = _ops()
+    n = 232965
+    rp, ci = prep.community_csr(n, 670.0, 512, 2048, 0.99, 1234)
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
+    drp, dci, dv = _dev(rp, ci, v)
+    b8 = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=8)
+    b32 = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=32)
+    del dci, dv
+    mb8 = (n + 7) // 8
+    r32 = ops.bsr_reblock32(b8[0], b8[1], b8[2], mb=mb8, bs=8)
+    torch.cuda.synchronize()
+    assert torch.equal(r32[0], b32[0]) and torch.equal(r32[1], b32[1])
+    assert torch.equal(r32[2], b32[2]), "re-blocked values differ from csr2bsr at bs 32"
