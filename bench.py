@@ -72,12 +72,13 @@ WORKLOADS = {
     "products_bsr16_f16_an": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                   p_in=0.97, bs=16, K=512, dtype="fp16", analysed=True),
     # config 5 on the grouped stream (spmm_bsr16_group_analysis_f16 once, groups of
-    # `grouped` block rows sharing their B-row copies; spmm_bsrmm_grouped_f16 timed)
+    # `grouped` block rows sharing their B-row copies, "auto" = the library's choice
+    # per matrix; spmm_bsrmm_grouped_f16 timed)
     "products_bsr16_f16_grp": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
-                                   p_in=0.97, bs=16, K=512, dtype="fp16", grouped=4),
+                                   p_in=0.97, bs=16, K=512, dtype="fp16", grouped="auto"),
     "products_rcm_bsr16_f16_grp": dict(kind="bsr", n=2449029, avg_deg=27.0, cmin=32, cmax=512,
                                        p_in=0.97, bs=16, K=512, dtype="fp16", reorder="rcm",
-                                       grouped=4),
+                                       grouped="auto"),
     # configs 3 and north_star's products bs 32 on the grouped bs 32 stream
     # (spmm_bsr32_group_analysis_f32 once; spmm_bsrmm_grouped_f32 timed)
     "reddit_bsr32_grp": dict(kind="bsr", n=232965, avg_deg=670.0, cmin=512, cmax=2048, p_in=0.99,
@@ -942,7 +943,8 @@ def run_bsr(args, W, world, rank, dev, dist):
     h = ops.Handle()
     fn = ops.bsrmm if dt == "fp32" else ops.bsrmm_f16
     an = bool(W.get("analysed") or W.get("reblock"))
-    gw = int(args.group_rows or W.get("grouped") or 0)
+    gsel = args.group_rows or W.get("grouped") or 0
+    gw = -1 if gsel == "auto" else int(gsel)  # -1: grouped, W chosen by the library
     analysis_ms = analysis_first_ms = None
     grp = None
     if gw:
@@ -950,7 +952,8 @@ def run_bsr(args, W, world, rank, dev, dist):
             raise SystemExit("the grouped streams are bs 16 fp16 and bs 32 fp32")
         Grouped = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
         grp, analysis_first_ms, analysis_ms = _timed_analysis(
-            lambda: Grouped(d_brp, d_bci, d_bv, mb=mb, group_rows=gw, handle=h))
+            lambda: Grouped(d_brp, d_bci, d_bv, mb=mb, group_rows=max(gw, 0), handle=h))
+        gw = grp.W
         del d_bv
 
         def fn(rp_, ci_, _v, B_, *, mb, kb, n, bs, ldb, C, ldc, order_b=ops.ORDER_ROW,
@@ -1140,18 +1143,19 @@ def run_bsr(args, W, world, rank, dev, dist):
         # Beside the drop-in line (not `value`): the grouped stream (groups of 4 block
         # rows sharing their B-row copies, analysis once, timed apart).
         g4, a_ms, a_rep = _timed_analysis(lambda: ops.GroupedBsr16(d_brp, d_bci, d_bv, mb=mb,
-                                                                   group_rows=4, handle=h))
+                                                                   group_rows=0, handle=h))
         e_g, k_g = timed_loop(lambda: g4.mm(B, kb=mb, n=K, ldb=K, C=C, ldc=K), h, args.steps,
                               args.warmup, 1, dist)
-        ni = (g4.bytes - 256) // (64 + 4 * 512)
+        ni = (g4.bytes - 256) // (64 + g4.W * 512)
         rec["grouped_entry"] = {
-            "entry": "spmm_bsr16_group_analysis_f16 (4 block rows per group) once + "
-                     "spmm_bsrmm_grouped_f16 per step",
+            "entry": f"spmm_bsr16_group_analysis_f16 (groupRows 0: the library chose "
+                     f"{g4.W} block rows per group) once + spmm_bsrmm_grouped_f16 per step",
+            "group_rows": g4.W,
             "value": round(2.0 * nnz * K * args.steps / e_g / 1e9, 2), "unit": "GFLOP/s",
             "ms_per_step": round(e_g / args.steps * 1e3, 4), "kernel_ms": round(k_g, 4),
             "analysis_ms_first_call": round(a_ms, 3), "analysis_ms_repeat": round(a_rep, 3),
             "items": int(ni),
-            "mfma_executed_TFLOPs": round(ni * 4 * 2.0 * 256 * K / (k_g / 1e3) / 1e12, 2),
+            "mfma_executed_TFLOPs": round(ni * g4.W * 2.0 * 256 * K / (k_g / 1e3) / 1e12, 2),
             **_epoch_loop(a_rep, e_g / args.steps * 1e3, elapsed / args.steps * 1e3)}
         g4.close()
         del g4

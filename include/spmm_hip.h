@@ -286,7 +286,10 @@ spmm_status_t spmm_bsrmm_analysed_f16(spmm_handle_t handle, int mb, int kb, int 
 
 /* The grouped bs = 16 fp16 stream (an extension, once per matrix like the
  * analyses above; DESIGN.md §4 "The grouped stream"). groupRows (2, 4 or 8;
- * 0 = 4) adjacent block rows form a group whose waves share one copy of each
+ * 0 = the library's choice per matrix: the size query counts the items of
+ * every W and keeps the one its time model ranks first, so a reordered graph
+ * whose neighbouring rows share few columns gets 2; word 0 of the buffer holds
+ * the W taken) adjacent block rows form a group whose waves share one copy of each
  * B row the union of their nonzero columns needs: on a reordered graph
  * neighbouring block rows need mostly the same rows (products stand-in: the
  * union is 0.43 of the (block row, column) pairs at 4 rows, 0.29 at 8).

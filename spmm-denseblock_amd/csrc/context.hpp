@@ -65,7 +65,7 @@ struct spmm_context {
   // (group.cpp). Cleared by that call and by a size query of other arguments.
   struct GroupPending {
     bool valid = false;
-    int bs = 0, W = 0, dir = 0, mb = 0, nnzb = 0;
+    int bs = 0, W = 0, req = -1, dir = 0, mb = 0, nnzb = 0;  // req: the caller's groupRows
     const void *rp = nullptr, *ci = nullptr, *val = nullptr;
     long long nitems = 0;
     int max_col = -1;

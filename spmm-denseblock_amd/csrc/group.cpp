@@ -29,7 +29,8 @@
 // and its second ran the masks and PASS 1 again behind two synchronisations.
 //
 // Buffer layout (caller-owned device memory, bufferBytes from the first call):
-//   [0, 256)                 reserved header
+//   [0, 256)                 header: word 0 = W, the block rows per group (the
+//                            library's choice when groupRows was 0); the rest zero
 //   item_ptr[ngroups + 1]    int32, the items of group g are [item_ptr[g], item_ptr[g+1])
 //   rows[nitems][E]          int32, B row of each entry (-1: padding)
 //   bs 16: afrag[nitems][W][128]  uint32, lane l of wave w: A[l & 15][4 (l >> 4) .. + 3] fp16 x 4
@@ -70,8 +71,8 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
   if ((dir != SPMM_DIRECTION_ROW && dir != SPMM_DIRECTION_COLUMN) || mb < 0 || nnzb < 0 ||
       !bufferBytes)
     return SPMM_STATUS_INVALID_VALUE;
-  const int W = groupRows == 0 ? (BS == 16 ? 4 : 2) : groupRows;
-  if (W != 2 && W != 4 && (BS == 32 || W != 8)) return SPMM_STATUS_INVALID_VALUE;
+  if (groupRows != 0 && groupRows != 2 && groupRows != 4 && (BS == 32 || groupRows != 8))
+    return SPMM_STATUS_INVALID_VALUE;
   if (mb > 0 && !bsrRowPtr) return SPMM_STATUS_INVALID_VALUE;
   if (nnzb > 0 && (!bsrColInd || !bsrVal)) return SPMM_STATUS_INVALID_VALUE;
   // the mask and fill kernels read the values as f32x4 (BS 32) / u16x4 (BS 16)
@@ -79,29 +80,43 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
   if (nnzb > 0 && reinterpret_cast<uintptr_t>(bsrVal) % (BS == 32 ? 16 : 8) != 0)
     return SPMM_STATUS_INVALID_VALUE;
   const int E = BS == 16 ? 16 : 8;  // entries per item
-  const int ngroups = (mb + W - 1) / W;
   hipStream_t st = handle->stream;
   auto& pend = handle->grp_pending;
-  const bool same = pend.valid && pend.bs == BS && pend.W == W && pend.dir == (int)dir &&
+  const bool same = pend.valid && pend.bs == BS && pend.req == groupRows && pend.dir == (int)dir &&
                     pend.mb == mb && pend.nnzb == nnzb && pend.rp == bsrRowPtr &&
                     pend.ci == bsrColInd && pend.val == bsrVal;
   if (!same) {
-    // the size query: masks [nnzb], item pointers [ngroups + 1] and the stats in grp_pend,
-    // per-group counts and largest block columns [2 ngroups] in the scratch
+    // The size query. Candidates: groupRows itself, or at BS 16 with groupRows = 0 every W
+    // (2, 4, 8), of which the one with the least modelled time is kept (below); BS 32 with 0
+    // takes 2. grp_pend holds the masks [nnzb], per candidate the item pointers
+    // [ngroups + 1], and per candidate 32 B of stats; the scratch the per-group counts and
+    // largest block columns [2 ngroups] per candidate.
     pend.valid = false;
+    int cand[3] = {groupRows, 0, 0}, nc = 1;
+    if (groupRows == 0) {
+      if (BS == 16) {
+        cand[0] = 2;
+        cand[1] = 4;
+        cand[2] = 8;
+        nc = 3;
+      } else {
+        cand[0] = 2;
+      }
+    }
     const size_t mk_bytes = align256((size_t)nnzb * 4);
-    const size_t ptr_off = mk_bytes;
-    const size_t stat_off = align256(ptr_off + (size_t)(ngroups + 1) * 4);
-    if (spmm_status_t s = ensure_group_pending(handle, stat_off + 256)) return s;
-    if (spmm_status_t s = ensure_scratch(handle, (size_t)ngroups * 8 + 8)) return s;
+    size_t ptr_off[3], cnt_off[3], stat_off = mk_bytes, scr = 0;
+    for (int i = 0; i < nc; ++i) {
+      const int ng = (mb + cand[i] - 1) / cand[i];
+      ptr_off[i] = stat_off;
+      stat_off = align256(stat_off + (size_t)(ng + 1) * 4);
+      cnt_off[i] = scr;
+      scr += align256((size_t)ng * 8);
+    }
+    if (spmm_status_t s = ensure_group_pending(handle, stat_off + 32 * nc)) return s;
+    if (spmm_status_t s = ensure_scratch(handle, scr + 8)) return s;
     char* pb = static_cast<char*>(handle->grp_pend);
     unsigned* dmk = reinterpret_cast<unsigned*>(pb);
-    int* dptr = reinterpret_cast<int*>(pb + ptr_off);
-    long long* dtot = reinterpret_cast<long long*>(pb + stat_off);
-    int* dstat = reinterpret_cast<int*>(pb + stat_off + 8);
-    int* dcnt = static_cast<int*>(handle->scratch);
-    int* dmaxj = dcnt + ngroups;
-    hipError_t e = hipMemsetAsync(pb + stat_off, 0, 16, st);
+    hipError_t e = hipMemsetAsync(pb + stat_off, 0, 32 * nc, st);
     if (e != hipSuccess) return from_hip(e);
     if (nnzb > 0 && mb > 0) {
       spmm_status_t s = BS == 16
@@ -109,35 +124,65 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
           : launch_bsr32_analysis(handle, dir, nnzb, static_cast<const float*>(bsrVal), dmk, nullptr);
       if (s) return s;
     }
-    if (mb > 0) {
-      if (spmm_status_t s = launch_grp_build(handle, W, BS, false, mb, nnzb, ngroups, bsrRowPtr,
-                                             bsrColInd, dmk, dcnt, dmaxj, nullptr, nullptr, nullptr,
-                                             nullptr))
-        return s;
-      if (spmm_status_t s = launch_scan_counts(handle, dcnt, ngroups, dptr, dtot)) return s;
-      if (spmm_status_t s = launch_grp_stats(handle, dmaxj, ngroups, dstat)) return s;
-    } else {
-      e = hipMemsetAsync(dptr, 0, 4, st);
-      if (e != hipSuccess) return from_hip(e);
-      e = hipMemsetAsync(dstat, 0xff, 4, st);  // max_col -1
-      if (e != hipSuccess) return from_hip(e);
+    for (int i = 0; i < nc; ++i) {
+      const int ng = (mb + cand[i] - 1) / cand[i];
+      int* dptr = reinterpret_cast<int*>(pb + ptr_off[i]);
+      long long* dtot = reinterpret_cast<long long*>(pb + stat_off + 32 * i);
+      int* dstat = reinterpret_cast<int*>(pb + stat_off + 32 * i + 8);
+      int* dcnt = reinterpret_cast<int*>(static_cast<char*>(handle->scratch) + cnt_off[i]);
+      int* dmaxj = dcnt + ng;
+      if (mb > 0) {
+        if (spmm_status_t s = launch_grp_build(handle, cand[i], BS, false, mb, nnzb, ng, bsrRowPtr,
+                                               bsrColInd, dmk, dcnt, dmaxj, nullptr, nullptr,
+                                               nullptr, nullptr))
+          return s;
+        if (spmm_status_t s = launch_scan_counts(handle, dcnt, ng, dptr, dtot)) return s;
+        if (spmm_status_t s = launch_grp_stats(handle, dmaxj, ng, dstat)) return s;
+      } else {
+        e = hipMemsetAsync(dptr, 0, 4, st);
+        if (e == hipSuccess) e = hipMemsetAsync(dstat, 0xff, 4, st);  // max_col -1
+        if (e != hipSuccess) return from_hip(e);
+      }
     }
-    struct { long long total; int max_col, bad; } host{};
-    e = hipMemcpyAsync(&host, dtot, 16, hipMemcpyDeviceToHost, st);
+    struct Stat { long long total; int max_col, bad, pad[4]; } host[3]{};
+    static_assert(sizeof(Stat) == 32, "stats record");
+    e = hipMemcpyAsync(host, pb + stat_off, 32 * nc, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return from_hip(e);
-    if (host.bad) return SPMM_STATUS_INVALID_VALUE;  // a bad row pointer or negative block column
-    if (host.total > INT_MAX) return SPMM_STATUS_NOT_SUPPORTED;  // int32 item pointers
-    const long long nitems = host.total;
+    if (host[0].bad) return SPMM_STATUS_INVALID_VALUE;  // a bad row pointer or negative block column
+    // The choice at BS 16: modelled time items(W) * (kCopy + W) per column tile. An item
+    // costs its 16 B-row copies and barrier once per workgroup (kCopy, in units of one
+    // wave's 16 MFMAs and transposed reads of the item) plus W waves' MFMAs, every wave
+    // multiplying every item whether its block row holds the entries or not. kCopy = 2.74
+    // fits round 4's products stand-in (1.39 M items at W = 2, 0.88 M at W = 4: 3.19
+    // against 2.87 ms); it picks W = 2 where the rows share few columns (a union about
+    // the sum of the rows') and W = 4 or 8 where they share many.
+    int pick = 0;
+    if (nc > 1) {
+      constexpr double kCopy = 2.74;
+      double best = -1.0;
+      for (int i = 0; i < nc; ++i) {
+        const double t = (double)host[i].total * (kCopy + cand[i]);
+        if (best < 0.0 || t < best) {
+          best = t;
+          pick = i;
+        }
+      }
+    }
+    const int W = cand[pick];
+    const int ngroups = (mb + W - 1) / W;
+    if (host[pick].total > INT_MAX) return SPMM_STATUS_NOT_SUPPORTED;  // int32 item pointers
+    const long long nitems = host[pick].total;
     pend.rows_off = align256(256 + (size_t)(ngroups + 1) * 4);
     pend.wmask_off = align256(pend.rows_off + (size_t)nitems * E * 4);  // bs 32 only
     pend.afrag_off = BS == 16 ? pend.wmask_off : align256(pend.wmask_off + (size_t)nitems * W * 4);
     pend.need = pend.afrag_off + (size_t)nitems * W * (BS == 16 ? 512 : 1024);
     pend.nitems = nitems;
-    pend.max_col = host.max_col;
-    pend.ptr_off = ptr_off;
+    pend.max_col = host[pick].max_col;
+    pend.ptr_off = ptr_off[pick];
     pend.bs = BS;
     pend.W = W;
+    pend.req = groupRows;
     pend.dir = (int)dir;
     pend.mb = mb;
     pend.nnzb = nnzb;
@@ -146,6 +191,8 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
     pend.val = bsrVal;
     pend.valid = true;
   }
+  const int W = pend.W;
+  const int ngroups = (mb + W - 1) / W;
   if (!buffer) {
     *bufferBytes = pend.need;
     return SPMM_STATUS_SUCCESS;
@@ -156,6 +203,7 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
   char* buf = static_cast<char*>(buffer);
   const char* pb = static_cast<const char*>(handle->grp_pend);
   hipError_t e = hipMemsetAsync(buf, 0, 256, st);
+  if (e == hipSuccess) e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(buf), W, 1, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(buf + 256, pb + pend.ptr_off, (size_t)(ngroups + 1) * 4,
                        hipMemcpyDeviceToDevice, st);

@@ -336,6 +336,8 @@ class _Grouped:
         check(fn(*args, _ptr(buf), byref(size)), self.ANALYSIS)
         self.buffer = buf
         self.bytes = size.value
+        # block rows per group: the header's word 0 (the library's choice when group_rows = 0)
+        self.W = int(buf[:4].view(torch.int32).item()) if size.value >= 4 else group_rows
 
     def mm(self, B: torch.Tensor, *, kb: int, n: int, ldb: int, C: torch.Tensor, ldc: int,
            order_b: int = ORDER_ROW, order_c: int = ORDER_ROW, alpha: float = 1.0,
@@ -370,13 +372,14 @@ class _Grouped:
 class GroupedBsr16(_Grouped):
     """spmm_bsr16_group_analysis_f16 on a bs = 16 fp16 BSR matrix (once), then
     .mm(...) = spmm_bsrmm_grouped_f16: the grouped stream, groups of
-    group_rows adjacent block rows sharing their B-row copies."""
+    group_rows adjacent block rows sharing their B-row copies (0: the library
+    picks 2, 4 or 8 per matrix; .W holds the choice)."""
 
     BS, VT = 16, torch.float16
     ANALYSIS, PRODUCT = "spmm_bsr16_group_analysis_f16", "spmm_bsrmm_grouped_f16"
     RELEASE = "spmm_bsr16_group_release"
 
-    def __init__(self, rowptr, colind, val, *, mb: int, group_rows: int = 4,
+    def __init__(self, rowptr, colind, val, *, mb: int, group_rows: int = 0,
                  direction: int = DIRECTION_ROW, handle: Handle | None = None):
         super().__init__(rowptr, colind, val, mb=mb, group_rows=group_rows, direction=direction,
                          handle=handle)

@@ -1541,3 +1541,66 @@ def test_bsr_reblock32_matches_csr2bsr32_full_size(device):
     torch.cuda.synchronize()
     assert torch.equal(r32[0], b32[0]) and torch.equal(r32[1], b32[1])
     assert torch.equal(r32[2], b32[2]), "re-blocked values differ from csr2bsr at bs 32"
+
+
+def _grouped_items(rp, ci, v, bs, W, mb):
+    """Items of the group analysis restated on the host (test_group_analysis_layout's
+    grouping): per group of W block rows, the union of their blocks' nonzero
+    columns cut into items of 16 (bs 16)."""
+    E = 16 if bs == 16 else 8
+    vb = v.astype(np.float32).reshape(-1, bs, bs)
+    nz = [np.nonzero((np.abs(vb[k]) > 0).any(axis=0))[0] for k in range(vb.shape[0])]
+    items = 0
+    for g in range(-(-mb // W)):
+        ent = set()
+        for br in range(g * W, min(mb, g * W + W)):
+            for k in range(rp[br], rp[br + 1]):
+                ent.update(int(ci[k]) * bs + int(c) for c in nz[k])
+        items += -(-len(ent) // E)
+    return items
+
+
+def _auto_group_rows(oracle, device, shared):
+    """groupRows = 0 at bs 16: the library analyses W = 2, 4 and 8 and keeps the
+    least items(W) * (2.74 + W) (group.cpp's model). The choice must be that
+    minimum over the host restatement of the items, the buffer must equal an
+    explicit analysis with that W byte for byte (its header word 0 holds W),
+    and the product must match the oracle. Returns the choice."""
+    ops = _ops()
+    rng = np.random.default_rng(5 + shared)
+    mb, kb = 48, 96
+    rows = []
+    for br in range(mb):
+        if shared:  # a band of block columns around the diagonal: neighbours share most
+            c = np.arange(max(0, br - 3), min(kb, br + 4))
+        else:       # every block row its own two columns
+            c = np.array([(2 * br) % kb, (2 * br + 1) % kb])
+        rows.append(np.sort(c))
+    rp = np.concatenate([[0], np.cumsum([len(c) for c in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    v = rng.uniform(-1, 1, rp[-1] * 256).astype(np.float16)
+    cost = {W: _grouped_items(rp, ci, v, 16, W, mb) * (2.74 + W) for W in (2, 4, 8)}
+    want = min(cost, key=lambda W: (cost[W], W))
+    drp, dci, dv = _dev(rp, ci, v)
+    auto = ops.GroupedBsr16(drp, dci, dv, mb=mb, group_rows=0)
+    assert auto.W == want, (auto.W, cost)
+    manual = ops.GroupedBsr16(drp, dci, dv, mb=mb, group_rows=want)
+    assert manual.W == want and torch.equal(auto.buffer, manual.buffer)
+    n = 256
+    Bh = rng.uniform(-1, 1, (kb * 16, n)).astype(np.float16)
+    C = torch.zeros((mb * 16, n), device=device)
+    auto.mm(torch.from_numpy(Bh).to(device), kb=kb, n=n, ldb=n, C=C, ldc=n)
+    torch.cuda.synchronize()
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, 16, rp, ci, v, Bh, n, 0, half=True)
+    assert_normwise(C.cpu().numpy(), ref, absd, TOL_F16_ACC, f"auto W={auto.W}")
+    auto.close()
+    manual.close()
+    return want
+
+
+def test_group_rows_chosen_by_the_library(oracle, device):
+    """Neighbouring block rows sharing most columns (a banded pattern) and
+    sharing none pick different W through _auto_group_rows: more rows per group
+    where they share."""
+    ws = [_auto_group_rows(oracle, device, s) for s in (True, False)]
+    assert ws == [4, 2], ws
