@@ -876,6 +876,23 @@ def run_csr(args, W, world, rank, dev, dist):
     return rec, (rp, ci, K)
 
 
+def _side_traffic(workload: str, kernel: str, K: int, dt: str, nnzb: int, comp: int,
+                  kms: float) -> dict:
+    """Counter bytes of a side entry (grouped / analysed) beside a drop-in line: the
+    record of the standalone workload that runs the same entry on the same matrix
+    (tools/pmc_bytes.sh), under the same key rule as the line's own traffic."""
+    tr = bsr_traffic({"workload": workload, "kernel": kernel, "K": K, "dtype": dt, "nnzb": nnzb,
+                      "layout_BC": "row", "variant": bsr_variant(),
+                      "kernel_src": kernel_source_tag()})
+    out = {"compulsory_bytes": comp, "traffic": tr, "traffic_from": workload}
+    if tr:
+        t = kms / 1e3
+        out.update(traffic_GBps=round(tr / t / 1e9, 1),
+                   traffic_frac=round(tr / t / 1e9 / HBM_PEAK_GBPS, 4),
+                   traffic_over_compulsory=round(tr / comp, 3))
+    return out
+
+
 def _timed_analysis(make):
     """A group analysis timed twice (host wall clock to the end of its work on the
     stream): the first call on the handle (it loads the analysis kernels and grows
@@ -1156,6 +1173,8 @@ def run_bsr(args, W, world, rank, dev, dist):
             "analysis_ms_first_call": round(a_ms, 3), "analysis_ms_repeat": round(a_rep, 3),
             "items": int(ni),
             "mfma_executed_TFLOPs": round(ni * g4.W * 2.0 * 256 * K / (k_g / 1e3) / 1e12, 2),
+            **_side_traffic(args.workload + "_grp", "bsr16_f16_grp_kernel", K, dt, nnzb,
+                            ntiles * g4.bytes + s * b_rows * K + 4 * mb * bs * K, k_g),
             **_epoch_loop(a_rep, e_g / args.steps * 1e3, elapsed / args.steps * 1e3)}
         g4.close()
         del g4
@@ -1175,6 +1194,8 @@ def run_bsr(args, W, world, rank, dev, dist):
             "analysis_ms_first_call": round(a_ms, 3), "analysis_ms_repeat": round(a_rep, 3),
             "mfma_executed_TFLOPs": round(mfma_flops / (k_g / 1e3) / 1e12, 2),
             "mfma_frac": round(mfma_flops / (k_g / 1e3) / 1e12 / peak, 4),
+            **_side_traffic(args.workload + "_grp", "bsr32_f32_grp_kernel", K, dt, nnzb,
+                            ntiles * g2.bytes + s * b_rows * K + 4 * mb * bs * K, k_g),
             **_epoch_loop(a_rep, e_g / args.steps * 1e3, elapsed / args.steps * 1e3)}
         g2.close()
         del g2
@@ -1211,7 +1232,8 @@ def run_bsr(args, W, world, rank, dev, dist):
             "frac": round(comp_an / t_an / 1e9 / HBM_PEAK_GBPS, 4),
             "bytes_model": "compulsory, analysed: masks + the nonzero columns' values",
             "mfma_executed_TFLOPs": round(mfma_flops / t_an / 1e12, 2),
-            "mfma_frac": round(mfma_flops / t_an / 1e12 / peak, 4)}
+            "mfma_frac": round(mfma_flops / t_an / 1e12 / peak, 4),
+            **_side_traffic(args.workload + "_an", kname, K, dt, nnzb, comp_an, k_an)}
     return rec, None
 
 
