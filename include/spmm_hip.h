@@ -321,11 +321,10 @@ spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction
  * INVALID_VALUE for a buffer this handle has no analysis of, another mb, or a
  * kb the analysed block columns do not fit (a column >= kb);
  * NOT_SUPPORTED when n % 8 != 0, a row-major ldb % 8 != 0 or B is not 16-B
- * aligned (spmm_bsrmm_ex_f16 serves those shapes). Non-finite B is GROUPED:
- * an inf / NaN in B row J*16 + c reaches every row of a group (all its block
- * rows) when any of its block rows holds a value other than +-0 in that
- * column; with finite B the product equals spmm_bsrmm_ex_f16's within the
- * fp32 bar. */
+ * aligned (spmm_bsrmm_ex_f16 serves those shapes). Non-finite B follows the
+ * column-granular contract of the drop-in stream (spmm_set_bsr_options above):
+ * each wave clears the B values of the entries its block row does not hold;
+ * with finite B the product equals spmm_bsrmm_ex_f16's within the fp32 bar. */
 spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n,
                                      const void* buffer, float alpha, const uint16_t* B, int ldb,
                                      spmm_order_t orderB, float beta, float* C, int ldc,

@@ -2615,18 +2615,21 @@ __global__ __launch_bounds__(256) void bsr_generic_kernel(
 // Release form: W = 4, P = 3, three waves per SIMD, one item per barrier:
 // products stand-in K = 512 2.44-2.62 ms against 3.77 for the column stream
 // (profiles/r04n/, profiles/r04o/).
-// Non-finite B: a B row of the item meets the W block rows' A fragments, zeros
-// included, so an inf / NaN in it reaches every row of the group whenever one
-// of its block rows holds a value in that column (the grouped contract,
-// include/spmm_hip.h).
+// Non-finite B: column-granular, as the drop-in stream (round 5). The analysis
+// records per (item, wave) which entries the wave's block row holds with a value
+// other than +-0; the wave zeroes the other entries' values in its B fragments
+// before the MFMAs, so an inf / NaN in a B row reaches only the block rows that
+// hold a value in its column (round 4's GROUPED contract let it reach every row
+// of the group through the fragments' zeros).
 // ---------------------------------------------------------------------------
 
 template <int W, int P, bool CROW, int OCC = 0, int IPB = 1, bool AL = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1)))
 void bsr16_f16_grp_kernel(
     int mb, int n, const int* __restrict__ item_ptr, const int* __restrict__ rows,
-    const unsigned* __restrict__ afrag, const _Float16* __restrict__ B, int ldb, float alpha,
-    float beta, float* __restrict__ C, int ldc, int xm, int ngroups, int ntt) {
+    const unsigned* __restrict__ wmask, const unsigned* __restrict__ afrag,
+    const _Float16* __restrict__ B, int ldb, float alpha, float beta, float* __restrict__ C,
+    int ldc, int xm, int ngroups, int ntt) {
   static_assert(W == 2 || W == 4 || W == 8, "waves per group");
   static_assert(P >= 2 && P <= 6, "stages");
   constexpr int COLS = 256, kRowB = 512, kCh = 32, kT = 16, kStage = 16 * kRowB;
@@ -2685,6 +2688,9 @@ void bsr16_f16_grp_kernel(
   int nis = 0;  // vector-memory operations issued by this wave
   // row indices of the next IPB items to issue (scalars; rows 2 cc and 2 cc + 1 of copy cc)
   int ra[IPB][kCpw], rb[IPB][kCpw];
+  // this wave's held-entry masks (bit e: its block row holds entry e with a value other
+  // than +-0): of the next IPB items to issue, and of the items in each ring slot
+  unsigned wmn[IPB], wms[P];
   typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
   u32x2a fan[P];  // A fragments in flight (asm-only registers)
   int stamp[P];
@@ -2692,11 +2698,14 @@ void bsr16_f16_grp_kernel(
   for (int s = 0; s < P; ++s) {
     fan[s] = u32x2a{0u, 0u};
     stamp[s] = -64;
+    wms[s] = 0u;
   }
 #pragma unroll
-  for (int i = 0; i < IPB; ++i)
+  for (int i = 0; i < IPB; ++i) {
+    wmn[i] = 0u;
 #pragma unroll
     for (int j = 0; j < kCpw; ++j) ra[i][j] = rb[i][j] = -1;
+  }
   const int ilast = max(i1 - 1, i0);
   // row indices of items it .. it + IPB - 1 (clamped) by scalar loads (lgkmcnt): lane L of
   // copy j needs rows[it][2 (w kCpw + j) + L / 32]. Vector loads retire in issue order
@@ -2712,11 +2721,13 @@ void bsr16_f16_grp_kernel(
         ra[i][j] = s2[2 * j];
         rb[i][j] = s2[2 * j + 1];
       }
+      wmn[i] = wmask[(size_t)min(it + i, ilast) * W + w];
     }
   };
   // item `it` (rows ra / rb [i]) into stage slot `s`: its copies and A fragment issued
   auto issue = [&](int it, int s, int i) {
     char* const stage = smem + s * kSlot;
+    wms[s] = wmn[i];
 #pragma unroll
     for (int j = 0; j < kCpw; ++j) {
       const int rw = (lane >> 5) ? rb[i][j] : ra[i][j];
@@ -2775,6 +2786,22 @@ void bsr16_f16_grp_kernel(
         : "v"(tra[8]), "v"(tra[9]), "v"(tra[10]), "v"(tra[11]), "v"(tra[12]), "v"(tra[13]),
           "v"(tra[14]), "v"(tra[15]), "n"(s * kSlot)
         : "memory");
+    // Column-granular non-finite contract: the entries this wave's block row does not
+    // hold (its fragment is zero there) have their B values zeroed in the fragment, so
+    // an inf / NaN in those B rows meets no 0 * inf. Lane (g, c) holds k = 4 g .. 4 g + 3
+    // of the B fragment, as of the A fragment: nibble g of the wave's mask.
+    const unsigned wm = wms[s];
+    if (wm != 0xffffu) {  // wave-uniform; all 16 held: nothing to clear
+      const unsigned nib = (wm >> (4 * g)) & 0xfu;
+      const unsigned lo = ((nib & 1u) ? 0xffffu : 0u) | ((nib & 2u) ? 0xffff0000u : 0u);
+      const unsigned hi = ((nib & 4u) ? 0xffffu : 0u) | ((nib & 8u) ? 0xffff0000u : 0u);
+#pragma unroll
+      for (int t = 0; t < kT; ++t) {
+        u32x2a v = __builtin_bit_cast(u32x2a, fb[t]);
+        v = u32x2a{v[0] & lo, v[1] & hi};
+        fb[t] = __builtin_bit_cast(f16x4, v);
+      }
+    }
 #pragma unroll
     for (int t = 0; t < kT; ++t)
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(fa, fb[t], acc[t], 0, 0, 0);
@@ -3686,7 +3713,7 @@ __global__ __launch_bounds__(256) void grp_build_kernel(int mb, int nnzb, int ng
                                                         unsigned* __restrict__ wmask) {
   constexpr unsigned kAll = BS == 32 ? 0xffffffffu : 0xffffu;
   constexpr int E = BS == 16 ? 16 : 8;
-  constexpr bool HELD = BS == 32;
+  constexpr bool HELD = true;  // per-(item, wave) held-entry masks at both block sizes
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= ngroups) return;
   int cur[W], end[W];
@@ -3934,8 +3961,9 @@ spmm_status_t launch_bsrmm_grouped_f32(spmm_context* ctx, int W, int mb, int n, 
 
 spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, int ngroups,
                                        const int* item_ptr, const int* rows,
-                                       const unsigned* afrag, const uint16_t* B16, int ldb,
-                                       float alpha, float beta, float* C, int ldc, bool crow) {
+                                       const unsigned* wmask, const unsigned* afrag,
+                                       const uint16_t* B16, int ldb, float alpha, float beta,
+                                       float* C, int ldc, bool crow) {
   if (mb == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   const _Float16* B = reinterpret_cast<const _Float16*>(B16);
   const int slot = timing_begin(ctx);
@@ -3985,12 +4013,12 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
   do {                                                                                           \
     if (crow)                                                                                    \
       hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, true, O_, IPB_, AL_>), grid,               \
-                         dim3(64 * W_), 0, ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb,     \
-                         alpha, beta, C, ldc, xm, ngroups, ntt);                                 \
+                         dim3(64 * W_), 0, ctx->stream, mb, n, item_ptr, rows, wmask, afrag, B,   \
+                         ldb, alpha, beta, C, ldc, xm, ngroups, ntt);                            \
     else                                                                                         \
       hipLaunchKernelGGL((bsr16_f16_grp_kernel<W_, P_, false, O_, IPB_, AL_>), grid,              \
-                         dim3(64 * W_), 0, ctx->stream, mb, n, item_ptr, rows, afrag, B, ldb,     \
-                         alpha, beta, C, ldc, xm, ngroups, ntt);                                 \
+                         dim3(64 * W_), 0, ctx->stream, mb, n, item_ptr, rows, wmask, afrag, B,   \
+                         ldb, alpha, beta, C, ldc, xm, ngroups, ntt);                            \
   } while (0)
 #define GRP_LAUNCH1(W_, P_, O_, IPB_) GRP_LAUNCH2(W_, P_, O_, IPB_, false)
 #ifdef SPMM_TUNING

@@ -170,8 +170,9 @@ spmm_status_t launch_bsr16_grp_fill(spmm_context* ctx, long long nitems, int W, 
                                     unsigned* afrag);
 spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, int ngroups,
                                        const int* item_ptr, const int* rows,
-                                       const unsigned* afrag, const uint16_t* B16, int ldb,
-                                       float alpha, float beta, float* C, int ldc, bool crow);
+                                       const unsigned* wmask, const unsigned* afrag,
+                                       const uint16_t* B16, int ldb, float alpha, float beta,
+                                       float* C, int ldc, bool crow);
 // the group analyses' device merge (grp_build_kernel: PASS 1 checks the row pointer
 // and counts, PASS 2 writes)
 spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int mb, int nnzb,

@@ -33,9 +33,11 @@
 //                            library's choice when groupRows was 0); the rest zero
 //   item_ptr[ngroups + 1]    int32, the items of group g are [item_ptr[g], item_ptr[g+1])
 //   rows[nitems][E]          int32, B row of each entry (-1: padding)
+//   wmask[nitems][W]              uint32, bit e: entry e is a nonzero column of wave w's
+//                                 block row (bs 32: the MFMAs it runs; bs 16: the B values
+//                                 its fragments keep)
 //   bs 16: afrag[nitems][W][128]  uint32, lane l of wave w: A[l & 15][4 (l >> 4) .. + 3] fp16 x 4
-//   bs 32: wmask[nitems][W]       uint32, bit e: entry e is a column of wave w's block row
-//          afrag[nitems][W][32][8] fp32, A[row][entry] of wave w's block row
+//   bs 32: afrag[nitems][W][32][8] fp32, A[row][entry] of wave w's block row
 // The handle records the layout by buffer address (spmm_context::group_plans).
 #include <hip/hip_runtime.h>
 
@@ -174,8 +176,8 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
     if (host[pick].total > INT_MAX) return SPMM_STATUS_NOT_SUPPORTED;  // int32 item pointers
     const long long nitems = host[pick].total;
     pend.rows_off = align256(256 + (size_t)(ngroups + 1) * 4);
-    pend.wmask_off = align256(pend.rows_off + (size_t)nitems * E * 4);  // bs 32 only
-    pend.afrag_off = BS == 16 ? pend.wmask_off : align256(pend.wmask_off + (size_t)nitems * W * 4);
+    pend.wmask_off = align256(pend.rows_off + (size_t)nitems * E * 4);
+    pend.afrag_off = align256(pend.wmask_off + (size_t)nitems * W * 4);
     pend.need = pend.afrag_off + (size_t)nitems * W * (BS == 16 ? 512 : 1024);
     pend.nitems = nitems;
     pend.max_col = host[pick].max_col;
@@ -300,6 +302,7 @@ spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n
   return launch_bsrmm_grouped_f16(
       handle, plan.W, mb, n, plan.ngroups, reinterpret_cast<const int*>(buf + 256),
       reinterpret_cast<const int*>(buf + plan.rows_off),
+      reinterpret_cast<const unsigned*>(buf + plan.wmask_off),
       reinterpret_cast<const unsigned*>(buf + plan.afrag_off), Bx, ldbx, alpha, beta, C, ldc,
       orderC == SPMM_ORDER_ROW);
 }

@@ -1055,14 +1055,11 @@ def test_bsrmm_grouped_f16(oracle, device, W, n, ob, oc, alpha, beta):
     grp.close()
 
 
-def grouped_nonfinite_block_rows(rp, ci, v, bs, W, mb, bad_rows):
-    """The GROUPED non-finite contract of spmm_bsrmm_grouped_f16
-    (include/spmm_hip.h), predicted from the pattern on the host: a non-finite
-    B row J * bs + c reaches every row of every block row of group G (block
-    rows W G .. W G + W - 1) when any block row of G stores block column J
-    with a value other than +-0 in its column c (that makes (J, c) an entry of
-    the group's union, and each block row's fragment meets it, zeros
-    included); no other row. v: [nnzb, bs, bs] row-major block values.
+def colgran_nonfinite_block_rows(rp, ci, v, bs, mb, bad_rows):
+    """The column-granular non-finite contract (include/spmm_hip.h), predicted
+    from the pattern on the host: a non-finite B row J * bs + c reaches every
+    row of block row I iff I stores block column J with a value other than +-0
+    in its column c; no other row. v: [nnzb, bs, bs] row-major block values.
     Returns a bool per block row."""
     held = np.zeros(mb, bool)
     blk_row = np.repeat(np.arange(mb), np.diff(rp))
@@ -1071,29 +1068,26 @@ def grouped_nonfinite_block_rows(rp, ci, v, bs, W, mb, bad_rows):
         k = np.nonzero(ci == J)[0]
         k = k[(v[k, :, c] != 0).any(axis=1)]
         held[blk_row[k]] = True
-    grp = held.reshape(-1, W).any(axis=1) if mb % W == 0 else \
-        np.pad(held, (0, -mb % W)).reshape(-1, W).any(axis=1)
-    return np.repeat(grp, W)[:mb]
+    return held
 
 
 @pytest.mark.parametrize("W", [2, 4, 8])
 @pytest.mark.parametrize("bad", ["nan", "inf"])
 def test_bsrmm_grouped_f16_nonfinite_contract(device, W, bad):
-    """An inf / NaN in B through the grouped stream: exactly the block rows
-    grouped_nonfinite_block_rows predicts are non-finite in every element
-    (the whole group, the rows whose own blocks hold no value in that column
-    included), every other element finite and within the bar of the same
-    product on B with those rows zeroed. The column-sparse generator makes
-    explicit all-zero blocks and single-column blocks, so the groups that
-    store the block column only with a zero column stay finite."""
+    """An inf / NaN in B through the grouped stream: the contract is the drop-in
+    stream's column-granular one (round 5; round 4's GROUPED contract spread it
+    to the whole group). Exactly the block rows colgran_nonfinite_block_rows
+    predicts are non-finite in every element; another block row of the same
+    group stays finite and equals the run on B with those rows zeroed, bit for
+    bit; a column whose blocks hold it only as zeros and a column no block
+    stores reach no row. The case must have groups that contain both a hit and
+    a spared block row (where the two contracts differ)."""
     ops = _ops()
     rng = np.random.default_rng(7 * W + (bad == "inf"))
     mb, kb, n = 37, 60, 256
     rp, ci, v = _column_sparse_bsr(rng, mb, kb, 16, 0.3)
     v16 = v.astype(np.float16)
     B = rng.uniform(-1, 1, (kb * 16, n)).astype(np.float16)
-    # bad rows: a column some block holds a value in, one whose blocks hold it only as
-    # zeros (if the pattern has one), and one no block stores
     vb = v16.astype(np.float32).reshape(-1, 16, 16)
     col_nz = np.zeros((kb, 16), bool)
     col_st = np.zeros(kb, bool)
@@ -1108,8 +1102,10 @@ def test_bsrmm_grouped_f16_nonfinite_contract(device, W, bad):
         bad_rows.append(int(zero_only[0][0]) * 16 + int(zero_only[0][1]))
     if len(unstored):
         bad_rows.append(int(unstored[0]) * 16 + 5)
-    want = grouped_nonfinite_block_rows(rp, ci, vb, 16, W, mb, bad_rows)
-    assert 0 < want.sum() < mb, "the case must hit some groups and spare others"
+    want = colgran_nonfinite_block_rows(rp, ci, vb, 16, mb, bad_rows)
+    grp_any = np.pad(want, (0, -mb % W)).reshape(-1, W).any(axis=1)
+    assert 0 < want.sum() < np.repeat(grp_any, W)[:mb].sum(), (
+        "the case must have a group with both a hit and a spared block row")
     B0 = B.copy()
     B0[bad_rows] = 0
     B[bad_rows] = np.float16(np.nan if bad == "nan" else np.inf)

@@ -420,13 +420,13 @@ def test_grouped_bs16_f16_full_size(oracle, device, W, reorder):
 
 
 def test_grouped_bs16_nonfinite_contract_full_size(device):
-    """The grouped stream's non-finite contract (GROUPED, include/spmm_hip.h)
-    at full size: the products stand-in at K = 512, W = 4, three B rows set to
-    NaN (a hub column, a mid-popularity one and n - 1). The NaN block rows
-    must be exactly the groups the host predicts from the CSR pattern (any
-    block row of the group holds a value in that column); the column-granular
-    prediction of the drop-in stream is a strict subset of it. Every other
-    element equals the run on B with those rows zeroed, bit for bit."""
+    """The grouped stream's non-finite contract at full size: the products
+    stand-in at K = 512, W = 4, three B rows set to NaN (a hub column, a
+    mid-popularity one and n - 1). Since round 5 it is the drop-in stream's
+    column-granular contract: the NaN block rows must be exactly those holding
+    a value in a NaN row's column (predicted from the CSR pattern), a strict
+    subset of their groups (round 4's GROUPED contract). Every other element
+    equals the run on B with those rows zeroed, bit for bit."""
     ops = _ops()
     rp, ci, n = _graph("products", False)
     K, bs, W = 512, 16, 4
@@ -436,13 +436,12 @@ def test_grouped_bs16_nonfinite_contract_full_size(device):
     order = np.argsort(-deg, kind="stable")
     nan_rows = np.array(sorted({int(order[0]), int(order[n // 50]), n - 1}), dtype=np.int64)
     row_of = np.repeat(np.arange(n), np.diff(rp))
-    hit_col = np.zeros(mb, bool)  # column-granular (the drop-in stream)
+    hit_col = np.zeros(mb, bool)  # column-granular
     for r in nan_rows:  # a value that rounds to fp16 zero leaves its column empty
         hit_col[np.unique(row_of[(ci == r) & (v != 0)] // bs)] = True
     ngrp = -(-mb // W)
-    hit_grp = np.pad(hit_col, (0, ngrp * W - mb)).reshape(ngrp, W).any(axis=1)
-    want_h = np.repeat(hit_grp, W)[:mb]
-    assert want_h.sum() > hit_col.sum() > 0, "the case must separate the two contracts"
+    hit_grp = np.repeat(np.pad(hit_col, (0, ngrp * W - mb)).reshape(ngrp, W).any(axis=1), W)[:mb]
+    assert hit_grp.sum() > hit_col.sum() > 0, "the case must separate the two contracts"
     drp, dci, dv = _dev(rp, ci, v)
     brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
     del drp, dci, dv
@@ -462,7 +461,7 @@ def test_grouped_bs16_nonfinite_contract_full_size(device):
     torch.cuda.synchronize()
     grp.close()
     nanrow = torch.isnan(C).view(mb, bs * K)
-    want = torch.from_numpy(want_h).to(device)
+    want = torch.from_numpy(hit_col).to(device)
     assert torch.equal(nanrow.any(dim=1), want) and torch.equal(nanrow.all(dim=1), want), (
         f"NaN block rows {int(nanrow.any(dim=1).sum())} (whole: {int(nanrow.all(dim=1).sum())}), "
         f"expected {int(want.sum())}")
