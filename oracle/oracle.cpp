@@ -117,18 +117,26 @@ void oracle_csrmm_d(int m, int n, const int* rowptr, const int* colind, const do
 // the norm-wise tolerance |C - C64| <= tol * absdot.
 void oracle_csrmm_f64(int m, int n, const int* rowptr, const int* colind, const float* val,
                       int base, const float* B, int ldb, int orderB, double* C, double* absdot) {
+  // Nonzeros outer, output columns inner: each output still sums its terms in nonzero
+  // order (the same double additions as a column-outer loop, bit for bit), but a row-major
+  // B row is read contiguously, so a whole products-sized product checks in seconds.
 #pragma omp parallel for schedule(dynamic, 64)
   for (int r = 0; r < m; ++r) {
     const int j0 = rowptr[r] - base, j1 = rowptr[r + 1] - base;
+    double* acc = C + (size_t)r * n;
+    double* aa = absdot ? absdot + (size_t)r * n : nullptr;
     for (int c = 0; c < n; ++c) {
-      double acc = 0.0, aa = 0.0;
-      for (int j = j0; j < j1; ++j) {
-        const double b = B[at(colind[j] - base, c, ldb, orderB)];
-        acc += (double)val[j] * b;
-        aa += std::fabs((double)val[j] * b);
+      acc[c] = 0.0;
+      if (aa) aa[c] = 0.0;
+    }
+    for (int j = j0; j < j1; ++j) {
+      const double v = (double)val[j];
+      const int row = colind[j] - base;
+      for (int c = 0; c < n; ++c) {
+        const double t = v * (double)B[at(row, c, ldb, orderB)];
+        acc[c] += t;
+        if (aa) aa[c] += std::fabs(t);
       }
-      C[(size_t)r * n + c] = acc;
-      if (absdot) absdot[(size_t)r * n + c] = aa;
     }
   }
 }

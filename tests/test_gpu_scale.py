@@ -1,6 +1,9 @@
 """Path B at BASELINE's full sizes.
 
-Two checks per result:
+Checks per result:
+* every row against the f64 oracle of the whole product (_check_oracle_all,
+  round 5: the oracle's nonzero-outer loop reads B rows contiguously, so the
+  10^8-nonzero products check in seconds on the box's host cores);
 * sampled rows against the f64 oracle (oracle_csrmm_f64 on the same CSR
   values the BSR / hybrid arrays were built from: the product is the same
   matrix's), as the reference's own differential bar does
@@ -86,6 +89,17 @@ def _check_oracle_rows(oracle, got, rp, ci, v, B, rows, tol, what):
     assert_normwise(g, ref, absd, tol, f"{what}: {rows.size} sampled rows vs the f64 oracle")
 
 
+def _check_oracle_all(oracle, got, rp, ci, v, B, tol, what):
+    """Every row of got against the f64 oracle of the whole CSR product (B read
+    row-major, contiguous per nonzero: seconds on the box's host cores)."""
+    n = rp.size - 1
+    K = B.shape[1]
+    Bh = B.float().cpu().numpy()
+    ref, absd = oracle_csrmm_f64(oracle, n, K, rp, ci, v, Bh, K, 0)
+    del Bh
+    assert_normwise(got[:n].cpu().numpy(), ref, absd, tol, f"{what}: every row vs the f64 oracle")
+
+
 def _within(got, ref, absd, tol, what):
     err = (got - ref).abs()
     bound = tol * absd + 1e-30
@@ -117,6 +131,7 @@ def test_reddit_scale_bsr32_and_hybrid_vs_csr(oracle, device):
     brp_h = brp.cpu().numpy()
     rows = _sample_rows(brp_h, bs, n, 11, _segmented_block_rows(brp_h))
     _check_oracle_rows(oracle, Cb, rp, ci, v, B, rows, TOL_F32, "reddit bs32 BSR")
+    _check_oracle_all(oracle, Cb, rp, ci, v, B, TOL_F32, "reddit bs32 BSR")
     _within(Cb[:n], Cc, absd, 2 * TOL_F32, "reddit bs32 BSR vs CSR")
     assert not bool(Cb[n:].any()), "padding rows of C must be zero"
     del brp, bci, bval
@@ -162,6 +177,7 @@ def test_products_scale_bsr16_f16_vs_csr(oracle, device):
     assert int(bci.numel()) > 4_000_000
     rows = _sample_rows(brp.cpu().numpy(), bs, n, 13)
     _check_oracle_rows(oracle, Cb, rp, ci, v, B16, rows, TOL_F16_ACC, "products bs16 fp16 BSR")
+    _check_oracle_all(oracle, Cb, rp, ci, v, B16, TOL_F16_ACC, "products bs16 fp16 BSR")
     _within(Cb[:n], Cc, absd, 2 * TOL_F16_ACC, "products bs16 fp16 BSR vs CSR")
 
 
@@ -286,6 +302,7 @@ def test_analysed_bs32_full_size(oracle, device, kind, reorder):
     what = f"analysed bs32 {kind}{' RCM' if reorder else ''} (nnzb {nnzb})"
     rows = _sample_rows(brp_h, bs, n, 21 + 2 * reorder + (kind == "products"), seg)
     _check_oracle_rows(oracle, Ca, rp, ci, v, B, rows, TOL_F32, what)
+    _check_oracle_all(oracle, Ca, rp, ci, v, B, TOL_F32, what)
     _within(Ca[:n], Cc, absd, 2 * TOL_F32, what + " vs CSR")
     assert not bool(Ca[n:].any()), "padding rows of C must be zero"
     assert torch.equal(Ca, Cd), what + ": differs from the drop-in column stream"
@@ -324,6 +341,7 @@ def test_analysed_bs16_f16_full_size(oracle, device, reorder):
     what = f"analysed bs16 fp16 products{' RCM' if reorder else ''} (nnzb {nnzb})"
     rows = _sample_rows(brp.cpu().numpy(), bs, n, 31 + reorder)
     _check_oracle_rows(oracle, Ca, rp, ci, v, B16, rows, TOL_F16_ACC, what)
+    _check_oracle_all(oracle, Ca, rp, ci, v, B16, TOL_F16_ACC, what)
     _within(Ca[:n], Cc, absd, 2 * TOL_F16_ACC, what + " vs CSR")
     assert torch.equal(Ca, Cd), what + ": differs from the drop-in column stream"
 
@@ -414,6 +432,7 @@ def test_grouped_bs16_f16_full_size(oracle, device, W, reorder):
     what = f"grouped W={W} bs16 fp16 products{' RCM' if reorder else ''}"
     rows = _sample_rows(brp.cpu().numpy(), bs, n, 41 + W + reorder)
     _check_oracle_rows(oracle, Cg, rp, ci, v, B16, rows, TOL_F16_ACC, what)
+    _check_oracle_all(oracle, Cg, rp, ci, v, B16, TOL_F16_ACC, what)
     _within(Cg[:n], Cc, absd, 2 * TOL_F16_ACC, what + " vs CSR")
     assert not bool(Cg[n:].any()), "padding rows of C must be zero"
     grp.close()
@@ -501,6 +520,7 @@ def test_grouped_bs32_full_size(oracle, device, kind, reorder, W):
     what = f"grouped W={W} bs32 {kind}{' RCM' if reorder else ''}"
     rows = _sample_rows(brp_h, bs, n, 61 + W + 2 * reorder + (kind == "products"), seg)
     _check_oracle_rows(oracle, Cg, rp, ci, v, B, rows, TOL_F32, what)
+    _check_oracle_all(oracle, Cg, rp, ci, v, B, TOL_F32, what)
     _within(Cg[:n], Cc, absd, 2 * TOL_F32, what + " vs CSR")
     assert not bool(Cg[n:].any()), "padding rows of C must be zero"
     # every segmented block row (seg above holds the shortest and the longest)
