@@ -209,6 +209,13 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
   if (e == hipSuccess)
     e = hipMemcpyAsync(buf + 256, pb + pend.ptr_off, (size_t)(ngroups + 1) * 4,
                        hipMemcpyDeviceToDevice, st);
+  // the alignment gaps between the sections are zeroed, so the buffer's bytes are a
+  // function of the matrix alone (an analysis compares byte for byte with another)
+  const size_t gaps[3][2] = {{256 + (size_t)(ngroups + 1) * 4, pend.rows_off},
+                             {pend.rows_off + (size_t)nitems * E * 4, pend.wmask_off},
+                             {pend.wmask_off + (size_t)nitems * W * 4, pend.afrag_off}};
+  for (const auto& g : gaps)
+    if (e == hipSuccess && g[1] > g[0]) e = hipMemsetAsync(buf + g[0], 0, g[1] - g[0], st);
   if (e != hipSuccess) return from_hip(e);
   if (nitems) {
     // the entry sources in the workspace (the masks stay in grp_pend)
