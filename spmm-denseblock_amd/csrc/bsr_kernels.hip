@@ -939,8 +939,12 @@ __global__ __launch_bounds__(256) void bsr16_analysis_kernel(int nnzb, int rowdi
 // With a CSR remainder (crp, the fused hybrid: m rows, 32 per block row) the
 // key is (32 x blocks + remainder entries) / 8: a dense block's MFMA work
 // weighs about as much as 32 remainder gathers.
+// G > 1: i is a group of G block rows (bsr_small_grp_kernel; m = the block rows), keyed by its
+// blocks >> gshift.
 __device__ __forceinline__ int block_row_key(int i, const int* __restrict__ rowptr,
-                                             const int* __restrict__ crp, int m, int sub) {
+                                             const int* __restrict__ crp, int m, int sub,
+                                             int G = 1, int gshift = 0) {
+  if (G > 1) return min((rowptr[min((i + 1) * G, m)] - rowptr[i * G]) >> gshift, 1023);
   // sub: 32-row halves of bs-64 block rows (the SUB column stream), two sub-blocks each
   const int nb = (rowptr[(i >> sub) + 1] - rowptr[i >> sub]) << sub;
   if (!crp) return min(nb, 1023);
@@ -949,12 +953,13 @@ __device__ __forceinline__ int block_row_key(int i, const int* __restrict__ rowp
 }
 __global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int* __restrict__ rowptr,
                                                                const int* __restrict__ crp, int m,
-                                                               int sub, int* __restrict__ order) {
+                                                               int sub, int* __restrict__ order,
+                                                               int G = 1, int gshift = 0) {
   __shared__ int cnt[1024];
   const int t = threadIdx.x;
   cnt[t] = 0;
   __syncthreads();
-  for (int i = t; i < mb; i += 1024) atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m, sub)], 1);
+  for (int i = t; i < mb; i += 1024) atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m, sub, G, gshift)], 1);
   __syncthreads();
   const int own = cnt[t];
   for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan
@@ -966,7 +971,7 @@ __global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int
   cnt[t] -= own;  // exclusive
   __syncthreads();
   for (int i = t; i < mb; i += 1024)
-    order[atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m, sub)], 1)] = i;
+    order[atomicAdd(&cnt[1023 - block_row_key(i, rowptr, crp, m, sub, G, gshift)], 1)] = i;
 }
 
 // ---------------------------------------------------------------------------
@@ -2454,7 +2459,8 @@ template <int BS, int VEC, bool ROWD, bool CROW>
 __global__ __launch_bounds__(256) void bsr_small_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
-    float* __restrict__ C, int ldc, int xm) {
+    float* __restrict__ C, int ldc, int xm, const int* __restrict__ dirty = nullptr,
+    int gtiles = 0) {
   static_assert(BS == 2 || BS == 4 || BS == 8, "bs 2 / 4 / 8");
   static_assert(VEC == 1 || VEC == 2, "VEC 1 / 2");
   constexpr int E = BS * BS;
@@ -2464,6 +2470,8 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
   const int wg = xcd_block_row(blockIdx.x, gridDim.x, xm);
   const int br = __builtin_amdgcn_readfirstlane(wg * 4 + (threadIdx.x >> 6));
   if (br >= mb) return;
+  // behind bsr_small_grp_kernel: only the 128-column tiles of groups it flagged
+  if (dirty && !dirty[(br / (32 / BS)) * gtiles + (int)(blockIdx.y * 64 * VEC) / 128]) return;
   const int col0 = blockIdx.y * 64 * VEC + lane * VEC;
   const bool col_ok = col0 < n;
   const int col_ld = col_ok ? col0 : 0;
@@ -2549,6 +2557,312 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
       for (int v = 0; v < VEC; ++v) {
         float* p = C + (size_t)(col0 + v) * ldc + row;
         p[0] = epi(acc[r][v], alpha, beta, p);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 2 / 4 / 8, fp32, row-major B: the grouped MFMA stream (round 5; the
+// drop-in entry's default for these block sizes). bsr_small_kernel gathers a
+// B row per (block row, nonzero column) pair: 37.8 M gathers of 512 B on the
+// reddit stand-in at bs 8, 19 GB through L2 for 0.12 GB of distinct B, and one
+// v_readlane per FMA. Here one wave owns G = 32 / bs adjacent block rows (32
+// output rows) x 128 columns and walks the UNION of their block columns in
+// ascending order: a B row J * bs + c is loaded once for the whole group and
+// multiplied by v_mfma_f32_32x32x1_2b_f32 into all 32 rows at once, the rows of
+// block rows that do not hold (J, c) taking a zero A value. On the reddit
+// stand-in that is 11.1 M B rows at bs 8 (0.29 of the pairs), 6.2 M at bs 4.
+//  * The merge, in batches of 64 candidates (Q = 64 / G per block row, lane =
+//    (block row, candidate)): the batch takes, from every block row, its
+//    candidates up to the smallest last candidate of any block row that goes on
+//    past the batch (so every block column of the batch is complete across the
+//    group and the batches come in ascending block-column order), ranks the
+//    accepted (J, row) keys in LDS (one broadcast pass over the 64 keys) and
+//    writes the batch's union steps: J and, per block row, the block holding J
+//    (-1: none). Block columns out of order or repeated inside a row are taken
+//    one batch at a time as a prefix of their row, so any input is multiplied
+//    whole (in ascending order a batch takes at least one candidate). The next
+//    batch's candidates are loaded as soon as a batch is merged.
+//  * Per union step (ring of 4 slots, like bsr_small_kernel: A two steps ahead,
+//    B one step ahead of the MFMAs): lane (h, j) loads row j % bs of the block its
+//    row j's block row holds (bs floats, zero when none); a column c is active
+//    when any of the 32 rows has a value other than +-0 in it (bs ballots); the
+//    bs B rows go out as 8-B buffer loads (lane (h, j): columns 4j + 2h, + 1, the
+//    cs2 layout), an inactive column's from a resource of zero records (no
+//    memory traffic); every active column is two MFMAs.
+//  * Numerics: a v_mfma_f32_32x32x1 accumulation is one fused multiply-add per
+//    output, and a row takes its own block row's (J, c) in ascending order, the
+//    other entries adding 0 * b: for sorted block columns each output is the
+//    oracle's sequential fp32 FMA chain. The column-granular contract: a tile
+//    whose group meets an inf / NaN B value in an active column (one ballot per
+//    step) stores nothing and is flagged; bsr_small_kernel, launched behind it
+//    on the same stream, recomputes the flagged tiles (its waves of clean tiles
+//    exit at once), since 0 * inf would reach the rows of block rows without a
+//    value in that column.
+// ---------------------------------------------------------------------------
+#ifndef SPMM_SGRP_OCC
+#define SPMM_SGRP_OCC 1
+#endif
+#ifndef SPMM_SGRP_PF
+#define SPMM_SGRP_PF 1
+#endif
+#ifndef SPMM_SGRP_LPT
+#define SPMM_SGRP_LPT 1
+#endif
+template <int BS, bool ROWD, bool CROW>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OCC))) void bsr_small_grp_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc, int xm, int* __restrict__ dirty,
+    const int* __restrict__ order) {
+  static_assert(BS == 2 || BS == 4 || BS == 8, "bs 2 / 4 / 8");
+  constexpr int G = 32 / BS;  // block rows per group: 32 output rows
+  constexpr int Q = 64 / G;   // candidates per block row and batch
+  constexpr int E = BS * BS;
+  constexpr int R = 4;        // ring slots: A of step s + 2, B of step s + 1, MFMAs of step s
+  constexpr int NQ = 128;     // union-step queue (a batch adds at most 64)
+  constexpr int kNone = 0x7fffffff;
+  constexpr unsigned long long kSeg = (1ull << Q) - 1;
+  __shared__ __attribute__((aligned(16))) unsigned skey[64];  // a batch's keys (J << 5 | row)
+  __shared__ unsigned sskey[64];                              // the same, ranked
+  __shared__ int sblk[64];                                    // their blocks, ranked
+  __shared__ int suj[NQ];                                     // queued step -> block column J
+  __shared__ __attribute__((aligned(16))) int suk[NQ * G];    // step, block row -> block (-1)
+  __shared__ __attribute__((aligned(16))) float tile[CROW ? 4 : 128 * 36];
+
+  const int lane = threadIdx.x;
+  const int j = lane & 31, h = lane >> 5;
+  const int g = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, gridDim.x, xm);
+  const int jt = blockIdx.y * 128;
+  // merge role: block row lr of the group, candidate lq
+  const int lr = lane / Q, lq = lane % Q;
+  const int lbr = g * G + lr;
+  int lp = lbr < mb ? rowptr[lbr] : 0;
+  const int le = lbr < mb ? rowptr[lbr + 1] : 0;
+  // step role: output row j is row gi of block row grow of the group
+  const int grow = j / BS, gi = j % BS;
+  const unsigned boff = 4u * (unsigned)min(jt + 4 * j + 2 * h, n - 2);
+
+  int cj = lp + lq < le ? colind[lp + lq] : kNone;  // the next batch's candidates
+  float pf0 = 0.f, pf1 = 0.f;                        // prefetches of the batch's blocks
+  int qh = 0, qt = 0;  // union steps queued / taken
+  bool done = false;
+
+  // one batch: appends its union steps at qh, returns their number (0: every row done)
+  auto merge = [&]() -> int {
+    const bool valid = lp + lq < le;
+    const bool more = lp + Q < le;  // the row goes on past this batch
+    const int lastv = lq == Q - 1 && more ? cj : kNone;
+    int cut = kNone;
+#pragma unroll
+    for (int r = 0; r < G; ++r) cut = min(cut, __builtin_amdgcn_readlane(lastv, r * Q + Q - 1));
+    const int prev = __builtin_amdgcn_update_dpp(0, cj, 0x111, 0xf, 0xf, false);  // row_shr:1
+    const bool bad = !valid || cj > cut || (lq > 0 && prev >= cj);
+    const unsigned long long badm = __builtin_amdgcn_ballot_w64(bad);
+    bool acc = ((badm >> (lr * Q)) & kSeg & ((2ull << lq) - 1)) == 0;
+    unsigned long long accm = __builtin_amdgcn_ballot_w64(acc);
+    if (accm == 0) {  // no prefix below the cut (unsorted input): the first row's head alone
+      const unsigned long long heads = __builtin_amdgcn_ballot_w64(valid && lq == 0);
+      if (heads == 0) return 0;
+      const int f = __builtin_ctzll(heads);
+      accm = 1ull << f;
+      acc = lane == f;
+    }
+    const int kblk = lp + lq;
+    lp += __builtin_popcountll((accm >> (lr * Q)) & kSeg);
+    // the batch's blocks toward L2 now, a batch before their steps load them (the loads
+    // are used by the next merge, when they have long landed)
+    asm volatile("" ::"v"(pf0), "v"(pf1));
+    if (SPMM_SGRP_PF && acc) {
+      const float* blk = val + (size_t)kblk * E;
+      pf0 = blk[0];
+      pf1 = E * 4 > 128 ? blk[32] : 0.f;
+    }
+    const unsigned key = acc ? ((unsigned)cj << 5) | (unsigned)lr : 0xffffffffu;
+    skey[lane] = key;
+    __syncthreads();
+    int rank = 0;
+#pragma unroll
+    for (int m = 0; m < 64; m += 4) {
+      const uint4 k4 = *reinterpret_cast<const uint4*>(&skey[m]);
+      rank += (k4.x < key) + (k4.y < key) + (k4.z < key) + (k4.w < key);
+    }
+    if (acc) {
+      sskey[rank] = key;
+      sblk[rank] = kblk;
+    }
+    __syncthreads();
+    const int nacc = __builtin_popcountll(accm);
+    const unsigned mkey = lane < nacc ? sskey[lane] : 0u;
+    const int mblk = lane < nacc ? sblk[lane] : 0;
+    const unsigned pkey = lane > 0 && lane < nacc ? sskey[lane - 1] : 0u;
+    const bool first = lane < nacc && (lane == 0 || (pkey >> 5) != (mkey >> 5));
+    const unsigned long long fm = __builtin_amdgcn_ballot_w64(first);
+    const int q = (qh + __builtin_popcountll(fm & (~0ull >> (63 - lane))) - 1) & (NQ - 1);
+    const int nun = __builtin_popcountll(fm);
+    if (lane < nun) {
+      int* row = &suk[((qh + lane) & (NQ - 1)) * G];
+#pragma unroll
+      for (int r = 0; r < G; r += 4) *reinterpret_cast<int4*>(row + r) = int4{-1, -1, -1, -1};
+    }
+    __syncthreads();
+    if (lane < nacc) {
+      suk[q * G + (int)(mkey & 31u)] = mblk;
+      if (first) suj[q] = (int)(mkey >> 5);
+    }
+    __syncthreads();
+    cj = lp + lq < le ? colind[lp + lq] : kNone;
+    return nun;
+  };
+
+  float ar[R][BS];    // A: row gi of the block row grow's block of the step (zero: none)
+  int kbr[R], jr[R];  // its block (-1: none), the step's block column (uniform)
+  bool vr[R];         // the step exists (uniform)
+  unsigned act[R];    // active columns (uniform)
+  f32x2 bx[R][BS];    // B rows J * bs + c, this lane's two columns
+  auto load_a = [&](int s) {
+    const bool v = qt < qh;
+    const int qi = qt & (NQ - 1);
+    const int J = v ? __builtin_amdgcn_readfirstlane(suj[qi]) : 0;
+    const int kb = v ? suk[qi * G + grow] : -1;
+    qt += v ? 1 : 0;
+    vr[s] = v;
+    jr[s] = J;
+    kbr[s] = kb;
+    const size_t kk = kb >= 0 ? (size_t)kb : 0;  // block 0 stands in (selected away)
+    const float* src = val + kk * E + (ROWD ? gi * BS : gi);
+    if constexpr (ROWD && BS == 8) {
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        ar[s][c] = x0[c];
+        ar[s][4 + c] = x1[c];
+      }
+    } else if constexpr (ROWD && BS == 4) {
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ar[s][c] = x0[c];
+    } else if constexpr (ROWD) {
+      const f32x2 x0 = *reinterpret_cast<const f32x2*>(src);
+      ar[s][0] = x0[0];
+      ar[s][1] = x0[1];
+    } else {
+#pragma unroll
+      for (int c = 0; c < BS; ++c) ar[s][c] = src[c * BS];
+    }
+  };
+  auto load_b = [&](int s) {
+    unsigned m = 0;
+#pragma unroll
+    for (int c = 0; c < BS; ++c) {
+      ar[s][c] = kbr[s] >= 0 ? ar[s][c] : 0.f;
+      if (__builtin_amdgcn_ballot_w64((__float_as_uint(ar[s][c]) & 0x7fffffffu) != 0u)) m |= 1u << c;
+    }
+    act[s] = m;
+    // one resource over the step's bs B rows; an inactive column's offset is past its end,
+    // so its load returns zeros without a memory access
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(B + (size_t)jr[s] * BS * ldb), 0, BS * ldb * 4, 0x00020000);
+#pragma unroll
+    for (int c = 0; c < BS; ++c)
+      bx[s][c] = __builtin_bit_cast(
+          f32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                     rs, boff + ((m >> c) & 1u ? (unsigned)(c * ldb) * 4u : 0x80000000u), 0, 0));
+  };
+
+  f32x32 u0, u1;  // MFMA halves u = 0, 1 (output columns 4j + 2b + u of block b)
+#pragma unroll
+  for (int e = 0; e < 32; ++e) u0[e] = u1[e] = 0.f;
+  auto consume = [&](int s) {
+    const unsigned m = act[s];
+#pragma unroll
+    for (int c = 0; c < BS; ++c) {
+      if ((m >> c) & 1u) {
+        // the MFMAs' accumulators as values of one use each: hipcc then accumulates in
+        // place (dst = srcC) instead of copying 64 registers around every branch
+        asm volatile("" : "+a"(u0), "+a"(u1));
+        u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(ar[s][c], bx[s][c][0], u0, 0, 0, 0);
+        u1 = __builtin_amdgcn_mfma_f32_32x32x1f32(ar[s][c], bx[s][c][1], u1, 0, 0, 0);
+      }
+    }
+  };
+
+  // the queue holds at least R + 2 steps before every round (or every row is done): the
+  // prologue takes 2 and a round R, so a slot is empty only once every row is done
+  auto refill = [&]() {
+    while (!done && qh - qt < R + 2) {
+      const int nun = merge();
+      if (nun == 0) done = true;
+      qh += nun;
+    }
+  };
+  refill();
+  load_a(0);
+  load_a(1);
+  load_b(0);
+  while (vr[0]) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {  // a step past the end multiplies nothing (act 0)
+      load_a((s + 2) % R);
+      load_b((s + 1) % R);
+      consume(s);
+    }
+    asm volatile("" : "+a"(u0), "+a"(u1));  // the accumulators stay in AGPRs through the merge
+    refill();
+    asm volatile("" : "+a"(u0), "+a"(u1));
+  }
+
+  // A tile that met a non-finite B value is left to bsr_small_kernel (the next launch):
+  // 0 * inf would reach the rows of block rows without a value in that column. Such a
+  // value, multiplied into all 32 rows (by a or by 0), leaves an accumulator inf or NaN,
+  // and no finite product does short of overflow (which bsr_small_kernel repeats), so
+  // the accumulators tell.
+  unsigned mx = 0;
+#pragma unroll
+  for (int e = 0; e < 32; ++e)
+    mx = max(mx, max(__float_as_uint(u0[e]) & 0x7fffffffu, __float_as_uint(u1[e]) & 0x7fffffffu));
+  const bool nonfinite = __builtin_amdgcn_ballot_w64(mx >= 0x7f800000u) != 0;
+  if (lane == 0) dirty[g * gridDim.y + blockIdx.y] = nonfinite ? 1 : 0;
+  if (nonfinite) return;
+  const size_t row0 = (size_t)g * 32;
+  if constexpr (CROW) {
+    const int col = jt + 4 * j;
+    if (col >= n) return;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (g * G + row / BS >= mb) continue;
+      f32x4* p = reinterpret_cast<f32x4*>(C + (row0 + row) * ldc + col);
+      f32x4 v = {u0[e], u1[e], u0[16 + e], u1[16 + e]};
+      if (beta == 0.f) {
+        v *= alpha;
+      } else {
+        const f32x4 c = *p;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
+      }
+      *p = v;
+    }
+  } else {
+    constexpr int kTs = 36;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+      tile[(4 * j) * kTs + row] = u0[e];
+      tile[(4 * j + 1) * kTs + row] = u1[e];
+      tile[(4 * j + 2) * kTs + row] = u0[16 + e];
+      tile[(4 * j + 3) * kTs + row] = u1[16 + e];
+    }
+    __syncthreads();
+    if (g * G + j / BS < mb) {
+      for (int it = 0; it < 64; ++it) {
+        const int jl = 2 * it + h;
+        if (jt + jl < n) {
+          float* p = C + (size_t)(jt + jl) * ldc + row0 + j;
+          *p = epi(tile[jl * kTs + j], alpha, beta, p);
+        }
       }
     }
   }
@@ -3253,6 +3567,15 @@ constexpr int kBsr16F16Cm = 4725;
 //  16.6 ms against 18.5 for the full-panel kernel).
 
 #ifdef SPMM_TUNING
+// SPMM_SMALL_GRP=0: bs 2 / 4 / 8 on bsr_small_kernel instead of the grouped MFMA
+// stream, for A/B timing
+bool small_grp_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SPMM_SMALL_GRP");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
 int variant_override() {
   static const int var = [] {
     const char* e = getenv("SPMM_BSR_VARIANT");
@@ -3269,6 +3592,7 @@ int order_override() {
   return force;
 }
 #else
+constexpr bool small_grp_enabled() { return true; }
 constexpr int variant_override() { return -1; }
 constexpr int order_override() { return 0; }
 #endif
@@ -3537,6 +3861,82 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     SPMM_BSR_DISPATCH(bsr16_f32_mfma_kernel, SPMM_COMMA kBsr16Default, grid, dim3(64 * waves),
                       ctx->stream, rowd, brow, crow, mb, n, rowptr, colind, val, B, ldb, alpha,
                       beta, C, ldc);
+  } else if ((bs == 2 || bs == 4 || bs == 8) && brow && !dense_sem && nnzb > 0 && n >= 4 &&
+             n % 4 == 0 && ldb % 2 == 0 && aligned(B, 8) && aligned(val, 16) &&
+             (!crow || (ldc % 4 == 0 && aligned(C, 16))) && kb < (1 << 26) &&
+             (size_t)ldb * bs * 4 < (1u << 31) &&
+             small_grp_enabled()) {
+    // the grouped MFMA stream: 32 / bs block rows per wave share each B row of their union
+    const int ngroups = (mb + 32 / bs - 1) / (32 / bs);
+    const dim3 grid(ngroups, (n + 127) / 128);
+    if (spmm_status_t st = ensure_scratch(ctx, (size_t)ngroups * grid.y * sizeof(int))) {
+      timing_end(ctx, slot);
+      return st;
+    }
+    int* dirty = static_cast<int*>(ctx->scratch);
+    // a shallow grid (a few waves per resident slot): groups longest first, else the
+    // XCD-chunked order
+    const int* ord = nullptr;
+    {
+      const long slots = 12L * ctx->num_cus;
+      if (SPMM_SGRP_LPT && (long)ngroups * grid.y <= kLptRounds * slots) {
+        if (spmm_status_t st = spmm::ensure_order_buffer(ctx, ngroups)) {
+          timing_end(ctx, slot);
+          return st;
+        }
+        const double mean = (double)nnzb / ngroups;
+        int gshift = 0;
+        while ((4.0 * mean) / (1 << gshift) > 1023.0) ++gshift;
+        hipLaunchKernelGGL(block_row_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, ngroups,
+                           rowptr, nullptr, mb, 0, ctx->order, 32 / bs, gshift);
+        ord = ctx->order;
+      }
+    }
+#ifdef SPMM_TUNING
+    static const int xm = [] {
+      const char* e = getenv("SPMM_SMALL_GRP_XM");
+      return e ? atoi(e) : 8;
+    }();
+#else
+    constexpr int xm = 8;
+#endif
+#define SGRP_ONE(BS_, RD_, CR_)                                                                  \
+  hipLaunchKernelGGL((bsr_small_grp_kernel<BS_, RD_, CR_>), grid, dim3(64), 0, ctx->stream, mb, \
+                     n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm, dirty, ord)
+#define SGRP_LAUNCH(BS_)                                                                         \
+  do {                                                                                           \
+    if (rowd && crow) SGRP_ONE(BS_, true, true);                                                 \
+    else if (rowd) SGRP_ONE(BS_, true, false);                                                   \
+    else if (crow) SGRP_ONE(BS_, false, true);                                                   \
+    else SGRP_ONE(BS_, false, false);                                                            \
+  } while (0)
+    if (bs == 8) SGRP_LAUNCH(8);
+    else if (bs == 4) SGRP_LAUNCH(4);
+    else SGRP_LAUNCH(2);
+#undef SGRP_LAUNCH
+#undef SGRP_ONE
+    // the tiles it flagged (a non-finite B value met): bsr_small_kernel recomputes them
+    const bool v2 = n > 64;  // n % 4 == 0, ldb % 2 == 0 and B 8-B aligned above
+    const dim3 fgrid((mb + 3) / 4, (n + (v2 ? 127 : 63)) / (v2 ? 128 : 64));
+#define SFIX_ONE(BS_, V_, RD_, CR_)                                                              \
+  hipLaunchKernelGGL((bsr_small_kernel<BS_, V_, RD_, CR_>), fgrid, dim3(256), 0, ctx->stream, mb, \
+                     n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, 8, dirty, (int)grid.y)
+#define SFIX_LAUNCH(BS_, V_)                                                                     \
+  do {                                                                                           \
+    if (rowd && crow) SFIX_ONE(BS_, V_, true, true);                                             \
+    else if (rowd) SFIX_ONE(BS_, V_, true, false);                                               \
+    else if (crow) SFIX_ONE(BS_, V_, false, true);                                               \
+    else SFIX_ONE(BS_, V_, false, false);                                                        \
+  } while (0)
+    if (bs == 8) {
+      if (v2) SFIX_LAUNCH(8, 2); else SFIX_LAUNCH(8, 1);
+    } else if (bs == 4) {
+      if (v2) SFIX_LAUNCH(4, 2); else SFIX_LAUNCH(4, 1);
+    } else {
+      if (v2) SFIX_LAUNCH(2, 2); else SFIX_LAUNCH(2, 1);
+    }
+#undef SFIX_LAUNCH
+#undef SFIX_ONE
   } else if ((bs == 2 || bs == 4 || bs == 8) && brow && !dense_sem) {
     // the lane-group VALU kernel: 2 floats per lane when B allows 8-B gathers
     const bool v2 = n > 64 && n % 2 == 0 && ldb % 2 == 0 && aligned(B, 8);

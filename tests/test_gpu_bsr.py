@@ -986,6 +986,122 @@ def test_small_bs_lane_group_bit_exact(oracle, device, bs, direction, n):
     assert (dC.cpu().numpy() == want2).all(), f"bs {bs}: alpha / beta epilogue"
 
 
+def _grouped_small_bsr(rng, bs, mb, kb, sorted_cols=True):
+    """Block rows in runs that share block columns (neighbouring rows of a
+    community), power-law lengths from empty to past several merge batches,
+    about half the columns of each block empty."""
+    rows = []
+    for br in range(mb):
+        L = int(min(kb, rng.pareto(1.2) * 6)) if br % 7 != 3 else 0
+        home = (br // 3) * 5 % kb
+        near = (home + rng.integers(0, 24, L)) % kb
+        far = rng.integers(0, kb, max(L // 3, 0))
+        c = np.unique(np.concatenate([near, far]))[:L] if L else np.zeros(0, np.int64)
+        if not sorted_cols:
+            c = rng.permutation(c)
+        rows.append(c)
+    rp = np.concatenate([[0], np.cumsum([len(c) for c in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    vb = rng.uniform(-1, 1, (rp[-1], bs, bs)).astype(np.float32)
+    for k in range(vb.shape[0]):
+        vb[k][:, rng.random(bs) < 0.5] = 0.0
+    return rp, ci, vb
+
+
+@pytest.mark.parametrize("bs", [2, 4, 8])
+@pytest.mark.parametrize("direction", [0, 1])
+@pytest.mark.parametrize("n,oc", [(128, 0), (384, 0), (64, 0), (256, 1)])
+def test_small_bs_grouped_stream_bit_exact(oracle, device, bs, direction, n, oc):
+    """bs 2 / 4 / 8 on the grouped MFMA stream (bsr_small_grp_kernel: 32 / bs
+    block rows per wave walk the union of their block columns): every element
+    is the oracle's sequential fp32 FMA chain bit for bit, over rows that span
+    many merge batches, runs of rows sharing columns, empty rows, a last group
+    cut short, several 128-column tiles and column-major C; alpha / beta."""
+    ops = _ops()
+    rng = np.random.default_rng(1000 * bs + 100 * direction + n + oc)
+    G = 32 // bs
+    mb, kb = 5 * G + 3, 160
+    rp, ci, vb = _grouped_small_bsr(rng, bs, mb, kb)
+    if direction == 1:
+        vb = np.ascontiguousarray(vb.transpose(0, 2, 1))  # the same blocks stored by column
+    v = vb.reshape(-1)
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B.reshape(-1))
+    m = mb * bs
+    oc_ = ops.ORDER_COL if oc else ops.ORDER_ROW
+    ldc = m if oc else n
+    for alpha, beta in ((1.0, 0.0), (0.5, -2.0)):
+        C0 = rng.uniform(-1, 1, m * n).astype(np.float32)
+        dC = _dev(C0)[0] if beta else torch.full((m * n,), float("nan"), device=device)
+        ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=ldc, alpha=alpha,
+                  beta=beta, direction=direction, order_c=oc_)
+        torch.cuda.synchronize()
+        want = oracle_bsrmm_f32(oracle, direction, mb, n, bs, rp, ci, v, B, n, 0, alpha, beta,
+                                C0 if beta else None, ldc, oc)
+        got = dC.cpu().numpy()
+        assert (got == want).all(), f"bs {bs}: {int((got != want).sum())} elements differ"
+
+
+@pytest.mark.parametrize("bs", [2, 4, 8])
+def test_small_bs_grouped_nonfinite_contract(oracle, device, bs):
+    """inf / NaN B rows on the grouped stream: column-granular exactly (an
+    element is non-finite iff its block row stores a block whose column meets a
+    non-finite B value with a value in it), whatever the other block rows of its
+    group hold; every other element bit-identical to the run on B with those
+    rows zeroed (the flagged tiles are recomputed by bsr_small_kernel)."""
+    ops = _ops()
+    rng = np.random.default_rng(77 + bs)
+    mb, kb, n = 6 * (32 // bs) + 1, 120, 256
+    rp, ci, vb = _grouped_small_bsr(rng, bs, mb, kb)
+    v = vb.reshape(-1)
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    # rows a stored block uses (a value in its column) and rows only empty columns meet
+    used = np.zeros(kb * bs, bool)
+    for k in range(rp[-1]):
+        used[ci[k] * bs + np.nonzero(np.any(vb[k] != 0, axis=0))[0]] = True
+    bad_used = rng.choice(np.nonzero(used)[0], 3, replace=False)
+    bad_unused = rng.choice(np.nonzero(~used)[0], 2, replace=False)
+    Bbad = B.copy()
+    Bbad[bad_used[0], 5] = np.inf
+    Bbad[bad_used[1], :] = np.nan
+    Bbad[bad_used[2], 130:140] = -np.inf
+    Bbad[bad_unused] = np.nan
+    Bz = np.where(np.isfinite(Bbad), Bbad, np.float32(0.0))
+    want = oracle_bsrmm_f32(oracle, 0, mb, n, bs, rp, ci, v, Bz, n, 0).reshape(mb * bs, n)
+    expect_nf = np.zeros((mb * bs, n), bool)
+    for br in range(mb):
+        for k in range(rp[br], rp[br + 1]):
+            for c in np.nonzero(np.any(vb[k] != 0, axis=0))[0]:
+                expect_nf[br * bs:(br + 1) * bs] |= ~np.isfinite(Bbad[ci[k] * bs + c])[None, :]
+    assert expect_nf.any()
+    drp, dci, dv, dB = _dev(rp, ci, v, Bbad.reshape(-1))
+    dC = torch.full((mb * bs * n,), 7.0, device=device)
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n)
+    torch.cuda.synchronize()
+    got = dC.cpu().numpy().reshape(mb * bs, n)
+    assert np.array_equal(~np.isfinite(got), expect_nf), "non-finite pattern"
+    assert (got[~expect_nf] == want[~expect_nf]).all(), "finite elements"
+
+
+@pytest.mark.parametrize("bs", [2, 8])
+def test_small_bs_grouped_unsorted_columns(oracle, device, bs):
+    """Block columns out of order inside rows (and so not sharing batches):
+    the grouped stream still multiplies every block, within the fp32 bar of the
+    f64 oracle."""
+    ops = _ops()
+    rng = np.random.default_rng(55 + bs)
+    mb, kb, n = 4 * (32 // bs) + 2, 90, 128
+    rp, ci, vb = _grouped_small_bsr(rng, bs, mb, kb, sorted_cols=False)
+    v = vb.reshape(-1)
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B.reshape(-1))
+    dC = torch.full((mb * bs * n,), float("nan"), device=device)
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n)
+    torch.cuda.synchronize()
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
+    assert_normwise(dC.cpu().numpy().reshape(mb * bs, n), ref, absd, TOL_F32, f"bs {bs} unsorted")
+
+
 @pytest.mark.parametrize("n,oc", [(128, 0), (256, 0), (96, 1)])
 def test_bsr64_matches_bs32_sub_blocks(oracle, device, n, oc):
     """bs 64 runs the bs 32 column stream on each block's 32 x 32 sub-blocks:
