@@ -2610,17 +2610,24 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
 #ifndef SPMM_SGRP_LPT
 #define SPMM_SGRP_LPT 1
 #endif
+#ifndef SPMM_SGRP_DB
+#define SPMM_SGRP_DB 1
+#endif
+#ifndef SPMM_SGRP_XM
+#define SPMM_SGRP_XM 8
+#endif
 template <int BS, bool ROWD, bool CROW>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OCC))) void bsr_small_grp_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc, int xm, int* __restrict__ dirty,
-    const int* __restrict__ order) {
+    const int* __restrict__ order, int nnzb) {
   static_assert(BS == 2 || BS == 4 || BS == 8, "bs 2 / 4 / 8");
   constexpr int G = 32 / BS;  // block rows per group: 32 output rows
   constexpr int Q = 64 / G;   // candidates per block row and batch
   constexpr int E = BS * BS;
-  constexpr int R = 4;        // ring slots: A of step s + 2, B of step s + 1, MFMAs of step s
+  constexpr int DB = SPMM_SGRP_DB;  // B rows loaded DB steps ahead of their MFMAs, A DB + 1
+  constexpr int R = 4;        // ring slots: A of step s + DB + 1, B of step s + DB, MFMAs of step s
   constexpr int NQ = 128;     // union-step queue (a batch adds at most 64)
   constexpr int kNone = 0x7fffffff;
   constexpr unsigned long long kSeg = (1ull << Q) - 1;
@@ -2633,7 +2640,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
 
   const int lane = threadIdx.x;
   const int j = lane & 31, h = lane >> 5;
-  const int g = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, gridDim.x, xm);
+  // Groups go to the XCDs in chunks of xm (neighbours share B rows in one L2). With `order`
+  // (a shallow grid) the chunks come longest first: order[] ranks them and the grid has
+  // nchunks * xm waves, those past the last group exiting at once.
+  int g;
+  if (order) {
+    const int b = blockIdx.x, nch = gridDim.x / xm, full = nch / 8 * 8 * xm;
+    const int slot = b < full ? (b / 8 / xm) * 8 + b % 8 : nch / 8 * 8 + (b - full) / xm;
+    const int member = b < full ? (b / 8) % xm : (b - full) % xm;
+    g = order[slot] * xm + member;
+    if (g * G >= mb) return;
+  } else {
+    g = xcd_block_row(blockIdx.x, gridDim.x, xm);
+  }
   const int jt = blockIdx.y * 128;
   // merge role: block row lr of the group, candidate lq
   const int lr = lane / Q, lq = lane % Q;
@@ -2717,10 +2736,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
   };
 
   float ar[R][BS];    // A: row gi of the block row grow's block of the step (zero: none)
-  int kbr[R], jr[R];  // its block (-1: none), the step's block column (uniform)
+  int jr[R];          // the step's block column (uniform)
   bool vr[R];         // the step exists (uniform)
   unsigned act[R];    // active columns (uniform)
   f32x2 bx[R][BS];    // B rows J * bs + c, this lane's two columns
+  // A through one buffer resource from the group's first block: a block row without the
+  // step's block column reads past the resource's end, zeros without a memory access
+  const int kbase = __builtin_amdgcn_readfirstlane(lp);  // lane 0: the group's first block
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(val + (size_t)kbase * E), 0,
+      (unsigned)min((long long)(nnzb - kbase) * E * 4, 0x7fffffffLL), 0x00020000);
+  const unsigned aoff = 4u * (unsigned)(ROWD ? gi * BS : gi);
   auto load_a = [&](int s) {
     const bool v = qt < qh;
     const int qi = qt & (NQ - 1);
@@ -2729,37 +2755,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
     qt += v ? 1 : 0;
     vr[s] = v;
     jr[s] = J;
-    kbr[s] = kb;
-    const size_t kk = kb >= 0 ? (size_t)kb : 0;  // block 0 stands in (selected away)
-    const float* src = val + kk * E + (ROWD ? gi * BS : gi);
+    const unsigned off = kb >= 0 ? (unsigned)(kb - kbase) * (E * 4) + aoff : 0x80000000u;
     if constexpr (ROWD && BS == 8) {
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
+      const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
+      const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off + 16, 0, 0));
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         ar[s][c] = x0[c];
         ar[s][4 + c] = x1[c];
       }
     } else if constexpr (ROWD && BS == 4) {
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
 #pragma unroll
       for (int c = 0; c < 4; ++c) ar[s][c] = x0[c];
     } else if constexpr (ROWD) {
-      const f32x2 x0 = *reinterpret_cast<const f32x2*>(src);
+      const f32x2 x0 = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsa, off, 0, 0));
       ar[s][0] = x0[0];
       ar[s][1] = x0[1];
     } else {
 #pragma unroll
-      for (int c = 0; c < BS; ++c) ar[s][c] = src[c * BS];
+      for (int c = 0; c < BS; ++c)
+        ar[s][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsa, off + 4 * c * BS, 0, 0));
     }
   };
   auto load_b = [&](int s) {
     unsigned m = 0;
 #pragma unroll
-    for (int c = 0; c < BS; ++c) {
-      ar[s][c] = kbr[s] >= 0 ? ar[s][c] : 0.f;
-      if (__builtin_amdgcn_ballot_w64((__float_as_uint(ar[s][c]) & 0x7fffffffu) != 0u)) m |= 1u << c;
-    }
+    for (int c = 0; c < BS; ++c)
+      m |= (unsigned)(__builtin_amdgcn_ballot_w64((__float_as_uint(ar[s][c]) & 0x7fffffffu) != 0u) != 0) << c;
     act[s] = m;
     // one resource over the step's bs B rows; an inactive column's offset is past its end,
     // so its load returns zeros without a memory access
@@ -2789,24 +2812,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
     }
   };
 
-  // the queue holds at least R + 2 steps before every round (or every row is done): the
-  // prologue takes 2 and a round R, so a slot is empty only once every row is done
+  // the queue holds at least R + DB + 1 steps before every round (or every row is done): the
+  // prologue takes DB + 1 and a round R, so a slot is empty only once every row is done
   auto refill = [&]() {
-    while (!done && qh - qt < R + 2) {
+    while (!done && qh - qt < R + DB + 1) {
       const int nun = merge();
       if (nun == 0) done = true;
       qh += nun;
     }
   };
   refill();
-  load_a(0);
-  load_a(1);
-  load_b(0);
+#pragma unroll
+  for (int s = 0; s < DB + 1; ++s) load_a(s);
+#pragma unroll
+  for (int s = 0; s < DB; ++s) load_b(s);
   while (vr[0]) {
 #pragma unroll
     for (int s = 0; s < R; ++s) {  // a step past the end multiplies nothing (act 0)
-      load_a((s + 2) % R);
-      load_b((s + 1) % R);
+      load_a((s + DB + 1) % R);
+      load_b((s + DB) % R);
       consume(s);
     }
     asm volatile("" : "+a"(u0), "+a"(u1));  // the accumulators stay in AGPRs through the merge
@@ -3864,7 +3888,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
   } else if ((bs == 2 || bs == 4 || bs == 8) && brow && !dense_sem && nnzb > 0 && n >= 4 &&
              n % 4 == 0 && ldb % 2 == 0 && aligned(B, 8) && aligned(val, 16) &&
              (!crow || (ldc % 4 == 0 && aligned(C, 16))) && kb < (1 << 26) &&
-             (size_t)ldb * bs * 4 < (1u << 31) &&
+             (size_t)ldb * bs * 4 < (1u << 31) && (size_t)(32 / bs) * kb * bs * bs * 4 < (1u << 31) &&
              small_grp_enabled()) {
     // the grouped MFMA stream: 32 / bs block rows per wave share each B row of their union
     const int ngroups = (mb + 32 / bs - 1) / (32 / bs);
@@ -3874,35 +3898,36 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       return st;
     }
     int* dirty = static_cast<int*>(ctx->scratch);
-    // a shallow grid (a few waves per resident slot): groups longest first, else the
+    constexpr int xm = SPMM_SGRP_XM;  // groups per XCD chunk
+    // a shallow grid (a few waves per resident slot): groups longest first (reddit bs 8
+    // 1.50 -> 1.37 ms: 2.4 waves per slot, group loads up to 2.7x the mean), else the
     // XCD-chunked order
     const int* ord = nullptr;
+    dim3 lgrid = grid;
     {
       const long slots = 12L * ctx->num_cus;
       if (SPMM_SGRP_LPT && (long)ngroups * grid.y <= kLptRounds * slots) {
-        if (spmm_status_t st = spmm::ensure_order_buffer(ctx, ngroups)) {
+        // chunks of xm groups, longest first (block_row_order_kernel keyed by a chunk's blocks)
+        // (chunks of xm groups ranked together, XCD chunks kept: 1.41-1.43 ms on reddit bs 8
+        // against 1.37 for single groups, the same box; profiles/r05b/small_grp/)
+        const int cx = SPMM_SGRP_LPT == 2 ? xm : 1;
+        const int nch = (ngroups + cx - 1) / cx;
+        if (spmm_status_t st = spmm::ensure_order_buffer(ctx, nch)) {
           timing_end(ctx, slot);
           return st;
         }
-        const double mean = (double)nnzb / ngroups;
+        const double mean = (double)nnzb / nch;
         int gshift = 0;
         while ((4.0 * mean) / (1 << gshift) > 1023.0) ++gshift;
-        hipLaunchKernelGGL(block_row_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, ngroups,
-                           rowptr, nullptr, mb, 0, ctx->order, 32 / bs, gshift);
+        hipLaunchKernelGGL(block_row_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, nch,
+                           rowptr, nullptr, mb, 0, ctx->order, 32 / bs * cx, gshift);
         ord = ctx->order;
+        lgrid.x = nch * cx;
       }
     }
-#ifdef SPMM_TUNING
-    static const int xm = [] {
-      const char* e = getenv("SPMM_SMALL_GRP_XM");
-      return e ? atoi(e) : 8;
-    }();
-#else
-    constexpr int xm = 8;
-#endif
 #define SGRP_ONE(BS_, RD_, CR_)                                                                  \
-  hipLaunchKernelGGL((bsr_small_grp_kernel<BS_, RD_, CR_>), grid, dim3(64), 0, ctx->stream, mb, \
-                     n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, xm, dirty, ord)
+  hipLaunchKernelGGL((bsr_small_grp_kernel<BS_, RD_, CR_>), lgrid, dim3(64), 0, ctx->stream, mb, \
+                     n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, SPMM_SGRP_LPT != 2 && ord ? 1 : xm, dirty, ord, nnzb)
 #define SGRP_LAUNCH(BS_)                                                                         \
   do {                                                                                           \
     if (rowd && crow) SGRP_ONE(BS_, true, true);                                                 \
