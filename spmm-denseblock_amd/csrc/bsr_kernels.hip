@@ -2604,6 +2604,7 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
 #ifndef SPMM_SGRP_OCC
 #define SPMM_SGRP_OCC 1
 #endif
+
 #ifndef SPMM_SGRP_PF
 #define SPMM_SGRP_PF 1
 #endif
@@ -2616,12 +2617,68 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
 #ifndef SPMM_SGRP_XM
 #define SPMM_SGRP_XM 8
 #endif
+#ifndef SPMM_SGRP_PROBE
+#define SPMM_SGRP_PROBE 1
+#endif
+
+// The grouped stream's choice per matrix (small_grp_probe_kernel, launched before it on the
+// same stream). Block rows that share few block columns gain nothing from the union and lose
+// to the MFMA's 32 rows; such a matrix is left to bsr_small_kernel whole. Up to 1024 groups
+// spread over the matrix are sampled, one wave each: P = 64 / G sample blocks per group, probe
+// p being block row (5p + 3) % G's block at position (p + 1/2) / P (a prefix would not do: a
+// community's out-of-community columns sort first), searched for in every block row of the
+// group by one lane (binary search over its sorted block columns). The mean of 1 / holders
+// estimates the union steps per block; the sums go to stat[0..1]. The grouped stream gives the
+// whole matrix up past kGiveUp, a little above the break-even of the two kernels on the reddit
+// stand-in (bs 8: 2.0 ms for 6.3 M blocks on the lane-group kernel against 1.37 ms for
+// 2.75 M union steps, 0.64; bs 4 0.40; bs 2 0.20); a uniform-random pattern (the reference's
+// test_bsrmm) sits near 1, reddit at 0.44 / 0.20 / 0.10. Per matrix, not per group: a group
+// given up runs its block rows one wave each on the lane-group kernel, and one long group
+// there (a hub) made a 0.1-ms tail on reddit; the probes inside the stream itself cost 8-13 %
+// (their chains of dependent loads at every wave's start).
+template <int BS>
+__global__ __launch_bounds__(64) void small_grp_probe_kernel(int mb, int ngroups,
+                                                             const int* __restrict__ rowptr,
+                                                             const int* __restrict__ colind,
+                                                             float* __restrict__ stat) {
+  constexpr int G = 32 / BS, P = 64 / G;
+  const int g = (int)(((long long)blockIdx.x * ngroups) / gridDim.x);
+  const int lane = threadIdx.x, pp = lane / G;
+  const int prow = g * G + (pp * 5 + 3) % G, srow = g * G + lane % G;
+  const int ps = prow < mb ? rowptr[prow] : 0, pe = prow < mb ? rowptr[prow + 1] : 0;
+  const bool pvalid = pe > ps;
+  const int pj = pvalid ? colind[ps + (int)(((2LL * pp + 1) * (pe - ps)) / (2 * P))] : -1;
+  int lo = srow < mb ? rowptr[srow] : 0;
+  const int se = srow < mb ? rowptr[srow + 1] : 0;
+  int hi = se;
+  while (pvalid && lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (colind[mid] < pj) lo = mid + 1;
+    else hi = mid;
+  }
+  const unsigned long long held = __builtin_amdgcn_ballot_w64(pvalid && lo < se && colind[lo] == pj);
+  const unsigned long long pv = __builtin_amdgcn_ballot_w64(pvalid);
+  float est = 0.f;
+  int nv = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    if ((pv >> (p * G)) & 1ull) {
+      est += 1.f / (float)max(__builtin_popcountll((held >> (p * G)) & ((1ull << G) - 1ull)), 1);
+      ++nv;
+    }
+  }
+  if (lane == 0 && nv) {
+    atomicAdd(&stat[0], est);
+    atomicAdd(&stat[1], (float)nv);
+  }
+}
+
 template <int BS, bool ROWD, bool CROW>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OCC))) void bsr_small_grp_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc, int xm, int* __restrict__ dirty,
-    const int* __restrict__ order, int nnzb) {
+    const int* __restrict__ order, int nnzb, const float* __restrict__ stat) {
   static_assert(BS == 2 || BS == 4 || BS == 8, "bs 2 / 4 / 8");
   constexpr int G = 32 / BS;  // block rows per group: 32 output rows
   constexpr int Q = 64 / G;   // candidates per block row and batch
@@ -2652,6 +2709,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
     if (g * G >= mb) return;
   } else {
     g = xcd_block_row(blockIdx.x, gridDim.x, xm);
+  }
+  // small_grp_probe_kernel's estimate of union steps per block: past kGiveUp the matrix is
+  // left to bsr_small_kernel (its block rows share too little)
+  {
+    constexpr float kGiveUp = BS == 8 ? 0.70f : (BS == 4 ? 0.45f : 0.25f);
+    if (SPMM_SGRP_PROBE && stat[0] > kGiveUp * stat[1]) {
+      if (lane == 0) dirty[g * gridDim.y + blockIdx.y] = 1;
+      return;
+    }
   }
   const int jt = blockIdx.y * 128;
   // merge role: block row lr of the group, candidate lq
@@ -2843,6 +2909,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
   // value, multiplied into all 32 rows (by a or by 0), leaves an accumulator inf or NaN,
   // and no finite product does short of overflow (which bsr_small_kernel repeats), so
   // the accumulators tell.
+  // the accumulators were last written by MFMAs hipcc may not see through the asm pins:
+  // 24 wait states before the first read (MFMA -> VALU read of its result)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(u0), "+a"(u1));
   unsigned mx = 0;
 #pragma unroll
   for (int e = 0; e < 32; ++e)
@@ -3893,11 +3962,12 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     // the grouped MFMA stream: 32 / bs block rows per wave share each B row of their union
     const int ngroups = (mb + 32 / bs - 1) / (32 / bs);
     const dim3 grid(ngroups, (n + 127) / 128);
-    if (spmm_status_t st = ensure_scratch(ctx, (size_t)ngroups * grid.y * sizeof(int))) {
+    if (spmm_status_t st = ensure_scratch(ctx, (size_t)ngroups * grid.y * sizeof(int) + 256)) {
       timing_end(ctx, slot);
       return st;
     }
-    int* dirty = static_cast<int*>(ctx->scratch);
+    float* stat = static_cast<float*>(ctx->scratch);  // the probe's sums
+    int* dirty = reinterpret_cast<int*>(static_cast<char*>(ctx->scratch) + 256);
     constexpr int xm = SPMM_SGRP_XM;  // groups per XCD chunk
     // a shallow grid (a few waves per resident slot): groups longest first (reddit bs 8
     // 1.50 -> 1.37 ms: 2.4 waves per slot, group loads up to 2.7x the mean), else the
@@ -3927,7 +3997,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     }
 #define SGRP_ONE(BS_, RD_, CR_)                                                                  \
   hipLaunchKernelGGL((bsr_small_grp_kernel<BS_, RD_, CR_>), lgrid, dim3(64), 0, ctx->stream, mb, \
-                     n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, SPMM_SGRP_LPT != 2 && ord ? 1 : xm, dirty, ord, nnzb)
+                     n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, SPMM_SGRP_LPT != 2 && ord ? 1 : xm, dirty, ord, nnzb, \
+                     stat)
 #define SGRP_LAUNCH(BS_)                                                                         \
   do {                                                                                           \
     if (rowd && crow) SGRP_ONE(BS_, true, true);                                                 \
@@ -3935,6 +4006,21 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     else if (crow) SGRP_ONE(BS_, false, true);                                                   \
     else SGRP_ONE(BS_, false, false);                                                            \
   } while (0)
+    // the choice per matrix first (small_grp_probe_kernel), then the stream
+    if (hipError_t e = hipMemsetAsync(stat, 0, 2 * sizeof(float), ctx->stream)) {
+      timing_end(ctx, slot);
+      return from_hip(e);
+    }
+    const dim3 pgrid(std::min(ngroups, 1024));
+    if (bs == 8)
+      hipLaunchKernelGGL(small_grp_probe_kernel<8>, pgrid, dim3(64), 0, ctx->stream, mb, ngroups,
+                         rowptr, colind, stat);
+    else if (bs == 4)
+      hipLaunchKernelGGL(small_grp_probe_kernel<4>, pgrid, dim3(64), 0, ctx->stream, mb, ngroups,
+                         rowptr, colind, stat);
+    else
+      hipLaunchKernelGGL(small_grp_probe_kernel<2>, pgrid, dim3(64), 0, ctx->stream, mb, ngroups,
+                         rowptr, colind, stat);
     if (bs == 8) SGRP_LAUNCH(8);
     else if (bs == 4) SGRP_LAUNCH(4);
     else SGRP_LAUNCH(2);

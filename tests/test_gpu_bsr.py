@@ -1043,6 +1043,37 @@ def test_small_bs_grouped_stream_bit_exact(oracle, device, bs, direction, n, oc)
 
 
 @pytest.mark.parametrize("bs", [2, 4, 8])
+def test_small_bs_grouped_mixed_sharing(oracle, device, bs):
+    """Groups whose block rows share their block columns stay on the grouped
+    stream and groups of uniform-random rows (little sharing) are handed to
+    bsr_small_kernel: one matrix holding both is bit-exact with the sequential
+    oracle, with alpha / beta."""
+    ops = _ops()
+    rng = np.random.default_rng(900 + bs)
+    G = 32 // bs
+    mb, kb, n = 8 * G, 400, 128
+    rows = []
+    for br in range(mb):
+        if (br // G) % 2 == 0:   # a band shared by the group
+            c = np.unique((br // G) * 13 + rng.integers(0, 40, 30))
+        else:                    # uniform random
+            c = np.unique(rng.integers(0, kb, 30))
+        rows.append(np.sort(c % kb))
+    rp = np.concatenate([[0], np.cumsum([len(c) for c in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    v = rng.uniform(-1, 1, rp[-1] * bs * bs).astype(np.float32)
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, mb * bs * n).astype(np.float32)
+    drp, dci, dv, dB, dC = _dev(rp, ci, v, B.reshape(-1), C0)
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n, alpha=0.75,
+              beta=0.5)
+    torch.cuda.synchronize()
+    want = oracle_bsrmm_f32(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0, 0.75, 0.5, C0, n, 0)
+    got = dC.cpu().numpy()
+    assert (got == want).all(), f"bs {bs}: {int((got != want).sum())} elements differ"
+
+
+@pytest.mark.parametrize("bs", [2, 4, 8])
 def test_small_bs_grouped_nonfinite_contract(oracle, device, bs):
     """inf / NaN B rows on the grouped stream: column-granular exactly (an
     element is non-finite iff its block row stores a block whose column meets a
