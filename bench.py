@@ -1093,7 +1093,9 @@ def run_bsr(args, W, world, rank, dev, dist):
              ("bsr32_f32_cs2_kernel" if bs == 32 else
               "bsr32_f32_cs2_kernel (bs 64 sub-blocks)" if bs == 64 else
               "bsr16_f16_cs_kernel" if cs16 else "bsr16_cm_kernel") if cm else
-             f"bsr_small_kernel<{bs}>" if bs in (2, 4, 8) and dt == "fp32" else
+             # bs 2 / 4 / 8: the grouped MFMA stream (bsr_small_grp_kernel) on matrices whose
+             # block rows share their columns, the lane-group kernel on the rest
+             f"bsr_small_grp_kernel<{bs}>" if bs in (2, 4, 8) and dt == "fp32" else
              f"bsr{bs} register-fragment kernel")
     tkey = {"workload": args.workload, "kernel": kname, "K": K, "dtype": dt, "nnzb": nnzb,
             "layout_BC": args.bsr_layout,
