@@ -129,6 +129,13 @@ spmm_status_t spmm_set_csr_options(spmm_handle_t handle, int flags);
  * analysed entries (which then ignore the masks) and the hybrid's BSR part.
  * Same result as the default on finite inputs, within the fp32 bar. */
 #define SPMM_BSR_DENSE_BLOCK_PRODUCT 1
+/* SPMM_BSR_SMALL_GROUPED: bs 2 / 4 / 8 (row-major B) take the grouped MFMA stream
+ * (32 / bs block rows per wave share each B row of their column
+ * union) whatever the matrix's size. By default it is taken from 2^20 stored
+ * blocks up, where its fixed cost (a sharing probe and a block-row order,
+ * about 40 us) is under a tenth of the product; below, and on matrices the probe
+ * finds unshared, the lane-group VALU kernel runs. Same result bit for bit. */
+#define SPMM_BSR_SMALL_GROUPED 2
 spmm_status_t spmm_set_bsr_options(spmm_handle_t handle, int flags);
 
 /* Build options of the loaded library (bit flags): SPMM_BUILD_TUNING is set

@@ -3958,7 +3958,10 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
              n % 4 == 0 && ldb % 2 == 0 && aligned(B, 8) && aligned(val, 16) &&
              (!crow || (ldc % 4 == 0 && aligned(C, 16))) && kb < (1 << 26) &&
              (size_t)ldb * bs * 4 < (1u << 31) && (size_t)(32 / bs) * kb * bs * bs * 4 < (1u << 31) &&
+             (nnzb >= (1 << 20) || (ctx->bsr_flags & SPMM_BSR_SMALL_GROUPED)) &&
              small_grp_enabled()) {
+    // (from 2^20 blocks: its fixed cost, the probe and the order, about 40 us, made the
+    // reference sweep's small cells up to 2x slower; SPMM_BSR_SMALL_GROUPED forces it)
     // the grouped MFMA stream: 32 / bs block rows per wave share each B row of their union
     const int ngroups = (mb + 32 / bs - 1) / (32 / bs);
     const dim3 grid(ngroups, (n + 127) / 128);

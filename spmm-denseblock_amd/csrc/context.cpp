@@ -266,7 +266,7 @@ spmm_status_t spmm_set_hybrid_options(spmm_handle_t h, int flags) {
 
 spmm_status_t spmm_set_bsr_options(spmm_handle_t h, int flags) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
-  if (flags & ~SPMM_BSR_DENSE_BLOCK_PRODUCT) return SPMM_STATUS_INVALID_VALUE;
+  if (flags & ~(SPMM_BSR_DENSE_BLOCK_PRODUCT | SPMM_BSR_SMALL_GROUPED)) return SPMM_STATUS_INVALID_VALUE;
   h->bsr_flags = flags;
   return SPMM_STATUS_SUCCESS;
 }

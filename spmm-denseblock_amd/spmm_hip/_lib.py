@@ -36,6 +36,7 @@ HYBRID_FUSED = 1
 HYBRID_TWO_LAUNCH = 2
 HYBRID_SPLIT_BF16 = 4
 BSR_DENSE_BLOCK_PRODUCT = 1
+BSR_SMALL_GROUPED = 2
 BUILD_TUNING = 1
 
 

@@ -986,6 +986,15 @@ def test_small_bs_lane_group_bit_exact(oracle, device, bs, direction, n):
     assert (dC.cpu().numpy() == want2).all(), f"bs {bs}: alpha / beta epilogue"
 
 
+def _grouped_handle():
+    """A handle whose bs 2 / 4 / 8 products take the grouped MFMA stream at any size
+    (SPMM_BSR_SMALL_GROUPED; by default only from 2^20 blocks)."""
+    from spmm_hip._lib import BSR_SMALL_GROUPED
+    h = _ops().Handle()
+    h.set_bsr_options(BSR_SMALL_GROUPED)
+    return h
+
+
 def _grouped_small_bsr(rng, bs, mb, kb, sorted_cols=True):
     """Block rows in runs that share block columns (neighbouring rows of a
     community), power-law lengths from empty to past several merge batches,
@@ -1018,6 +1027,7 @@ def test_small_bs_grouped_stream_bit_exact(oracle, device, bs, direction, n, oc)
     many merge batches, runs of rows sharing columns, empty rows, a last group
     cut short, several 128-column tiles and column-major C; alpha / beta."""
     ops = _ops()
+    h = _grouped_handle()
     rng = np.random.default_rng(1000 * bs + 100 * direction + n + oc)
     G = 32 // bs
     mb, kb = 5 * G + 3, 160
@@ -1034,7 +1044,7 @@ def test_small_bs_grouped_stream_bit_exact(oracle, device, bs, direction, n, oc)
         C0 = rng.uniform(-1, 1, m * n).astype(np.float32)
         dC = _dev(C0)[0] if beta else torch.full((m * n,), float("nan"), device=device)
         ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=ldc, alpha=alpha,
-                  beta=beta, direction=direction, order_c=oc_)
+                  beta=beta, direction=direction, order_c=oc_, handle=h)
         torch.cuda.synchronize()
         want = oracle_bsrmm_f32(oracle, direction, mb, n, bs, rp, ci, v, B, n, 0, alpha, beta,
                                 C0 if beta else None, ldc, oc)
@@ -1049,6 +1059,7 @@ def test_small_bs_grouped_mixed_sharing(oracle, device, bs):
     bsr_small_kernel: one matrix holding both is bit-exact with the sequential
     oracle, with alpha / beta."""
     ops = _ops()
+    h = _grouped_handle()
     rng = np.random.default_rng(900 + bs)
     G = 32 // bs
     mb, kb, n = 8 * G, 400, 128
@@ -1066,7 +1077,7 @@ def test_small_bs_grouped_mixed_sharing(oracle, device, bs):
     C0 = rng.uniform(-1, 1, mb * bs * n).astype(np.float32)
     drp, dci, dv, dB, dC = _dev(rp, ci, v, B.reshape(-1), C0)
     ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n, alpha=0.75,
-              beta=0.5)
+              beta=0.5, handle=h)
     torch.cuda.synchronize()
     want = oracle_bsrmm_f32(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0, 0.75, 0.5, C0, n, 0)
     got = dC.cpu().numpy()
@@ -1081,6 +1092,7 @@ def test_small_bs_grouped_nonfinite_contract(oracle, device, bs):
     group hold; every other element bit-identical to the run on B with those
     rows zeroed (the flagged tiles are recomputed by bsr_small_kernel)."""
     ops = _ops()
+    h = _grouped_handle()
     rng = np.random.default_rng(77 + bs)
     mb, kb, n = 6 * (32 // bs) + 1, 120, 256
     rp, ci, vb = _grouped_small_bsr(rng, bs, mb, kb)
@@ -1107,7 +1119,7 @@ def test_small_bs_grouped_nonfinite_contract(oracle, device, bs):
     assert expect_nf.any()
     drp, dci, dv, dB = _dev(rp, ci, v, Bbad.reshape(-1))
     dC = torch.full((mb * bs * n,), 7.0, device=device)
-    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n)
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n, handle=h)
     torch.cuda.synchronize()
     got = dC.cpu().numpy().reshape(mb * bs, n)
     assert np.array_equal(~np.isfinite(got), expect_nf), "non-finite pattern"
@@ -1120,6 +1132,7 @@ def test_small_bs_grouped_unsorted_columns(oracle, device, bs):
     the grouped stream still multiplies every block, within the fp32 bar of the
     f64 oracle."""
     ops = _ops()
+    h = _grouped_handle()
     rng = np.random.default_rng(55 + bs)
     mb, kb, n = 4 * (32 // bs) + 2, 90, 128
     rp, ci, vb = _grouped_small_bsr(rng, bs, mb, kb, sorted_cols=False)
@@ -1127,7 +1140,7 @@ def test_small_bs_grouped_unsorted_columns(oracle, device, bs):
     B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
     drp, dci, dv, dB = _dev(rp, ci, v, B.reshape(-1))
     dC = torch.full((mb * bs * n,), float("nan"), device=device)
-    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n)
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n, handle=h)
     torch.cuda.synchronize()
     ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
     assert_normwise(dC.cpu().numpy().reshape(mb * bs, n), ref, absd, TOL_F32, f"bs {bs} unsorted")
