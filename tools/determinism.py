@@ -126,11 +126,28 @@ def main():
         h.close()
     del d, C, B
     torch.cuda.empty_cache()
+    # community-ordered reddit stand-in, bs 8 / 2: the grouped small-bs MFMA stream (merge in
+    # LDS, longest-first groups; reddit_bsr8 / reddit_bsr2)
+    n = 232965
+    rp, ci = prep.community_csr(n, 670.0, 512, 2048, 0.99, 1234)
+    v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
+    drp, dci, dv = [torch.from_numpy(a).to(dev) for a in (rp, ci, v)]
+    for bs2 in (8, 2):
+        mb2 = (n + bs2 - 1) // bs2
+        B2 = torch.rand((mb2 * bs2, K), device=dev) * 2 - 1
+        C2 = torch.empty((mb2 * bs2, K), device=dev)
+        brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs2)
+
+        def run():
+            ops.bsrmm(brp, bci, bval, B2, mb=mb2, kb=mb2, n=K, bs=bs2, ldb=K, C=C2, ldc=K)
+            return C2
+        bad += check(f"reddit bsr{bs2} (grouped small-bs stream)", run, reps)
+        del brp, bci, bval, B2, C2
+        torch.cuda.empty_cache()
+    del drp, dci, dv
     # RCM-reordered reddit stand-in, bs 32: the longest-first order with
     # segments of the outlier rows (partial tiles + fix-up) and the fused
     # hybrid on the same matrix (longest-first order)
-    n = 232965
-    rp, ci = prep.community_csr(n, 670.0, 512, 2048, 0.99, 1234)
     rp, ci = prep.permute_csr(rp, ci, np.random.default_rng(9).permutation(n).astype(np.int32))
     rp, ci = prep.permute_csr(rp, ci, prep.reorder(rp, ci, "rcm"))
     v = np.random.default_rng(2).uniform(-1, 1, ci.size).astype(np.float32)
