@@ -995,6 +995,19 @@ def _grouped_handle():
     return h
 
 
+def test_bsr_options_flags(device):
+    """spmm_set_bsr_options takes SPMM_BSR_DENSE_BLOCK_PRODUCT and
+    SPMM_BSR_SMALL_GROUPED, alone or together, and refuses any other bit."""
+    from spmm_hip._lib import BSR_DENSE_BLOCK_PRODUCT, BSR_SMALL_GROUPED, SpmmError
+    h = _ops().Handle()
+    for f in (0, BSR_DENSE_BLOCK_PRODUCT, BSR_SMALL_GROUPED,
+              BSR_DENSE_BLOCK_PRODUCT | BSR_SMALL_GROUPED):
+        h.set_bsr_options(f)
+    with pytest.raises(SpmmError):
+        h.set_bsr_options(4)
+    h.close()
+
+
 def _grouped_small_bsr(rng, bs, mb, kb, sorted_cols=True):
     """Block rows in runs that share block columns (neighbouring rows of a
     community), power-law lengths from empty to past several merge batches,
