@@ -1042,7 +1042,9 @@ def run_bsr(args, W, world, rank, dev, dist):
     active_pairs = int(torch.unique(((d_r // bs) * mb + d_c // bs) * (bs // 2) +
                                     (d_c % bs) % (bs // 2)).numel())
     # bs 64 streams 32 x 32 sub-blocks: nonzero columns per 32-row half
-    active_cols32 = int(torch.unique((d_r // 32) * n + d_c).numel()) if bs == 64 else active_cols
+    # (and bs 2 / 4 / 8: the grouped MFMA stream's union over 32-row groups)
+    active_cols32 = (int(torch.unique((d_r // 32) * n + d_c).numel()) if bs in (2, 4, 8, 64)
+                     else active_cols)
     b_rows = int(torch.unique(d_c).numel())  # distinct B rows the product touches
     del d_r, d_c
     # output columns per workgroup (bs 32: 128; bs 16: 256)
@@ -1056,6 +1058,11 @@ def run_bsr(args, W, world, rank, dev, dist):
         mfma_flops = active_cols * 2.0 * bs * K
     elif cm and bs == 64:
         # the same per nonzero column of a 32 x 32 sub-block
+        mfma_flops = active_cols32 * 2.0 * 32 * K
+    elif bs in (2, 4, 8) and dt == "fp32":
+        # the grouped small-bs stream (bsr_small_grp_kernel, when its sharing probe keeps the
+        # matrix, as on the reddit stand-in): two v_mfma_f32_32x32x1_2b_f32 per (32-row
+        # group, nonzero column) of the union and 128 output columns
         mfma_flops = active_cols32 * 2.0 * 32 * K
     elif cs16:
         # column stream: items of 16 nonzero columns packed across blocks, one
@@ -1138,10 +1145,12 @@ def run_bsr(args, W, world, rank, dev, dist):
                       "SURVEY 8d full-panel model"),
                   "upper_GBps": round(cm_bytes / t / 1e9, 1),
                   "traffic_key": tkey,
-                  "mfma_executed_flops_per_launch": mfma_flops if bs >= 16 else None,
-                  "mfma_executed_TFLOPs": round(mfma_flops / t / 1e12, 2) if bs >= 16 else None,
+                  "mfma_executed_flops_per_launch": mfma_flops if bs >= 16 or dt == "fp32" else None,
+                  "mfma_executed_TFLOPs": (round(mfma_flops / t / 1e12, 2)
+                                           if bs >= 16 or dt == "fp32" else None),
                   "mfma_peak": peak,
-                  "mfma_frac": round(mfma_flops / t / 1e12 / peak, 4) if bs >= 16 else None,
+                  "mfma_frac": (round(mfma_flops / t / 1e12 / peak, 4)
+                                if bs >= 16 or dt == "fp32" else None),
                   "dense_block_equivalent_TFLOPs": round(dense_flops / t / 1e12, 2),
                   "full_panel_model_bytes_per_launch": kbytes,
                   "full_panel_model_GBps": round(kbytes / t / 1e9, 1)},
