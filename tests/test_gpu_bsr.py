@@ -1065,6 +1065,40 @@ def test_small_bs_grouped_stream_bit_exact(oracle, device, bs, direction, n, oc)
         assert (got == want).all(), f"bs {bs}: {int((got != want).sum())} elements differ"
 
 
+@pytest.mark.parametrize("bs", [2, 8])
+@pytest.mark.parametrize("n,ldb,ldc,order_b", [(4, 4, 4, 0), (68, 72, 76, 0), (200, 200, 204, 0),
+                                               (132, 0, 132, 1)])
+def test_small_bs_grouped_shapes(oracle, device, bs, n, ldb, ldc, order_b):
+    """The grouped small-bs stream at output widths that are not a whole 128-column
+    tile (4, 68, 200, 132), with leading dimensions past n and a column-major B
+    (staged row-major first): bit-exact with the sequential oracle."""
+    ops = _ops()
+    h = _grouped_handle()
+    rng = np.random.default_rng(31 * bs + n)
+    G = 32 // bs
+    mb, kb = 3 * G + 1, 70
+    rp, ci, vb = _grouped_small_bsr(rng, bs, mb, kb)
+    v = vb.reshape(-1)
+    k = kb * bs
+    B = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    if order_b == 0:
+        Bd = np.zeros((k, ldb), np.float32)
+        Bd[:, :n] = B
+        ldbx = ldb
+    else:
+        Bd = np.ascontiguousarray(B.T)
+        ldbx = k
+    drp, dci, dv, dB = _dev(rp, ci, v, Bd.reshape(-1))
+    m = mb * bs
+    dC = torch.full((m * ldc,), float("nan"), device=device)
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=ldbx, C=dC, ldc=ldc,
+              order_b=ops.ORDER_COL if order_b else ops.ORDER_ROW, handle=h)
+    torch.cuda.synchronize()
+    want = oracle_bsrmm_f32(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0).reshape(m, n)
+    got = dC.cpu().numpy().reshape(m, ldc)[:, :n]
+    assert (got == want).all(), f"bs {bs} n {n}: {int((got != want).sum())} elements differ"
+
+
 @pytest.mark.parametrize("bs", [2, 4, 8])
 def test_small_bs_grouped_mixed_sharing(oracle, device, bs):
     """Groups whose block rows share their block columns stay on the grouped
