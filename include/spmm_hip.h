@@ -316,7 +316,9 @@ spmm_status_t spmm_bsrmm_analysed_f16(spmm_handle_t handle, int mb, int kb, int 
  * spmm_bsr16_group_release or another analysis into the same buffer).
  * INVALID_VALUE for a bad dir / groupRows, negative sizes, null pointers that
  * are needed, a row pointer that does not run 0 .. nnzb, a negative block
- * column, or a short buffer; NOT_SUPPORTED past 2^31 - 1 items. */
+ * column, block columns not strictly increasing within a block row (sorted,
+ * no duplicates, as the csr2bsr output), or a short buffer; NOT_SUPPORTED
+ * past 2^31 - 1 items. */
 spmm_status_t spmm_bsr16_group_analysis_f16(spmm_handle_t handle, spmm_direction_t dir, int mb,
                                             int nnzb, int groupRows, const int* bsrRowPtr,
                                             const int* bsrColInd, const uint16_t* bsrVal,

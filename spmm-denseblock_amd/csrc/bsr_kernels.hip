@@ -4205,183 +4205,6 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
   return from_hip(hipGetLastError());
 }
 
-// ---------------------------------------------------------------------------
-// The group analysis on the device (spmm_bsr16_group_analysis_f16 /
-// spmm_bsr32_group_analysis_f32): one thread per group of W block
-// rows merges their sorted block-column lists and walks the union of the column
-// masks per block column J in (J, c) order. PASS 1 counts the group's items (E
-// entries each, the last padded) and records its largest block column (INT_MIN: a
-// negative block column or a decreasing row pointer in the group); PASS 2, with
-// the item pointers, writes each entry's B row (J * BS + c, -1: padding), per
-// wave the block holding it (-1: none; BS 32 also -1 where that block's column c
-// is all zeros) and, at BS 32, the per-(item, wave) masks of held entries.
-// ---------------------------------------------------------------------------
-template <int W, int BS, bool PASS2>
-__global__ __launch_bounds__(256) void grp_build_kernel(int mb, int nnzb, int ngroups,
-                                                        const int* __restrict__ rp,
-                                                        const int* __restrict__ ci,
-                                                        const unsigned* __restrict__ mk,
-                                                        int* __restrict__ cnt, int* __restrict__ maxj,
-                                                        const int* __restrict__ item_ptr,
-                                                        int* __restrict__ rows, int* __restrict__ src,
-                                                        unsigned* __restrict__ wmask) {
-  constexpr unsigned kAll = BS == 32 ? 0xffffffffu : 0xffffu;
-  constexpr int E = BS == 16 ? 16 : 8;
-  constexpr bool HELD = true;  // per-(item, wave) held-entry masks at both block sizes
-  const int g = blockIdx.x * 256 + threadIdx.x;
-  if (g >= ngroups) return;
-  int cur[W], end[W];
-  // the row pointer is checked here, before it indexes the block columns: within
-  // [0, nnzb], never decreasing, rp[0] = 0 and rp[mb] = nnzb (a group with a bad
-  // row walks nothing and reports INT_MIN)
-  bool bad = (g == 0 && rp[0] != 0) || (g == ngroups - 1 && rp[mb] != nnzb);
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    const int br = g * W + w;
-    cur[w] = br < mb ? rp[br] : 0;
-    end[w] = br < mb ? rp[br + 1] : 0;
-    bad |= end[w] < cur[w] || cur[w] < 0 || end[w] > nnzb;
-  }
-  if (bad) {
-#pragma unroll
-    for (int w = 0; w < W; ++w) end[w] = cur[w] = 0;
-  }
-  long long e = 0;  // entries so far
-  int hi = -1;
-  const size_t base = PASS2 ? (size_t)item_ptr[g] * E : 0;
-  unsigned wm[W];
-#pragma unroll
-  for (int w = 0; w < W; ++w) wm[w] = 0u;
-  auto entry = [&](int row, const int (&kw)[W], const unsigned (&mw)[W], int c) {
-    if constexpr (PASS2) {
-      const size_t x = base + (size_t)e;
-      rows[x] = row;
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const int s = row < 0 || (HELD && !((mw[w] >> c) & 1u)) ? -1 : kw[w];
-        src[x * W + w] = s;
-        if (HELD && s >= 0) wm[w] |= 1u << (int)(e % E);
-      }
-      if (HELD && e % E == E - 1) {
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          wmask[(x / E) * W + w] = wm[w];
-          wm[w] = 0u;
-        }
-      }
-    }
-    ++e;
-  };
-  for (;;) {
-    int J = -1;
-#pragma unroll
-    for (int w = 0; w < W; ++w)
-      if (cur[w] < end[w] && (J < 0 || ci[cur[w]] < J)) J = ci[cur[w]];
-    if (J < 0) {  // the end, or a negative block column ahead
-#pragma unroll
-      for (int w = 0; w < W; ++w) bad |= cur[w] < end[w];
-      break;
-    }
-    hi = max(hi, J);
-    unsigned u = 0;
-    int kw[W];
-    unsigned mw[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      kw[w] = -1;
-      mw[w] = 0u;
-      if (cur[w] < end[w] && ci[cur[w]] == J) {
-        kw[w] = cur[w];
-        mw[w] = mk[cur[w]] & kAll;
-        u |= mw[w];
-        ++cur[w];
-      }
-    }
-    while (u) {
-      const int c = __builtin_ctz(u);
-      u &= u - 1u;
-      entry(J * BS + c, kw, mw, c);
-    }
-  }
-  {
-    int kw[W];
-    unsigned mw[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      kw[w] = -1;
-      mw[w] = 0u;
-    }
-    while (e % E) entry(-1, kw, mw, 0);
-  }
-  if constexpr (!PASS2) {
-    const long long items = e / E;
-    cnt[g] = items > INT_MAX ? INT_MAX : (int)items;
-    maxj[g] = bad ? INT_MIN : hi;
-  }
-}
-
-spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int mb, int nnzb,
-                               int ngroups, const int* rp, const int* ci, const unsigned* mk,
-                               int* cnt, int* maxj, const int* item_ptr, int* rows, int* src,
-                               unsigned* wmask) {
-  if (ngroups == 0) return SPMM_STATUS_SUCCESS;
-  const dim3 grid((ngroups + 255) / 256);
-#define GRP_BUILD(W_, BS_)                                                                       \
-  do {                                                                                           \
-    if (pass2)                                                                                   \
-      hipLaunchKernelGGL((grp_build_kernel<W_, BS_, true>), grid, dim3(256), 0, ctx->stream, mb, \
-                         nnzb, ngroups, rp, ci, mk, cnt, maxj, item_ptr, rows, src, wmask);       \
-    else                                                                                         \
-      hipLaunchKernelGGL((grp_build_kernel<W_, BS_, false>), grid, dim3(256), 0, ctx->stream,    \
-                         mb, nnzb, ngroups, rp, ci, mk, cnt, maxj, item_ptr, rows, src, wmask);  \
-  } while (0)
-  if (BS == 16) {
-    if (W == 8) GRP_BUILD(8, 16);
-    else if (W == 4) GRP_BUILD(4, 16);
-    else GRP_BUILD(2, 16);
-  } else {
-    if (W == 4) GRP_BUILD(4, 32);
-    else GRP_BUILD(2, 32);
-  }
-#undef GRP_BUILD
-  return from_hip(hipGetLastError());
-}
-
-// One workgroup: stats[0] = max maxj (-1 when n = 0), stats[1] = any INT_MIN.
-__global__ __launch_bounds__(1024) void grp_stats_kernel(const int* __restrict__ maxj, int n,
-                                                         int* __restrict__ stats) {
-  __shared__ int smax[16], sbad[16];
-  int hi = -1, bad = 0;
-  for (int i = threadIdx.x; i < n; i += 1024) {
-    const int x = maxj[i];
-    bad |= x == INT_MIN;
-    hi = max(hi, x);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    hi = max(hi, __shfl_xor(hi, o));
-    bad |= __shfl_xor(bad, o);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    smax[threadIdx.x >> 6] = hi;
-    sbad[threadIdx.x >> 6] = bad;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < 16; ++w) {
-      hi = max(hi, smax[w]);
-      bad |= sbad[w];
-    }
-    stats[0] = hi;
-    stats[1] = bad;
-  }
-}
-
-spmm_status_t launch_grp_stats(spmm_context* ctx, const int* maxj, int n, int* stats) {
-  hipLaunchKernelGGL(grp_stats_kernel, dim3(1), dim3(1024), 0, ctx->stream, maxj, n, stats);
-  return from_hip(hipGetLastError());
-}
-
 spmm_status_t launch_bsr16_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
                                     const int* rows, const int* src, const uint16_t* val,
                                     unsigned* afrag) {

@@ -173,11 +173,13 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
                                        const unsigned* wmask, const unsigned* afrag,
                                        const uint16_t* B16, int ldb, float alpha, float beta,
                                        float* C, int ldc, bool crow);
-// the group analyses' device merge (grp_build_kernel: PASS 1 checks the row pointer
-// and counts, PASS 2 writes)
+// the group analyses' device merge (group_kernels.hip; grp_build_kernel: PASS 1 checks
+// the row pointer and the block columns and counts, PASS 2 writes the entries), the
+// per-(item, wave) masks of held entries from the written sources
 spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int mb, int nnzb,
                                int ngroups, const int* rp, const int* ci, const unsigned* mk,
-                               int* cnt, int* maxj, const int* item_ptr, int* rows, int* src,
+                               int* cnt, int* maxj, const int* item_ptr, int* rows, int* src);
+spmm_status_t launch_grp_wmask(spmm_context* ctx, long long nitems, int W, int E, const int* src,
                                unsigned* wmask);
 // stats[0] = max over maxj[0..n), stats[1] = 1 if any maxj is INT_MIN (pass 1's "bad")
 spmm_status_t launch_grp_stats(spmm_context* ctx, const int* maxj, int n, int* stats);

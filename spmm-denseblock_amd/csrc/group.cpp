@@ -8,19 +8,19 @@
 //  size query (buffer == NULL):
 //  1. the device computes every block's column mask (bsr16 / bsr32_analysis_kernel,
 //     masks only);
-//  2. grp_build_kernel PASS 1, one thread per group of W adjacent block rows, checks
-//     the group's row pointer entries, merges the W sorted block-column lists and
-//     counts the items of the union of their nonzero columns in (block column J,
-//     column c) order, cut into items of E entries (16 at bs 16, 8 at bs 32; the
-//     last one padded with row -1);
+//  2. grp_build_kernel PASS 1 (group_kernels.hip), one wave per group of W adjacent
+//     block rows, checks the group's row pointer entries and block columns, merges
+//     the W sorted block-column lists and counts the items of the union of their
+//     nonzero columns in (block column J, column c) order, cut into items of E
+//     entries (16 at bs 16, 8 at bs 32; the last one padded with row -1);
 //  3. a one-workgroup scan sums the counts into the item pointers, a reduction
 //     finds the largest block column and any bad group; 16 bytes come back to the
 //     host (the analysis's one synchronisation) and size the buffer;
 //  filling call (the caller's buffer, same arguments):
 //  4. PASS 2 writes the B row J*bs + c of each entry and, per wave w of the group,
-//     the block of row w holding block column J (-1: none; at bs 32 also -1 when
-//     that block's column c is all zeros, plus the per-(item, wave) mask of the
-//     entries whose source is a block: the MFMAs that wave runs);
+//     the block of row w holding (J, c) (-1: none, or that block's column c is all
+//     zeros); grp_wmask_kernel then ORs the per-(item, wave) masks of the entries
+//     whose source is a block (the MFMAs that wave runs at bs 32);
 //  5. the fill kernels write each wave's A fragment of each item.
 // The filling call reuses the size query's device results (handle->grp_pending):
 // the arrays must not change between the two calls, as between cuSPARSE's
@@ -136,7 +136,7 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
       if (mb > 0) {
         if (spmm_status_t s = launch_grp_build(handle, cand[i], BS, false, mb, nnzb, ng, bsrRowPtr,
                                                bsrColInd, dmk, dcnt, dmaxj, nullptr, nullptr,
-                                               nullptr, nullptr))
+                                               nullptr))
           return s;
         if (spmm_status_t s = launch_scan_counts(handle, dcnt, ng, dptr, dtot)) return s;
         if (spmm_status_t s = launch_grp_stats(handle, dmaxj, ng, dstat)) return s;
@@ -225,7 +225,10 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
     if (spmm_status_t s = launch_grp_build(handle, W, BS, true, mb, nnzb, ngroups, bsrRowPtr,
                                            bsrColInd, reinterpret_cast<const unsigned*>(pb), nullptr,
                                            nullptr, reinterpret_cast<const int*>(buf + 256), drows,
-                                           dsrc, reinterpret_cast<unsigned*>(buf + pend.wmask_off)))
+                                           dsrc))
+      return s;
+    if (spmm_status_t s = launch_grp_wmask(handle, nitems, W, E, dsrc,
+                                           reinterpret_cast<unsigned*>(buf + pend.wmask_off)))
       return s;
     spmm_status_t s = BS == 16
         ? launch_bsr16_grp_fill(handle, nitems, W, dir, drows, dsrc,

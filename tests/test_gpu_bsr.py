@@ -1552,6 +1552,100 @@ def test_group_analysis_layout(device, bs, W):
     grp.close()
 
 
+def _long_row_bsr(rng, mb, kb, bs, lengths):
+    """Block rows of the given lengths (block columns drawn sorted from kb) whose
+    blocks hold a random set of nonzero columns (about 30 %, none in some blocks)."""
+    counts = rng.choice(lengths, mb)
+    rp = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    ci = np.concatenate([np.sort(rng.choice(kb, c, replace=False)) for c in counts] +
+                        [np.zeros(0, np.int64)]).astype(np.int32)
+    nnzb = int(rp[-1])
+    active = rng.random((nnzb, bs)) < 0.3
+    active[::7] = False  # explicit all-zero blocks
+    v = rng.uniform(-1, 1, (nnzb, bs, bs)) * (rng.random((nnzb, bs, bs)) < 0.3)
+    v[np.arange(nnzb)[:, None], rng.integers(bs, size=(nnzb, bs)), np.arange(bs)[None, :]] = 0.5
+    v = (v * active[:, None, :]).astype(np.float32)  # ROW blocks: [block][row][column]
+    return rp, ci, v.reshape(-1), active
+
+
+@pytest.mark.parametrize("bs,W", [(16, 2), (16, 4), (16, 8), (32, 2), (32, 4)])
+def test_group_analysis_layout_long_rows(device, bs, W):
+    """The device merge (group_kernels.hip, one wave per group, windows of 64 / W block
+    columns per row) on rows far longer than a window and of very different lengths in
+    one group (0 .. 600 blocks): item pointers, entry rows and the per-(item, wave) held
+    masks equal the numpy restatement of the grouping."""
+    ops = _ops()
+    rng = np.random.default_rng(7 * bs + W)
+    mb, kb = 37, 600
+    rp, ci, v, active = _long_row_bsr(rng, mb, kb, bs, [0, 1, 3, 17, 40, 200, 600])
+    E = 16 if bs == 16 else 8
+    vv = v.astype(np.float16) if bs == 16 else v
+    ngroups = (mb + W - 1) // W
+    want_ptr, want_rows, want_wm = [0], [], []
+    for g in range(ngroups):
+        held = []
+        for br in range(g * W, g * W + W):
+            h = set()
+            if br < mb:
+                for k in range(rp[br], rp[br + 1]):
+                    h.update(int(ci[k]) * bs + int(c) for c in np.nonzero(active[k])[0])
+            held.append(h)
+        ent = sorted(set().union(*held))
+        ent += [-1] * (-len(ent) % E)
+        for it in range(len(ent) // E):
+            for w in range(W):
+                want_wm.append(sum(1 << e for e in range(E) if ent[it * E + e] in held[w]))
+        want_rows += ent
+        want_ptr.append(want_ptr[-1] + len(ent) // E)
+    drp, dci, dv = _dev(rp, ci, vv)
+    G = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
+    grp = G(drp, dci, dv, mb=mb, group_rows=W)
+    buf = grp.buffer.cpu().numpy()
+    ptr = buf[256:256 + 4 * (ngroups + 1)].view(np.int32)
+    assert np.array_equal(ptr, np.array(want_ptr, np.int32)), "item pointers"
+    rows_off = (256 + 4 * (ngroups + 1) + 255) // 256 * 256
+    got_rows = buf[rows_off:rows_off + 4 * len(want_rows)].view(np.int32)
+    assert np.array_equal(got_rows, np.array(want_rows, np.int32)), "entry rows"
+    wm_off = (rows_off + 4 * len(want_rows) + 255) // 256 * 256
+    got_wm = buf[wm_off:wm_off + 4 * len(want_wm)].view(np.uint32)
+    assert np.array_equal(got_wm, np.array(want_wm, np.uint32)), "held-entry masks"
+    grp.close()
+
+
+@pytest.mark.parametrize("bs", [16, 32])
+@pytest.mark.parametrize("fault", ["duplicate", "descending", "negative"])
+def test_group_analysis_rejects_unsorted_block_columns(device, bs, fault):
+    """Block columns must be strictly increasing within a block row (include/spmm_hip.h):
+    a duplicate, a descending pair (within a merge window and across windows) or a
+    negative block column is INVALID_VALUE from the size query, with no fault; the same
+    handle then analyses the good matrix."""
+    from spmm_hip._lib import INVALID_VALUE, SpmmError
+    ops = _ops()
+    rng = np.random.default_rng(31 + bs)
+    mb, kb = 9, 300
+    rp, ci, v, _ = _long_row_bsr(rng, mb, kb, bs, [120])
+    vv = v.astype(np.float16) if bs == 16 else v
+    G = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
+    h = ops.Handle()
+    for at in (5, 32, 100):  # inside the first window, at a window edge, past it
+        b = ci.copy()
+        k = int(rp[4]) + at
+        if fault == "duplicate":
+            b[k] = b[k - 1]
+        elif fault == "descending":
+            b[k - 1], b[k] = b[k], b[k - 1]
+        else:
+            b[k] = -3
+        drp, dci, dv = _dev(rp, b, vv)
+        with pytest.raises(SpmmError) as e:
+            G(drp, dci, dv, mb=mb, handle=h)
+        assert e.value.status == INVALID_VALUE
+    drp, dci, dv = _dev(rp, ci, vv)
+    G(drp, dci, dv, mb=mb, handle=h).close()
+    torch.cuda.synchronize()
+    h.close()
+
+
 @pytest.mark.parametrize("bs", [16, 32])
 def test_group_analysis_row_pointer_checked_on_device(device, bs):
     """The group analysis checks the row pointer on the device (grp_build_kernel

@@ -209,7 +209,8 @@ def test_inflight_check_flags_a_spilled_load():
 import isa_store_hazard as ish  # noqa: E402
 
 _ALL_ASM = [os.path.join(PKG, "build", f"{k}-hip-amdgcn-amd-amdhsa-gfx950.s")
-            for k in ("csr_kernels", "bsr_kernels", "convert_kernels", "f64_kernels")]
+            for k in ("csr_kernels", "bsr_kernels", "convert_kernels", "f64_kernels",
+                      "group_kernels")]
 
 
 def test_no_store_data_hazard_in_shipped_code():
