@@ -884,7 +884,7 @@ __global__ __launch_bounds__(256) void bsr32_analysis_kernel(int nnzb, int rowdi
 // 4 halves of each. ROW: lane (r = L / 4, q = L % 4) holds row r, columns 4q ..
 // 4q + 3, and writes them to the column-major copy; COLUMN: lane L holds column
 // L / 4, rows 4 (L % 4) .. + 3.
-constexpr int kAna16Bpw = 4;
+constexpr int kAna16Bpw = 8;
 
 __global__ __launch_bounds__(256) void bsr16_analysis_kernel(int nnzb, int rowdir,
                                                              const uint16_t* __restrict__ val,
@@ -3304,60 +3304,6 @@ void bsr16_f16_grp_kernel(
   }
 }
 
-// A fragments of the grouped stream (the device half of the group analysis):
-// one wave per kGrpFillFpw consecutive (item, wave of the group) fragments; lane
-// (g, r) gets A[r][entries 4g .. 4g + 3] of that wave's block row, src[item][e][w]
-// the block holding entry e (-1: none, zero), entry e's column rows[item][e] & 15
-// (-1: padding, zero). Every load is issued unconditionally (an absent entry reads
-// val[0] and is zeroed after), so a wave's gathers for all its fragments are in
-// flight together: one fragment per wave left the kernel latency-bound.
-constexpr int kGrpFillFpw = 4;
-
-__global__ __launch_bounds__(256) void bsr16_grp_fill_kernel(long long nwork, int W, int rowdir,
-                                                             const int* __restrict__ rows,
-                                                             const int* __restrict__ src,
-                                                             const uint16_t* __restrict__ val,
-                                                             unsigned* __restrict__ afrag) {
-  const int lane = threadIdx.x & 63;
-  const long long wk0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kGrpFillFpw;
-  if (wk0 >= nwork) return;
-  const long long item0 = wk0 / W;
-  const int w0 = (int)(wk0 - item0 * W);
-  const int g = lane >> 4, r = lane & 15;
-  int row[kGrpFillFpw][4], k[kGrpFillFpw][4];
-#pragma unroll
-  for (int f = 0; f < kGrpFillFpw; ++f) {
-    // fragment wk0 + f (past the end: wk0 again, loaded and not stored)
-    const int wf = w0 + (wk0 + f < nwork ? f : 0);
-    const long long item = item0 + wf / W;
-    const int w = wf % W;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = 4 * g + q;
-      row[f][q] = rows[item * 16 + e];
-      k[f][q] = src[(item * 16 + e) * W + w];
-    }
-  }
-  unsigned short h[kGrpFillFpw][4];
-#pragma unroll
-  for (int f = 0; f < kGrpFillFpw; ++f)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool ok = row[f][q] >= 0 && k[f][q] >= 0;
-      const int c = row[f][q] & 15;
-      const size_t x = ok ? (size_t)k[f][q] * 256 + (rowdir ? r * 16 + c : c * 16 + r) : 0;
-      h[f][q] = val[x];
-      if (!ok) h[f][q] = 0;
-    }
-#pragma unroll
-  for (int f = 0; f < kGrpFillFpw; ++f) {
-    if (wk0 + f >= nwork) break;
-    unsigned* dst = afrag + (size_t)(wk0 + f) * 128 + 2 * lane;
-    dst[0] = (unsigned)h[f][0] | ((unsigned)h[f][1] << 16);
-    dst[1] = (unsigned)h[f][2] | ((unsigned)h[f][3] << 16);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // bs = 32 fp32, GROUPED item stream (spmm_bsr32_group_analysis_f32 once per
 // matrix + spmm_bsrmm_grouped_f32; row-major B and C, K tiles of 128). The bs 16
@@ -3567,54 +3513,6 @@ void bsr32_f32_grp_kernel(
       for (int i = 0; i < 4; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
     }
     *p = v;
-  }
-}
-
-// A fragments of the grouped bs 32 stream: one wave per kGrpFillFpw consecutive (item,
-// wave of the group) fragments, loads issued unconditionally as at bs 16; lane L writes
-// A[j = L / 2][entries 4 (L & 1) .. + 3] of that wave's block row, src[item][e][w] the
-// block holding entry e (-1: none, zero), entry e's column rows[item][e] & 31 (-1:
-// padding, zero). Layout per (item, wave): [32 rows][8 entries] floats.
-__global__ __launch_bounds__(256) void bsr32_grp_fill_kernel(long long nwork, int W, int rowdir,
-                                                             const int* __restrict__ rows,
-                                                             const int* __restrict__ src,
-                                                             const float* __restrict__ val,
-                                                             float* __restrict__ afrag) {
-  const int lane = threadIdx.x & 63;
-  const long long wk0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kGrpFillFpw;
-  if (wk0 >= nwork) return;
-  const long long item0 = wk0 / W;
-  const int w0 = (int)(wk0 - item0 * W);
-  const int r = lane >> 1, e0 = 4 * (lane & 1);
-  int row[kGrpFillFpw][4], k[kGrpFillFpw][4];
-#pragma unroll
-  for (int f = 0; f < kGrpFillFpw; ++f) {
-    // fragment wk0 + f (past the end: wk0 again, loaded and not stored)
-    const int wf = w0 + (wk0 + f < nwork ? f : 0);
-    const long long item = item0 + wf / W;
-    const int w = wf % W;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = e0 + q;
-      row[f][q] = rows[item * 8 + e];
-      k[f][q] = src[(item * 8 + e) * W + w];
-    }
-  }
-  f32x4 v[kGrpFillFpw];
-#pragma unroll
-  for (int f = 0; f < kGrpFillFpw; ++f)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool ok = row[f][q] >= 0 && k[f][q] >= 0;
-      const int c = row[f][q] & 31;
-      const size_t x = ok ? (size_t)k[f][q] * 1024 + (rowdir ? r * 32 + c : c * 32 + r) : 0;
-      v[f][q] = val[x];
-      if (!ok) v[f][q] = 0.f;
-    }
-#pragma unroll
-  for (int f = 0; f < kGrpFillFpw; ++f) {
-    if (wk0 + f >= nwork) break;
-    *reinterpret_cast<f32x4*>(afrag + (size_t)(wk0 + f) * 256 + 8 * r + e0) = v[f];
   }
 }
 
@@ -4202,32 +4100,6 @@ spmm_status_t launch_bsrmm_f16(spmm_context* ctx, spmm_direction_t dir, int mb, 
                        rowd, rowptr, colind, val, B, ldb, brow, alpha, beta, C, ldc, crow);
   }
   timing_end(ctx, slot);
-  return from_hip(hipGetLastError());
-}
-
-spmm_status_t launch_bsr16_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
-                                    const int* rows, const int* src, const uint16_t* val,
-                                    unsigned* afrag) {
-  const long long nwork = nitems * W;
-  if (nwork == 0) return SPMM_STATUS_SUCCESS;
-  const long long per_block = 4 * kGrpFillFpw;  // 4 waves, kGrpFillFpw fragments each
-  hipLaunchKernelGGL(bsr16_grp_fill_kernel, dim3((unsigned)((nwork + per_block - 1) / per_block)),
-                     dim3(256), 0,
-                     ctx->stream, nwork, W, dir == SPMM_DIRECTION_ROW ? 1 : 0, rows, src, val,
-                     afrag);
-  return from_hip(hipGetLastError());
-}
-
-spmm_status_t launch_bsr32_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
-                                    const int* rows, const int* src, const float* val,
-                                    float* afrag) {
-  const long long nwork = nitems * W;
-  if (nwork == 0) return SPMM_STATUS_SUCCESS;
-  const long long per_block = 4 * kGrpFillFpw;  // 4 waves, kGrpFillFpw fragments each
-  hipLaunchKernelGGL(bsr32_grp_fill_kernel, dim3((unsigned)((nwork + per_block - 1) / per_block)),
-                     dim3(256), 0,
-                     ctx->stream, nwork, W, dir == SPMM_DIRECTION_ROW ? 1 : 0, rows, src, val,
-                     afrag);
   return from_hip(hipGetLastError());
 }
 

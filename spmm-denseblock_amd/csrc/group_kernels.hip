@@ -1,5 +1,6 @@
-// group_kernels.hip — the device merge of the group analyses (spmm_bsr16_group_analysis_f16
-// / spmm_bsr32_group_analysis_f32, group.cpp; DESIGN.md §4, "The grouped stream").
+// group_kernels.hip — the device merge and the bs 32 A-fragment fill of the group analyses
+// (spmm_bsr16_group_analysis_f16 / spmm_bsr32_group_analysis_f32, group.cpp; DESIGN.md §4,
+// "The grouped stream").
 //
 // A group is W adjacent block rows. Its entries are the union of the rows' nonzero block
 // columns, each block column J expanded to the columns c its holders' column masks mark,
@@ -26,10 +27,13 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdint>
 
 #include "context.hpp"
 
 namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
 #pragma unroll
@@ -226,6 +230,190 @@ __global__ __launch_bounds__(256) void grp_wmask_kernel(long long nwork, int W,
   wmask[t] = m;
 }
 
+// A fragments of the grouped bs 32 stream (layout per (item, wave w): [32 rows][8 entries]
+// fp32, A[row][entry] of block row w of the group; zero where src = -1). One wave per run of
+// kFill32Items consecutive items of one w: its 64 entries (lane t: item t / 8, entry t % 8)
+// name the blocks holding them; each distinct block is read once, whole and coalesced (lane
+// (j, h): row j, columns 16h .. 16h + 15 of a ROW block; column j, rows 16h .. of a COLUMN
+// block; the next block's loads in flight while this one is placed), transposed into LDS
+// (column c at c * 33, conflict-free) and its entries' columns copied into the run's
+// fragments in LDS, which go out as 1-KB coalesced stores. Round 4's form gathered each
+// entry's column straight from the block (32 lines of 128 B for 128 B), L2-bound: 1.8 ms
+// on the reddit stand-in.
+constexpr int kFill32Items = 8;
+constexpr int kFill32Ring = 3;
+
+__global__ __launch_bounds__(64) void bsr32_grp_fill_kernel(long long nitems, int W, int rowdir,
+                                                            const int* __restrict__ rows,
+                                                            const int* __restrict__ src,
+                                                            const float* __restrict__ val,
+                                                            float* __restrict__ afrag) {
+  __shared__ float blk[32 * 33];                      // [column][row], padded
+  __shared__ f32x4 frag[kFill32Items * 256 / 4];      // [item][row][entry]
+  const int lane = threadIdx.x;
+  const long long u = blockIdx.x;
+  const int w = (int)(u % W);
+  const long long item0 = (u / W) * kFill32Items;
+  const int nf = (int)min((long long)kFill32Items, nitems - item0);
+  const long long it = item0 + (lane >> 3);
+  const int row = it < nitems ? rows[it * 8 + (lane & 7)] : -1;
+  const int k = row >= 0 ? src[(it * 8 + (lane & 7)) * W + w] : -1;
+  const int c = row & 31;
+#pragma unroll
+  for (int q = 0; q < kFill32Items; ++q) frag[q * 64 + lane] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int j = lane >> 1, h = lane & 1;
+  const size_t off = (size_t)j * 32 + 16 * h;  // 16 floats: row (ROW) or column (COLUMN) j
+  // their LDS places: ROW A[j][16h + i] -> column 16h + i; COLUMN A[16h + i][j] -> column j
+  const int pbase = rowdir ? 16 * h * 33 + j : j * 33 + 16 * h, pstep = rowdir ? 33 : 1;
+  // a ring of kFill32Ring blocks in flight: slot s is placed, then refilled with the next
+  // block not yet issued (static slot indices: no register moves wait on a load)
+  f32x4 ring[kFill32Ring][4];
+  int rb[kFill32Ring];
+  unsigned long long unissued = __builtin_amdgcn_ballot_w64(k >= 0);
+  // every slot loads unconditionally (one resource per block; none left: an offset past
+  // its end, zeros without a memory access), so the counted waits stay exact
+  auto issue = [&](int s) {
+    rb[s] = unissued ? __builtin_amdgcn_readlane(k, __builtin_ctzll(unissued)) : -1;
+    unissued &= ~__builtin_amdgcn_ballot_w64(k == rb[s]);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(val + (size_t)max(rb[s], 0) * 1024), 0, 4096, 0x00020000);
+    const unsigned o = rb[s] >= 0 ? (unsigned)off * 4u : 0x80000000u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      ring[s][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16u * q, 0, 0));
+  };
+  auto place = [&](const f32x4 (&x)[4], int b) {
+    __syncthreads();  // the previous block's columns are read
+#pragma unroll
+    for (int i = 0; i < 16; ++i) blk[pbase + i * pstep] = x[i >> 2][i & 3];
+    __syncthreads();
+    // the block's entries, two per step: lanes 0-31 the first, 32-63 the second
+    unsigned long long todo = __builtin_amdgcn_ballot_w64(k == b);
+    while (todo) {
+      const int ta = __builtin_ctzll(todo);
+      todo &= todo - 1ull;
+      const int tb = todo ? __builtin_ctzll(todo) : -1;
+      if (tb >= 0) todo &= todo - 1ull;
+      const int t = lane < 32 ? ta : tb;
+      const int ct = __builtin_amdgcn_readlane(c, ta);
+      const int cb = tb >= 0 ? __builtin_amdgcn_readlane(c, tb) : 0;
+      if (t >= 0) {
+        const int r = lane & 31;
+        const float v = blk[(lane < 32 ? ct : cb) * 33 + r];
+        reinterpret_cast<float*>(frag)[(t >> 3) * 256 + r * 8 + (t & 7)] = v;
+      }
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < kFill32Ring; ++s) issue(s);
+  bool more = rb[0] >= 0;
+  while (more) {
+#pragma unroll
+    for (int s = 0; s < kFill32Ring; ++s) {
+      if (rb[s] < 0) {
+        more = false;
+        break;
+      }
+      place(ring[s], rb[s]);
+      issue(s);
+    }
+  }
+  __syncthreads();
+  f32x4* dst = reinterpret_cast<f32x4*>(afrag);
+  for (int f = 0; f < nf; ++f)
+    dst[((item0 + f) * W + w) * 64 + lane] = frag[f * 64 + lane];
+}
+
+// A fragments of the grouped bs 16 fp16 stream, the same way (layout per (item, wave w):
+// 128 uint32, lane l of the product's wave holding A[l & 15][4 (l >> 4) .. + 3] as fp16 x 4,
+// i.e. half 64 (e >> 2) + 4 r + (e & 3) for row r, entry e). One wave per run of
+// kFill16Items items of one w (64 entries: lane t item t / 16, entry t % 16); each distinct
+// 512-B block is read once (lane (j, q): 4 halves of row j (ROW) or column j (COLUMN) at 4q),
+// transposed into LDS (column c at c * 17 halves), and its entries' columns (16 lanes each,
+// four entries per step) placed into the run's fragments in LDS, stored 512 B at a time.
+constexpr int kFill16Items = 4;
+constexpr int kFill16Ring = 6;
+
+__global__ __launch_bounds__(64) void bsr16_grp_fill_kernel(long long nitems, int W, int rowdir,
+                                                            const int* __restrict__ rows,
+                                                            const int* __restrict__ src,
+                                                            const uint16_t* __restrict__ val,
+                                                            unsigned* __restrict__ afrag) {
+  __shared__ uint16_t blk[16 * 17];                    // [column][row], padded
+  __shared__ uint2 frag[kFill16Items * 64];            // [item][lane of the product's wave]
+  const int lane = threadIdx.x;
+  const long long u = blockIdx.x;
+  const int w = (int)(u % W);
+  const long long item0 = (u / W) * kFill16Items;
+  const int nf = (int)min((long long)kFill16Items, nitems - item0);
+  const long long it = item0 + (lane >> 4);
+  const int row = it < nitems ? rows[it * 16 + (lane & 15)] : -1;
+  const int k = row >= 0 ? src[(it * 16 + (lane & 15)) * W + w] : -1;
+  const int c = row & 15;
+#pragma unroll
+  for (int q = 0; q < kFill16Items; ++q) frag[q * 64 + lane] = uint2{0u, 0u};
+  const int j = lane >> 2, q4 = lane & 3;
+  const size_t off = (size_t)j * 16 + 4 * q4;  // 4 halves: row (ROW) or column (COLUMN) j
+  // ROW A[j][4q + i] -> column 4q + i; COLUMN A[4q + i][j] -> column j
+  const int pbase = rowdir ? 4 * q4 * 17 + j : j * 17 + 4 * q4, pstep = rowdir ? 17 : 1;
+  uint2 ring[kFill16Ring];
+  int rb[kFill16Ring];
+  unsigned long long unissued = __builtin_amdgcn_ballot_w64(k >= 0);
+  auto issue = [&](int s) {  // as at bs 32: unconditional loads
+    rb[s] = unissued ? __builtin_amdgcn_readlane(k, __builtin_ctzll(unissued)) : -1;
+    unissued &= ~__builtin_amdgcn_ballot_w64(k == rb[s]);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(val + (size_t)max(rb[s], 0) * 256), 0, 512, 0x00020000);
+    const unsigned o = rb[s] >= 0 ? (unsigned)off * 2u : 0x80000000u;
+    ring[s] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, o, 0, 0));
+  };
+  auto place = [&](uint2 x, int b) {
+    __syncthreads();  // the previous block's columns are read
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      blk[pbase + i * pstep] = (uint16_t)((i < 2 ? x.x : x.y) >> (16 * (i & 1)));
+    __syncthreads();
+    // the block's entries, four per step: lanes 16s .. 16s + 15 the s-th
+    unsigned long long todo = __builtin_amdgcn_ballot_w64(k == b);
+    while (todo) {
+      int ts[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        ts[s4] = todo ? __builtin_ctzll(todo) : -1;
+        if (todo) todo &= todo - 1ull;
+      }
+      const int s4 = lane >> 4, r = lane & 15;
+      const int t = s4 == 0 ? ts[0] : s4 == 1 ? ts[1] : s4 == 2 ? ts[2] : ts[3];
+      int cs[4];
+#pragma unroll
+      for (int x4 = 0; x4 < 4; ++x4) cs[x4] = ts[x4] >= 0 ? __builtin_amdgcn_readlane(c, ts[x4]) : 0;
+      const int ct = s4 == 0 ? cs[0] : s4 == 1 ? cs[1] : s4 == 2 ? cs[2] : cs[3];
+      if (t >= 0) {
+        const int e = t & 15;
+        reinterpret_cast<uint16_t*>(frag)[(t >> 4) * 256 + 64 * (e >> 2) + 4 * r + (e & 3)] =
+            blk[ct * 17 + r];
+      }
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < kFill16Ring; ++s) issue(s);
+  bool more = rb[0] >= 0;
+  while (more) {
+#pragma unroll
+    for (int s = 0; s < kFill16Ring; ++s) {
+      if (rb[s] < 0) {
+        more = false;
+        break;
+      }
+      place(ring[s], rb[s]);
+      issue(s);
+    }
+  }
+  __syncthreads();
+  uint2* dst = reinterpret_cast<uint2*>(afrag);
+  for (int f = 0; f < nf; ++f) dst[((item0 + f) * W + w) * 64 + lane] = frag[f * 64 + lane];
+}
+
 // One workgroup: stats[0] = max maxj (-1 when n = 0), stats[1] = any INT_MIN.
 __global__ __launch_bounds__(1024) void grp_stats_kernel(const int* __restrict__ maxj, int n,
                                                          int* __restrict__ stats) {
@@ -295,6 +483,26 @@ spmm_status_t launch_grp_wmask(spmm_context* ctx, long long nitems, int W, int E
     hipLaunchKernelGGL(grp_wmask_kernel<16>, grid, dim3(256), 0, ctx->stream, nwork, W, src, wmask);
   else
     hipLaunchKernelGGL(grp_wmask_kernel<8>, grid, dim3(256), 0, ctx->stream, nwork, W, src, wmask);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_bsr16_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
+                                    const int* rows, const int* src, const uint16_t* val,
+                                    unsigned* afrag) {
+  if (nitems == 0) return SPMM_STATUS_SUCCESS;
+  const long long units = (nitems + kFill16Items - 1) / kFill16Items * W;
+  hipLaunchKernelGGL(bsr16_grp_fill_kernel, dim3((unsigned)units), dim3(64), 0, ctx->stream, nitems,
+                     W, dir == SPMM_DIRECTION_ROW ? 1 : 0, rows, src, val, afrag);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_bsr32_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
+                                    const int* rows, const int* src, const float* val,
+                                    float* afrag) {
+  if (nitems == 0) return SPMM_STATUS_SUCCESS;
+  const long long units = (nitems + kFill32Items - 1) / kFill32Items * W;
+  hipLaunchKernelGGL(bsr32_grp_fill_kernel, dim3((unsigned)units), dim3(64), 0, ctx->stream, nitems,
+                     W, dir == SPMM_DIRECTION_ROW ? 1 : 0, rows, src, val, afrag);
   return from_hip(hipGetLastError());
 }
 

@@ -1609,7 +1609,53 @@ def test_group_analysis_layout_long_rows(device, bs, W):
     wm_off = (rows_off + 4 * len(want_rows) + 255) // 256 * 256
     got_wm = buf[wm_off:wm_off + 4 * len(want_wm)].view(np.uint32)
     assert np.array_equal(got_wm, np.array(want_wm, np.uint32)), "held-entry masks"
+    # the A fragments (fill kernels): A[r][c] of the block of row w holding (J, c), zero
+    # where that row holds no such nonzero column or the entry is padding
+    nitems = len(want_rows) // E
+    af_off = (wm_off + 4 * nitems * W + 255) // 256 * 256
+    ent = np.array(want_rows, np.int64).reshape(nitems, E)
+    item_group = np.repeat(np.arange(ngroups), np.diff(want_ptr))
+    vb = vv.reshape(-1, bs, bs)
+    where = {(br, int(ci[k])): k for br in range(mb) for k in range(rp[br], rp[br + 1])}
+    want_af = np.zeros((nitems, W, bs, E), vb.dtype)  # [item][w][row][entry]
+    for w in range(W):
+        held = np.array(want_wm, np.int64).reshape(nitems, W)[:, w]
+        for it, e in zip(*np.nonzero((held[:, None] >> np.arange(E)) & 1)):
+            J, c = divmod(int(ent[it, e]), bs)
+            want_af[it, w, :, e] = vb[where[(int(item_group[it]) * W + w, J)], :, c]
+    if bs == 32:
+        got_af = buf[af_off:af_off + 4 * want_af.size].view(np.float32).reshape(want_af.shape)
+    else:  # half 64 (e >> 2) + 4 r + (e & 3) of each (item, w)
+        raw = buf[af_off:af_off + 2 * want_af.size].view(np.float16).reshape(nitems, W, 256)
+        r_, e_ = np.meshgrid(np.arange(16), np.arange(16), indexing="ij")
+        got_af = raw[:, :, 64 * (e_ >> 2) + 4 * r_ + (e_ & 3)]
+    assert np.array_equal(got_af.view(np.uint32 if bs == 32 else np.uint16),
+                          want_af.view(np.uint32 if bs == 32 else np.uint16)), "A fragments"
     grp.close()
+
+
+@pytest.mark.parametrize("bs", [16, 32])
+def test_group_analysis_column_blocks(device, bs):
+    """A matrix given as COLUMN blocks (each block stored transposed) gives the same
+    analysis buffer, byte for byte, as the same matrix given as ROW blocks: the fill
+    kernels read either layout."""
+    from spmm_hip._lib import DIRECTION_COLUMN
+    ops = _ops()
+    rng = np.random.default_rng(55 + bs)
+    mb, kb = 21, 300
+    rp, ci, v, _ = _long_row_bsr(rng, mb, kb, bs, [0, 2, 9, 60, 150])
+    vv = v.astype(np.float16) if bs == 16 else v
+    vcol = np.ascontiguousarray(vv.reshape(-1, bs, bs).transpose(0, 2, 1)).reshape(-1)
+    G = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
+    W = 4 if bs == 16 else 2
+    drp, dci, dv = _dev(rp, ci, vv)
+    a = G(drp, dci, dv, mb=mb, group_rows=W)
+    want = a.buffer.cpu().numpy().copy()
+    a.close()
+    drp, dci, dvc = _dev(rp, ci, vcol)
+    b = G(drp, dci, dvc, mb=mb, group_rows=W, direction=DIRECTION_COLUMN)
+    assert np.array_equal(b.buffer.cpu().numpy(), want)
+    b.close()
 
 
 @pytest.mark.parametrize("bs", [16, 32])
