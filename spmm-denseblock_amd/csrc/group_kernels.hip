@@ -238,8 +238,11 @@ __global__ __launch_bounds__(256) void grp_wmask_kernel(long long nwork, int W,
 // block; the next block's loads in flight while this one is placed), transposed into LDS
 // (column c at c * 33, conflict-free) and its entries' columns copied into the run's
 // fragments in LDS, which go out as 1-KB coalesced stores. Round 4's form gathered each
-// entry's column straight from the block (32 lines of 128 B for 128 B), L2-bound: 1.8 ms
-// on the reddit stand-in.
+// entry's column straight from the block (32 lines of 128 B for 128 B used); both run
+// 1.8 ms on the reddit stand-in (3.0 on products): every held block's 4 KB are read once
+// either way and the fragments written, about 9 GB at 5 TB/s (16.6 GB at 5.4 on
+// products), so the gain is in L2 requests, not time. The bs 16 form below gained 11 %
+// (1.26 -> 1.12 ms on products).
 constexpr int kFill32Items = 8;
 constexpr int kFill32Ring = 3;
 
