@@ -241,8 +241,8 @@ __global__ __launch_bounds__(256) void grp_wmask_kernel(long long nwork, int W,
 // entry's column straight from the block (32 lines of 128 B for 128 B used); both run
 // 1.8 ms on the reddit stand-in (3.0 on products): every held block's 4 KB are read once
 // either way and the fragments written, about 9 GB at 5 TB/s (16.6 GB at 5.4 on
-// products), so the gain is in L2 requests, not time. The bs 16 form below gained 11 %
-// (1.26 -> 1.12 ms on products).
+// products), so the gain is in L2 requests, not time. At bs 16 (below) the chunked form
+// took the fill from 1.26 to 0.86 ms on products.
 constexpr int kFill32Items = 8;
 constexpr int kFill32Ring = 3;
 
@@ -327,22 +327,25 @@ __global__ __launch_bounds__(64) void bsr32_grp_fill_kernel(long long nitems, in
     dst[((item0 + f) * W + w) * 64 + lane] = frag[f * 64 + lane];
 }
 
-// A fragments of the grouped bs 16 fp16 stream, the same way (layout per (item, wave w):
-// 128 uint32, lane l of the product's wave holding A[l & 15][4 (l >> 4) .. + 3] as fp16 x 4,
-// i.e. half 64 (e >> 2) + 4 r + (e & 3) for row r, entry e). One wave per run of
-// kFill16Items items of one w (64 entries: lane t item t / 16, entry t % 16); each distinct
-// 512-B block is read once (lane (j, q): 4 halves of row j (ROW) or column j (COLUMN) at 4q),
-// transposed into LDS (column c at c * 17 halves), and its entries' columns (16 lanes each,
-// four entries per step) placed into the run's fragments in LDS, stored 512 B at a time.
+// A fragments of the grouped bs 16 fp16 stream (layout per (item, wave w): 128 uint32, lane
+// l of the product's wave holding A[l & 15][4 (l >> 4) .. + 3] as fp16 x 4, i.e. half
+// 64 (e >> 2) + 4 r + (e & 3) for row r, entry e). One wave per run of kFill16Items items of
+// one w, lane t owning entry t (item t / 16, entry t % 16). The run's distinct blocks are read
+// kFill16Chunk at a time, whole and coalesced (lane (j, q): 4 halves of row j (ROW) or column
+// j (COLUMN) at 4q), all in flight together, and transposed into LDS (column c at c * 17
+// halves); then every lane copies the 16 rows of its entry's column, if its block is in the
+// chunk, into the run's fragments in LDS, which are stored 512 B at a time. Two barriers
+// per chunk of blocks: a form that placed one block at a time (two barriers and a ballot
+// walk per block) ran 1.12 ms on the products stand-in, round 4's column gathers 1.26 ms.
 constexpr int kFill16Items = 4;
-constexpr int kFill16Ring = 6;
+constexpr int kFill16Chunk = 8;
 
 __global__ __launch_bounds__(64) void bsr16_grp_fill_kernel(long long nitems, int W, int rowdir,
                                                             const int* __restrict__ rows,
                                                             const int* __restrict__ src,
                                                             const uint16_t* __restrict__ val,
                                                             unsigned* __restrict__ afrag) {
-  __shared__ uint16_t blk[16 * 17];                    // [column][row], padded
+  __shared__ uint16_t blk[kFill16Chunk][16 * 17];      // per block: [column][row], padded
   __shared__ uint2 frag[kFill16Items * 64];            // [item][lane of the product's wave]
   const int lane = threadIdx.x;
   const long long u = blockIdx.x;
@@ -356,60 +359,43 @@ __global__ __launch_bounds__(64) void bsr16_grp_fill_kernel(long long nitems, in
 #pragma unroll
   for (int q = 0; q < kFill16Items; ++q) frag[q * 64 + lane] = uint2{0u, 0u};
   const int j = lane >> 2, q4 = lane & 3;
-  const size_t off = (size_t)j * 16 + 4 * q4;  // 4 halves: row (ROW) or column (COLUMN) j
+  const unsigned off = 2u * (unsigned)(j * 16 + 4 * q4);  // 4 halves: row (ROW) or column (COLUMN) j
   // ROW A[j][4q + i] -> column 4q + i; COLUMN A[4q + i][j] -> column j
   const int pbase = rowdir ? 4 * q4 * 17 + j : j * 17 + 4 * q4, pstep = rowdir ? 17 : 1;
-  uint2 ring[kFill16Ring];
-  int rb[kFill16Ring];
+  // this lane's entry: its 16 halves' places in the run's fragments
+  const int e = lane & 15;
+  const int fbase = (lane >> 4) * 256 + 64 * (e >> 2) + (e & 3);
   unsigned long long unissued = __builtin_amdgcn_ballot_w64(k >= 0);
-  auto issue = [&](int s) {  // as at bs 32: unconditional loads
-    rb[s] = unissued ? __builtin_amdgcn_readlane(k, __builtin_ctzll(unissued)) : -1;
-    unissued &= ~__builtin_amdgcn_ballot_w64(k == rb[s]);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t*>(val + (size_t)max(rb[s], 0) * 256), 0, 512, 0x00020000);
-    const unsigned o = rb[s] >= 0 ? (unsigned)off * 2u : 0x80000000u;
-    ring[s] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, o, 0, 0));
-  };
-  auto place = [&](uint2 x, int b) {
-    __syncthreads();  // the previous block's columns are read
+  while (unissued) {
+    int bk[kFill16Chunk];
+    uint2 x[kFill16Chunk];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      blk[pbase + i * pstep] = (uint16_t)((i < 2 ? x.x : x.y) >> (16 * (i & 1)));
-    __syncthreads();
-    // the block's entries, four per step: lanes 16s .. 16s + 15 the s-th
-    unsigned long long todo = __builtin_amdgcn_ballot_w64(k == b);
-    while (todo) {
-      int ts[4];
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        ts[s4] = todo ? __builtin_ctzll(todo) : -1;
-        if (todo) todo &= todo - 1ull;
-      }
-      const int s4 = lane >> 4, r = lane & 15;
-      const int t = s4 == 0 ? ts[0] : s4 == 1 ? ts[1] : s4 == 2 ? ts[2] : ts[3];
-      int cs[4];
-#pragma unroll
-      for (int x4 = 0; x4 < 4; ++x4) cs[x4] = ts[x4] >= 0 ? __builtin_amdgcn_readlane(c, ts[x4]) : 0;
-      const int ct = s4 == 0 ? cs[0] : s4 == 1 ? cs[1] : s4 == 2 ? cs[2] : cs[3];
-      if (t >= 0) {
-        const int e = t & 15;
-        reinterpret_cast<uint16_t*>(frag)[(t >> 4) * 256 + 64 * (e >> 2) + 4 * r + (e & 3)] =
-            blk[ct * 17 + r];
-      }
+    for (int d = 0; d < kFill16Chunk; ++d) {
+      // every slot loads (none left: an offset past the resource's end, zeros without a
+      // memory access)
+      bk[d] = unissued ? __builtin_amdgcn_readlane(k, __builtin_ctzll(unissued)) : -1;
+      unissued &= ~__builtin_amdgcn_ballot_w64(k == bk[d]);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint16_t*>(val + (size_t)max(bk[d], 0) * 256), 0, 512, 0x00020000);
+      x[d] = __builtin_bit_cast(
+          uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, bk[d] >= 0 ? off : 0x80000000u, 0, 0));
     }
-  };
+    __syncthreads();  // the previous chunk's columns are read
 #pragma unroll
-  for (int s = 0; s < kFill16Ring; ++s) issue(s);
-  bool more = rb[0] >= 0;
-  while (more) {
+    for (int d = 0; d < kFill16Chunk; ++d)
 #pragma unroll
-    for (int s = 0; s < kFill16Ring; ++s) {
-      if (rb[s] < 0) {
-        more = false;
-        break;
-      }
-      place(ring[s], rb[s]);
-      issue(s);
+      for (int i = 0; i < 4; ++i)
+        blk[d][pbase + i * pstep] = (uint16_t)((i < 2 ? x[d].x : x[d].y) >> (16 * (i & 1)));
+    __syncthreads();
+    int slot = -1;
+#pragma unroll
+    for (int d = 0; d < kFill16Chunk; ++d)
+      if (bk[d] >= 0 && k == bk[d]) slot = d;
+    if (slot >= 0) {
+      const uint16_t* col = &blk[slot][c * 17];
+      uint16_t* dst = reinterpret_cast<uint16_t*>(frag) + fbase;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[4 * r] = col[r];
     }
   }
   __syncthreads();
