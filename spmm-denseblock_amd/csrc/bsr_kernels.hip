@@ -2620,6 +2620,14 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
 #ifndef SPMM_SGRP_PROBE
 #define SPMM_SGRP_PROBE 1
 #endif
+// union steps per ring slot at bs 2 / 4 (A/B on the reddit stand-in, profiles/r05c/ab_sp/:
+// bs 4 1.50 -> 1.41 ms at 2; bs 2 2.24 -> 2.18 at 2, 2.17 at 4, 2.66 at 8 (220 registers))
+#ifndef SPMM_SGRP_SP2
+#define SPMM_SGRP_SP2 4
+#endif
+#ifndef SPMM_SGRP_SP4
+#define SPMM_SGRP_SP4 2
+#endif
 
 // The grouped stream's choice per matrix (small_grp_probe_kernel, launched before it on the
 // same stream). Block rows that share few block columns gain nothing from the union and lose
@@ -2685,6 +2693,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
   constexpr int E = BS * BS;
   constexpr int DB = SPMM_SGRP_DB;  // B rows loaded DB steps ahead of their MFMAs, A DB + 1
   constexpr int R = 4;        // ring slots: A of step s + DB + 1, B of step s + DB, MFMAs of step s
+  // union steps per ring slot: at bs 2 / 4 several steps share a slot's bookkeeping (taken in
+  // queue order, so every row still adds its (J, c) in ascending order)
+  constexpr int SP = BS == 2 ? SPMM_SGRP_SP2 : (BS == 4 ? SPMM_SGRP_SP4 : 1);
+  constexpr int SC = SP * BS;  // columns per slot
   constexpr int NQ = 128;     // union-step queue (a batch adds at most 64)
   constexpr int kNone = 0x7fffffff;
   constexpr unsigned long long kSeg = (1ull << Q) - 1;
@@ -2801,11 +2813,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
     return nun;
   };
 
-  float ar[R][BS];    // A: row gi of the block row grow's block of the step (zero: none)
-  int jr[R];          // the step's block column (uniform)
-  bool vr[R];         // the step exists (uniform)
+  float ar[R][SC];    // A: row gi of the block row grow's block of each step (zero: none)
+  int jr[R][SP];      // the steps' block columns (uniform)
+  bool vr[R];         // the slot's first step exists (uniform)
   unsigned act[R];    // active columns (uniform)
-  f32x2 bx[R][BS];    // B rows J * bs + c, this lane's two columns
+  f32x2 bx[R][SC];    // B rows J * bs + c, this lane's two columns
   // A through one buffer resource from the group's first block: a block row without the
   // step's block column reads past the resource's end, zeros without a memory access
   const int kbase = __builtin_amdgcn_readfirstlane(lp);  // lane 0: the group's first block
@@ -2814,51 +2826,58 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
       (unsigned)min((long long)(nnzb - kbase) * E * 4, 0x7fffffffLL), 0x00020000);
   const unsigned aoff = 4u * (unsigned)(ROWD ? gi * BS : gi);
   auto load_a = [&](int s) {
-    const bool v = qt < qh;
-    const int qi = qt & (NQ - 1);
-    const int J = v ? __builtin_amdgcn_readfirstlane(suj[qi]) : 0;
-    const int kb = v ? suk[qi * G + grow] : -1;
-    qt += v ? 1 : 0;
-    vr[s] = v;
-    jr[s] = J;
-    const unsigned off = kb >= 0 ? (unsigned)(kb - kbase) * (E * 4) + aoff : 0x80000000u;
-    if constexpr (ROWD && BS == 8) {
-      const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
-      const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off + 16, 0, 0));
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        ar[s][c] = x0[c];
-        ar[s][4 + c] = x1[c];
+    for (int p = 0; p < SP; ++p) {
+      const bool v = qt < qh;
+      const int qi = qt & (NQ - 1);
+      const int J = v ? __builtin_amdgcn_readfirstlane(suj[qi]) : 0;
+      const int kb = v ? suk[qi * G + grow] : -1;
+      qt += v ? 1 : 0;
+      if (p == 0) vr[s] = v;
+      jr[s][p] = J;
+      const unsigned off = kb >= 0 ? (unsigned)(kb - kbase) * (E * 4) + aoff : 0x80000000u;
+      float* a = &ar[s][p * BS];
+      if constexpr (ROWD && BS == 8) {
+        const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
+        const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off + 16, 0, 0));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          a[c] = x0[c];
+          a[4 + c] = x1[c];
+        }
+      } else if constexpr (ROWD && BS == 4) {
+        const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] = x0[c];
+      } else if constexpr (ROWD) {
+        const f32x2 x0 = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsa, off, 0, 0));
+        a[0] = x0[0];
+        a[1] = x0[1];
+      } else {
+#pragma unroll
+        for (int c = 0; c < BS; ++c)
+          a[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsa, off + 4 * c * BS, 0, 0));
       }
-    } else if constexpr (ROWD && BS == 4) {
-      const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
-#pragma unroll
-      for (int c = 0; c < 4; ++c) ar[s][c] = x0[c];
-    } else if constexpr (ROWD) {
-      const f32x2 x0 = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsa, off, 0, 0));
-      ar[s][0] = x0[0];
-      ar[s][1] = x0[1];
-    } else {
-#pragma unroll
-      for (int c = 0; c < BS; ++c)
-        ar[s][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsa, off + 4 * c * BS, 0, 0));
     }
   };
   auto load_b = [&](int s) {
     unsigned m = 0;
 #pragma unroll
-    for (int c = 0; c < BS; ++c)
+    for (int c = 0; c < SC; ++c)
       m |= (unsigned)(__builtin_amdgcn_ballot_w64((__float_as_uint(ar[s][c]) & 0x7fffffffu) != 0u) != 0) << c;
     act[s] = m;
-    // one resource over the step's bs B rows; an inactive column's offset is past its end,
+    // one resource over each step's bs B rows; an inactive column's offset is past its end,
     // so its load returns zeros without a memory access
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(B + (size_t)jr[s] * BS * ldb), 0, BS * ldb * 4, 0x00020000);
 #pragma unroll
-    for (int c = 0; c < BS; ++c)
-      bx[s][c] = __builtin_bit_cast(
-          f32x2, __builtin_amdgcn_raw_buffer_load_b64(
-                     rs, boff + ((m >> c) & 1u ? (unsigned)(c * ldb) * 4u : 0x80000000u), 0, 0));
+    for (int p = 0; p < SP; ++p) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(B + (size_t)jr[s][p] * BS * ldb), 0, BS * ldb * 4, 0x00020000);
+#pragma unroll
+      for (int c = 0; c < BS; ++c)
+        bx[s][p * BS + c] = __builtin_bit_cast(
+            f32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                       rs, boff + ((m >> (p * BS + c)) & 1u ? (unsigned)(c * ldb) * 4u : 0x80000000u), 0, 0));
+    }
   };
 
   f32x32 u0, u1;  // MFMA halves u = 0, 1 (output columns 4j + 2b + u of block b)
@@ -2867,7 +2886,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
   auto consume = [&](int s) {
     const unsigned m = act[s];
 #pragma unroll
-    for (int c = 0; c < BS; ++c) {
+    for (int c = 0; c < SC; ++c) {
       if ((m >> c) & 1u) {
         // the MFMAs' accumulators as values of one use each: hipcc then accumulates in
         // place (dst = srcC) instead of copying 64 registers around every branch
@@ -2878,10 +2897,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
     }
   };
 
-  // the queue holds at least R + DB + 1 steps before every round (or every row is done): the
-  // prologue takes DB + 1 and a round R, so a slot is empty only once every row is done
+  // the queue holds at least (R + DB + 1) SP steps before every round (or every row is done):
+  // the prologue takes DB + 1 slots and a round R, so a slot is empty only once every row is done
   auto refill = [&]() {
-    while (!done && qh - qt < R + DB + 1) {
+    while (!done && qh - qt < (R + DB + 1) * SP) {
       const int nun = merge();
       if (nun == 0) done = true;
       qh += nun;
