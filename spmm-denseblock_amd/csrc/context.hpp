@@ -181,6 +181,9 @@ spmm_status_t launch_grp_build(spmm_context* ctx, int W, int BS, bool pass2, int
                                int* cnt, int* maxj, const int* item_ptr, int* rows, int* src);
 spmm_status_t launch_grp_wmask(spmm_context* ctx, long long nitems, int W, int E, const int* src,
                                unsigned* wmask);
+// the bs 16 column masks of the group analysis (16-B aligned values; masks only)
+spmm_status_t launch_grp_mask16(spmm_context* ctx, spmm_direction_t dir, int nnzb,
+                                const uint16_t* val, unsigned* masks);
 // stats[0] = max over maxj[0..n), stats[1] = 1 if any maxj is INT_MIN (pass 1's "bad")
 spmm_status_t launch_grp_stats(spmm_context* ctx, const int* maxj, int n, int* stats);
 // exclusive scan of count[0..n) into out[0..n] (out[0] = 0) and *total (one workgroup,

@@ -6,8 +6,8 @@
 // Once per matrix, like spmm_bsr16_analysis_f16 and cuSPARSE's SpMM preprocess
 // (the reference's rocsparse_bsrmm.h:102-256 has none), as two calls:
 //  size query (buffer == NULL):
-//  1. the device computes every block's column mask (bsr16 / bsr32_analysis_kernel,
-//     masks only);
+//  1. the device computes every block's column mask (bs 32: bsr32_analysis_kernel, masks
+//     only; bs 16: grp_mask16_kernel in group_kernels.hip for 16-B aligned values);
 //  2. grp_build_kernel PASS 1 (group_kernels.hip), one wave per group of W adjacent
 //     block rows, checks the group's row pointer entries and block columns, merges
 //     the W sorted block-column lists and counts the items of the union of their
@@ -121,9 +121,11 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
     hipError_t e = hipMemsetAsync(pb + stat_off, 0, 32 * nc, st);
     if (e != hipSuccess) return from_hip(e);
     if (nnzb > 0 && mb > 0) {
-      spmm_status_t s = BS == 16
-          ? launch_bsr16_analysis(handle, dir, nnzb, static_cast<const uint16_t*>(bsrVal), dmk, nullptr)
-          : launch_bsr32_analysis(handle, dir, nnzb, static_cast<const float*>(bsrVal), dmk, nullptr);
+      const auto* v16 = static_cast<const uint16_t*>(bsrVal);
+      spmm_status_t s =
+          BS == 32 ? launch_bsr32_analysis(handle, dir, nnzb, static_cast<const float*>(bsrVal), dmk, nullptr)
+          : reinterpret_cast<uintptr_t>(bsrVal) % 16 == 0 ? launch_grp_mask16(handle, dir, nnzb, v16, dmk)
+                                                          : launch_bsr16_analysis(handle, dir, nnzb, v16, dmk, nullptr);
       if (s) return s;
     }
     for (int i = 0; i < nc; ++i) {

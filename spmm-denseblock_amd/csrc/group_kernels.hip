@@ -403,6 +403,52 @@ __global__ __launch_bounds__(64) void bsr16_grp_fill_kernel(long long nitems, in
   for (int f = 0; f < nf; ++f) dst[((item0 + f) * W + w) * 64 + lane] = frag[f * 64 + lane];
 }
 
+// Column masks of bs 16 fp16 blocks for the group analysis (masks only; spmm_bsr16_analysis_f16
+// keeps bsr16_analysis_kernel, which also writes the column-major copy): bit c set when column
+// c holds a value other than +-0 (NaN and inf included). A half-wave per block, one 16-B load
+// per lane (8 halves: ROW row l / 2, columns 8 (l & 1) ..; COLUMN column l / 2, rows 8 (l & 1)
+// ..), kMask16Pairs block pairs per wave in flight. ROW: the 16 lanes of each parity OR their
+// flags (4 xor shuffles); COLUMN: one ballot. 16-B aligned values only (else the older kernel).
+constexpr int kMask16Pairs = 8;
+
+__global__ __launch_bounds__(256) void grp_mask16_kernel(long long nnzb, int rowdir,
+                                                         const uint16_t* __restrict__ val,
+                                                         unsigned* __restrict__ masks) {
+  const int lane = threadIdx.x & 63;
+  const long long k0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * (2 * kMask16Pairs);
+  if (k0 >= nnzb) return;
+  const int half = lane >> 5, l = lane & 31;
+  uint4 xs[kMask16Pairs];
+#pragma unroll
+  for (int p = 0; p < kMask16Pairs; ++p) {
+    const long long k = min(k0 + 2 * p + half, nnzb - 1);  // past the end: loaded, not stored
+    xs[p] = *reinterpret_cast<const uint4*>(val + (size_t)k * 256 + 8 * l);
+  }
+#pragma unroll
+  for (int p = 0; p < kMask16Pairs; ++p) {
+    const long long k = k0 + 2 * p + half;
+    const unsigned w[4] = {xs[p].x, xs[p].y, xs[p].z, xs[p].w};
+    unsigned f = 0u;  // bit i: half i of this lane's 8 is nonzero
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      f |= ((w[i] & 0x7fffu) != 0u ? 1u : 0u) << (2 * i) |
+           ((w[i] & 0x7fff0000u) != 0u ? 1u : 0u) << (2 * i + 1);
+    unsigned msk;
+    if (rowdir) {
+      unsigned o = f;
+#pragma unroll
+      for (int d = 2; d < 32; d <<= 1) o |= __shfl_xor(o, d, 64);
+      msk = __shfl(o, 32 * half, 64) | (__shfl(o, 32 * half + 1, 64) << 8);
+    } else {
+      const unsigned bb = (unsigned)(__builtin_amdgcn_ballot_w64(f != 0u) >> (32 * half));
+      msk = 0u;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) msk |= ((bb >> (2 * c)) & 3u ? 1u : 0u) << c;
+    }
+    if (l == 0 && k < nnzb) masks[k] = msk;
+  }
+}
+
 // One workgroup: stats[0] = max maxj (-1 when n = 0), stats[1] = any INT_MIN.
 __global__ __launch_bounds__(1024) void grp_stats_kernel(const int* __restrict__ maxj, int n,
                                                          int* __restrict__ stats) {
@@ -492,6 +538,16 @@ spmm_status_t launch_bsr32_grp_fill(spmm_context* ctx, long long nitems, int W, 
   const long long units = (nitems + kFill32Items - 1) / kFill32Items * W;
   hipLaunchKernelGGL(bsr32_grp_fill_kernel, dim3((unsigned)units), dim3(64), 0, ctx->stream, nitems,
                      W, dir == SPMM_DIRECTION_ROW ? 1 : 0, rows, src, val, afrag);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_grp_mask16(spmm_context* ctx, spmm_direction_t dir, int nnzb,
+                                const uint16_t* val, unsigned* masks) {
+  if (nnzb == 0) return SPMM_STATUS_SUCCESS;
+  const long long per_block = 4 * 2 * kMask16Pairs;  // 4 waves, kMask16Pairs block pairs each
+  hipLaunchKernelGGL(grp_mask16_kernel, dim3((unsigned)((nnzb + per_block - 1) / per_block)),
+                     dim3(256), 0, ctx->stream, (long long)nnzb, dir == SPMM_DIRECTION_ROW ? 1 : 0,
+                     val, masks);
   return from_hip(hipGetLastError());
 }
 
