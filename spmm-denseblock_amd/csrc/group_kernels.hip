@@ -243,8 +243,16 @@ __global__ __launch_bounds__(256) void grp_wmask_kernel(long long nwork, int W,
 // either way and the fragments written, about 9 GB at 5 TB/s (16.6 GB at 5.4 on
 // products), so the gain is in L2 requests, not time. At bs 16 (below) the chunked form
 // took the fill from 1.26 to 0.86 ms on products.
-constexpr int kFill32Items = 8;
-constexpr int kFill32Ring = 3;
+#ifndef SPMM_FILL32_ITEMS
+#define SPMM_FILL32_ITEMS 8
+#endif
+#ifndef SPMM_FILL32_RING
+#define SPMM_FILL32_RING 3
+#endif
+// items per wave (at most 8: 64 entries) and blocks in flight per wave; 4 items or 4 blocks
+// ran the same times (profiles/r05c/ab_fill32/): the fill is bound by its HBM traffic
+constexpr int kFill32Items = SPMM_FILL32_ITEMS;
+constexpr int kFill32Ring = SPMM_FILL32_RING;
 
 __global__ __launch_bounds__(64) void bsr32_grp_fill_kernel(long long nitems, int W, int rowdir,
                                                             const int* __restrict__ rows,
@@ -259,7 +267,8 @@ __global__ __launch_bounds__(64) void bsr32_grp_fill_kernel(long long nitems, in
   const long long item0 = (u / W) * kFill32Items;
   const int nf = (int)min((long long)kFill32Items, nitems - item0);
   const long long it = item0 + (lane >> 3);
-  const int row = it < nitems ? rows[it * 8 + (lane & 7)] : -1;
+  const bool mine = (lane >> 3) < kFill32Items;
+  const int row = mine && it < nitems ? rows[it * 8 + (lane & 7)] : -1;
   const int k = row >= 0 ? src[(it * 8 + (lane & 7)) * W + w] : -1;
   const int c = row & 31;
 #pragma unroll
