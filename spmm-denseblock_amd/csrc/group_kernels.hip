@@ -283,7 +283,8 @@ __global__ __launch_bounds__(64) void bsr32_grp_fill_kernel(long long nitems, in
   int rb[kFill32Ring];
   unsigned long long unissued = __builtin_amdgcn_ballot_w64(k >= 0);
   // every slot loads unconditionally (one resource per block; none left: an offset past
-  // its end, zeros without a memory access), so the counted waits stay exact
+  // its end, zeros without a memory access), so hipcc counts the waits inside the ring
+  // (vmcnt(8) for the slot placed while two are in flight; only the loop head waits more)
   auto issue = [&](int s) {
     rb[s] = unissued ? __builtin_amdgcn_readlane(k, __builtin_ctzll(unissued)) : -1;
     unissued &= ~__builtin_amdgcn_ballot_w64(k == rb[s]);
