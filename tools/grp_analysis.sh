@@ -22,7 +22,7 @@ for w in ${WLS:-reddit_bsr32_grp products_bsr32_grp products_bsr16_f16_grp}; do
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
     n = r["Name"]
-    if any(k in n for k in ("grp_build", "grp_wmask", "fill_kernel", "analysis_kernel", "grp_mask16", "grp_stats", "scan_kernel")):
+    if any(k in n for k in ("grp_build", "grp_wmask", "fill_kernel", "analysis_kernel", "grp_mask", "grp_stats", "scan_kernel")):
         print(f'  {int(r["Calls"]):4d} {float(r["AverageNs"]) / 1e3:9.1f} us  {n[:80]}')
 EOF
 done
