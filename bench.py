@@ -748,7 +748,7 @@ def run_csr(args, W, world, rank, dev, dist):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kms_max = float(t[0]), float(t[1])
-    crf = csr_roofline(shard.rows, shard.colind, K, kms)
+    crf = csr_roofline(shard.rows, shard.colind[int(shard.rowptr[0]):], K, kms)
     traffic = None
     if hot and K == W["K"] and nnz == W["nnz"] and world == 1:
         # counter bytes of the hot kernel on this workload's own shape (tools/pmc_bytes.sh)
@@ -770,7 +770,7 @@ def run_csr(args, W, world, rank, dev, dist):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("K") == K and tj.get("nnz") == int(shard.colind.size):
+            if tj.get("K") == K and tj.get("nnz") == shard.nnz:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -817,7 +817,7 @@ def run_csr(args, W, world, rank, dev, dist):
             "analysis_ms_first_call": round(a_ms, 3),
             # SURVEY 8(d)'s gather model (one B row per nonzero) passes the peak
             # here (the MALL serves the re-reads), so it is a rate, not a fraction
-            "gather_model_GBps": round(csr_bytes(shard.rows, int(shard.colind.size), K) /
+            "gather_model_GBps": round(csr_bytes(shard.rows, shard.nnz, K) /
                                        (k_hot / 1e3) / 1e9, 1)}
         hot_tr = csr_counter_bytes("products_csr_hot")
         if hot_tr:

@@ -310,7 +310,10 @@ spmm_status_t spmm_bsrmm_analysed_f16(spmm_handle_t handle, int mb, int kb, int 
  * synchronisation, no host data: it can be captured in a HIP graph once the
  * handle's workspace has grown to the matrix). The arrays must not change
  * between the two calls (as between cuSPARSE's bufferSize and preprocess);
- * a filling call without a size query of the same arguments runs one first.
+ * a filling call without a size query of the same arguments runs one first,
+ * and every size query recomputes (a matrix at the addresses of an earlier
+ * query is analysed afresh). Analyses on one handle from several threads run
+ * one after the other (the handle's pending record is locked per call).
  * The handle records the buffer's layout:
  * spmm_bsrmm_grouped_f16 on the same handle takes it (until
  * spmm_bsr16_group_release or another analysis into the same buffer).

@@ -107,6 +107,35 @@ void oracle_csrmm_f32(int m, int n, const int* rowptr, const int* colind, const 
   csrmm_seq<float>(m, n, rowptr, colind, val, base, B, ldb, orderB, alpha, beta, C, ldc, orderC);
 }
 
+// The association the HIP CSR kernels use, restated so that
+// their output can be checked bit for bit at any grid: a row of L nonzeros is
+// summed as pieces of T(L) = max(128, ceil(L / 16)) consecutive nonzeros from
+// the row's start, each the sequential fp32 FMA chain of csrmm_seq above
+// (gespmm_csrmm.h:124-129), and the pieces are added left to right from -0.
+// Rows of at most 128 nonzeros are therefore exactly csrmm_seq's chain.
+int oracle_csr_piece_len(int L) { return std::max(128, (int)(((unsigned)L + 15u) >> 4)); }
+
+void oracle_csrmm_pieces_f32(int m, int n, const int* rowptr, const int* colind,
+                             const float* val, int base, const float* B, int ldb, int orderB,
+                             float alpha, float beta, float* C, int ldc, int orderC) {
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int r = 0; r < m; ++r) {
+    const int j0 = rowptr[r] - base, j1 = rowptr[r + 1] - base;
+    const int T = oracle_csr_piece_len(j1 - j0);
+    for (int c = 0; c < n; ++c) {
+      volatile float x = -0.f;  // no reassociation of the piece sums
+      for (int p = j0; p < j1; p += T) {
+        float acc = 0.f;
+        for (int j = p; j < std::min(p + T, j1); ++j)
+          acc = std::fma(val[j], B[at(colind[j] - base, c, ldb, orderB)], acc);
+        x = x + acc;
+      }
+      float& out = C[at(r, c, ldc, orderC)];
+      out = beta == 0.f ? alpha * x : std::fma(beta, out, alpha * x);
+    }
+  }
+}
+
 void oracle_csrmm_d(int m, int n, const int* rowptr, const int* colind, const double* val,
                     int base, const double* B, int ldb, int orderB, double alpha, double beta,
                     double* C, int ldc, int orderC) {

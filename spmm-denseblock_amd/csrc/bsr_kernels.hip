@@ -2636,7 +2636,10 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
 // p being block row (5p + 3) % G's block at position (p + 1/2) / P (a prefix would not do: a
 // community's out-of-community columns sort first), searched for in every block row of the
 // group by one lane (binary search over its sorted block columns). The mean of 1 / holders
-// estimates the union steps per block; the sums go to stat[0..1]. The grouped stream gives the
+// estimates the union steps per block; the sums go to stat[0..1] as integers (1 / holders in
+// units of 1 / 720720, the lcm of 1..16, exact), so the choice does not depend on the order
+// the probes' atomic adds land in (a float sum could flip a near-threshold matrix between
+// runs). The grouped stream gives the
 // whole matrix up past kGiveUp, a little above the break-even of the two kernels on the reddit
 // stand-in (bs 8: 2.0 ms for 6.3 M blocks on the lane-group kernel against 1.37 ms for
 // 2.75 M union steps, 0.64; bs 4 0.40; bs 2 0.20); a uniform-random pattern (the reference's
@@ -2644,11 +2647,13 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
 // given up runs its block rows one wave each on the lane-group kernel, and one long group
 // there (a hub) made a 0.1-ms tail on reddit; the probes inside the stream itself cost 8-13 %
 // (their chains of dependent loads at every wave's start).
+constexpr unsigned kProbeUnit = 720720;  // lcm(1..16): 1 / holders for G <= 16 holders
+
 template <int BS>
 __global__ __launch_bounds__(64) void small_grp_probe_kernel(int mb, int ngroups,
                                                              const int* __restrict__ rowptr,
                                                              const int* __restrict__ colind,
-                                                             float* __restrict__ stat) {
+                                                             unsigned long long* __restrict__ stat) {
   constexpr int G = 32 / BS, P = 64 / G;
   const int g = (int)(((long long)blockIdx.x * ngroups) / gridDim.x);
   const int lane = threadIdx.x, pp = lane / G;
@@ -2666,18 +2671,19 @@ __global__ __launch_bounds__(64) void small_grp_probe_kernel(int mb, int ngroups
   }
   const unsigned long long held = __builtin_amdgcn_ballot_w64(pvalid && lo < se && colind[lo] == pj);
   const unsigned long long pv = __builtin_amdgcn_ballot_w64(pvalid);
-  float est = 0.f;
-  int nv = 0;
+  unsigned long long est = 0;  // sum of 720720 / holders: exact
+  unsigned nv = 0;
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     if ((pv >> (p * G)) & 1ull) {
-      est += 1.f / (float)max(__builtin_popcountll((held >> (p * G)) & ((1ull << G) - 1ull)), 1);
+      est += kProbeUnit /
+             (unsigned)max(__builtin_popcountll((held >> (p * G)) & ((1ull << G) - 1ull)), 1);
       ++nv;
     }
   }
   if (lane == 0 && nv) {
     atomicAdd(&stat[0], est);
-    atomicAdd(&stat[1], (float)nv);
+    atomicAdd(&stat[1], (unsigned long long)nv);
   }
 }
 
@@ -2686,7 +2692,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc, int xm, int* __restrict__ dirty,
-    const int* __restrict__ order, int nnzb, const float* __restrict__ stat) {
+    const int* __restrict__ order, int nnzb, const unsigned long long* __restrict__ stat) {
   static_assert(BS == 2 || BS == 4 || BS == 8, "bs 2 / 4 / 8");
   constexpr int G = 32 / BS;  // block rows per group: 32 output rows
   constexpr int Q = 64 / G;   // candidates per block row and batch
@@ -2726,7 +2732,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
   // left to bsr_small_kernel (its block rows share too little)
   {
     constexpr float kGiveUp = BS == 8 ? 0.70f : (BS == 4 ? 0.45f : 0.25f);
-    if (SPMM_SGRP_PROBE && stat[0] > kGiveUp * stat[1]) {
+    if (SPMM_SGRP_PROBE && (double)stat[0] > (double)kGiveUp * kProbeUnit * (double)stat[1]) {
       if (lane == 0) dirty[g * gridDim.y + blockIdx.y] = 1;
       return;
     }
@@ -3886,7 +3892,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       timing_end(ctx, slot);
       return st;
     }
-    float* stat = static_cast<float*>(ctx->scratch);  // the probe's sums
+    // the probe's integer sums
+    unsigned long long* stat = static_cast<unsigned long long*>(ctx->scratch);
     int* dirty = reinterpret_cast<int*>(static_cast<char*>(ctx->scratch) + 256);
     constexpr int xm = SPMM_SGRP_XM;  // groups per XCD chunk
     // a shallow grid (a few waves per resident slot): groups longest first (reddit bs 8
@@ -3927,7 +3934,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     else SGRP_ONE(BS_, false, false);                                                            \
   } while (0)
     // the choice per matrix first (small_grp_probe_kernel), then the stream
-    if (hipError_t e = hipMemsetAsync(stat, 0, 2 * sizeof(float), ctx->stream)) {
+    if (hipError_t e = hipMemsetAsync(stat, 0, 2 * sizeof(*stat), ctx->stream)) {
       timing_end(ctx, slot);
       return from_hip(e);
     }

@@ -62,7 +62,10 @@ struct spmm_context {
   // The size query of a group analysis (buffer == NULL) leaves its device results
   // (column masks, item pointers) in grp_pend for the filling call with the same
   // arguments, which then needs neither those kernels again nor any host round trip
-  // (group.cpp). Cleared by that call and by a size query of other arguments.
+  // (group.cpp). Every size query recomputes it (the arrays' contents may have
+  // changed at the same addresses); the filling call consumes it. grp_mu holds
+  // the record for a whole analysis call, so two threads analysing on one handle
+  // run one after the other.
   struct GroupPending {
     bool valid = false;
     int bs = 0, W = 0, req = -1, dir = 0, mb = 0, nnzb = 0;  // req: the caller's groupRows
@@ -75,6 +78,7 @@ struct spmm_context {
   GroupPending grp_pending;
   void* grp_pend = nullptr;
   size_t grp_pend_bytes = 0;
+  std::mutex grp_mu;
 
   // Kernel timing ring.
   bool timing = false;

@@ -108,47 +108,83 @@ __device__ __forceinline__ float rdlanef(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-// Split rows. A row whose nonzeros span merge-path waves w_a .. w_b is
-// finished by the last of those waves to arrive, in the same launch:
-//  * waves w_a .. w_b - 1 end inside the row and leave their partial in their
-//    carry slot; w_b, where the row ends, leaves its partial in its head slot
-//    instead of writing C;
-//  * after its stores have completed (s_waitcnt vmcnt(0)), each of them adds 1
-//    to the row's ticket, tickets[tile * nwaves + w_a] (an agent-scope atomic),
-//    and the wave whose add completes w_b - w_a + 1 arrivals resets the ticket
-//    and writes the row:
-//      C = fma(alpha, ((c_a + c_{a+1}) + ... + c_{b-1}), epi(head))
-//    which is, bit for bit, the two-launch form it replaces (the kernel wrote
-//    epi(head) to C, a fix-up kernel then added alpha * the carries in wave
-//    order).
-// The partials cross workgroups (and XCDs) by MI355X_MICROARCH.md's
-// counter hand-off: sc1 stores and sc1 loads of every handed-off word, each
-// storing wave's vmcnt(0) before its add, the last adder loading only after
-// its add has returned. Tickets are zero between launches (tickets of the
-// handle, never shared with other buffers).
+// Pieces: the association of a row's sum, a function of the row alone
+// (DESIGN.md §3c). A row of L nonzeros is summed as consecutive pieces of
+//   T(L) = max(kPieceMin, ceil(L / kMaxPieces))
+// nonzeros counted from the row's first nonzero, each a sequential fp32 FMA
+// chain from zero in CSR order, and the pieces are added left to right from -0:
+//   x = ((-0 + p_0) + p_1) + ... + p_{np-1},   C = epi(x)
+// (-0 + p = p bit for bit, so a row of at most kPieceMin nonzeros is the
+// reference's own sequential chain, gespmm_csrmm.h:124-129). Merge-path wave
+// boundaries are moved onto piece boundaries (snap_cut), so every piece is
+// summed by one wave, and C does not depend on the grid, on the rows around
+// the row (shards, chunks) or on the entry point.
+constexpr int kPieceMin = 128;
+constexpr int kPiecesLog = 4;
+constexpr int kMaxPieces = 1 << kPiecesLog;
+
+__device__ __forceinline__ int piece_len(int L) {
+  return max(kPieceMin, (int)(((unsigned)L + (kMaxPieces - 1)) >> kPiecesLog));
+}
+
+// The merge-path point (i, j) of a wave boundary (i row ends and j nonzeros
+// consumed), moved off any piece: a cut strictly inside row i goes down to the
+// piece boundary at or before it (the row's start for a one-piece row), and a
+// cut between the row's last nonzero and its end marker moves past the marker.
+// Both waves of a boundary apply it to the same diagonal, so they agree.
+__device__ __forceinline__ void snap_cut(const int* __restrict__ rowptr, int rp0, int m, int& i,
+                                         int& j) {
+  if (i >= m) return;
+  const int rs = rowptr[i] - rp0;
+  if (j <= rs) return;
+  const int re = rowptr[i + 1] - rp0;
+  if (j >= re) {
+    ++i;
+    j = re;
+    return;
+  }
+  const int T = piece_len(re - rs);
+  j = rs + (j - rs) / T * T;
+}
+
+// Split rows. A row whose pieces lie in several waves is finished by the last
+// of them to arrive, in the same launch:
+//  * each of its waves stores every piece it summed in the row's piece slots,
+//    slot (key, k): key = tile * nwaves + the wave of the row's start diagonal
+//    ((row + start) / per, unique among the launch's split rows), k = the
+//    piece number;
+//  * after its stores have completed (s_waitcnt vmcnt(0)) each wave adds its
+//    piece count to the row's ticket, tickets[key] (an agent-scope atomic), and
+//    the wave whose add completes the row's np pieces resets the ticket and
+//    writes C = epi(((-0 + s_0) + s_1) + ...), the arithmetic of a row that one
+//    wave sums whole.
+// The slots cross workgroups (and XCDs) by MI355X_MICROARCH.md's counter
+// hand-off: sc1 stores and sc1 loads of every handed-off word, each storing
+// wave's vmcnt(0) before its add, the last adder loading only after its add
+// has returned. Tickets are zero between launches (tickets of the handle,
+// never shared with other buffers).
 __device__ __forceinline__ void st_sc1(float* p, float x) {
   __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Adds this wave's arrival to *t (lane 0); true in the wave that completes
-// `count` arrivals, which also resets *t for the next launch.
-__device__ __forceinline__ bool split_row_arrive(int* t, int count, int lane) {
+// Adds this wave's `add` pieces to *t (lane 0); true in the wave whose add
+// completes `count`, which also resets *t for the next launch.
+__device__ __forceinline__ bool split_row_arrive(int* t, int add, int count, int lane) {
   int old = 0;
-  if (lane == 0) old = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) old = __hip_atomic_fetch_add(t, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __builtin_amdgcn_readlane(old, 0);
-  if (old + 1 != count) return false;
+  if (old + add != count) return false;
   if (lane == 0) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
-// Workspace of the split rows: carry and head slots for every (column tile,
-// wave), `stride` floats each: the launch's column-tile width (kWave * VEC;
-// kWave for the K <= 64 group kernel). The host sizes each of the two arrays
-// for the widest grid at that width (csrmm_carry_bytes).
+// Piece slots of the split rows: kMaxPieces slots of `stride` floats per key
+// (column tile x wave): stride = the launch's column-tile width (kWave * VEC;
+// kWave for the K <= 64 group kernel). The host sizes the array for the widest
+// grid at that width (csrmm_carry_bytes).
 struct SplitWs {
-  float* carry;
-  float* head;
+  float* slots;
   int stride;
 };
 
@@ -185,6 +221,68 @@ __device__ __forceinline__ int merge_search2(const int* __restrict__ rowptr, int
   return lo;
 }
 
+// A wave's range of the merge path after the snap, and what it shares with its
+// neighbours: [(i0, j0), (i1, j1)); row i0 began in an earlier wave (head),
+// row i1 continues past this wave (carry; j1 then lies strictly inside it).
+struct WaveRange {
+  int i0, j0, i1, j1;
+  int rs0;       // start of row i0 (relative nonzero index)
+  int rs1, re1;  // start / end of row i1 (when carry)
+  bool head, carry;
+};
+
+__device__ __forceinline__ WaveRange wave_range(const int* __restrict__ rowptr, int rp0, int m,
+                                                long long nnz, long long d0, long long d1,
+                                                int lane) {
+  const int ires = merge_search2(rowptr, rp0, m, nnz, d0, d1, lane);
+  WaveRange r;
+  r.i0 = __builtin_amdgcn_readlane(ires, 0);
+  r.i1 = __builtin_amdgcn_readlane(ires, 32);
+  r.j0 = (int)(d0 - r.i0);
+  r.j1 = (int)(d1 - r.i1);
+  snap_cut(rowptr, rp0, m, r.i0, r.j0);
+  snap_cut(rowptr, rp0, m, r.i1, r.j1);
+  r.rs0 = r.i0 < m ? rowptr[r.i0] - rp0 : 0;
+  r.rs1 = r.i1 < m ? rowptr[r.i1] - rp0 : 0;
+  r.carry = r.i1 < m && r.j1 > r.rs1;
+  r.re1 = r.carry ? rowptr[r.i1 + 1] - rp0 : 0;
+  r.head = r.i0 < r.i1 && r.rs0 < r.j0;
+  return r;
+}
+
+// Per-row piece state of a wave (wave-uniform scalars). The wave's events
+// are row ends (cur_end) and piece boundaries inside a row (next_pb), both
+// relative nonzero indices; ev is the nearer one. A split row's pieces go to
+// its slots (key), any other row's are added into the running sum.
+struct PieceState {
+  int cur_end;   // end of row i (INT_MAX for the carry row)
+  int re;        // real end of row i
+  int T;         // piece length of row i
+  int pk;        // current piece number
+  int next_pb;   // next piece boundary inside row i (INT_MAX: none)
+  int ev;        // min(cur_end, next_pb)
+  bool split;    // row i is split: pieces to the slots
+  int stored;    // pieces of row i this wave has stored
+  size_t key;    // ticket index of row i (split rows)
+  __device__ __forceinline__ void begin(int rs, int re_, int cur_end_, int jfirst) {
+    cur_end = cur_end_;
+    re = re_;
+    T = piece_len(re_ - rs);
+    pk = jfirst > rs ? (jfirst - rs) / T : 0;
+    const unsigned nb = (unsigned)rs + (unsigned)(pk + 1) * (unsigned)T;
+    next_pb = nb < (unsigned)re_ ? (int)nb : INT_MAX;
+    ev = min(cur_end, next_pb);
+    stored = 0;
+  }
+  __device__ __forceinline__ void next_piece() {
+    ++pk;
+    const unsigned nb = (unsigned)next_pb + (unsigned)T;
+    next_pb = nb < (unsigned)re ? (int)nb : INT_MAX;
+    ev = min(cur_end, next_pb);
+  }
+  __device__ __forceinline__ int npieces(int rs) const { return (re - rs + T - 1) / T; }
+};
+
 template <int VEC, bool NT, int HOT = 0>
 __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
     int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
@@ -208,21 +306,17 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   const long long d0 = min((long long)w * per, total);
   const long long d1 = min(d0 + per, total);
 
-  const int ires = merge_search2(rowptr, rp0, m, nnz, d0, d1, lane);
-  const int i0 = rdlane(ires, 0);
-  const int i1 = rdlane(ires, 32);
-  const int j0 = (int)(d0 - i0);
-  const int j1 = (int)(d1 - i1);
+  const WaveRange wr = wave_range(rowptr, rp0, m, nnz, d0, d1, lane);
+  const int i0 = wr.i0, i1 = wr.i1, j0 = wr.j0, j1 = wr.j1;
+  if (i0 >= m) return;  // past the last row (an empty range)
   const int aoff = rp0 - base;  // array offset of relative nnz 0
   const int J = j1 - j0;
-  const int slot = ct * nwaves + w;
-  // the first row this wave finishes began in an earlier wave: its partial goes
-  // to the head slot (split rows, above)
-  const int rs0 = i0 < i1 ? rowptr[i0] - rp0 : 0;
-  const bool split_head = i0 < i1 && rs0 < j0;
-  bool head_pending = split_head;
-  float* const carry_p = sws.carry + (size_t)slot * sws.stride + lane * VEC;
-  float* const head_p = sws.head + (size_t)slot * sws.stride + lane * VEC;
+  const size_t tkeys = (size_t)ct * nwaves;  // this column tile's tickets
+  const size_t sf = sws.stride;
+  auto key_of = [&](int r, int rs) { return tkeys + (size_t)(((long long)r + rs) / per); };
+  auto slot_p = [&](size_t key, int k) {
+    return sws.slots + (key * kMaxPieces + k) * sf + lane * VEC;
+  };
 
   // Row ends: lane l holds raw rowptr[rbase+1+l] for 64 rows, reloaded in
   // place when exhausted (one pipeline drain per 64 rows). The load is free
@@ -232,11 +326,29 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   int rbase = i0;
   int rev = load_rowends(rbase);
   int i = i0;
-  int cur_end = (i < i1) ? rdlane(rev, 0) - rp0 : INT_MAX;
+  PieceState ps;
+  if (i0 < i1) {
+    const int re0 = rdlane(rev, 0) - rp0;
+    ps.begin(wr.rs0, re0, re0, j0);
+    ps.split = wr.head;
+  } else if (wr.carry) {  // the whole range lies inside row i0 = i1
+    ps.begin(wr.rs0, wr.re1, INT_MAX, j0);
+    ps.split = true;
+  } else {
+    ps.cur_end = ps.next_pb = ps.ev = INT_MAX;
+    ps.split = false;
+  }
+  if (ps.split) ps.key = key_of(i0, wr.rs0);
 
-  float acc[VEC];
+  float acc[VEC], tot[VEC];
 #pragma unroll
-  for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
+  for (int c = 0; c < VEC; ++c) {
+    acc[c] = 0.f;
+    tot[c] = -0.f;
+  }
+  // the split head row, once it has ended: its key, pieces stored here, np
+  size_t head_key = 0;
+  int head_stored = 0, head_np = 0;
 
   const float* Bb = B - (size_t)base * ldb;  // row 0 of B for 1-based colind
   float* Ct = C + col0;
@@ -245,26 +357,17 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Bb), 0, 0xffffffff, 0x00020000);
   const unsigned ldb4 = 4u * (unsigned)ldb;
 
-  auto emit = [&](int row) {
-    if (head_pending) {  // the end of a split row: the raw partial to the head slot
-      head_pending = false;
-#pragma unroll
-      for (int c = 0; c < VEC; ++c) {
-        st_sc1(head_p + c, acc[c]);
-        acc[c] = 0.f;
-      }
-      return;
-    }
+  auto epi_store = [&](int row, const float (&x)[VEC]) {
     float* cp = Ct + (size_t)row * ldc;
     vec out;
     if (beta == 0.f) {
 #pragma unroll
-      for (int c = 0; c < VEC; ++c) vset<VEC>(out, c, alpha * acc[c]);
+      for (int c = 0; c < VEC; ++c) vset<VEC>(out, c, alpha * x[c]);
     } else {
       const vec old = vload<VEC>(col_ok ? cp : Ct);
 #pragma unroll
       for (int c = 0; c < VEC; ++c)
-        vset<VEC>(out, c, __builtin_fmaf(beta, vget<VEC>(old, c), alpha * acc[c]));
+        vset<VEC>(out, c, __builtin_fmaf(beta, vget<VEC>(old, c), alpha * x[c]));
     }
     if (col_ok) {
       if constexpr (NT) {
@@ -276,17 +379,71 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
         vstore<VEC>(cp, out);
       }
     }
+  };
+  auto store_piece = [&]() {
+    float* sp = slot_p(ps.key, ps.pk);
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) st_sc1(sp + c, acc[c]);
+    ++ps.stored;
+  };
+  // the piece ending at ps.next_pb (row i continues)
+  auto end_piece = [&]() {
+    if (ps.split) {
+      store_piece();
+    } else {
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) tot[c] = tot[c] + acc[c];
+    }
 #pragma unroll
     for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
+    ps.next_piece();
+  };
+  // row i ends at ps.cur_end
+  auto end_row = [&]() {
+    if (ps.split) {  // the split head row: its last piece to the slots
+      store_piece();
+      head_key = ps.key;
+      head_stored = ps.stored;
+      head_np = ps.pk + 1;
+    } else {
+      float x[VEC];
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) x[c] = tot[c] + acc[c];
+      epi_store(i, x);
+    }
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) {
+      acc[c] = 0.f;
+      tot[c] = -0.f;
+    }
   };
   auto advance_row = [&]() {
+    const int rs = ps.cur_end;  // the row just ended here
     ++i;
     if (i - rbase == kWave) {
       rbase += kWave;
       rev = load_rowends(rbase);
       settle(rev);
     }
-    cur_end = (i < i1) ? rdlane(rev, i - rbase) - rp0 : INT_MAX;
+    if (i < i1) {
+      const int re = rdlane(rev, i - rbase) - rp0;
+      ps.begin(rs, re, re, rs);
+      ps.split = false;
+    } else if (wr.carry) {
+      ps.begin(rs, wr.re1, INT_MAX, rs);
+      ps.split = true;
+      ps.key = key_of(i, rs);
+    } else {
+      ps.cur_end = ps.next_pb = ps.ev = INT_MAX;
+    }
+  };
+  auto event = [&]() {
+    if (ps.cur_end <= ps.next_pb) {
+      end_row();
+      advance_row();
+    } else {
+      end_piece();
+    }
   };
 
   // nnz are processed in groups of kU aligned to absolute array positions:
@@ -371,10 +528,7 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
         const int a = ag + u;
         if (a >= A0 && a < A1) {
           const int j = a - aoff;
-          while (cur_end <= j) {  // cur_end is INT_MAX once i reaches i1
-            emit(i);
-            advance_row();
-          }
+          while (ps.ev <= j) event();  // ev is INT_MAX past the last event
 #pragma unroll
           for (int c = 0; c < VEC; ++c) acc[c] = __builtin_fmaf(vsrc[u], src[u][c], acc[c]);
         }
@@ -393,67 +547,32 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
   }
   // Rows whose end marker lies at or before j1 but after the last nnz.
   while (i < i1) {
-    emit(i);
+    end_row();
     advance_row();
   }
-  // Carry: the partial of row i1 accumulated over [max(j0, start(i1)), j1).
-  bool has_carry = false;
-  int rs1 = 0;
-  if (i1 < m && J > 0) {
-    rs1 = rowptr[i1] - rp0;
-    has_carry = j1 > rs1;
-  }
-  if (has_carry) {
+  // The carry row's pieces summed here: the last one ends at j1, a piece boundary.
+  if (wr.carry && J > 0) store_piece();
+  const bool carry_here = wr.carry && ps.stored > 0;
+  if (!head_np && !carry_here) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces are stored
+  // the last arrival of a split row writes it
+  auto finish = [&](int r, size_t key, int np) {
+    const float* sp = slot_p(key, 0);
+    float x[VEC];
 #pragma unroll
-    for (int c = 0; c < VEC; ++c) st_sc1(carry_p + c, acc[c]);
-  }
-  if (!split_head && !has_carry) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partials are stored
-  // the last arrival of a split row writes it (w_a .. w_b: the row's waves)
-  auto finish = [&](int r, int wa, int wb) {
-    const size_t sf = sws.stride;
-    const float* cw = sws.carry + ((size_t)ct * nwaves + wa) * sf + lane * VEC;
-    float sum[VEC], x[VEC];
+    for (int c = 0; c < VEC; ++c) x[c] = -0.f;
+    for (int k = 0; k < np; ++k) {
 #pragma unroll
-    for (int c = 0; c < VEC; ++c) sum[c] = ld_sc1(cw + c);
-    for (int w2 = wa + 1; w2 < wb; ++w2) {
-      cw += sf;
-#pragma unroll
-      for (int c = 0; c < VEC; ++c) sum[c] = sum[c] + ld_sc1(cw + c);
+      for (int c = 0; c < VEC; ++c) x[c] = x[c] + ld_sc1(sp + c);
+      sp += sf;
     }
-    const float* hw = sws.head + ((size_t)ct * nwaves + wb) * sf + lane * VEC;
-#pragma unroll
-    for (int c = 0; c < VEC; ++c) x[c] = ld_sc1(hw + c);
-    if (!col_ok) return;
-    float* cp = Ct + (size_t)r * ldc;
-    vec out;
-    if (beta == 0.f) {
-#pragma unroll
-      for (int c = 0; c < VEC; ++c) vset<VEC>(out, c, alpha * x[c]);
-    } else {
-      const vec old = vload<VEC>(cp);
-#pragma unroll
-      for (int c = 0; c < VEC; ++c)
-        vset<VEC>(out, c, __builtin_fmaf(beta, vget<VEC>(old, c), alpha * x[c]));
-    }
-#pragma unroll
-    for (int c = 0; c < VEC; ++c) vset<VEC>(out, c, __builtin_fmaf(alpha, sum[c], vget<VEC>(out, c)));
-    if constexpr (NT) {
-#pragma unroll
-      for (int c = 0; c < VEC; ++c) __builtin_nontemporal_store(vget<VEC>(out, c), cp + c);
-    } else {
-      vstore<VEC>(cp, out);
-    }
+    epi_store(r, x);
   };
-  if (split_head) {
-    const int wa = (int)(((long long)i0 + rs0) / per);
-    if (split_row_arrive(tickets + (size_t)ct * nwaves + wa, w - wa + 1, lane)) finish(i0, wa, w);
-  }
-  if (has_carry) {
-    const int re1 = rowptr[i1 + 1] - rp0;
-    const int wa = (int)(((long long)i1 + rs1) / per), wb = (int)(((long long)i1 + re1) / per);
-    if (split_row_arrive(tickets + (size_t)ct * nwaves + wa, wb - wa + 1, lane))
-      finish(i1, wa, wb);
+  if (head_np && split_row_arrive(tickets + head_key, head_stored, head_np, lane))
+    finish(i0, head_key, head_np);
+  if (carry_here) {
+    const int np = ps.npieces(wr.rs1);
+    if (split_row_arrive(tickets + ps.key, ps.stored, np, lane)) finish(i1, ps.key, np);
   }
 }
 
@@ -463,12 +582,13 @@ __global__ __launch_bounds__(kWG) void csr_mergepath_kernel(
 // wave's merge-path range per step. A step is one G-row gather with per-lane
 // colind / val loads instead of per-nnz v_readlane and scalar address
 // arithmetic, which is what bounds the main kernel at small K.
-// Each group accumulates its own partial of the current row; at a row end the
-// groups before the end position are folded in and the G partials summed
-// across groups (log2 G cross-lane steps). Products of a row are thus summed
-// in G interleaved chains — within the fp32 bar, not bit-identical to the
-// sequential order (SPMM_CSR_SEQUENTIAL_ROWS keeps the main kernel).
-// Carries use the VEC = 1 fix-up (columns 0..31 of a slot).
+// Each group accumulates its own partial of the current piece; at a piece or
+// row end the groups before the end position are folded in and the G partials
+// summed across groups (log2 G cross-lane steps). Products of a piece are thus
+// summed in G interleaved chains by array position mod G — within the fp32
+// bar, not bit-identical to the sequential order (SPMM_CSR_SEQUENTIAL_ROWS
+// keeps the main kernel) — and the pieces are combined as in the main kernel,
+// so C depends on the row and its array position mod 64 only.
 template <bool NT, int LPG, int PD, bool HOT = false>
 __global__ __launch_bounds__(kWG) void csr_group_kernel(
     int m, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
@@ -490,36 +610,35 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
   const long long per = (total + nwaves - 1) / nwaves;
   const long long d0 = min((long long)w * per, total);
   const long long d1 = min(d0 + per, total);
-  const int ires = merge_search2(rowptr, rp0, m, nnz, d0, d1, lane);
-  const int i0 = rdlane(ires, 0);
-  const int i1 = rdlane(ires, 32);
-  const int j0 = (int)(d0 - i0);
-  const int j1 = (int)(d1 - i1);
+  const WaveRange wr = wave_range(rowptr, rp0, m, nnz, d0, d1, lane);
+  const int i0 = wr.i0, i1 = wr.i1, j0 = wr.j0, j1 = wr.j1;
+  if (i0 >= m) return;
   const int aoff = rp0 - base;
-  const int slot = w;
-  // split rows (above): column c of a slot is float c (the VEC = 1 layout)
-  const int rs0 = i0 < i1 ? rowptr[i0] - rp0 : 0;
-  const bool split_head = i0 < i1 && rs0 < j0;
-  bool head_pending = split_head;
-  float* const carry_p = sws.carry + (size_t)slot * sws.stride + col;
-  float* const head_p = sws.head + (size_t)slot * sws.stride + col;
+  const size_t sf = sws.stride;  // kWave: column c of a slot is float c
+  auto key_of = [&](int r, int rs) { return (size_t)(((long long)r + rs) / per); };
 
   auto load_rowends = [&](int rb) -> int { return rowptr[min(rb + 1 + lane, m)]; };
   int rbase = i0;
   int rev = load_rowends(rbase);
   int i = i0;
-  int cur_end = (i < i1) ? rdlane(rev, 0) - rp0 : INT_MAX;
-  auto advance_row = [&]() {
-    ++i;
-    if (i - rbase == kWave) {
-      rbase += kWave;
-      rev = load_rowends(rbase);
-      settle(rev);
-    }
-    cur_end = (i < i1) ? rdlane(rev, i - rbase) - rp0 : INT_MAX;
-  };
+  PieceState ps;
+  if (i0 < i1) {
+    const int re0 = rdlane(rev, 0) - rp0;
+    ps.begin(wr.rs0, re0, re0, j0);
+    ps.split = wr.head;
+  } else if (wr.carry) {
+    ps.begin(wr.rs0, wr.re1, INT_MAX, j0);
+    ps.split = true;
+  } else {
+    ps.cur_end = ps.next_pb = ps.ev = INT_MAX;
+    ps.split = false;
+  }
+  if (ps.split) ps.key = key_of(i0, wr.rs0);
+  size_t head_key = 0;
+  int head_stored = 0, head_np = 0;
 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 tot = {-0.f, -0.f, -0.f, -0.f};
   const float* Bb = B - (size_t)base * ldb;
   // Sum of the G group partials, in every lane of the same column slot:
   // rotations inside 16-lane rows (v_add_f32_dpp row_ror: one instruction per
@@ -536,27 +655,25 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
     }
     return v;
   };
-  auto emit = [&](int row) {
-    const f32x4 t = fold(acc);
-    if (head_pending) {  // the end of a split row: the summed partial to the head slot
-      head_pending = false;
-      if (grp == 0) {
+  auto store_piece = [&](const f32x4& t) {
+    if (grp == 0) {
+      float* sp = sws.slots + (ps.key * kMaxPieces + ps.pk) * sf + col;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) st_sc1(head_p + c, t[c]);
-      }
-      acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      return;
+      for (int c = 0; c < 4; ++c) st_sc1(sp + c, t[c]);
     }
+    ++ps.stored;
+  };
+  auto epi_store = [&](int row, const f32x4& x) {
     if (grp == 0 && col_ok) {
       float* cp = C + (size_t)row * ldc + col;
       f32x4 out;
       if (beta == 0.f) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) out[c] = alpha * t[c];
+        for (int c = 0; c < 4; ++c) out[c] = alpha * x[c];
       } else {
         const f32x4 old = *reinterpret_cast<const f32x4*>(cp);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) out[c] = __builtin_fmaf(beta, old[c], alpha * t[c]);
+        for (int c = 0; c < 4; ++c) out[c] = __builtin_fmaf(beta, old[c], alpha * x[c]);
       }
       if constexpr (NT) {
 #pragma unroll
@@ -565,7 +682,54 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
         *reinterpret_cast<f32x4*>(cp) = out;
       }
     }
+  };
+  auto end_piece = [&]() {
+    const f32x4 t = fold(acc);
+    if (ps.split) {
+      store_piece(t);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) tot[c] = tot[c] + t[c];
+    }
     acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    ps.next_piece();
+  };
+  auto end_row = [&]() {
+    const f32x4 t = fold(acc);
+    if (ps.split) {  // the split head row: its last piece to the slots
+      store_piece(t);
+      head_key = ps.key;
+      head_stored = ps.stored;
+      head_np = ps.pk + 1;
+    } else {
+      f32x4 x;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[c] = tot[c] + t[c];
+      epi_store(i, x);
+    }
+    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    tot = f32x4{-0.f, -0.f, -0.f, -0.f};
+  };
+  auto advance_row = [&]() {
+    const int rs = ps.cur_end;
+    ++i;
+    if (i - rbase == kWave) {
+      rbase += kWave;
+      rev = load_rowends(rbase);
+      settle(rev);
+    }
+    if (i < i1) {
+      const int re = rdlane(rev, i - rbase) - rp0;
+      ps.begin(rs, re, re, rs);
+      ps.split = false;
+    } else if (wr.carry) {
+      ps.begin(rs, wr.re1, INT_MAX, rs);
+      ps.split = true;
+      ps.key = key_of(i, rs);
+    } else {
+      ps.cur_end = ps.next_pb = ps.ev = INT_MAX;
+      ps.split = false;
+    }
   };
 
   // Steps of G nnz aligned to absolute array positions (as the main kernel):
@@ -589,8 +753,8 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
     if constexpr (HOT) c &= 0x7fffffff;
     return *reinterpret_cast<const f32x4*>(Bb + (size_t)c * ldb + col_ld);
   };
-  // One step's products: groups before a row end inside the step belong to
-  // the ending row(s).
+  // One step's products: groups before an event (piece or row end) inside the
+  // step belong to the piece that ends there.
   auto consume = [&](int s, const f32x4& b, float v) {
     const int q0 = gs + G * s;
     const int p = q0 + grp;
@@ -598,16 +762,23 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
     f32x4 prod;
 #pragma unroll
     for (int c = 0; c < 4; ++c) prod[c] = ok ? v * b[c] : 0.f;
-    while (cur_end - (q0 - aoff) < G) {  // cur_end is INT_MAX once i reaches i1
-      const int e = cur_end - (q0 - aoff);
+    // events inside the range only (ev is INT_MAX past the last one): the carry row's
+    // piece boundary at j1 ends this wave's share, stored after the loop, and the
+    // rows ending at j1 are emitted there too
+    while (ps.ev < j1 && ps.ev - (q0 - aoff) < G) {
+      const int e = ps.ev - (q0 - aoff);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const bool mine = grp < e;
         acc[c] += mine ? prod[c] : 0.f;
         prod[c] = mine ? 0.f : prod[c];
       }
-      emit(i);
-      advance_row();
+      if (ps.cur_end <= ps.next_pb) {
+        end_row();
+        advance_row();
+      } else {
+        end_piece();
+      }
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[c] += prod[c];
@@ -642,48 +813,31 @@ __global__ __launch_bounds__(kWG) void csr_group_kernel(
     }
   }
   while (i < i1) {
-    emit(i);
+    end_row();
     advance_row();
   }
-  bool has_carry = false;
-  int rs1 = 0;
-  if (i1 < m && j1 > j0) {
-    rs1 = rowptr[i1] - rp0;
-    has_carry = j1 > rs1;
-  }
-  if (has_carry) {
-    const f32x4 t = fold(acc);
-    if (grp == 0) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) st_sc1(carry_p + c, t[c]);
-    }
-  }
-  if (!split_head && !has_carry) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partials are stored
+  if (wr.carry && j1 > j0) store_piece(fold(acc));
+  const bool carry_here = wr.carry && ps.stored > 0;
+  if (!head_np && !carry_here) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces are stored
   // the last arrival writes the row: lane l column l (n <= 64)
-  auto finish = [&](int r, int wa, int wb) {
-    const size_t sf = sws.stride;
-    const float* cw = sws.carry + (size_t)wa * sf + lane;
-    float sum = ld_sc1(cw);
-    for (int w2 = wa + 1; w2 < wb; ++w2) {
-      cw += sf;
-      sum = sum + ld_sc1(cw);
+  auto finish = [&](int r, size_t key, int np) {
+    const float* sp = sws.slots + key * kMaxPieces * sf + lane;
+    float x = -0.f;
+    for (int k = 0; k < np; ++k) {
+      x = x + ld_sc1(sp);
+      sp += sf;
     }
-    const float x = ld_sc1(sws.head + (size_t)wb * sf + lane);
     if (lane >= n) return;
     float* cp = C + (size_t)r * ldc + lane;
-    float out = beta == 0.f ? alpha * x : __builtin_fmaf(beta, *cp, alpha * x);
-    out = __builtin_fmaf(alpha, sum, out);
+    const float out = beta == 0.f ? alpha * x : __builtin_fmaf(beta, *cp, alpha * x);
     if constexpr (NT) __builtin_nontemporal_store(out, cp); else *cp = out;
   };
-  if (split_head) {
-    const int wa = (int)(((long long)i0 + rs0) / per);
-    if (split_row_arrive(tickets + wa, w - wa + 1, lane)) finish(i0, wa, w);
-  }
-  if (has_carry) {
-    const int re1 = rowptr[i1 + 1] - rp0;
-    const int wa = (int)(((long long)i1 + rs1) / per), wb = (int)(((long long)i1 + re1) / per);
-    if (split_row_arrive(tickets + wa, wb - wa + 1, lane)) finish(i1, wa, wb);
+  if (head_np && split_row_arrive(tickets + head_key, head_stored, head_np, lane))
+    finish(i0, head_key, head_np);
+  if (carry_here) {
+    const int np = ps.npieces(wr.rs1);
+    if (split_row_arrive(tickets + ps.key, ps.stored, np, lane)) finish(i1, ps.key, np);
   }
 }
 
@@ -958,21 +1112,24 @@ spmm_status_t launch_csr_hot_analysis(spmm_context* ctx, int k, long long nnz, c
 }
 
 namespace {
-// Floats of ONE of the two split-row arrays (carry, head): a slot of tile
-// floats per (column tile, wave) at the capped wave count. The tiles of any
-// VEC cover at most roundup(n, 256) columns (tile = 64 * VEC, VEC <= 4), and
-// the group kernel's single tile of kWave floats is within that too, so one
+// Floats of the piece slots: kMaxPieces slots of one column tile's width per
+// (column tile, wave) at the capped wave count. The tiles of a launch cover
+// roundup(n, 64 * VEC) columns, at most the width below for any VEC
+// pick_vec can choose at this n (VEC 4 only past 128 columns, VEC 2 past 64),
+// and the group kernel's single tile of kWave floats is within it too, so one
 // size serves every launch of this n.
 size_t split_array_floats(spmm_context* ctx, int n) {
   const int wpc = ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu : 16;
   const size_t nw = (size_t)ctx->num_cus * wpc;  // the grid's cap (csr_nwaves)
-  return nw * (((size_t)n + 255) & ~(size_t)255);
+  const size_t un = (size_t)n;
+  const size_t width = n > 128 ? (un + 255) & ~(size_t)255 : (n > 64 ? 128 : 64);
+  return nw * kMaxPieces * width;
 }
 }  // namespace
 
 size_t csrmm_carry_bytes(spmm_context* ctx, int m, int n) {
   (void)m;  // the grid does not depend on m or nnz beyond the cap: size it for the cap
-  return 2 * split_array_floats(ctx, n) * sizeof(float) + 256;
+  return split_array_floats(ctx, n) * sizeof(float) + 256;
 }
 
 spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* rowptr,
@@ -986,11 +1143,10 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   const int nw = csr_nwaves(ctx, m, nnz_hint);
   dim3 grid((nw + kWavesPerWG - 1) / kWavesPerWG, ntiles);
   dim3 block(kWG);
-  // split rows: carry and head slots in the workspace (sized by csrmm_carry_bytes for
-  // the largest grid), tickets of the handle (zero between launches)
+  // split rows: piece slots in the workspace (sized by csrmm_carry_bytes for the
+  // largest grid), tickets of the handle (zero between launches)
   SplitWs sws;
-  sws.carry = static_cast<float*>(carry_ws);
-  sws.head = sws.carry + split_array_floats(ctx, n);
+  sws.slots = static_cast<float*>(carry_ws);
   sws.stride = tile;
   if (spmm_status_t st = ensure_tickets(ctx, (size_t)nw * ntiles)) return st;
   int* tickets = ctx->tickets;

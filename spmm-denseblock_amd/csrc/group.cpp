@@ -25,6 +25,7 @@
 // The filling call reuses the size query's device results (handle->grp_pending):
 // the arrays must not change between the two calls, as between cuSPARSE's
 // bufferSize and preprocess calls. It launches kernels and async copies only.
+// Every size query recomputes those results, whatever ran before it.
 // Round 4's first form merged on the host (0.27-0.46 s on the products stand-in),
 // and its second ran the masks and PASS 1 again behind two synchronisations.
 //
@@ -83,10 +84,14 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
     return SPMM_STATUS_INVALID_VALUE;
   const int E = BS == 16 ? 16 : 8;  // entries per item
   hipStream_t st = handle->stream;
+  std::lock_guard<std::mutex> glk(handle->grp_mu);  // the pending record, call to call
   auto& pend = handle->grp_pending;
-  const bool same = pend.valid && pend.bs == BS && pend.req == groupRows && pend.dir == (int)dir &&
-                    pend.mb == mb && pend.nnzb == nnzb && pend.rp == bsrRowPtr &&
-                    pend.ci == bsrColInd && pend.val == bsrVal;
+  // Only a filling call reuses the pending size query, and only one of the same
+  // arguments: a size query always runs, since the arrays at the same addresses may
+  // hold another matrix by now (a caching allocator hands addresses out again).
+  const bool same = buffer && pend.valid && pend.bs == BS && pend.req == groupRows &&
+                    pend.dir == (int)dir && pend.mb == mb && pend.nnzb == nnzb &&
+                    pend.rp == bsrRowPtr && pend.ci == bsrColInd && pend.val == bsrVal;
   if (!same) {
     // The size query. Candidates: groupRows itself, or at BS 16 with groupRows = 0 every W
     // (2, 4, 8), of which the one with the least modelled time is kept (below); BS 32 with 0

@@ -4,9 +4,9 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm).
 Every rank holds the full dense B (replicated: 2.5 GB for products at K=256,
 far under 288 GB), owns a contiguous nnz-balanced row range of A, computes
 its rows of C with the HIP kernel, and the ranks exchange their rows of C
-over xGMI. Output rows are independent: a row that no merge-path
-wave splits is bit-identical to the 1-GPU result; a split row's carries are
-associated by where the wave boundaries fall (within the fp32 bar).
+over xGMI. Output rows are independent, and the kernels associate a row's
+sum by the row alone (pieces counted from the row's start),
+so every rank's rows are bit-identical to the 1-GPU result.
 
 Shards have unequal row counts. C is the caller's contiguous [m, K] matrix
 on every rank: the kernel writes this rank's rows in place, and the exchange
@@ -42,13 +42,17 @@ class Shard:
     bounds: np.ndarray      # [world+1] row bounds (nnz-balanced)
     row0: int
     row1: int
-    rowptr: np.ndarray      # local CSR, rebased to 0
-    colind: np.ndarray
+    rowptr: np.ndarray      # local CSR, rebased to pad = (global offset mod 64)
+    colind: np.ndarray      # pad leading filler entries (never read), then the rows'
     val: np.ndarray
 
     @property
     def rows(self) -> int:
         return self.row1 - self.row0
+
+    @property
+    def nnz(self) -> int:
+        return int(self.rowptr[-1] - self.rowptr[0])
 
     @property
     def max_rows(self) -> int:
@@ -57,12 +61,19 @@ class Shard:
 
 def make_shard(rowptr: np.ndarray, colind: np.ndarray, val: np.ndarray, rank: int,
                world: int) -> Shard:
-    """Cut rank's row range out of a global CSR (host side)."""
+    """Cut rank's row range out of a global CSR (host side). The local arrays
+    keep every nonzero's array position mod 64 (pad filler entries in front,
+    rowptr starting at pad): the K <= 64 lane-group kernel sums a row in
+    chains by array position mod its group count, so the shard's rows are
+    then bit-identical to the whole matrix's at every K."""
     bounds = prep.partition_rows(rowptr, world)
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
     j0, j1 = int(rowptr[r0]), int(rowptr[r1])
-    lrp = (rowptr[r0:r1 + 1] - j0).astype(np.int32)
-    return Shard(rank, world, bounds, r0, r1, lrp, colind[j0:j1], val[j0:j1])
+    pad = j0 % 64
+    lrp = (rowptr[r0:r1 + 1] - (j0 - pad)).astype(np.int32)
+    lci = np.concatenate([np.zeros(pad, colind.dtype), colind[j0:j1]])
+    lv = np.concatenate([np.zeros(pad, val.dtype), val[j0:j1]])
+    return Shard(rank, world, bounds, r0, r1, lrp, lci, lv)
 
 
 def stacked_block(n: int, nnz: int, max_deg: int, rank: int, world: int, seed: int = 1234,

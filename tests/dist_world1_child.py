@@ -74,6 +74,7 @@ def main() -> None:
     res["chunks4_within_bar"] = bool((err <= 2e-5 * absd + 1e-30).all())
     res["chunks4_max_rel"] = float((err / (absd + 1e-30)).max())
     res["chunks4_no_nan"] = not bool(torch.isnan(C4).any())
+    res["chunks4_bit_identical"] = bool(torch.equal(C4, Cw))
     res["exchange_requests_world1"] = len(sdist.exchange_chunk(C4, shard, 0, nch))
     t = torch.tensor([1.5, 2.5], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

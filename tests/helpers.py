@@ -39,6 +39,8 @@ def load_oracle() -> ctypes.CDLL:
         "oracle_random_array": (None, [I64, F, F, P]),
         "oracle_random_csr": (I64, [I, I, F, F, F, P, P, P, I64]),
         "oracle_csrmm_f32": (None, [I, I, P, P, P, I, P, I, I, F, F, P, I, I]),
+        "oracle_csrmm_pieces_f32": (None, [I, I, P, P, P, I, P, I, I, F, F, P, I, I]),
+        "oracle_csr_piece_len": (I, [I]),
         "oracle_csrmm_f64": (None, [I, I, P, P, P, I, P, I, I, P, P]),
         "oracle_csrmm_d": (None, [I, I, P, P, P, I, P, I, I, ctypes.c_double, ctypes.c_double,
                                   P, I, I]),
@@ -90,6 +92,25 @@ def oracle_csrmm_f32(L, m, n, rowptr, colind, val, B, ldb, order_b, alpha=1.0, b
     C = np.ascontiguousarray(C, np.float32).copy()
     L.oracle_csrmm_f32(m, n, ptr(rowptr), ptr(colind), ptr(val), base, ptr(B), ldb, order_b,
                        alpha, beta, ptr(C), ldc, order_c)
+    return C
+
+
+def oracle_csrmm_pieces_f32(L, m, n, rowptr, colind, val, B, ldb, order_b, alpha=1.0,
+                            beta=0.0, C=None, ldc=None, order_c=0, base=0):
+    """The HIP CSR kernels' association: sequential fp32 FMA
+    chains over pieces of max(128, ceil(L / 16)) nonzeros from each row's start,
+    added left to right; the main kernel matches it bit for bit at any grid."""
+    rowptr = np.ascontiguousarray(rowptr, np.int32)
+    colind = np.ascontiguousarray(colind, np.int32)
+    val = np.ascontiguousarray(val, np.float32)
+    B = np.ascontiguousarray(B, np.float32)
+    if ldc is None:
+        ldc = n if order_c == 0 else m
+    if C is None:
+        C = np.zeros(m * ldc if order_c == 0 else n * ldc, np.float32)
+    C = np.ascontiguousarray(C, np.float32).copy()
+    L.oracle_csrmm_pieces_f32(m, n, ptr(rowptr), ptr(colind), ptr(val), base, ptr(B), ldb,
+                              order_b, alpha, beta, ptr(C), ldc, order_c)
     return C
 
 

@@ -72,7 +72,7 @@ def _worker(rank, world, port, q):
             buf = torch.full((n, K), float("nan"))
             Cc = sdist.chunked_spmm(sh, buf, compute_chunk, nch)
             ok = ok and bool(np.array_equal(Cc.numpy(), full))
-        q.put((rank, ok, sh.bounds.tolist(), int(sh.colind.size)))
+        q.put((rank, ok, sh.bounds.tolist(), sh.nnz))
     finally:
         dist.destroy_process_group()
 

@@ -1414,6 +1414,47 @@ def test_bsrmm_grouped_f32(oracle, device, W, n, ob, oc, alpha, beta, direction)
     grp.close()
 
 
+@pytest.mark.parametrize("bs", [32, 16])
+def test_group_analysis_size_query_recomputes(device, bs):
+    """A size query abandoned on one matrix, then the values changed in place
+    (same addresses, other zero columns, as a caching allocator hands out), a
+    new size query and the fill: the buffer equals a fresh handle's analysis of
+    the new values byte for byte (every size query recomputes; group.cpp)."""
+    from ctypes import byref, c_size_t
+    from spmm_hip._lib import lib
+    ops = _ops()
+    rng = np.random.default_rng(77 + bs)
+    mb, kb = 23, 30
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.3)
+    nnzb = ci.size
+    keep = rng.random((nnzb, 1, bs)) >= 0.6  # other columns of every block zero
+    v2 = (rng.uniform(-1, 1, (nnzb, bs, bs)) * keep).astype(np.float32).reshape(-1)
+    vt = np.float16 if bs == 16 else np.float32
+    drp, dci, dv = _dev(rp, ci, v.astype(vt))
+    h, fresh_h = ops.Handle(), ops.Handle()
+    fn = getattr(lib(), "spmm_bsr16_group_analysis_f16" if bs == 16 else
+                 "spmm_bsr32_group_analysis_f32")
+    grp_cls = ops.GroupedBsr16 if bs == 16 else ops.GroupedBsr32
+
+    def args():
+        return (h.raw, ops.DIRECTION_ROW, mb, nnzb, 2, ops._ptr(drp), ops._ptr(dci), ops._ptr(dv))
+    size = c_size_t(0)
+    assert fn(*args(), None, byref(size)) == 0  # the query on the first values, abandoned
+    dv.copy_(torch.from_numpy(v2.astype(vt)))
+    size2 = c_size_t(0)
+    assert fn(*args(), None, byref(size2)) == 0
+    buf = torch.empty(max(size2.value, 1), dtype=torch.uint8, device=device)
+    assert fn(*args(), ops._ptr(buf), byref(size2)) == 0
+    fresh = grp_cls(drp, dci, dv, mb=mb, group_rows=2, handle=fresh_h)
+    torch.cuda.synchronize()
+    assert size2.value == fresh.bytes
+    assert torch.equal(buf[:size2.value], fresh.buffer[:fresh.bytes])
+    lib().spmm_bsr_group_release(h.raw, ops._ptr(buf))
+    fresh.close()
+    h.close()
+    fresh_h.close()
+
+
 def test_bsrmm_grouped_f32_checks(device):
     """A bs 16 analysis is not a bs 32 one; another mb, a kb below an analysed
     block column, a buffer without an analysis are INVALID_VALUE; W = 8 is

@@ -9,9 +9,9 @@
 * config 2: the ogbn-arxiv stand-in (n = 169,343, nnz = 1,166,243), K = 128,
   every element against the f64 oracle;
 * config 4: ogbn-products stand-in at K = 256, row-partitioned for 2 / 4 / 8
-  ranks on this one device (dist.make_shard, each shard into its slot of the
-  padded [world * max_rows, K] buffer the all-gather exchanges), reassembled
-  and compared with the whole-matrix run and sampled oracle rows; plus the
+  ranks on this one device (dist.make_shard, each shard written in place into
+  its rows of the contiguous C the exchange fills), bit-identical to the
+  whole-matrix run and checked on sampled oracle rows; plus the
   native single-process multi-GPU entry (spmm_csr_f32_multi over
   ncclCommInitAll on this box's one GPU).
 """
@@ -24,7 +24,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import TOL_F32, assert_normwise, oracle_csrmm_f64
+from helpers import TOL_F32, assert_normwise, oracle_csrmm_f64, oracle_csrmm_pieces_f32
 
 pytestmark = pytest.mark.gpu
 
@@ -83,7 +83,10 @@ def test_config2_arxiv_size(oracle, device):
     torch.cuda.synchronize()
     assert torch.equal(C, C2), "not deterministic"
     ref, absd = oracle_csrmm_f64(oracle, n, K, rp, ci, v, B, K, 0)
-    assert_normwise(C.cpu().numpy(), ref, absd, TOL_F32, "arxiv stand-in, every element")
+    got = C.cpu().numpy()
+    assert_normwise(got, ref, absd, TOL_F32, "arxiv stand-in, every element")
+    want = oracle_csrmm_pieces_f32(oracle, n, K, rp, ci, v, B, K, 0).reshape(n, K)
+    assert np.array_equal(got, want), "arxiv stand-in: not bit-identical to the piece oracle"
 
 
 @pytest.fixture(scope="module")
@@ -119,7 +122,6 @@ def test_config4_products_k256_row_shards(oracle, device, products_k256):
     drp, dci, dv = _dev(rp, ci, v)
     Cw = torch.empty((n, K), device=device)
     ops.csrmm(drp, dci, dv, B, n=K, k=n, ldb=K, C=Cw, ldc=K)
-    absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B.abs())
     del drp, dci, dv
     rng = np.random.default_rng(8)
     rows = _sample_rows(rp, n, rng)
@@ -137,8 +139,7 @@ def test_config4_products_k256_row_shards(oracle, device, products_k256):
             ops.csrmm(srp, sci, sv, B, m=sh.rows, n=K, k=n, ldb=K, C=C[sh.row0:sh.row1], ldc=K)
         torch.cuda.synchronize()
         assert C.shape == Cw.shape
-        err = (C - Cw).abs()
-        assert bool((err <= 2 * TOL_F32 * absd + 1e-30).all()), f"world {world} vs whole matrix"
+        assert torch.equal(C, Cw), f"world {world}: not bit-identical to the whole matrix"
         assert_normwise(C.cpu().numpy()[rows], ref, rabs, TOL_F32, f"world {world} sampled rows")
         assert [sh.rows for sh in shards] == list(np.diff(shards[0].bounds))
 
@@ -148,9 +149,9 @@ def test_config4_native_multi_entry(oracle, device, products_k256, chunks):
     """spmm_csr_f32_multi (include/spmm_multi.h) over ncclCommInitAll on this
     box's one GPU: the chunks' kernels write straight into the n x K C and
     run the per-chunk event chain of P > 1 (a one-part call has no peer to
-    exchange with). One chunk is the same kernel on the same rows as the
-    whole-matrix call (bit-identical); four chunks agree within the fp32
-    bar. The output is C itself: nothing past row n is written."""
+    exchange with). Any chunking is bit-identical to the whole-matrix call
+    (pieces: the association is the row's). The output is C itself: nothing
+    past row n is written."""
     from spmm_hip import ops, prep
     rp, ci, v, K = products_k256
     n = rp.size - 1
@@ -171,12 +172,7 @@ def test_config4_native_multi_entry(oracle, device, products_k256, chunks):
     assert 0 < comp[0] <= tot[0]
     torch.cuda.synchronize()
     assert bool(torch.isnan(Cm[n]).all())
-    got = Cm[:n]
-    if chunks == 1:
-        assert torch.equal(got, Cw)
-    else:
-        absd = ops.gespmm_csrmm(drp, dci, dv.abs(), B.abs())
-        assert bool(((got - Cw).abs() <= 2 * TOL_F32 * absd + 1e-30).all())
+    assert torch.equal(Cm[:n], Cw)
     mg.close()
 
 
@@ -249,4 +245,5 @@ def test_config4_torch_distributed_world1(tmp_path):
     assert res["backend"] == "nccl" and res["world"] == 1
     assert res["chunks1_bit_identical"]
     assert res["chunks4_within_bar"] and res["chunks4_no_nan"], res
+    assert res["chunks4_bit_identical"], res
     assert res["exchange_requests_world1"] == 0 and res["allreduce_max_ok"]

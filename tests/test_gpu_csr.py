@@ -1,9 +1,11 @@
 """Path A parity on the GPU: CSR x dense through the C ABI vs the oracle.
 
 Bar (north_star): within 1e-5 norm-wise relative of the reference semantics
-(sequential fp32 FMA in CSR order, gespmm_csrmm.h:124-129); in practice every
-row finished by one wave is bit-identical to the sequential oracle, which is
-asserted separately for small problems."""
+(sequential fp32 FMA in CSR order, gespmm_csrmm.h:124-129). Beyond the bar the
+main kernel is bit-identical to the piece oracle (oracle_csrmm_pieces_f32,
+DESIGN.md §3c) at every grid, and so to the sequential oracle on every row of
+at most 128 nonzeros; the K <= 64 lane-group kernel gives the same bits at
+every grid and shard."""
 from __future__ import annotations
 
 import ctypes
@@ -11,7 +13,8 @@ import ctypes
 import numpy as np
 import pytest
 
-from helpers import TOL_F32, assert_normwise, oracle_csrmm_f32, oracle_csrmm_f64
+from helpers import (TOL_F32, assert_normwise, oracle_csrmm_f32, oracle_csrmm_f64,
+                     oracle_csrmm_pieces_f32)
 
 pytestmark = pytest.mark.gpu
 
@@ -40,7 +43,13 @@ def _dev(*arrs):
     return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
 
 
-def _check_rowmajor(oracle, rp, ci, val, B, C, what, exact_expected=False):
+def _main_kernel(n: int) -> bool:
+    """The launch runs csr_mergepath_kernel (not the K <= 64 lane-group kernel):
+    row-major B / C with ld = n, default options."""
+    return n > 64 or n % 4 != 0
+
+
+def _check_rowmajor(oracle, rp, ci, val, B, C, what, exact_expected=False, pieces_exact=None):
     m, n = C.shape
     ref32 = oracle_csrmm_f32(oracle, m, n, rp, ci, val, B, B.shape[1], 0).reshape(m, n)
     ref64, absd = oracle_csrmm_f64(oracle, m, n, rp, ci, val, B, B.shape[1], 0)
@@ -49,6 +58,11 @@ def _check_rowmajor(oracle, rp, ci, val, B, C, what, exact_expected=False):
     assert_normwise(got, ref32.astype(np.float64), absd, TOL_F32, what + " vs seq-f32")
     if exact_expected:
         assert np.array_equal(got, ref32), what + ": expected bit-exact sequential FMA"
+    if pieces_exact if pieces_exact is not None else _main_kernel(n):
+        pcs = oracle_csrmm_pieces_f32(oracle, m, n, rp, ci, val, B, B.shape[1], 0).reshape(m, n)
+        bad = np.flatnonzero(~np.all(got == pcs, axis=1))
+        assert bad.size == 0, (f"{what}: {bad.size} rows differ from the piece oracle, "
+                               f"first {bad[:5].tolist()}")
     return float(np.mean(got == ref32))
 
 
@@ -145,12 +159,13 @@ def test_power_law_hubs_and_empty_rows(oracle, device, K):
     _ops().csrmm(drp, dci, dv, dB, n=K, k=5000, ldb=K, C=C, ldc=K, handle=h)
     torch.cuda.synchronize()
     _check_rowmajor(oracle, rp, ci, v, B, C, f"hubs K={K}")
-    # a second, differently cut grid gives the same answer up to carries
-    h.set_csr_waves_per_cu(32)
-    C2 = torch.empty_like(C)
-    _ops().csrmm(drp, dci, dv, dB, n=K, k=5000, ldb=K, C=C2, ldc=K, handle=h)
-    torch.cuda.synchronize()
-    _check_rowmajor(oracle, rp, ci, v, B, C2, f"hubs K={K} 32 waves/CU")
+    # differently cut grids give the same bits (pieces: the association is the row's)
+    for wpc in (32, 3):
+        h.set_csr_waves_per_cu(wpc)
+        C2 = torch.empty_like(C)
+        _ops().csrmm(drp, dci, dv, dB, n=K, k=5000, ldb=K, C=C2, ldc=K, handle=h)
+        torch.cuda.synchronize()
+        assert torch.equal(C, C2), f"K={K}: {wpc} waves/CU differs from 1"
 
 
 def test_unsplit_rows_bit_exact(oracle, device):
@@ -330,13 +345,14 @@ def test_products_scale_properties(oracle, device):
     assert bool((lin <= 3 * TOL_F32 * absd_full + 1e-30).all())
 
 
-def test_row_shards_match_whole_matrix(oracle, device):
+@pytest.mark.parametrize("K", [128, 32, 36])
+def test_row_shards_match_whole_matrix(oracle, device, K):
     """SURVEY §8e on one device: the rows of each nnz-balanced shard computed
-    alone equal the whole-matrix result — bit for bit where no wave splits
-    the row, within the fp32 bar everywhere."""
+    alone equal the whole-matrix result bit for bit (main kernel at K = 128 /
+    36, lane-group kernel at K = 32 on residue-preserving shard arrays)."""
     from spmm_hip import dist as sdist
     rng = np.random.default_rng(21)
-    m, k, K = 6000, 6000, 128
+    m, k = 6000, 6000
     rp, ci, v = _rand_csr(rng, m, k, 20, hub_rows=(10, 2500, 5999), hub_deg=3000)
     B = rng.uniform(-1, 1, (k, K)).astype(np.float32)
     drp, dci, dv, dB = _dev(rp, ci, v, B)
@@ -358,10 +374,8 @@ def test_row_shards_match_whole_matrix(oracle, device):
     for r0, r1, Cs in parts:
         got = Cs.cpu().numpy()
         assert_normwise(got, ref[r0:r1], absd[r0:r1], TOL_F32, f"shard {r0}:{r1}")
-        # Rows differ only where a wave boundary cuts them in one run or the
-        # other (one row per boundary, ~1 boundary per 512 rows + nnz here).
         same = np.all(got == whole[r0:r1], axis=1)
-        assert same.mean() > 0.9, (r0, r1, same.mean())
+        assert same.all(), (r0, r1, np.flatnonzero(~same)[:5])
 
 
 def test_permutation_invariance(oracle, device):
@@ -395,10 +409,9 @@ def test_colmajor_forms_match_rowmajor(device, m, K, beta):
     """cusparseScsrmm's layout (run_csrmm.cu:135-137: column-major B and C) at
     sizes where the staging transposes run many tiles, edge tiles and both the
     16-byte and the scalar transpose kernels: B transposed and C transposed
-    back are exact copies and the product is the same kernel, so the result is
-    bit-identical to the row-major call at beta = 0 (with beta, a row split
-    across waves adds its carries after beta * C in one form and before it in
-    the other: equal to rounding)."""
+    back are exact copies, the product is the same kernel and the transpose's
+    fma(beta, C, x) is the kernel's own epilogue, so the result is bit-identical
+    to the row-major call at every beta."""
     from spmm_hip import prep
     ops = _ops()
     rp, ci = prep.powerlaw_csr(m, 12 * m, 3000, 2.3, 3)
@@ -413,74 +426,23 @@ def test_colmajor_forms_match_rowmajor(device, m, K, beta):
     ops.csrmm(drp, dci, dv, dBc, n=K, k=m, ldb=m, order_b=ops.ORDER_COL, C=dCc, ldc=m,
               order_c=ops.ORDER_COL, beta=beta)
     torch.cuda.synchronize()
-    if beta == 0.0:
-        assert torch.equal(dCc.t(), dC)
-    else:  # rows split across waves associate beta * C with the carries differently
-        assert torch.allclose(dCc.t(), dC, rtol=1e-6, atol=1e-5)
-
-
-def merge_path_model(oracle, rp, ci, v, B, nwaves, alpha=1.0, beta=0.0, C0=None):
-    """C of the merge-path kernel restated on the host (csr_kernels.hip): the
-    (rows + nnz) path cut at diagonals w * per, per =
-    ceil((m + nnz) / nwaves); nnz j of row r lies in wave (r + j) // per and
-    the row's end in wave (r + re) // per. A row inside one wave is one
-    sequential fp32 FMA chain (gespmm_csrmm.h:124-129); a row split over waves
-    w_a .. w_b is ((c_a + c_{a+1}) + ... + c_{b-1}) + head, each term the chain
-    over that wave's share, the head (wave w_b's share) possibly empty.
-    Epilogue (alpha, beta, the old C0): an unsplit row is fma(beta, old,
-    alpha * acc) (alpha * acc at beta 0); a split row's last arrival writes
-    fma(alpha, sum, e), e = fma(beta, old, alpha * head) (alpha * head at beta
-    0). Restated in float32 numpy, so alpha and beta must be powers of two
-    (every product exact: each fma is one rounding of an exact sum, as
-    numpy's add)."""
-    for x in (alpha, beta):
-        assert x == 0 or float(np.log2(abs(x))).is_integer(), "alpha / beta: powers of two"
-    a32, b32 = np.float32(alpha), np.float32(beta)
-    m, K = rp.size - 1, B.shape[1]
-    nnz = int(rp[-1])
-    per = -(-(m + nnz) // nwaves)
-    seg_rp, seg_of = [0], []  # segments: CSR of sub-rows; row -> its segment ids
-    for r in range(m):
-        rs, re = int(rp[r]), int(rp[r + 1])
-        wa, wb = (r + rs) // per, (r + re) // per
-        ids = []
-        for w in range(wa, wb + 1):
-            lo, hi = max(rs, w * per - r), min(re, (w + 1) * per - r)
-            ids.append(len(seg_rp) - 1)
-            seg_rp.append(seg_rp[-1] + max(0, hi - lo))
-        seg_of.append(ids)
-    seg_rp = np.asarray(seg_rp, np.int32)
-    S = oracle_csrmm_f32(oracle, seg_rp.size - 1, K, seg_rp, ci, v, B, K, 0).reshape(-1, K)
-    C = np.empty((m, K), np.float32)
-
-    def epi(x, r):
-        return a32 * x if beta == 0.0 else b32 * C0[r] + a32 * x
-
-    for r, ids in enumerate(seg_of):
-        if len(ids) == 1:
-            C[r] = epi(S[ids[0]], r)
-            continue
-        acc = S[ids[0]].copy()
-        for s in ids[1:-1]:
-            acc = acc + S[s]
-        C[r] = a32 * acc + epi(S[ids[-1]], r)
-    return C
+    assert torch.equal(dCc.t(), dC)
 
 
 @pytest.mark.parametrize("K,opts,alpha,beta", [
     (128, 0, 1.0, 0.0), (512, 0, 1.0, 0.0), (256, 0, 1.0, 0.0), (32, 2, 1.0, 0.0),
     (64, 0, 1.0, 0.0), (128, 0, 2.0, 0.5), (512, 0, -0.5, 2.0), (256, 0, 0.25, -1.0),
-    (32, 2, 2.0, -0.5), (64, 0, -2.0, 0.5), (64, 0, 0.7, -1.3), (128, 0, 0.7, -1.3)])
-def test_split_rows_bit_exact_model(oracle, device, K, opts, alpha, beta):
-    """Every row, split or not, is bit-identical to merge_path_model: the
-    split rows finished in the same launch by their last-arriving wave (split
-    row tickets, csr_kernels.hip) sum their partials in wave order. Power-law
-    rows with hubs that span dozens of waves, empty rows, K at every vector
-    width of the main kernel (K = 32 with SPMM_CSR_SEQUENTIAL_ROWS; K = 64 is
-    the lane-group kernel, whose rows are interleaved chains: checked within
-    the bar). alpha != 1 and beta != 0 (a finite C0 read by the finishing
-    wave): bit-exact for powers of two, within the bar against the f64
-    oracle of alpha A B + beta C0 for any other pair."""
+    (32, 2, 2.0, -0.5), (64, 0, -2.0, 0.5), (64, 0, 0.7, -1.3), (128, 0, 0.7, -1.3),
+    (130, 0, 0.7, -1.3), (36, 0, 1.0, 0.0)])
+def test_split_rows_bit_exact_pieces(oracle, device, K, opts, alpha, beta):
+    """Every row, split over waves or not, is bit-identical to the piece oracle
+    (oracle_csrmm_pieces_f32): pieces of a split row stored by their waves and
+    added in piece order by the last arrival (split-row tickets,
+    csr_kernels.hip), at any alpha / beta (a finite C0 read by the finishing
+    wave). Power-law rows with hubs spanning dozens of waves, empty rows, K at
+    every vector width of the main kernel (K = 32 with SPMM_CSR_SEQUENTIAL_ROWS);
+    K = 64 / 36 run the lane-group kernel, whose pieces are interleaved chains:
+    within the bar, and the same bits at every grid."""
     from spmm_hip import prep
     from spmm_hip._lib import CSR_NT_STREAMS
     ops = _ops()
@@ -500,26 +462,45 @@ def test_split_rows_bit_exact_model(oracle, device, K, opts, alpha, beta):
     got = C.cpu().numpy()
     cus = torch.cuda.get_device_properties(device).multi_processor_count
     nwaves = min(-(-(m + ci.size) // 256), cus * 16)  # kMinItemsPerWave, csr_kernels.hip
-    pow2 = all(x == 0 or float(np.log2(abs(x))).is_integer() for x in (alpha, beta))
-    if K == 64 or not pow2:
+    per = -(-(m + ci.size) // nwaves)
+    split = np.array([(r + rp[r]) // per != (r + rp[r + 1]) // per for r in range(m)])
+    assert split.sum() > 50, "the case must split many rows"
+    if not _main_kernel(K) and not opts:  # the lane-group kernel
         ref, absd = oracle_csrmm_f64(oracle, m, K, rp, ci, v, B, K, 0)
         ref = alpha * ref + beta * C0.astype(np.float64)
         absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
         assert_normwise(got, ref, absd, TOL_F32, f"K={K} alpha={alpha} beta={beta}, split rows")
-        return
-    want = merge_path_model(oracle, rp, ci, v, B, nwaves, alpha, beta, C0)
-    per = -(-(m + ci.size) // nwaves)
-    split = np.array([(r + rp[r]) // per != (r + rp[r + 1]) // per for r in range(m)])
-    assert split.sum() > 50, "the case must split many rows"
-    bad = ~(got == want)
-    assert not bad.any(), (f"K={K}: {int(bad.any(axis=1).sum())} rows differ from the merge-path "
-                           f"model ({int(bad[split].any(axis=1).sum())} of {int(split.sum())} "
-                           f"split rows)")
-    # repeated launches: the tickets are back at zero after every launch
-    for _ in range(3):
+        want = got
+    else:
+        want = oracle_csrmm_pieces_f32(oracle, m, K, rp, ci, v, B, K, 0, alpha=alpha, beta=beta,
+                                       C=C0).reshape(m, K)
+        bad = ~(got == want)
+        assert not bad.any(), (f"K={K}: {int(bad.any(axis=1).sum())} rows differ from the piece "
+                               f"oracle ({int(bad[split].any(axis=1).sum())} of "
+                               f"{int(split.sum())} split rows)")
+    # repeated launches (tickets back at zero after every launch) and other grids
+    for wpc in (16, 16, 1, 5, 32):
+        h.set_csr_waves_per_cu(wpc)
         C = init()
         ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=C, ldc=K, alpha=alpha, beta=beta,
                   handle=h)
-    torch.cuda.synchronize()
-    assert np.array_equal(C.cpu().numpy(), want), "relaunch differs"
+        torch.cuda.synchronize()
+        assert np.array_equal(C.cpu().numpy(), want), f"{wpc} waves/CU differs"
     h.close()
+
+
+def test_dropin_equals_ex_entry(device):
+    """gespmm_csrmm (grid sized without nnz) and spmm_csrmm_ex_f32 (grid from
+    nnz) give the same bits: the association is the row's, not the grid's."""
+    from spmm_hip import prep
+    ops = _ops()
+    for m, nnz, K in ((20000, 400000, 128), (20000, 400000, 32), (6000, 900000, 256)):
+        rp, ci = prep.powerlaw_csr(m, nnz, m // 2, 2.1, 5)
+        v = np.random.default_rng(6).uniform(-1, 1, ci.size).astype(np.float32)
+        B = np.random.default_rng(7).uniform(-1, 1, (m, K)).astype(np.float32)
+        drp, dci, dv, dB = _dev(rp, ci, v, B)
+        Cd = ops.gespmm_csrmm(drp, dci, dv, dB)
+        Cx = torch.empty_like(Cd)
+        ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=Cx, ldc=K)
+        torch.cuda.synchronize()
+        assert torch.equal(Cd, Cx), (m, nnz, K)

@@ -54,8 +54,34 @@ def main():
                 ops.csrmm_hot(drp, tag, dv, Bn, n=K, k=n, ldb=K, C=Ch, ldc=K)
                 return Ch
             bad += check("csr K=128 (hot-column hints)", run_hot, reps)
-            bad += int((run_hot() != ops.gespmm_csrmm(drp, dci, dv, Bn)).sum())
-            del Bn, tag, Ch
+            ref = ops.gespmm_csrmm(drp, dci, dv, Bn)
+            bad += int((run_hot() != ref).sum())
+            # grid independence: other grids, the _ex entry, row shards
+            from spmm_hip import dist as sdist
+            for wpc in (4, 16, 32):
+                hx = ops.Handle()
+                hx.set_csr_waves_per_cu(wpc)
+                ops.csrmm(drp, dci, dv, Bn, n=K, k=n, ldb=K, C=Ch, ldc=K, handle=hx)
+                torch.cuda.synchronize()
+                d = int((Ch != ref).sum())
+                print(f"csr K=128 _ex entry, {wpc} waves/CU vs the drop-in: {d} differing",
+                      flush=True)
+                bad += d
+                hx.close()
+            for world in (2, 8):
+                Ch.fill_(float("nan"))
+                for r in range(world):
+                    sh = sdist.make_shard(rp, ci, v, r, world)
+                    srp, sci, sv = [torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                                    for a in (sh.rowptr, sh.colind, sh.val)]
+                    ops.csrmm(srp, sci, sv, Bn, m=sh.rows, n=K, k=n, ldb=K,
+                              C=Ch[sh.row0:sh.row1], ldc=K)
+                torch.cuda.synchronize()
+                d = int((Ch != ref).sum())
+                print(f"csr K=128 {world} row shards vs the whole matrix: {d} differing",
+                      flush=True)
+                bad += d
+            del Bn, tag, Ch, ref
         bad += check(f"csr2bsr bs={bs} (values)",
                      lambda: ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)[2], 2)
         brp, bci, bval = ops.csr2bsr(drp, dci, dv, m=n, n=n, bs=bs)
