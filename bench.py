@@ -1028,6 +1028,9 @@ def run_bsr(args, W, world, rank, dev, dist):
             fn(d_brp, d_bci, d_bv, B, mb=mb, kb=mb, n=K, bs=bs, ldb=K, C=C, ldc=K, handle=h)
 
     elapsed, kms = timed_loop(step, h, args.steps, args.warmup, 1, dist)
+    # bs 2 / 4 / 8 fp32: which kernel ran (the grouped MFMA stream from 2^20 blocks when its
+    # sharing probe keeps the matrix, else the lane-group VALU kernel; spmm_bsr_small_path)
+    small_path = h.small_bsr_path() if bs in (2, 4, 8) and dt == "fp32" and not an else None
     # The CSR path on the same matrix (the reference's question: does the
     # reordered BSR beat CSR?), fp32.
     d_rp, d_ci, d_v = (torch.from_numpy(a).to(dev) for a in (rp, ci, val))
@@ -1073,10 +1076,10 @@ def run_bsr(args, W, world, rank, dev, dist):
         # the same per nonzero column of a 32 x 32 sub-block
         mfma_flops = active_cols32 * 2.0 * 32 * K
     elif bs in (2, 4, 8) and dt == "fp32":
-        # the grouped small-bs stream (bsr_small_grp_kernel, when its sharing probe keeps the
-        # matrix, as on the reddit stand-in): two v_mfma_f32_32x32x1_2b_f32 per (32-row
-        # group, nonzero column) of the union and 128 output columns
-        mfma_flops = active_cols32 * 2.0 * 32 * K
+        # the grouped small-bs stream (bsr_small_grp_kernel) when it ran: two
+        # v_mfma_f32_32x32x1_2b_f32 per (32-row group, nonzero column) of the union and 128
+        # output columns; the lane-group VALU kernel runs no MFMA
+        mfma_flops = active_cols32 * 2.0 * 32 * K if small_path == 1 else None
     elif cs16:
         # column stream: items of 16 nonzero columns packed across blocks, one
         # v_mfma_f32_16x16x16_f16 per item and 16 output columns (the last
@@ -1084,11 +1087,10 @@ def run_bsr(args, W, world, rank, dev, dist):
         # for the columns it holds)
         mfma_flops = active_cols * 2.0 * bs * K
     else:
-        mfma_flops = dense_flops
+        mfma_flops = dense_flops if bs >= 16 or dt == "fp32" else None
     if grp is not None and bs == 16:
         # one v_mfma_f32_16x16x16_f16 per item, wave and 16 output columns
-        nitems = (grp.bytes - 256) // (64 + gw * 512)
-        mfma_flops = nitems * gw * 2.0 * 16 * 16 * K
+        mfma_flops = grp.nitems * gw * 2.0 * 16 * 16 * K
     # (bs 32 grouped: each wave runs the MFMAs of its own nonzero columns, the column
     # stream's count above)
     peak = MFMA_PEAK_TFLOPS[dt]
@@ -1115,7 +1117,8 @@ def run_bsr(args, W, world, rank, dev, dist):
               "bsr16_f16_cs_kernel" if cs16 else "bsr16_cm_kernel") if cm else
              # bs 2 / 4 / 8: the grouped MFMA stream (bsr_small_grp_kernel) on matrices whose
              # block rows share their columns, the lane-group kernel on the rest
-             f"bsr_small_grp_kernel<{bs}>" if bs in (2, 4, 8) and dt == "fp32" else
+             f"bsr_small_grp_kernel<{bs}>" if small_path == 1 else
+             f"bsr_small_kernel<{bs}> (lane-group VALU)" if small_path in (0, 2) else
              f"bsr{bs} register-fragment kernel")
     tkey = {"workload": args.workload, "kernel": kname, "K": K, "dtype": dt, "nnzb": nnzb,
             "layout_BC": args.bsr_layout,
@@ -1158,12 +1161,13 @@ def run_bsr(args, W, world, rank, dev, dist):
                       "SURVEY 8d full-panel model"),
                   "upper_GBps": round(cm_bytes / t / 1e9, 1),
                   "traffic_key": tkey,
-                  "mfma_executed_flops_per_launch": mfma_flops if bs >= 16 or dt == "fp32" else None,
+                  "mfma_executed_flops_per_launch": mfma_flops,
                   "mfma_executed_TFLOPs": (round(mfma_flops / t / 1e12, 2)
-                                           if bs >= 16 or dt == "fp32" else None),
+                                           if mfma_flops is not None else None),
                   "mfma_peak": peak,
                   "mfma_frac": (round(mfma_flops / t / 1e12 / peak, 4)
-                                if bs >= 16 or dt == "fp32" else None),
+                                if mfma_flops is not None else None),
+                  "small_bs_path": small_path,
                   "dense_block_equivalent_TFLOPs": round(dense_flops / t / 1e12, 2),
                   "full_panel_model_bytes_per_launch": kbytes,
                   "full_panel_model_GBps": round(kbytes / t / 1e9, 1)},
@@ -1187,7 +1191,7 @@ def run_bsr(args, W, world, rank, dev, dist):
                                                                    group_rows=0, handle=h))
         e_g, k_g = timed_loop(lambda: g4.mm(B, kb=mb, n=K, ldb=K, C=C, ldc=K), h, args.steps,
                               args.warmup, 1, dist)
-        ni = (g4.bytes - 256) // (64 + g4.W * 512)
+        ni = g4.nitems
         rec["grouped_entry"] = {
             "entry": f"spmm_bsr16_group_analysis_f16 (groupRows 0: the library chose "
                      f"{g4.W} block rows per group) once + spmm_bsrmm_grouped_f16 per step",
@@ -1259,6 +1263,44 @@ def run_bsr(args, W, world, rank, dev, dist):
             "mfma_frac": round(mfma_flops / t_an / 1e12 / peak, 4),
             **_side_traffic(args.workload + "_an", kname, K, dt, nnzb, comp_an, k_an)}
     return rec, None
+
+
+# BASELINE configs 3 and 5 and north_star's BSR target, measured beside the N = 1
+# headline (not `value`): each the drop-in call (spmm_bsrmm_ex_f32 / _f16, what
+# run_bsrmm.cu:148-171 calls) with its grouped and analysed entries
+BSR_SIDES = (("config3", "reddit_bsr32"), ("config5", "products_bsr16_f16"),
+             ("products_bsr32", "products_bsr32"))
+
+
+def bsr_side(args, workload: str, rank, dev, dist) -> dict:
+    """One BSR workload's line, compacted to what a side entry needs."""
+    import copy
+
+    import torch
+    a = copy.copy(args)
+    a.workload, a.K, a.dtype, a.group_rows, a.bsr_layout = workload, 0, None, 0, "row"
+    r, _ = run_bsr(a, WORKLOADS[workload], 1, rank, dev, dist)
+    rf = r["roofline"]
+    keys = ("entry", "group_rows", "ms_per_step", "kernel_ms", "analysis_ms_first_call",
+            "analysis_ms_repeat", "frac", "mfma_executed_TFLOPs", "mfma_frac", "traffic",
+            "traffic_GBps", "traffic_frac", "traffic_over_compulsory", "compulsory_bytes",
+            "epoch_loop")
+    out = {"workload": r["config"]["workload"], "data": r["data"],
+           "value": round(r["value"], 2), "unit": "GFLOP/s",
+           "ms_per_step": round(r["ms_per_step"], 4), "kernel": rf["kernel"],
+           "kernel_ms": rf["kernel_ms"], "roofline_frac": rf["frac"],
+           "bytes_per_launch": rf["bytes_per_launch"],
+           "mfma_executed_TFLOPs": rf["mfma_executed_TFLOPs"], "mfma_peak": rf["mfma_peak"],
+           "mfma_frac": rf["mfma_frac"], "traffic": rf["traffic"],
+           "traffic_frac": rf.get("traffic_frac"),
+           "traffic_over_compulsory": rf.get("traffic_over_compulsory"),
+           "nnzb": r["config"]["nnzb"], "block_fill": r["config"]["block_fill"],
+           "csr_same_matrix_ms": r["csr_same_matrix_ms"]}
+    for e in ("grouped_entry", "analysed_entry"):
+        if e in r:
+            out[e] = {k: r[e][k] for k in keys if k in r[e]}
+    torch.cuda.empty_cache()
+    return out
 
 
 def run_hybrid(args, W, world, rank, dev, dist):
@@ -1442,6 +1484,9 @@ def main() -> None:
                     help="SPMM_HYBRID_* flags (0 = library default, 1 = force fused, 2 = force two launches, "
                          "+4 = split-bf16 products in the dense-block part)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-bsr-sides", action="store_true",
+                    help="products_csr at N = 1: skip the config 3 / config 5 / products bs 32 "
+                         "side entries")
     ap.add_argument("--cpu-budget", type=float, default=6.0,
                     help="seconds of CPU work per cpu_baseline leg (row prefix rule)")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
@@ -1487,6 +1532,12 @@ def main() -> None:
     if weak and dist.is_initialized():
         runner = run_csr_weak
     rec, csr_inputs = runner(args, W, world, rank, dev, dist)
+    if world == 1 and args.workload == "products_csr" and not args.no_bsr_sides:
+        import torch
+        torch.cuda.empty_cache()
+        for key, wl in BSR_SIDES:
+            _progress(f"side entry {key}: {wl}")
+            rec[key] = bsr_side(args, wl, rank, dev, dist)
 
     if rank == 0:
         cpu = None

@@ -138,6 +138,15 @@ spmm_status_t spmm_set_csr_options(spmm_handle_t handle, int flags);
 #define SPMM_BSR_SMALL_GROUPED 2
 spmm_status_t spmm_set_bsr_options(spmm_handle_t handle, int flags);
 
+/* Which kernel the handle's last bs 2 / 4 / 8 fp32 product ran (a measurement
+ * aid: the choice does not change the result): *path = 0 the lane-group VALU
+ * kernel, 1 the grouped MFMA stream, 2 the grouped stream's branch whose
+ * sharing probe gave the matrix to the lane-group kernel, -1 no such product
+ * on this handle. Synchronises the handle's stream and reads the probe's sums
+ * back; call it right after the product (the next product on the handle
+ * reuses that scratch). */
+spmm_status_t spmm_bsr_small_path(spmm_handle_t handle, int* path);
+
 /* Build options of the loaded library (bit flags): SPMM_BUILD_TUNING is set
  * in an A/B build (make TUNING=1), whose kernel choice the environment may
  * override (SPMM_BSR_VARIANT, SPMM_BSR_ORDER, SPMM_CSR_GROUP_PD); a release

@@ -21,13 +21,17 @@
  * dimension ldc. Part p's local rows are cut into chunks of chunkRows =
  * spmm_multi_slot_rows(...) rows; with chunks > 1 the exchange of chunk c
  * (collective stream) runs while chunk c+1 is computed. The exchange moves
- * whole rows of ldc floats (the last row of a chunk n), so columns n..ldc-1
- * of another part's rows take that part's values.
+ * each chunk as one contiguous span of rows, so with ngpu > 1 C must be
+ * packed (ldc == n; SPMM_STATUS_NOT_SUPPORTED otherwise): padding columns
+ * between rows would travel with them and overwrite the caller's.
  *
- * Numerics: each device runs the 1-GPU kernel on its rows, so with
- * ngpu = 1 and chunks = 1 the result is bit-identical to spmm_csrmm_ex_f32 on
- * the whole matrix; otherwise a row is bit-identical unless a merge-path
- * wave boundary splits it (the carries' association depends on the shard).
+ * Numerics: each device runs the 1-GPU kernel on its rows, and the kernels
+ * associate a row's sum by the row alone (pieces from the row's start,
+ * DESIGN.md §3c), so C is bit-identical to spmm_csrmm_ex_f32 on the whole
+ * matrix for any ngpu, bounds and chunks — at n <= 64 (the lane-group
+ * kernel, whose chains follow array positions mod 64) when part p's arrays
+ * keep the whole matrix's nonzero positions mod 64 (views into the whole
+ * arrays, or copies offset as spmm_hip.dist.make_shard does).
  */
 #ifndef SPMM_MULTI_H
 #define SPMM_MULTI_H
@@ -76,7 +80,8 @@ int spmm_multi_slot_rows(int ngpu, const int* bounds, int chunks);
  *     arrays uploaded to device p works);
  *   partNnz[p]: host, rowPtr[p][rows_p] - rowPtr[p][0] (sizes the grid);
  *   B[p]: device p's replica of B, row-major, ldb >= n;
- *   C[p]: device p's m x n output, row-major, ldc >= n.
+ *   C[p]: device p's m x n output, row-major, ldc >= n (ldc == n when
+ *     ngpu > 1).
  * Asynchronous on the parts' streams; spmm_multi_synchronize waits. Status
  * behaviour of spmm_csrmm_ex_f32 for bad sizes / pointers. */
 spmm_status_t spmm_csr_f32_multi(spmm_multi_t ctx, int m, int n, int k, const int* bounds,

@@ -2648,6 +2648,13 @@ __global__ __launch_bounds__(256) void bsr_small_kernel(
 // there (a hub) made a 0.1-ms tail on reddit; the probes inside the stream itself cost 8-13 %
 // (their chains of dependent loads at every wave's start).
 constexpr unsigned kProbeUnit = 720720;  // lcm(1..16): 1 / holders for G <= 16 holders
+// the grouped stream gives the matrix up (to bsr_small_kernel) past kGiveUp union steps per
+// block; also evaluated on the host by spmm_bsr_small_path
+__host__ __device__ inline bool small_grp_gives_up(int bs, unsigned long long est,
+                                                   unsigned long long nv) {
+  const float kGiveUp = bs == 8 ? 0.70f : (bs == 4 ? 0.45f : 0.25f);
+  return (double)est > (double)kGiveUp * kProbeUnit * (double)nv;
+}
 
 template <int BS>
 __global__ __launch_bounds__(64) void small_grp_probe_kernel(int mb, int ngroups,
@@ -2731,8 +2738,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPMM_SGRP_OC
   // small_grp_probe_kernel's estimate of union steps per block: past kGiveUp the matrix is
   // left to bsr_small_kernel (its block rows share too little)
   {
-    constexpr float kGiveUp = BS == 8 ? 0.70f : (BS == 4 ? 0.45f : 0.25f);
-    if (SPMM_SGRP_PROBE && (double)stat[0] > (double)kGiveUp * kProbeUnit * (double)stat[1]) {
+    if (SPMM_SGRP_PROBE && small_grp_gives_up(BS, stat[0], stat[1])) {
       if (lane == 0) dirty[g * gridDim.y + blockIdx.y] = 1;
       return;
     }
@@ -3933,6 +3939,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     else if (crow) SGRP_ONE(BS_, false, true);                                                   \
     else SGRP_ONE(BS_, false, false);                                                            \
   } while (0)
+    ctx->small_path = 1;  // the probe's sums decide (spmm_bsr_small_path)
+    ctx->small_path_bs = bs;
     // the choice per matrix first (small_grp_probe_kernel), then the stream
     if (hipError_t e = hipMemsetAsync(stat, 0, 2 * sizeof(*stat), ctx->stream)) {
       timing_end(ctx, slot);
@@ -3976,6 +3984,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
 #undef SFIX_LAUNCH
 #undef SFIX_ONE
   } else if ((bs == 2 || bs == 4 || bs == 8) && brow && !dense_sem) {
+    ctx->small_path = 0;
     // the lane-group VALU kernel: 2 floats per lane when B allows 8-B gathers
     const bool v2 = n > 64 && n % 2 == 0 && ldb % 2 == 0 && aligned(B, 8);
     const dim3 grid((mb + 3) / 4, (n + (v2 ? 127 : 63)) / (v2 ? 128 : 64));
@@ -4292,3 +4301,17 @@ spmm_status_t launch_bsrmm_grouped_f16(spmm_context* ctx, int W, int mb, int n, 
 }
 
 }  // namespace spmm
+
+extern "C" spmm_status_t spmm_bsr_small_path(spmm_handle_t handle, int* path) {
+  if (!handle) return SPMM_STATUS_NOT_INITIALIZED;
+  if (!path) return SPMM_STATUS_INVALID_VALUE;
+  *path = handle->small_path;
+  if (handle->small_path != 1) return SPMM_STATUS_SUCCESS;
+  unsigned long long st[2] = {0, 0};
+  hipError_t e = hipMemcpyAsync(st, handle->scratch, sizeof(st), hipMemcpyDeviceToHost,
+                                handle->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(handle->stream);
+  if (e != hipSuccess) return spmm::from_hip(e);
+  if (SPMM_SGRP_PROBE && small_grp_gives_up(handle->small_path_bs, st[0], st[1])) *path = 2;
+  return SPMM_STATUS_SUCCESS;
+}

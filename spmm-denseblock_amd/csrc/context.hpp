@@ -31,6 +31,9 @@ struct spmm_context {
   int csr_flags = SPMM_CSR_NT_STREAMS;  // SPMM_CSR_* option bits (default: nt streams)
   int hybrid_flags = 0;                 // SPMM_HYBRID_* option bits
   int bsr_flags = 0;                    // SPMM_BSR_* option bits
+  // the last bs 2 / 4 / 8 fp32 product: -1 none, 0 the lane-group kernel, 1 the
+  // grouped stream's branch (its probe's sums, left at scratch[0..15], decide)
+  int small_path = -1, small_path_bs = 0;
 
   // Device workspace (grown, never shrunk; freed in spmm_destroy).
   void* ws = nullptr;

@@ -218,6 +218,8 @@ spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int*
     if (bounds[p + 1] < bounds[p] || partNnz[p] < 0) return SPMM_STATUS_INVALID_VALUE;
   if (m == 0 || n == 0) return SPMM_STATUS_SUCCESS;
   if (!rowPtr || !colInd || !val || !B || !C || ldb < n || ldc < n) return SPMM_STATUS_INVALID_VALUE;
+  // the exchange moves spans of whole rows: padding columns would overwrite the peers'
+  if (P > 1 && ldc != n) return SPMM_STATUS_NOT_SUPPORTED;
   for (int p = 0; p < P; ++p)
     if (!rowPtr[p] || !C[p] || (k > 0 && !B[p]) || (partNnz[p] > 0 && (!colInd[p] || !val[p])))
       return SPMM_STATUS_INVALID_VALUE;
@@ -228,10 +230,8 @@ spmm_status_t spmm_csr_f32_multi(spmm_multi_t c, int m, int n, int k, const int*
     lo = std::min(ch * cr, rows);
     hi = std::min(lo + cr, rows);
   };
-  // rows r0..r1 of a row-major C with leading dimension ldc as one span: whole
-  // rows of ldc floats, the last one n (the padding columns between the
-  // exchanged rows travel with them)
-  auto span = [&](int r0, int r1) { return (size_t)(r1 - r0 - 1) * ldc + n; };
+  // rows r0..r1 of the packed row-major C (ldc == n when P > 1) as one span
+  auto span = [&](int r0, int r1) { return (size_t)(r1 - r0) * n; };
   DeviceGuard guard;
   for (int p = 0; p < P; ++p) {
     auto& ev = c->chunk_done[p];

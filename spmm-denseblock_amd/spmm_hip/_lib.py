@@ -74,6 +74,7 @@ _PROTOS = {
     "spmm_set_hybrid_options": (c_int, [_P, c_int]),
     "spmm_set_bsr_options": (c_int, [_P, c_int]),
     "spmm_get_build_options": (c_int, []),
+    "spmm_bsr_small_path": (c_int, [c_void_p, c_void_p]),
     "spmm_gespmm_csrmm_f32": (c_int, [c_int, c_int, _P, _P, _P, _P, _P, _P]),
     "spmm_scsrmm": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, POINTER(c_float), _P,
                             _P, _P, _P, _P, c_int, POINTER(c_float), _P, c_int]),

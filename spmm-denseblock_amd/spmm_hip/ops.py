@@ -75,6 +75,15 @@ class Handle:
     def set_bsr_options(self, flags: int) -> None:
         check(lib().spmm_set_bsr_options(self._h, flags), "spmm_set_bsr_options")
 
+    def small_bsr_path(self) -> int:
+        """spmm_bsr_small_path: the kernel of the last bs 2 / 4 / 8 fp32 product
+        (0 lane-group VALU, 1 grouped MFMA stream, 2 grouped branch given up by
+        its probe, -1 none). Synchronises the handle's stream."""
+        from ctypes import byref, c_int
+        p = c_int(-1)
+        check(lib().spmm_bsr_small_path(self._h, byref(p)), "spmm_bsr_small_path")
+        return p.value
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             lib().spmm_destroy(self._h)
@@ -338,6 +347,11 @@ class _Grouped:
         self.bytes = size.value
         # block rows per group: the header's word 0 (the library's choice when group_rows = 0)
         self.W = int(buf[:4].view(torch.int32).item()) if size.value >= 4 else group_rows
+        # items: the last item pointer (item_ptr[ngroups] at byte 256 + 4 ngroups)
+        ng = -(-mb // self.W) if self.W > 0 else 0
+        off = 256 + 4 * ng
+        self.nitems = (int(buf[off:off + 4].view(torch.int32).item())
+                       if size.value >= off + 4 else 0)
 
     def mm(self, B: torch.Tensor, *, kb: int, n: int, ldb: int, C: torch.Tensor, ldc: int,
            order_b: int = ORDER_ROW, order_c: int = ORDER_ROW, alpha: float = 1.0,
