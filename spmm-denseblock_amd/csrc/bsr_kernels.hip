@@ -1026,8 +1026,14 @@ __global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int
 // br / 2, in that order, as if they were blocks of a bs-32 matrix whose
 // block columns are 2 bc and 2 bc + 1: virtual block index v, block v / 2,
 // sub-block column v & 1. mb is then the number of 32-row block rows.
+// C64 (n <= 64): a 64-column tile. Lane (j, h) loads one float of a B row
+// (column 2 j + h: the 64 lanes read 256 B) and each column of an item is ONE
+// v_mfma_f32_32x32x1_2b_f32 (block h of the instruction = column 2 j + h)
+// instead of two; the second accumulator is not kept. The 128-column tile
+// computed 128 columns at n = 64, half of them clamped copies (the reference's
+// own sweep at dim 64, benchmark.py:5-8: bs 32 and 64 took the dim-128 time).
 template <bool CROW, int XM, int P, int NA, bool O32 = false, bool PK = false, bool ANT = false,
-          bool MSK = false, bool SUB = false>
+          bool MSK = false, bool SUB = false, bool C64 = false>
 __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -1062,7 +1068,7 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
       k1 = rowptr[br + 1];
     }
   }
-  const int jt = blockIdx.y * 128;
+  const int jt = blockIdx.y * (C64 ? 64 : 128);
   const unsigned lds_a = (unsigned)reinterpret_cast<uintptr_t>(smem);
 
   int a_src[2];
@@ -1111,7 +1117,9 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   };
   const unsigned a_row = (unsigned)(j * 128);
   const int a_sw = (j >> 1) & 7;
-  const unsigned boff = 4u * (unsigned)min(jt + 4 * j + 2 * h, n - 2);  // byte offset in a row
+  // byte offset of this lane's B-row piece in a row (C64: one float, else two)
+  const unsigned boff = C64 ? 4u * (unsigned)min(jt + 2 * j + h, n - 1)
+                            : 4u * (unsigned)min(jt + 4 * j + 2 * h, n - 2);
   const size_t ldb4 = (size_t)ldb * 4;
   const unsigned ldb4u = (unsigned)ldb * 4u;
 
@@ -1152,15 +1160,16 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
       }
     }
   }
+  typedef typename std::conditional<C64, float, f32x2>::type brow_t;
   int kind[P], stamp[P];
-  float ra0[P], ra1[P];  // in flight: asm-only registers
-  f32x2 rb0[P], rb1[P];  // in flight: asm-only registers
+  float ra0[P], ra1[P];    // in flight: asm-only registers
+  brow_t rb0[P], rb1[P];   // in flight: asm-only registers
 #pragma unroll
   for (int s = 0; s < P; ++s) {
     kind[s] = 0;
     stamp[s] = -64;
     ra0[s] = ra1[s] = 0.f;
-    rb0[s] = rb1[s] = f32x2{0.f, 0.f};
+    rb0[s] = rb1[s] = brow_t{};
   }
 
   // next block: its column chunk, A landed, its mask, the copy of block k + DA
@@ -1216,8 +1225,18 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
            4u * (unsigned)(c & 3);
   };
   // B row c of the current block's panel into r (in flight: asm-only register)
-  auto load_row = [&](f32x2& r, int c) {
-    if constexpr (O32)
+  auto load_row = [&](brow_t& r, int c) {
+    if constexpr (C64 && O32)
+      asm volatile("global_load_dword %0, %1, %2"
+                   : "=&v"(r)
+                   : "v"(boff + (unsigned)c * ldb4u), "s"(bblk)
+                   : "memory");
+    else if constexpr (C64)
+      asm volatile("global_load_dword %0, %1, %2"
+                   : "=&v"(r)
+                   : "v"(boff), "s"(bblk + (size_t)c * ldb4)
+                   : "memory");
+    else if constexpr (O32)
       asm volatile("global_load_dwordx2 %0, %1, %2"
                    : "=&v"(r)
                    : "v"(boff + (unsigned)c * ldb4u), "s"(bblk)
@@ -1237,7 +1256,22 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
       // consume the item issued P steps ago. The asm runs for empty slots too
       // (their count is old: no wait), so on every path the slot's registers
       // are read by it before the produce step below writes them again.
-      {
+      if constexpr (C64) {
+        float b0, b1, a0, a1;
+        asm volatile(SPMM_VM_LADDER("%4")
+                     "s_waitcnt lgkmcnt(0)\n\t"
+                     "v_mov_b32 %0, %5\n\t"
+                     "v_mov_b32 %1, %6\n\t"
+                     "v_mov_b32 %2, %7\n\t"
+                     "v_mov_b32 %3, %8"
+                     : "=&v"(b0), "=&v"(b1), "=&v"(a0), "=&v"(a1)
+                     : "s"(nis - stamp[s]), "v"(rb0[s]), "v"(rb1[s]), "v"(ra0[s]), "v"(ra1[s])
+                     : "scc", "memory");
+        if (kind[s]) {
+          u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(a0, b0, u0, 0, 0, 0);
+          if (kind[s] == 2) u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(a1, b1, u0, 0, 0, 0);
+        }
+      } else {
         f32x2 b0, b1;
         float a0, a1;
         asm volatile(SPMM_VM_LADDER("%4")
@@ -1316,12 +1350,19 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
         }
       }
     }
-    asm volatile("" : "+a"(u0), "+a"(u1));
+    if constexpr (C64)
+      asm volatile("" : "+a"(u0));
+    else
+      asm volatile("" : "+a"(u0), "+a"(u1));
     if (fin) break;
   }
   // nothing is in flight after the last round; the full wait makes that
   // visible to the register check (tests/test_isa_waits.py)
-  if constexpr (MSK)
+  if constexpr (C64 && MSK)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0) : "v"(cnext), "v"(mnext) : "memory");
+  else if constexpr (C64)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0) : "v"(cnext) : "memory");
+  else if constexpr (MSK)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)"
                  : "+a"(u0), "+a"(u1)
                  : "v"(cnext), "v"(mnext)
@@ -1329,7 +1370,40 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   else
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : "v"(cnext) : "memory");
 
-  if constexpr (CROW) {
+  if constexpr (CROW && C64) {
+    // lane (j, h): rows (e & 3) + 8 (e >> 2) + 4 h, columns 2 j (block 0) and 2 j + 1
+    const int col = jt + 2 * j;
+    if (col >= n) return;
+    if (pidx >= 0) {  // a segment of a split row: the raw tile to its partial (128-float rows)
+      float* pt = part + ((size_t)pidx * gridDim.y + blockIdx.y) * 32 * 128;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+        *reinterpret_cast<f32x2*>(pt + row * 128 + 2 * j) = f32x2{u0[e], u0[16 + e]};
+      }
+      return;
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA -> AGPR read
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const size_t row = (size_t)br * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      f32x2* p = reinterpret_cast<f32x2*>(C + row * ldc + col);
+      f32x2 v;
+      asm volatile("v_accvgpr_read_b32 %0, %2\n\t"
+                   "v_accvgpr_read_b32 %1, %3"
+                   : "=v"(v[0]), "=v"(v[1])
+                   : "a"(u0[e]), "a"(u0[16 + e])
+                   : "memory");
+      if (beta == 0.f) {
+        v *= alpha;
+      } else {
+        const f32x2 c = *p;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
+      }
+      *p = v;
+    }
+  } else if constexpr (CROW) {
     const int col = jt + 4 * j;
     if (col >= n) return;
     if (pidx >= 0) {  // a segment of a split row: the raw tile to its partial
@@ -1376,14 +1450,19 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
-      tile[(4 * j) * kTs + row] = u0[e];
-      tile[(4 * j + 1) * kTs + row] = u1[e];
-      tile[(4 * j + 2) * kTs + row] = u0[16 + e];
-      tile[(4 * j + 3) * kTs + row] = u1[16 + e];
+      if constexpr (C64) {
+        tile[(2 * j) * kTs + row] = u0[e];
+        tile[(2 * j + 1) * kTs + row] = u0[16 + e];
+      } else {
+        tile[(4 * j) * kTs + row] = u0[e];
+        tile[(4 * j + 1) * kTs + row] = u1[e];
+        tile[(4 * j + 2) * kTs + row] = u0[16 + e];
+        tile[(4 * j + 3) * kTs + row] = u1[16 + e];
+      }
     }
     __builtin_amdgcn_s_waitcnt(0);
     const size_t row = (size_t)br * 32 + j;
-    for (int it = 0; it < 64; ++it) {
+    for (int it = 0; it < (C64 ? 32 : 64); ++it) {
       const int jl = 2 * it + h;
       if (jt + jl < n) {
         float* p = C + (size_t)(jt + jl) * ldc + row;
@@ -3797,37 +3876,56 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
         return st;
       }
       const dim3 g2(sg ? nsg : mb, grid.y);
-#define CS2_LAUNCH(...)                                                                          \
+      // n <= 64: the 64-column tile (C64; grid.y is 1 either way, so the segments'
+      // partial layout is the same)
+      const bool c64 = n <= 64;
+#define CS2_ONE(C64_, O32_, PK_, ANT_)                                                           \
   do {                                                                                           \
     if (crow)                                                                                    \
-      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, 6, 3, __VA_ARGS__>), g2, dim3(64), 0,   \
-                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
-                         ord, sg, pt, masks);                                                    \
+      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, 6, 3, O32_, PK_, ANT_, false, false,    \
+                                               C64_>),                                           \
+                         g2, dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,       \
+                         alpha, beta, C, ldc, ord, sg, pt, masks);                               \
     else                                                                                         \
-      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, 6, 3, __VA_ARGS__>), g2, dim3(64), 0,  \
-                         ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,   \
-                         ord, nullptr, nullptr, masks);                                          \
+      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, 6, 3, O32_, PK_, ANT_, false, false,   \
+                                               C64_>),                                           \
+                         g2, dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,       \
+                         alpha, beta, C, ldc, ord, nullptr, nullptr, masks);                     \
+  } while (0)
+#define CS2_LAUNCH(O32_, PK_, ANT_)                                                              \
+  do {                                                                                           \
+    if (c64) CS2_ONE(true, O32_, PK_, ANT_);                                                     \
+    else CS2_ONE(false, O32_, PK_, ANT_);                                                        \
+  } while (0)
+#define MSK_ONE(C64_, O32_)                                                                      \
+  do {                                                                                           \
+    if (crow)                                                                                    \
+      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, 6, 3, O32_, true, true, true, false,    \
+                                               C64_>),                                           \
+                         g2, dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,       \
+                         alpha, beta, C, ldc, ord, sg, pt, masks);                               \
+    else                                                                                         \
+      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, 6, 3, O32_, true, true, true, false,   \
+                                               C64_>),                                           \
+                         g2, dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,       \
+                         alpha, beta, C, ldc, ord, nullptr, nullptr, masks);                     \
   } while (0)
 #define MSK_LAUNCH(O32_)                                                                         \
   do {                                                                                           \
-    if (crow)                                                                                    \
-      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, 6, 3, O32_, true, true, true>), g2,     \
-                         dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha,    \
-                         beta, C, ldc, ord, sg, pt, masks);                                      \
-    else                                                                                         \
-      hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, 6, 3, O32_, true, true, true>), g2,    \
-                         dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha,    \
-                         beta, C, ldc, ord, nullptr, nullptr, masks);                            \
+    if (c64) MSK_ONE(true, O32_);                                                                \
+    else MSK_ONE(false, O32_);                                                                   \
   } while (0)
       // (4, 8 or 10 items in flight: 2.11-2.15 / 2.11-2.12 / 2.43 ms against 2.11 at 6 on
       // the products stand-in, profiles/r03_analysed_sweep.txt)
       if (msk && narrow) MSK_LAUNCH(true);
       else if (msk) MSK_LAUNCH(false);
 #undef MSK_LAUNCH
+#undef MSK_ONE
       else if (lv == kBsr32Cs) CS2_LAUNCH(true, true, true);
       else if (lv == kBsr32CsNoNt) CS2_LAUNCH(true, true, false);
       else CS2_LAUNCH(false, true, true);  // kBsr32CsWideLdb
 #undef CS2_LAUNCH
+#undef CS2_ONE
       if (spl)
         hipLaunchKernelGGL(seg_fixup_kernel, dim3(nspl, grid.y), dim3(256), 0, ctx->stream, n,
                            spl, pt, alpha, beta, C, ldc);
@@ -3844,16 +3942,22 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       timing_end(ctx, slot);
       return st;
     }
+#define SUB_ONE(CR_, O32_, C64_)                                                                 \
+  hipLaunchKernelGGL((bsr32_f32_cs2_kernel<CR_, 32, 6, 3, O32_, true, true, false, true, C64_>),  \
+                     g2, dim3(64), 0, ctx->stream, mb2, n, rowptr, colind, val, B, ldb, alpha,   \
+                     beta, C, ldc, ord, nullptr, nullptr, nullptr)
 #define SUB_LAUNCH(CR_, O32_)                                                                    \
-  hipLaunchKernelGGL((bsr32_f32_cs2_kernel<CR_, 32, 6, 3, O32_, true, true, false, true>), g2,    \
-                     dim3(64), 0, ctx->stream, mb2, n, rowptr, colind, val, B, ldb, alpha, beta, \
-                     C, ldc, ord, nullptr, nullptr, nullptr)
+  do {                                                                                           \
+    if (n <= 64) SUB_ONE(CR_, O32_, true);  /* the 64-column tile */                             \
+    else SUB_ONE(CR_, O32_, false);                                                              \
+  } while (0)
     if (crow) {
       if (narrow) SUB_LAUNCH(true, true); else SUB_LAUNCH(true, false);
     } else {
       if (narrow) SUB_LAUNCH(false, true); else SUB_LAUNCH(false, false);
     }
 #undef SUB_LAUNCH
+#undef SUB_ONE
   } else if (bs == 32 && vec_ok) {
     const int waves = n <= 32 ? 1 : (n <= 64 ? 2 : 4);
     dim3 grid(mb, (n + 32 * waves - 1) / (32 * waves));

@@ -569,6 +569,60 @@ def _column_sparse_bsr(rng, mb, kb, bs, p):
 @pytest.mark.parametrize("n", [64, 128, 264, 520])
 @pytest.mark.parametrize("layout", ["row", "col"])
 def test_column_sparse_blocks(oracle, device, bs, dtype, n, layout):
+    _column_sparse_blocks(oracle, device, bs, dtype, n, layout)
+
+
+@pytest.mark.parametrize("bs", [32, 64])
+@pytest.mark.parametrize("n", [64, 36, 8])
+@pytest.mark.parametrize("layout", ["row", "col"])
+def test_narrow_tile_bit_exact(oracle, device, bs, n, layout):
+    """n <= 64 runs the column stream's 64-column tile (bsr32_f32_cs2_kernel
+    C64, bs 32 and the bs 64 sub-block stream; the reference sweeps dim 64,
+    benchmark.py:5-8). Every column is the same MFMA chain as in the 128-column
+    tile: C equals the first n columns of the n = 128 product on [B | B2] bit
+    for bit, and the sequential fp32 oracle (rocsparse_bsrmm_template<float>'s
+    order) bit for bit; both layouts, alpha / beta on the column-major one."""
+    ops = _ops()
+    rng = np.random.default_rng(640 + n + bs)
+    mb, kb = 19, 40
+    rp, ci, v = _column_sparse_bsr(rng, mb, kb, bs, 0.35)
+    m, k = mb * bs, kb * bs
+    B = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    B2 = np.concatenate([B, rng.uniform(-1, 1, (k, 128 - n)).astype(np.float32)], axis=1)
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    alpha, beta = (1.0, 0.0) if layout == "row" else (0.5, -1.5)
+
+    def run(Bh, nn, c0):
+        ldb = nn
+        if layout == "row":
+            drp, dci, dv, dB = _dev(rp, ci, v, Bh.reshape(-1))
+            dC = torch.full((m * nn,), float("nan"), device=device)
+            ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=nn, bs=bs, ldb=ldb, C=dC, ldc=nn)
+            torch.cuda.synchronize()
+            return dC.cpu().numpy().reshape(m, nn)
+        drp, dci, dv, dB, dC = _dev(rp, ci, v, np.ascontiguousarray(Bh.T).reshape(-1),
+                                    np.ascontiguousarray(c0.T).reshape(-1))
+        ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=nn, bs=bs, ldb=k, order_b=ops.ORDER_COL,
+                  C=dC, ldc=m, order_c=ops.ORDER_COL, alpha=alpha, beta=beta)
+        torch.cuda.synchronize()
+        return dC.cpu().numpy().reshape(nn, m).T
+
+    got = run(B, n, C0)
+    C0w = np.concatenate([C0, np.zeros((m, 128 - n), np.float32)], axis=1)
+    wide = run(B2, 128, C0w)
+    assert np.array_equal(got, wide[:, :n]), "the 64-column tile differs from the 128-column one"
+    ref = oracle_bsrmm_f32(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0, alpha=alpha, beta=beta,
+                           C=C0.reshape(-1) if layout == "col" else None).reshape(m, n)
+    ref64, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
+    if layout == "col":
+        ref64 = alpha * ref64 + beta * C0.astype(np.float64)
+        absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+    assert_normwise(got, ref64, absd, TOL_F32, f"narrow tile bs={bs} n={n} {layout}")
+    if layout == "row":
+        assert np.array_equal(got, ref), "not the sequential fp32 chain"
+
+
+def _column_sparse_blocks(oracle, device, bs, dtype, n, layout):
     """Blocks with empty columns (the column-masked kernels fetch only the B
     rows of nonzero A columns and skip MFMA steps of empty ones): explicit
     zero blocks, single-column blocks, quarter-full and full blocks, empty

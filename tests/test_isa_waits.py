@@ -44,7 +44,7 @@ def bsr_asm() -> str:
 
 # The LDS-DMA kernels the library ships (bsr_kernels.hip dispatch): every
 # instantiation of each family must be audited.
-SHIPPED_DMA = {"bsr32_f32_lds_kernel": 6, "bsr32_f32_cs2_kernel": 10, "bsr16_cm_kernel": 8,
+SHIPPED_DMA = {"bsr32_f32_lds_kernel": 6, "bsr32_f32_cs2_kernel": 20, "bsr16_cm_kernel": 8,
                "bsr16_f16_grp_kernel": 6, "bsr32_f32_grp_kernel": 2,
                "bsr16_f16_cs_kernel": 6}
 
