@@ -1370,6 +1370,9 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
   else
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+a"(u0), "+a"(u1) : "v"(cnext) : "memory");
 
+  // Row-major C goes out non-temporal (C is written once and never re-read here: its
+  // lines would displace the B rows neighbouring block rows share; products stand-in
+  // 3.25 -> 3.15 ms, reddit unchanged, profiles/r06/ab_cs2b.log)
   if constexpr (CROW && C64) {
     // lane (j, h): rows (e & 3) + 8 (e >> 2) + 4 h, columns 2 j (block 0) and 2 j + 1
     const int col = jt + 2 * j;
@@ -1401,7 +1404,7 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
 #pragma unroll
         for (int i = 0; i < 2; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
       }
-      *p = v;
+      __builtin_nontemporal_store(v, p);
     }
   } else if constexpr (CROW) {
     const int col = jt + 4 * j;
@@ -1442,7 +1445,7 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
       }
-      *p = v;
+      __builtin_nontemporal_store(v, p);
     }
   } else {
     constexpr int kTs = 36;
