@@ -1,5 +1,5 @@
 #!/bin/bash
-# Closing pass on one GPU box (release library), round ${ROUND:-r05}: the whole GPU suite, smoke,
+# Closing pass on one GPU box (release library), round ${ROUND:-r06}: the whole GPU suite, smoke,
 # the default bench line (CPU baseline legs and side lines included) and its rocprofv3 kernel
 # trace, bench.py's N > 1 path rehearsed at world 1 through torch.distributed.run, every workload
 # line, counter bytes of every BSR / hybrid workload's kernel and of the plain and hot CSR
@@ -10,10 +10,10 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd); export TMPDIR=/tmp
-RD=${ROUND:-r05}
+RD=${ROUND:-r06}
 O=$R/gpurun_out/final_$RD; mkdir -p $O
 stop() { rc=$1; if [ "$rc" -ge 124 ]; then echo "GPU step fault rc=$rc, stopping"; exit "$rc"; fi; }
-BSR_WLS="reddit_bsr32 products_bsr32 reddit_bsr32_an products_bsr32_an reddit_bsr32_grp products_bsr32_grp products_bsr16_f16 products_bsr16_f16_an products_bsr16_f16_grp products_rcm_bsr16_f16_grp reddit_rcm_bsr32 reddit_rcm_bsr32_an products_rcm_bsr32_an reddit_bsr8 reddit_bsr4 reddit_bsr2 reddit_bsr64 reddit_bsr8_rb32 reddit_hybrid32 products_hybrid32"
+BSR_WLS="reddit_bsr32 products_bsr32 products_rcm_bsr16_f16 products_rcm_bsr32 reddit_bsr32_an products_bsr32_an reddit_bsr32_grp products_bsr32_grp products_bsr16_f16 products_bsr16_f16_an products_bsr16_f16_grp products_rcm_bsr16_f16_grp reddit_rcm_bsr32 reddit_rcm_bsr32_an products_rcm_bsr32_an reddit_bsr8 reddit_bsr4 reddit_bsr2 reddit_bsr64 reddit_bsr8_rb32 reddit_hybrid32 products_hybrid32"
 PH=${PHASE:-abpcs}
 if [[ $PH == *a* ]]; then
 echo "== gpu suite"
@@ -45,7 +45,7 @@ fi
 if [[ $PH == *c* ]]; then
 echo "== counter bytes, plain and hot CSR"
 rm -rf gpurun_out/pmcb/kt_products_csr* gpurun_out/pmcb/fetch_products_csr* gpurun_out/pmcb/write_products_csr*
-WLS="products_csr products_csr_hot" BENCH_EXTRA="--no-hot-side" bash tools/pmc_bytes.sh; stop $?
+WLS="products_csr products_csr_hot" BENCH_EXTRA="--no-hot-side --no-bsr-sides" bash tools/pmc_bytes.sh; stop $?
 cp gpurun_out/pmcb/bytes.jsonl $O/csr_bytes.jsonl
 echo "== determinism"; timeout -k 10 900 python tools/determinism.py 3 > $O/determinism.log 2>&1; rc=$?; tail -3 $O/determinism.log; stop $rc
 fi
