@@ -113,7 +113,7 @@ void oracle_csrmm_f32(int m, int n, const int* rowptr, const int* colind, const 
 // the row's start, each the sequential fp32 FMA chain of csrmm_seq above
 // (gespmm_csrmm.h:124-129), and the pieces are added left to right from -0.
 // Rows of at most 128 nonzeros are therefore exactly csrmm_seq's chain.
-int oracle_csr_piece_len(int L) { return std::max(128, (int)(((unsigned)L + 15u) >> 4)); }
+int oracle_csr_piece_len(int L) { return std::max(128, (int)(((unsigned)L + 63u) >> 6)); }
 
 void oracle_csrmm_pieces_f32(int m, int n, const int* rowptr, const int* colind,
                              const float* val, int base, const float* B, int ldb, int orderB,

@@ -168,7 +168,8 @@ spmm_status_t spmm_create(spmm_handle_t* handle) {
 
 spmm_status_t spmm_destroy(spmm_handle_t h) {
   if (!h) return SPMM_STATUS_NOT_INITIALIZED;
-  if (h->ws || h->scratch || h->order || h->tickets || h->grp_pend)
+  if (h->grp_cols) (void)hipFreeAsync(h->grp_cols, h->stream);
+  if (h->ws || h->scratch || h->order || h->tickets || h->grp_pend || h->grp_cols)
     (void)hipStreamSynchronize(h->stream);
   if (h->ws) (void)hipFree(h->ws);
   if (h->grp_pend) (void)hipFree(h->grp_pend);

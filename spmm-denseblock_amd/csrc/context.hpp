@@ -81,6 +81,9 @@ struct spmm_context {
   GroupPending grp_pending;
   void* grp_pend = nullptr;
   size_t grp_pend_bytes = 0;
+  // the compact column copy of a pending bs 32 ROW analysis (4 KB per block, stream-ordered
+  // allocation): freed by the filling call that uses it, or by the next size query
+  void* grp_cols = nullptr;
   std::mutex grp_mu;
 
   // Kernel timing ring.
@@ -201,6 +204,14 @@ spmm_status_t launch_scan_counts(spmm_context* ctx, const int* count, int n, int
 spmm_status_t launch_bsr32_grp_fill(spmm_context* ctx, long long nitems, int W, spmm_direction_t dir,
                                     const int* rows, const int* src, const float* val,
                                     float* afrag);
+// the bs 32 group analysis in one pass over A: masks plus the compact column copy of ROW
+// blocks (cols: nnzb * 1024 floats, or null), and the fill from those columns (masks: the
+// compact copy's ranks; null: cols = the COLUMN blocks' own values)
+spmm_status_t launch_grp_mask32(spmm_context* ctx, spmm_direction_t dir, int nnzb, const float* val,
+                                unsigned* masks, float* cols);
+spmm_status_t launch_bsr32_grp_fillc(spmm_context* ctx, long long nitems, int W, const int* rows,
+                                     const int* src, const float* cols, const unsigned* masks,
+                                     float* afrag);
 spmm_status_t launch_bsrmm_grouped_f32(spmm_context* ctx, int W, int mb, int n, int ngroups,
                                        const int* item_ptr, const int* rows,
                                        const unsigned* wmask, const float* afrag, const float* B,

@@ -120,7 +120,9 @@ __device__ __forceinline__ float rdlanef(float v, int l) {
 // summed by one wave, and C does not depend on the grid, on the rows around
 // the row (shards, chunks) or on the entry point.
 constexpr int kPieceMin = 128;
-constexpr int kPiecesLog = 4;
+// 64 pieces at most (16 in the first form: a hub row's pieces of ceil(L / 16) nonzeros put
+// up to 3.1x the mean share in one wave on the arxiv stand-in, 1.4x at 64)
+constexpr int kPiecesLog = 6;
 constexpr int kMaxPieces = 1 << kPiecesLog;
 
 __device__ __forceinline__ int piece_len(int L) {

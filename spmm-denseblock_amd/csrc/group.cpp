@@ -21,7 +21,11 @@
 //     the block of row w holding (J, c) (-1: none, or that block's column c is all
 //     zeros); grp_wmask_kernel then ORs the per-(item, wave) masks of the entries
 //     whose source is a block (the MFMAs that wave runs at bs 32);
-//  5. the fill kernels write each wave's A fragment of each item.
+//  5. the fill kernels write each wave's A fragment of each item. At bs 32 the size
+//     query's mask kernel (grp_mask32_kernel) also leaves a compact column-major copy of
+//     ROW blocks' nonzero columns in a transient stream-ordered allocation (4 KB per
+//     block, freed by the filling call), and the fill reads only those columns: one pass
+//     over A instead of two (COLUMN blocks: the fill reads their columns in place).
 // The filling call reuses the size query's device results (handle->grp_pending):
 // the arrays must not change between the two calls, as between cuSPARSE's
 // bufferSize and preprocess calls. It launches kernels and async copies only.
@@ -125,12 +129,29 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
     unsigned* dmk = reinterpret_cast<unsigned*>(pb);
     hipError_t e = hipMemsetAsync(pb + stat_off, 0, 32 * nc, st);
     if (e != hipSuccess) return from_hip(e);
+    // a previous size query's column copy (its filling call never came, or was captured)
+    if (handle->grp_cols) {
+      e = hipFreeAsync(handle->grp_cols, st);
+      handle->grp_cols = nullptr;
+      if (e != hipSuccess) return from_hip(e);
+    }
     if (nnzb > 0 && mb > 0) {
       const auto* v16 = static_cast<const uint16_t*>(bsrVal);
-      spmm_status_t s =
-          BS == 32 ? launch_bsr32_analysis(handle, dir, nnzb, static_cast<const float*>(bsrVal), dmk, nullptr)
-          : reinterpret_cast<uintptr_t>(bsrVal) % 16 == 0 ? launch_grp_mask16(handle, dir, nnzb, v16, dmk)
+      spmm_status_t s;
+      if (BS == 32) {
+        // ROW blocks: the compact column copy the fill reads (without the memory for it, the
+        // fill reads the blocks again)
+        if (dir == SPMM_DIRECTION_ROW &&
+            hipMallocAsync(&handle->grp_cols, (size_t)nnzb * 4096, st) != hipSuccess) {
+          (void)hipGetLastError();
+          handle->grp_cols = nullptr;
+        }
+        s = launch_grp_mask32(handle, dir, nnzb, static_cast<const float*>(bsrVal), dmk,
+                              static_cast<float*>(handle->grp_cols));
+      } else {
+        s = reinterpret_cast<uintptr_t>(bsrVal) % 16 == 0 ? launch_grp_mask16(handle, dir, nnzb, v16, dmk)
                                                           : launch_bsr16_analysis(handle, dir, nnzb, v16, dmk, nullptr);
+      }
       if (s) return s;
     }
     for (int i = 0; i < nc; ++i) {
@@ -237,14 +258,38 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
     if (spmm_status_t s = launch_grp_wmask(handle, nitems, W, E, dsrc,
                                            reinterpret_cast<unsigned*>(buf + pend.wmask_off)))
       return s;
-    spmm_status_t s = BS == 16
-        ? launch_bsr16_grp_fill(handle, nitems, W, dir, drows, dsrc,
+    float* afrag = reinterpret_cast<float*>(buf + pend.afrag_off);
+    // a captured fill reads the values themselves: a graph replayed later must not read the
+    // transient column copy, which the next size query frees
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const bool capturing =
+        hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+    spmm_status_t s;
+    if (BS == 16)
+      s = launch_bsr16_grp_fill(handle, nitems, W, dir, drows, dsrc,
                                 static_cast<const uint16_t*>(bsrVal),
-                                reinterpret_cast<unsigned*>(buf + pend.afrag_off))
-        : launch_bsr32_grp_fill(handle, nitems, W, dir, drows, dsrc,
-                                static_cast<const float*>(bsrVal),
-                                reinterpret_cast<float*>(buf + pend.afrag_off));
+                                reinterpret_cast<unsigned*>(afrag));
+    else if (dir == SPMM_DIRECTION_COLUMN)  // a column of a COLUMN block is contiguous
+      s = launch_bsr32_grp_fillc(handle, nitems, W, drows, dsrc, static_cast<const float*>(bsrVal),
+                                 nullptr, afrag);
+    else if (handle->grp_cols && !capturing)
+      s = launch_bsr32_grp_fillc(handle, nitems, W, drows, dsrc,
+                                 static_cast<const float*>(handle->grp_cols),
+                                 reinterpret_cast<const unsigned*>(pb), afrag);
+    else
+      s = launch_bsr32_grp_fill(handle, nitems, W, dir, drows, dsrc,
+                                static_cast<const float*>(bsrVal), afrag);
     if (s) return s;
+  }
+  // the column copy is spent; under stream capture it stays for the next size query (or
+  // spmm_destroy) to free, the free being no node of the caller's graph
+  if (handle->grp_cols && BS == 32) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+      hipError_t fe = hipFreeAsync(handle->grp_cols, st);
+      handle->grp_cols = nullptr;
+      if (fe != hipSuccess) return from_hip(fe);
+    }
   }
   std::lock_guard<std::mutex> lk(handle->mu);
   spmm_context::GroupPlan plan{W, mb, ngroups, nitems, pend.need, pend.rows_off, pend.afrag_off,

@@ -337,6 +337,119 @@ __global__ __launch_bounds__(64) void bsr32_grp_fill_kernel(long long nitems, in
     dst[((item0 + f) * W + w) * 64 + lane] = frag[f * 64 + lane];
 }
 
+// Round 6: the analysis in one pass over A. The column masks (grp_mask32_kernel, in the size
+// query) also write, for ROW blocks, a compact column-major copy of each block's nonzero
+// columns: block k's column c, when nonzero, at cols[k * 1024 + 32 p ..], p the rank of c
+// among the block's nonzero columns (a transient slot of 4 KB per block, of which only the
+// nonzero columns are written). The fill (bsr32_grp_fillc_kernel) then reads 128 B per entry
+// from it (COLUMN blocks: straight from the values, whose columns are contiguous) instead of
+// every held block's 4 KB: the analysis read A twice, once for the masks and once in the fill
+// above (1.24 + 1.80 ms of 3.36 on the reddit stand-in, 2.01 + 3.08 of 5.45 on products,
+// profiles/r05c/grp_b6_mask32_tried.txt). The fragments are the same bytes either way.
+// One wave per block, four per workgroup; ROW: lane (j, h) loads row j, columns 16h .. 16h + 15
+// (four 16-B loads), a ballot per column pair (i, 16 + i) gives both bits, and each nonzero
+// column goes out as one 128-B line per half-wave. COLUMN: lane L loads floats 16L .. 16L + 15
+// = column L / 2, half L & 1; one ballot.
+__global__ __launch_bounds__(256) void grp_mask32_kernel(long long nnzb, int rowdir,
+                                                         const float* __restrict__ val,
+                                                         unsigned* __restrict__ masks,
+                                                         float* __restrict__ cols) {
+  const int lane = threadIdx.x & 63;
+  const long long k = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= nnzb) return;
+  const float* blk = val + (size_t)k * 1024;
+  unsigned msk = 0;
+  if (rowdir) {
+    const int j = lane & 31, h = lane >> 5;
+    f32x4 x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = *reinterpret_cast<const f32x4*>(blk + j * 32 + 16 * h + 4 * q);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const unsigned long long b =
+          __builtin_amdgcn_ballot_w64((__float_as_uint(x[i >> 2][i & 3]) & 0x7fffffffu) != 0u);
+      msk |= ((unsigned)b != 0u ? 1u : 0u) << i;
+      msk |= ((unsigned)(b >> 32) != 0u ? 1u : 0u) << (16 + i);
+    }
+    if (cols) {
+      float* dst = cols + (size_t)k * 1024 + j;
+      const unsigned below = msk & ((1u << (16 * h)) - 1u);  // columns of the other half first
+      int p = __builtin_popcount(below);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if ((msk >> (16 * h + i)) & 1u) {  // uniform over the half-wave
+          dst[32 * p] = x[i >> 2][i & 3];
+          ++p;
+        }
+      }
+    }
+  } else {
+    f32x4 x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = *reinterpret_cast<const f32x4*>(blk + 16 * lane + 4 * q);
+    unsigned t = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t |= __float_as_uint(x[q][e]) & 0x7fffffffu;
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(t != 0u);
+#pragma unroll
+    for (int c = 0; c < 32; ++c) msk |= (((b >> (2 * c)) & 3ull) != 0ull ? 1u : 0u) << c;
+  }
+  if (lane == 0) masks[k] = msk;
+}
+
+// The fill from columns: one wave per run of kFill32Items items of one w, lane t naming entry
+// t (item t / 8, entry t % 8) and the place of its column (masks: the compact copy's rank;
+// none: a COLUMN block's own column). Eight lanes read one entry's 128 B (lane q: rows
+// 4q .. 4q + 3), eight entries per load instruction, all of the run's loads in flight
+// together; the run's fragments are assembled in LDS and go out as 1-KB coalesced stores.
+__global__ __launch_bounds__(64) void bsr32_grp_fillc_kernel(long long nitems, int W,
+                                                             const int* __restrict__ rows,
+                                                             const int* __restrict__ src,
+                                                             const float* __restrict__ cols,
+                                                             const unsigned* __restrict__ masks,
+                                                             float* __restrict__ afrag) {
+  __shared__ f32x4 frag[kFill32Items * 256 / 4];  // [item][row][entry]
+  const int lane = threadIdx.x;
+  const long long u = blockIdx.x;
+  const int w = (int)(u % W);
+  const long long item0 = (u / W) * kFill32Items;
+  const int nf = (int)min((long long)kFill32Items, nitems - item0);
+  const long long it = item0 + (lane >> 3);
+  const bool mine = (lane >> 3) < kFill32Items;
+  const int row = mine && it < nitems ? rows[it * 8 + (lane & 7)] : -1;
+  const int k = row >= 0 ? src[(it * 8 + (lane & 7)) * W + w] : -1;
+  const int c = row & 31;
+  // the entry's column: cols + 1024 k + 32 rank (k < 2^31: the offset fits 64 bits as lo / hi)
+  const int rank = k >= 0 ? (masks ? __builtin_popcount(masks[k] & ((1u << c) - 1u)) : c) : 0;
+#pragma unroll
+  for (int q = 0; q < kFill32Items; ++q) frag[q * 64 + lane] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q = lane & 7, er = lane >> 3;
+  int kt[kFill32Items];
+  f32x4 x[kFill32Items];
+#pragma unroll
+  for (int r = 0; r < kFill32Items; ++r) {
+    const int t = r * 8 + er;  // item r of the run, entry er
+    kt[r] = __shfl(k, t, 64);
+    const int rk = __shfl(rank, t, 64);
+    x[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kt[r] >= 0)
+      x[r] = *reinterpret_cast<const f32x4*>(cols + (size_t)kt[r] * 1024 + 32 * rk + 4 * q);
+  }
+  __syncthreads();  // the zeroed fragments
+  float* fr = reinterpret_cast<float*>(frag);
+#pragma unroll
+  for (int r = 0; r < kFill32Items; ++r)
+    if (kt[r] >= 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fr[r * 256 + (4 * q + i) * 8 + er] = x[r][i];
+  __syncthreads();
+  f32x4* dst = reinterpret_cast<f32x4*>(afrag);
+  for (int f = 0; f < nf; ++f)
+    dst[((item0 + f) * W + w) * 64 + lane] = frag[f * 64 + lane];
+}
+
 // A fragments of the grouped bs 16 fp16 stream (layout per (item, wave w): 128 uint32, lane
 // l of the product's wave holding A[l & 15][4 (l >> 4) .. + 3] as fp16 x 4, i.e. half
 // 64 (e >> 2) + 4 r + (e & 3) for row r, entry e). One wave per run of kFill16Items items of
@@ -548,6 +661,25 @@ spmm_status_t launch_bsr32_grp_fill(spmm_context* ctx, long long nitems, int W, 
   const long long units = (nitems + kFill32Items - 1) / kFill32Items * W;
   hipLaunchKernelGGL(bsr32_grp_fill_kernel, dim3((unsigned)units), dim3(64), 0, ctx->stream, nitems,
                      W, dir == SPMM_DIRECTION_ROW ? 1 : 0, rows, src, val, afrag);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_grp_mask32(spmm_context* ctx, spmm_direction_t dir, int nnzb, const float* val,
+                                unsigned* masks, float* cols) {
+  if (nnzb == 0) return SPMM_STATUS_SUCCESS;
+  hipLaunchKernelGGL(grp_mask32_kernel, dim3((unsigned)(((long long)nnzb + 3) / 4)), dim3(256), 0,
+                     ctx->stream, (long long)nnzb, dir == SPMM_DIRECTION_ROW ? 1 : 0, val, masks,
+                     dir == SPMM_DIRECTION_ROW ? cols : nullptr);
+  return from_hip(hipGetLastError());
+}
+
+spmm_status_t launch_bsr32_grp_fillc(spmm_context* ctx, long long nitems, int W, const int* rows,
+                                     const int* src, const float* cols, const unsigned* masks,
+                                     float* afrag) {
+  if (nitems == 0) return SPMM_STATUS_SUCCESS;
+  const long long units = (nitems + kFill32Items - 1) / kFill32Items * W;
+  hipLaunchKernelGGL(bsr32_grp_fillc_kernel, dim3((unsigned)units), dim3(64), 0, ctx->stream, nitems,
+                     W, rows, src, cols, masks, afrag);
   return from_hip(hipGetLastError());
 }
 

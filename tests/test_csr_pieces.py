@@ -19,7 +19,7 @@ import pytest
 from helpers import (TOL_F32, assert_normwise, oracle_csrmm_f32, oracle_csrmm_f64,
                      oracle_csrmm_pieces_f32)
 
-PIECE_MIN, MAX_PIECES = 128, 16
+PIECE_MIN, MAX_PIECES = 128, 64
 
 
 def piece_len(L: int) -> int:

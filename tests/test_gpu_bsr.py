@@ -1825,6 +1825,42 @@ def test_group_analysis_row_pointer_checked_on_device(device, bs):
     h.close()
 
 
+@pytest.mark.parametrize("W", [2, 4])
+def test_group32_one_pass_fill_equals_block_fill(device, W):
+    """The bs 32 analysis in one pass over A (group_kernels.hip: the masks' kernel leaves a
+    compact copy of ROW blocks' nonzero columns, the fill reads 128 B per entry from it)
+    writes the same buffer, byte for byte, as the block fill, which reads every held
+    block's 4 KB again (run here by capturing the filling call: a captured fill reads the
+    values themselves). Some 60 k blocks, rows of 0 .. 400 blocks."""
+    from ctypes import byref, c_size_t, c_void_p
+    from spmm_hip._lib import lib
+    ops = _ops()
+    rng = np.random.default_rng(900 + W)
+    mb, kb = 1500, 2000
+    rp, ci, v, _ = _long_row_bsr(rng, mb, kb, 32, [0, 3, 20, 45, 90, 400])
+    drp, dci, dv = _dev(rp, ci, v)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        h = ops.Handle(s)
+        ref = ops.GroupedBsr32(drp, dci, dv, mb=mb, group_rows=W, handle=h)  # one pass
+        fn = lib().spmm_bsr32_group_analysis_f32
+        args = (h.raw, 0, mb, int(ci.size), W, c_void_p(drp.data_ptr()), c_void_p(dci.data_ptr()),
+                c_void_p(dv.data_ptr()))
+        size = c_size_t(0)
+        assert fn(*args, None, byref(size)) == 0 and size.value == ref.bytes
+        buf = torch.full((size.value,), 0xA5, dtype=torch.uint8, device=device)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            h.set_stream(s)
+            assert fn(*args, c_void_p(buf.data_ptr()), byref(size)) == 0
+        g.replay()
+        s.synchronize()
+        assert torch.equal(buf, ref.buffer[:size.value]), "one-pass fill differs from the block fill"
+        ref.close()
+        h.close()
+
+
 @pytest.mark.parametrize("bs", [16, 32])
 def test_group_analysis_fill_is_graph_capturable(device, bs):
     """The filling call of the group analysis only launches kernels and async
