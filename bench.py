@@ -135,9 +135,9 @@ WORKLOADS = {
 METRIC = "SpMM GFLOP/s (2*nnz*K/t) + achieved HBM GB/s, ogbn-products K=128"
 
 
-BSR_TRAFFIC = os.path.join(ROOT, "profiles", "r05_final", "bsr_bytes.jsonl")
+BSR_TRAFFIC = os.path.join(ROOT, "profiles", "r06_final", "bsr_bytes.jsonl")
 # counter bytes of the CSR kernels per workload (tools/pmc_bytes.sh)
-CSR_TRAFFIC = os.path.join(ROOT, "profiles", "r05_final", "csr_bytes.jsonl")
+CSR_TRAFFIC = os.path.join(ROOT, "profiles", "r06_final", "csr_bytes.jsonl")
 
 
 def csr_counter_bytes(workload: str):

@@ -356,7 +356,13 @@ spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n
  * block row multiplies only its own nonzero columns (the analysis records them
  * per item), so C is bit-identical to spmm_bsrmm_ex_f32 /
  * spmm_bsrmm_analysed_f32 with the same column-granular non-finite contract.
- * Same two phases, checks and handle record as spmm_bsr16_group_analysis_f16. */
+ * Same two phases, checks and handle record as spmm_bsr16_group_analysis_f16.
+ * The analysis reads A once: for ROW blocks the size query keeps a compact copy
+ * of the blocks' nonzero columns in a stream-ordered allocation of 4 KB per block
+ * (hipMallocAsync on the handle's stream), which the filling call reads and frees;
+ * a filling call under stream capture reads the values instead and leaves the
+ * copy to the next size query or spmm_destroy. Without memory for the copy the
+ * filling call reads the blocks themselves; the buffer's bytes are the same. */
 spmm_status_t spmm_bsr32_group_analysis_f32(spmm_handle_t handle, spmm_direction_t dir, int mb,
                                             int nnzb, int groupRows, const int* bsrRowPtr,
                                             const int* bsrColInd, const float* bsrVal,

@@ -59,6 +59,24 @@ def _wl(rec) -> str:
     return rec["config"]["workload"].split(":")[0]
 
 
+def load_bytes(pass_dir: str) -> dict:
+    """Counter bytes per launch by workload (tools/pmc_bytes.sh records of the same pass):
+    the lines were measured before those records existed, so their `traffic` is filled
+    from here where it is missing."""
+    out = {}
+    for name in ("csr_bytes.jsonl", "bsr_bytes.jsonl"):
+        path = os.path.join(pass_dir, name)
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            for line in f:
+                if line.startswith("{"):
+                    r = json.loads(line)
+                    if r.get("counter_bytes_per_launch"):
+                        out[r["workload"]] = r
+    return out
+
+
 def load(pass_dir: str):
     head = None
     with open(os.path.join(pass_dir, "bench.log")) as f:
@@ -66,13 +84,32 @@ def load(pass_dir: str):
             if line.startswith("{"):
                 head = json.loads(line)
     lines = {}
+    cb = load_bytes(pass_dir)
     path = os.path.join(pass_dir, "workloads.jsonl")
     if os.path.exists(path):
         with open(path) as f:
             for line in f:
                 if line.startswith("{"):
                     r = json.loads(line)
+                    rf = r.setdefault("roofline", {})
+                    if not rf.get("traffic") and _wl(r) in cb:
+                        rf["traffic"] = cb[_wl(r)]["counter_bytes_per_launch"]
                     lines[_wl(r)] = r
+    if head:
+        rf = head["roofline"]
+        if not rf.get("traffic") and "products_csr" in cb:
+            rf["traffic"] = cb["products_csr"]["counter_bytes_per_launch"]
+        for key, wl in (("config3", "reddit_bsr32"), ("config5", "products_bsr16_f16"),
+                        ("products_bsr32", "products_bsr32")):
+            s = head.get(key)
+            if not s:
+                continue
+            for sub, suf in ((s, ""), (s.get("grouped_entry"), "_grp"), (s.get("analysed_entry"), "_an")):
+                rec = cb.get(wl + suf)
+                if sub is not None and not sub.get("traffic") and rec:
+                    sub["traffic"] = rec["counter_bytes_per_launch"]
+                    if sub is s and sub.get("kernel_ms"):
+                        sub["traffic_frac"] = rec["counter_bytes_per_launch"] / (sub["kernel_ms"] * 1e-3) / 8e12
     return head, lines
 
 
@@ -179,10 +216,10 @@ def entries_table(h: dict, lines: dict, src: str) -> str:
 def replace_block(path: str, name: str, text: str) -> None:
     with open(path) as f:
         s = f.read()
-    pat = re.compile(rf"(<!-- numbers:{name}:begin -->\n).*?(\n<!-- numbers:{name}:end -->)", re.S)
+    pat = re.compile(rf"(<!-- numbers:{name}:begin -->\n).*?(<!-- numbers:{name}:end -->)", re.S)
     if not pat.search(s):
         raise SystemExit(f"{path}: no numbers:{name} block")
-    s = pat.sub(lambda m: m.group(1) + text + m.group(2), s)
+    s = pat.sub(lambda m: m.group(1) + text + "\n" + m.group(2), s)
     with open(path, "w") as f:
         f.write(s)
 
