@@ -359,6 +359,7 @@ spmm_status_t spmm_bsrmm_grouped_f16(spmm_handle_t handle, int mb, int kb, int n
  * Same two phases, checks and handle record as spmm_bsr16_group_analysis_f16.
  * The analysis reads A once: for ROW blocks the size query keeps a compact copy
  * of the blocks' nonzero columns in a stream-ordered allocation of 4 KB per block
+ * (at most 16 GiB and a quarter of the free device memory)
  * (hipMallocAsync on the handle's stream), which the filling call reads and frees;
  * a filling call under stream capture reads the values instead and leaves the
  * copy to the next size query or spmm_destroy. Without memory for the copy the

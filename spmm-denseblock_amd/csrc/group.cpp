@@ -139,10 +139,16 @@ spmm_status_t group_analysis(spmm_handle_t handle, int BS, spmm_direction_t dir,
       const auto* v16 = static_cast<const uint16_t*>(bsrVal);
       spmm_status_t s;
       if (BS == 32) {
-        // ROW blocks: the compact column copy the fill reads (without the memory for it, the
-        // fill reads the blocks again)
-        if (dir == SPMM_DIRECTION_ROW &&
-            hipMallocAsync(&handle->grp_cols, (size_t)nnzb * 4096, st) != hipSuccess) {
+        // ROW blocks: the compact column copy the fill reads, a 4-KB slot per block, when that
+        // is at most kColsCap and a quarter of the free device memory (else, or without the
+        // memory, the fill reads the blocks again: the RCM products stand-in's 10.5 M blocks
+        // would take 43 GB for a copy of about 10)
+        constexpr size_t kColsCap = size_t(16) << 30;
+        const size_t want = (size_t)nnzb * 4096;
+        size_t free_b = 0, total_b = 0;
+        if (dir == SPMM_DIRECTION_ROW && want <= kColsCap &&
+            hipMemGetInfo(&free_b, &total_b) == hipSuccess && want <= free_b / 4 &&
+            hipMallocAsync(&handle->grp_cols, want, st) != hipSuccess) {
           (void)hipGetLastError();
           handle->grp_cols = nullptr;
         }
