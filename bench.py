@@ -155,6 +155,12 @@ def csr_counter_bytes(workload: str):
     return rec
 
 
+def default_wpc(rows_per_launch: int, hot: bool = False) -> int:
+    """The CSR grid's default waves per CU for a launch of that many rows
+    (csr_kernels.hip csr_nwaves: 12 from 2^20 rows on the plain kernel, else 16)."""
+    return 12 if rows_per_launch >= (1 << 20) and not hot else 16
+
+
 def kernel_source_tag() -> str:
     """First 16 hex digits of the SHA-256 of the BSR kernel source: counter
     bytes recorded for one build of the kernels are not reused for another."""
@@ -654,7 +660,7 @@ def run_csr_weak(args, W, world, rank, dev, dist):
                             f"B replicated ({ncols} rows), no collective in the step",
                 "n_per_rank": n, "nnz_per_rank": nnz, "n_total": ncols,
                 "nnz_total": int(tot[0]), "K": K, "parallelism": f"rows{world}",
-                "waves_per_cu": args.waves_per_cu or 16, "csr_options": args.csr_options},
+                "waves_per_cu": args.waves_per_cu or default_wpc(n), "csr_options": args.csr_options},
         roofline={"bound": "hbm", "peak": HBM_PEAK_GBPS, "unit": "GB/s", **crf,
                   "traffic": None, "kernel": f"csr_mergepath_kernel<{vec}>",
                   "kernel_ms": round(kms, 4), "kernel_ms_max_rank": round(kms_max, 4)},
@@ -788,7 +794,7 @@ def run_csr(args, W, world, rank, dev, dist):
                 "n": n, "nnz": nnz, "K": K, "max_deg": int(np.diff(rp).max()),
                 "parallelism": f"rows{world}" if world > 1 else "single",
                 "exchange_chunks": nch, "hip_graph": bool(GRAPH and world == 1),
-                "waves_per_cu": args.waves_per_cu or 16,
+                "waves_per_cu": args.waves_per_cu or default_wpc(n // max(world, 1) // max(nch, 1), hot),
                 "csr_options": args.csr_options, "layout_BC": args.csr_layout},
         roofline={"bound": "hbm", "peak": HBM_PEAK_GBPS, "unit": "GB/s", **crf,
                   "traffic": traffic,

@@ -989,9 +989,16 @@ int pick_vec(int n, const float* B, int ldb, const float* C, int ldc) {
 
 // Waves in the merge-path grid: enough that each gets >= kMinItemsPerWave
 // items, capped at the resident target (waves_per_cu x CUs) so the whole
-// grid runs in one round. nnz < 0 (unknown on the host) sizes from m.
-int csr_nwaves(spmm_context* ctx, int m, long long nnz) {
-  const int wpc = ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu : 16;
+// grid runs in one round. nnz < 0 (unknown on the host) sizes from m. The default
+// target is 16 waves per CU (4 workgroups), 12 (3) from 2^20 rows on the plain kernel:
+// products stand-in K = 128 4.23-4.25 ms at 12 against 4.34-4.36 at 16 (interleaved on
+// one box), K = 256 even; the hot-column kernel the other way (4.30-4.31 at 12 against
+// 4.17-4.18), the arxiv stand-in too (0.103 at 12 against 0.093); 10 and 14 (workgroup
+// counts the CUs do not divide evenly) 4.49 / 4.63-4.68 (profiles/r06/wpc/). The
+// association of every row's sum does not depend on the grid (pieces).
+int csr_nwaves(spmm_context* ctx, int m, long long nnz, bool hot) {
+  const int wpc = ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu
+                                             : (!hot && m >= (1 << 20) ? 12 : 16);
   const long long cap = (long long)ctx->num_cus * wpc;
   const long long total = nnz >= 0 ? (long long)m + nnz : (long long)m * 32;
 #ifdef SPMM_TUNING
@@ -1142,7 +1149,7 @@ spmm_status_t launch_csrmm_rowmajor(spmm_context* ctx, int m, int n, const int* 
   const int vec = pick_vec(n, B, ldb, C, ldc);
   const int tile = kWave * vec;
   const int ntiles = (n + tile - 1) / tile;
-  const int nw = csr_nwaves(ctx, m, nnz_hint);
+  const int nw = csr_nwaves(ctx, m, nnz_hint, hot != 0);
   dim3 grid((nw + kWavesPerWG - 1) / kWavesPerWG, ntiles);
   dim3 block(kWG);
   // split rows: piece slots in the workspace (sized by csrmm_carry_bytes for the
