@@ -156,9 +156,10 @@ def csr_counter_bytes(workload: str):
 
 
 def default_wpc(rows_per_launch: int, hot: bool = False) -> int:
-    """The CSR grid's default waves per CU for a launch of that many rows
-    (csr_kernels.hip csr_nwaves: 12 from 2^20 rows on the plain kernel, else 16)."""
-    return 12 if rows_per_launch >= (1 << 20) and not hot else 16
+    """The CSR grid's default waves per CU for a launch of that many rows, as the
+    library sizes it (spmm_csr_default_waves_per_cu)."""
+    from spmm_hip import _lib
+    return int(_lib.lib().spmm_csr_default_waves_per_cu(int(rows_per_launch), 1 if hot else 0))
 
 
 def kernel_source_tag() -> str:

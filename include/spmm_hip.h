@@ -98,6 +98,11 @@ spmm_status_t spmm_get_kernel_times(spmm_handle_t handle, float* ms, int max_cou
 /* Tuning knob for the CSR merge-path kernel: resident waves per CU the grid
  * is sized for (0 = default). */
 spmm_status_t spmm_set_csr_waves_per_cu(spmm_handle_t handle, int waves_per_cu);
+/* The target a handle without that setting sizes a CSR launch's grid for: 16
+ * waves per CU, 12 from 2^20 rows on the plain kernel (hot != 0: the
+ * spmm_csrmm_hot_f32 kernel, which keeps 16). Host-only; the result of the
+ * product does not depend on it. */
+int spmm_csr_default_waves_per_cu(int m, int hot);
 
 /* CSR kernel options (bit flags). SPMM_CSR_NT_STREAMS: read colind/val and
  * write C with non-temporal hints, keeping L2 / MALL for the B gathers. */

@@ -987,6 +987,10 @@ int pick_vec(int n, const float* B, int ldb, const float* C, int ldc) {
   return 1;
 }
 
+extern "C" int spmm_csr_default_waves_per_cu(int m, int hot) {
+  return !hot && m >= (1 << 20) ? 12 : 16;
+}
+
 // Waves in the merge-path grid: enough that each gets >= kMinItemsPerWave
 // items, capped at the resident target (waves_per_cu x CUs) so the whole
 // grid runs in one round. nnz < 0 (unknown on the host) sizes from m. The default
@@ -998,7 +1002,7 @@ int pick_vec(int n, const float* B, int ldb, const float* C, int ldc) {
 // association of every row's sum does not depend on the grid (pieces).
 int csr_nwaves(spmm_context* ctx, int m, long long nnz, bool hot) {
   const int wpc = ctx->csr_waves_per_cu > 0 ? ctx->csr_waves_per_cu
-                                             : (!hot && m >= (1 << 20) ? 12 : 16);
+                                             : spmm_csr_default_waves_per_cu(m, hot ? 1 : 0);
   const long long cap = (long long)ctx->num_cus * wpc;
   const long long total = nnz >= 0 ? (long long)m + nnz : (long long)m * 32;
 #ifdef SPMM_TUNING

@@ -70,6 +70,7 @@ _PROTOS = {
     "spmm_set_kernel_timing": (c_int, [_P, c_int]),
     "spmm_get_kernel_times": (c_int, [_P, POINTER(c_float), c_int, _PI]),
     "spmm_set_csr_waves_per_cu": (c_int, [_P, c_int]),
+    "spmm_csr_default_waves_per_cu": (c_int, [c_int, c_int]),
     "spmm_set_csr_options": (c_int, [_P, c_int]),
     "spmm_set_hybrid_options": (c_int, [_P, c_int]),
     "spmm_set_bsr_options": (c_int, [_P, c_int]),

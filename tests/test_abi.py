@@ -86,6 +86,12 @@ def test_status_strings_and_host_side_checks():
     assert L.spmm_csr_hot_analysis(None, 128, 4, 4, None, 0, 0, None) == 1
     assert L.spmm_csrmm_hot_f32(None, 1, 1, 1, 0, 1.0, None, None, None, 0, None, 1, 0, 0.0,
                                 None, 1, 0) == 1
+    # the CSR grid's default target (host-only): 12 waves per CU from 2^20 rows on the
+    # plain kernel, 16 below and for the hot-column kernel; bench.py reports it
+    assert L.spmm_csr_default_waves_per_cu(2449029, 0) == 12
+    assert L.spmm_csr_default_waves_per_cu((1 << 20) - 1, 0) == 16
+    assert L.spmm_csr_default_waves_per_cu(2449029, 1) == 16
+    assert L.spmm_csr_default_waves_per_cu(169343, 0) == 16
     d = ctypes.c_void_p()
     assert L.spmm_create_mat_descr(ctypes.byref(d)) == 0
     assert L.spmm_set_mat_index_base(d, 1) == 0
