@@ -98,7 +98,7 @@ def oracle_csrmm_f32(L, m, n, rowptr, colind, val, B, ldb, order_b, alpha=1.0, b
 def oracle_csrmm_pieces_f32(L, m, n, rowptr, colind, val, B, ldb, order_b, alpha=1.0,
                             beta=0.0, C=None, ldc=None, order_c=0, base=0):
     """The HIP CSR kernels' association: sequential fp32 FMA
-    chains over pieces of max(128, ceil(L / 16)) nonzeros from each row's start,
+    chains over pieces of max(128, ceil(L / 64)) nonzeros from each row's start,
     added left to right; the main kernel matches it bit for bit at any grid."""
     rowptr = np.ascontiguousarray(rowptr, np.int32)
     colind = np.ascontiguousarray(colind, np.int32)

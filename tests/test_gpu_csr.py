@@ -504,3 +504,47 @@ def test_dropin_equals_ex_entry(device):
         ops.csrmm(drp, dci, dv, dB, n=K, k=m, ldb=K, C=Cx, ldc=K)
         torch.cuda.synchronize()
         assert torch.equal(Cd, Cx), (m, nnz, K)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_shapes_grid_independent(oracle, device, seed):
+    """Random matrices (rows of 0 .. 3,000 nonzeros, hubs up to 9,000, empty rows),
+    random K among every kernel's widths, random alpha / beta and two random grids
+    (waves per CU 1 .. 32): the main kernel equals the piece oracle bit for bit at
+    both grids, the K <= 64 lane-group kernel gives the same bits at both grids and
+    is within the fp32 bar of the f64 product."""
+    ops = _ops()
+    rng = np.random.default_rng(7000 + seed)
+    m = int(rng.integers(1, 30000))
+    k = int(rng.integers(1, 20000))
+    K = int(rng.choice([1, 4, 8, 12, 16, 32, 36, 64, 96, 128, 130, 192, 256, 512]))
+    nhub = int(rng.integers(0, 6))
+    hubs = rng.choice(m, min(nhub, m), replace=False) if nhub else ()
+    rp, ci, v = _rand_csr(rng, m, k, min(int(rng.choice([0, 3, 20, 200, 3000])), k), hubs,
+                          int(rng.integers(1000, 9001)), float(rng.choice([0.0, 0.3])))
+    alpha = float(rng.choice([1.0, -0.5, 2.0]))
+    beta = float(rng.choice([0.0, 0.0, 0.75]))
+    B = rng.uniform(-1, 1, (k, K)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (m, K)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    got = []
+    for wpc in rng.choice(np.arange(1, 33), 2, replace=False):
+        h = ops.Handle()
+        h.set_csr_waves_per_cu(int(wpc))
+        C = torch.from_numpy(C0).to(device)
+        ops.csrmm(drp, dci, dv, dB, n=K, k=k, ldb=K, C=C, ldc=K, alpha=alpha, beta=beta, handle=h)
+        torch.cuda.synchronize()
+        got.append(C.cpu().numpy())
+        h.close()
+    what = f"m={m} k={k} K={K} nnz={ci.size} alpha={alpha} beta={beta}"
+    assert np.array_equal(got[0].view(np.uint32), got[1].view(np.uint32)), what + ": grids differ"
+    if _main_kernel(K):
+        want = oracle_csrmm_pieces_f32(oracle, m, K, rp, ci, v, B, K, 0, alpha=alpha, beta=beta,
+                                       C=C0).reshape(m, K)
+        bad = got[0].view(np.uint32) != want.view(np.uint32)
+        assert not bad.any(), f"{what}: {int(bad.sum())} elements differ from the piece oracle"
+    else:
+        ref, absd = oracle_csrmm_f64(oracle, m, K, rp, ci, v, B, K, 0)
+        ref = alpha * ref + beta * C0.astype(np.float64)
+        absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+        assert_normwise(got[0], ref, absd, TOL_F32, what)
