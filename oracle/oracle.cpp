@@ -109,7 +109,7 @@ void oracle_csrmm_f32(int m, int n, const int* rowptr, const int* colind, const 
 
 // The association the HIP CSR kernels use, restated so that
 // their output can be checked bit for bit at any grid: a row of L nonzeros is
-// summed as pieces of T(L) = max(128, ceil(L / 16)) consecutive nonzeros from
+// summed as pieces of T(L) = max(128, ceil(L / 64)) consecutive nonzeros from
 // the row's start, each the sequential fp32 FMA chain of csrmm_seq above
 // (gespmm_csrmm.h:124-129), and the pieces are added left to right from -0.
 // Rows of at most 128 nonzeros are therefore exactly csrmm_seq's chain.
@@ -123,7 +123,9 @@ void oracle_csrmm_pieces_f32(int m, int n, const int* rowptr, const int* colind,
     const int j0 = rowptr[r] - base, j1 = rowptr[r + 1] - base;
     const int T = oracle_csr_piece_len(j1 - j0);
     for (int c = 0; c < n; ++c) {
-      volatile float x = -0.f;  // no reassociation of the piece sums
+      // no reassociation of the piece sums; an empty row is one empty piece, +0 (the
+      // reference's accumulator before its first FMA: the kernels' -0 + (+0))
+      volatile float x = j1 > j0 ? -0.f : 0.f;
       for (int p = j0; p < j1; p += T) {
         float acc = 0.f;
         for (int j = p; j < std::min(p + T, j1); ++j)

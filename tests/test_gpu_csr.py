@@ -60,7 +60,7 @@ def _check_rowmajor(oracle, rp, ci, val, B, C, what, exact_expected=False, piece
         assert np.array_equal(got, ref32), what + ": expected bit-exact sequential FMA"
     if pieces_exact if pieces_exact is not None else _main_kernel(n):
         pcs = oracle_csrmm_pieces_f32(oracle, m, n, rp, ci, val, B, B.shape[1], 0).reshape(m, n)
-        bad = np.flatnonzero(~np.all(got == pcs, axis=1))
+        bad = np.flatnonzero(~np.all(got.view(np.uint32) == pcs.view(np.uint32), axis=1))  # bits
         assert bad.size == 0, (f"{what}: {bad.size} rows differ from the piece oracle, "
                                f"first {bad[:5].tolist()}")
     return float(np.mean(got == ref32))
@@ -474,7 +474,7 @@ def test_split_rows_bit_exact_pieces(oracle, device, K, opts, alpha, beta):
     else:
         want = oracle_csrmm_pieces_f32(oracle, m, K, rp, ci, v, B, K, 0, alpha=alpha, beta=beta,
                                        C=C0).reshape(m, K)
-        bad = ~(got == want)
+        bad = got.view(np.uint32) != want.view(np.uint32)  # bits, signed zeros included
         assert not bad.any(), (f"K={K}: {int(bad.any(axis=1).sum())} rows differ from the piece "
                                f"oracle ({int(bad[split].any(axis=1).sum())} of "
                                f"{int(split.sum())} split rows)")
