@@ -2078,3 +2078,80 @@ def test_group_rows_chosen_by_the_library(oracle, device):
     where they share."""
     ws = [_auto_group_rows(oracle, device, s) for s in (True, False)]
     assert ws == [4, 2], ws
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_random_shapes_bits(oracle, device, seed):
+    """Random BSR matrices (empty block rows, all-zero blocks and columns, rows of
+    0 .. 60 blocks), bs 2 / 4 / 8 / 32 / 64, n from 4 to 256, random alpha / beta:
+    the entries that share a stream's arithmetic give the same bits, signed zeros
+    included, and those DESIGN.md §6 calls bit-exact equal the sequential fp32
+    oracle bit for bit (bs 2 / 4 / 8 on both kernels, bs 32 / 64 on the column
+    stream at row-major C); bs 32: the drop-in, analysed and grouped entries are
+    bit-identical."""
+    from spmm_hip._lib import BSR_SMALL_GROUPED
+    ops = _ops()
+    rng = np.random.default_rng(9100 + seed)
+    bs = int(rng.choice([2, 4, 8, 32, 64]))
+    n = int(rng.choice([4, 8, 36, 64, 96, 128, 132, 256]))
+    mb = int(rng.integers(1, 120 if bs >= 32 else 900))
+    kb = int(rng.integers(1, 200 if bs >= 32 else 2000))
+    p = float(rng.choice([0.02, 0.1, 0.3]))
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, p, empty_rows=tuple(rng.choice(mb, min(3, mb), replace=False)))
+    vb = v.reshape(-1, bs, bs)
+    nnzb = vb.shape[0]
+    if nnzb:
+        vb[rng.random(nnzb) < 0.2] = 0.0                                    # all-zero blocks
+        vb[:, :, :][rng.random((nnzb, 1, bs)).repeat(bs, axis=1) < 0.4] = 0.0  # zero columns
+        vb[rng.random((nnzb, bs, bs)) < 0.3] = 0.0                           # explicit zeros
+    v = vb.reshape(-1)
+    alpha = float(rng.choice([1.0, -0.5, 2.0]))
+    beta = float(rng.choice([0.0, 0.0, 0.75]))
+    B = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (mb * bs, n)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v, B)
+    what = f"bs={bs} n={n} mb={mb} kb={kb} nnzb={nnzb} alpha={alpha} beta={beta}"
+
+    def run(flags=0, **kw):
+        h = ops.Handle()
+        h.set_bsr_options(flags)
+        C = torch.from_numpy(C0.copy()).to(device)
+        ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=C, ldc=n, alpha=alpha,
+                  beta=beta, handle=h, **kw)
+        torch.cuda.synchronize()
+        h.close()
+        return C
+
+    C = run()
+    ref = oracle_bsrmm_f32(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0, alpha=alpha, beta=beta,
+                           C=C0.reshape(-1)).reshape(mb * bs, n)
+    ref64, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
+    ref64 = alpha * ref64 + beta * C0.astype(np.float64)
+    absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+    got = C.cpu().numpy()
+    assert_normwise(got, ref64, absd, TOL_F32, what)
+    bits = lambda t: (t.view(torch.int32) if isinstance(t, torch.Tensor) else t.view(np.int32))
+    # block rows the column stream may cut into segments on a shallow grid (longer than 64
+    # blocks, bsr_kernels.hip cs2_segments) sum their partials in segment order
+    whole = np.repeat(np.diff(rp) <= 64, bs) if bs >= 32 else np.ones(mb * bs, bool)
+    assert np.array_equal(got[whole], ref[whole]), what + ": not the sequential fp32 chain"
+    bad = bits(got[whole]) != bits(ref[whole])
+    assert not bad.any(), f"{what}: {int(bad.sum())} signed zeros differ from the oracle"
+    wt = torch.from_numpy(whole).to(device)
+    if bs <= 8:
+        Cg = run(BSR_SMALL_GROUPED)
+        assert torch.equal(bits(Cg), bits(C)), what + ": grouped stream differs from the default"
+    if bs == 32:
+        masks, vcol = ops.bsr32_analysis(dv, nnzb=nnzb)
+        Ca = torch.from_numpy(C0.copy()).to(device)
+        ops.bsrmm_analysed(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n, ldb=n, C=Ca, ldc=n,
+                           alpha=alpha, beta=beta)
+        torch.cuda.synchronize()
+        assert torch.equal(bits(Ca), bits(C)), what + ": analysed entry differs"
+        if n % 4 == 0:
+            grp = ops.GroupedBsr32(drp, dci, dv, mb=mb)
+            Cg = torch.from_numpy(C0.copy()).to(device)
+            grp.mm(dB, kb=kb, n=n, ldb=n, C=Cg, ldc=n, alpha=alpha, beta=beta)
+            torch.cuda.synchronize()
+            assert torch.equal(bits(Cg[wt]), bits(C[wt])), what + ": grouped entry differs"
+            grp.close()
