@@ -538,6 +538,16 @@ def test_random_shapes_grid_independent(oracle, device, seed):
         h.close()
     what = f"m={m} k={k} K={K} nnz={ci.size} alpha={alpha} beta={beta}"
     assert np.array_equal(got[0].view(np.uint32), got[1].view(np.uint32)), what + ": grids differ"
+    # the column-major forms (cusparseScsrmm2's layout: staged through LDS-tiled transposes,
+    # the epilogue the kernel's own) give the same bits
+    dBc = torch.from_numpy(np.ascontiguousarray(B.T)).to(device)
+    Cc = torch.from_numpy(np.ascontiguousarray(C0.T)).to(device)
+    ops.csrmm(drp, dci, dv, dBc, m=m, n=K, k=k, ldb=k, order_b=ops.ORDER_COL, C=Cc, ldc=m,
+              order_c=ops.ORDER_COL, alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    colm = np.ascontiguousarray(Cc.cpu().numpy().T)
+    if _main_kernel(K):
+        assert np.array_equal(colm.view(np.uint32), got[0].view(np.uint32)), what + ": column-major"
     if _main_kernel(K):
         want = oracle_csrmm_pieces_f32(oracle, m, K, rp, ci, v, B, K, 0, alpha=alpha, beta=beta,
                                        C=C0).reshape(m, K)
