@@ -548,6 +548,13 @@ def test_random_shapes_grid_independent(oracle, device, seed):
     colm = np.ascontiguousarray(Cc.cpu().numpy().T)
     if _main_kernel(K):
         assert np.array_equal(colm.view(np.uint32), got[0].view(np.uint32)), what + ": column-major"
+        # the hot-column entry (a small budget, so some columns go each way): the same bits
+        tag = ops.csr_hot_analysis(dci, n=K, k=k, hot_bytes=int(rng.choice([1 << 12, 1 << 20])))
+        Ch = torch.from_numpy(C0).to(device)
+        ops.csrmm_hot(drp, tag, dv, dB, m=m, n=K, k=k, ldb=K, C=Ch, ldc=K, alpha=alpha, beta=beta)
+        torch.cuda.synchronize()
+        assert np.array_equal(Ch.cpu().numpy().view(np.uint32), got[0].view(np.uint32)), \
+            what + ": hot-column entry"
     if _main_kernel(K):
         want = oracle_csrmm_pieces_f32(oracle, m, K, rp, ci, v, B, K, 0, alpha=alpha, beta=beta,
                                        C=C0).reshape(m, K)
