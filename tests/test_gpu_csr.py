@@ -538,6 +538,21 @@ def test_random_shapes_grid_independent(oracle, device, seed):
         h.close()
     what = f"m={m} k={k} K={K} nnz={ci.size} alpha={alpha} beta={beta}"
     assert np.array_equal(got[0].view(np.uint32), got[1].view(np.uint32)), what + ": grids differ"
+    # row shards (dist.make_shard: positions mod 64 kept) written in place: the same bits,
+    # the lane-group kernel's too
+    from spmm_hip import dist as sdist
+    for world in (2, 3):
+        Cs = torch.from_numpy(C0).to(device)
+        for r in range(world):
+            sh = sdist.make_shard(rp, ci, v, r, world)
+            if sh.rows == 0:
+                continue
+            srp, sci, sv = _dev(sh.rowptr, sh.colind, sh.val)
+            ops.csrmm(srp, sci, sv, dB, m=sh.rows, n=K, k=k, ldb=K, C=Cs[sh.row0:sh.row1], ldc=K,
+                      alpha=alpha, beta=beta)
+        torch.cuda.synchronize()
+        assert np.array_equal(Cs.cpu().numpy().view(np.uint32), got[0].view(np.uint32)), \
+            f"{what}: {world} shards"
     # the column-major forms (cusparseScsrmm2's layout: staged through LDS-tiled transposes,
     # the epilogue the kernel's own) give the same bits
     dBc = torch.from_numpy(np.ascontiguousarray(B.T)).to(device)
