@@ -2155,3 +2155,52 @@ def test_random_shapes_bits(oracle, device, seed):
             torch.cuda.synchronize()
             assert torch.equal(bits(Cg[wt]), bits(C[wt])), what + ": grouped entry differs"
             grp.close()
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_shapes_bs16_f16_bits(oracle, device, seed):
+    """bs 16 fp16 (config 5's types) on random matrices with empty block rows and zero
+    blocks / columns, n 16 to 512: the drop-in and analysed entries give the same bits,
+    signed zeros included; both are within the fp16-input bar of the exact product, and
+    so is the grouped entry (W by the library)."""
+    ops = _ops()
+    rng = np.random.default_rng(9300 + seed)
+    bs = 16
+    n = int(rng.choice([16, 64, 128, 256, 264, 512]))
+    mb = int(rng.integers(1, 400))
+    kb = int(rng.integers(1, 600))
+    p = float(rng.choice([0.01, 0.05, 0.2]))
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, p, empty_rows=tuple(rng.choice(mb, min(3, mb), replace=False)))
+    vb = v.reshape(-1, bs, bs)
+    nnzb = vb.shape[0]
+    if nnzb:
+        vb[rng.random(nnzb) < 0.2] = 0.0
+        vb[rng.random((nnzb, 1, bs)).repeat(bs, axis=1) < 0.5] = 0.0
+    v16 = vb.reshape(-1).astype(np.float16)
+    alpha = float(rng.choice([1.0, -0.5]))
+    beta = float(rng.choice([0.0, 0.5]))
+    B16 = rng.uniform(-1, 1, (kb * bs, n)).astype(np.float16)
+    C0 = rng.uniform(-1, 1, (mb * bs, n)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, v16, B16)
+    what = f"bs16 fp16 n={n} mb={mb} kb={kb} nnzb={nnzb} alpha={alpha} beta={beta}"
+    C1 = torch.from_numpy(C0.copy()).to(device)
+    ops.bsrmm_f16(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=C1, ldc=n, alpha=alpha,
+                  beta=beta)
+    masks, vcol = ops.bsr16_analysis(dv, nnzb=nnzb)
+    C2 = torch.from_numpy(C0.copy()).to(device)
+    ops.bsrmm_analysed_f16(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n, ldb=n, C=C2, ldc=n,
+                           alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    assert torch.equal(C1.view(torch.int32), C2.view(torch.int32)), what + ": analysed differs"
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v16.astype(np.float32),
+                                 B16.astype(np.float32), n, 0)
+    ref = alpha * ref + beta * C0.astype(np.float64)
+    absd = abs(alpha) * absd + abs(beta) * np.abs(C0.astype(np.float64))
+    assert_normwise(C1.cpu().numpy(), ref, absd, TOL_F16_ACC, what)
+    if n % 8 == 0:
+        grp = ops.GroupedBsr16(drp, dci, dv, mb=mb)
+        C3 = torch.from_numpy(C0.copy()).to(device)
+        grp.mm(dB, kb=kb, n=n, ldb=n, C=C3, ldc=n, alpha=alpha, beta=beta)
+        torch.cuda.synchronize()
+        assert_normwise(C3.cpu().numpy(), ref, absd, TOL_F16_ACC, what + " grouped")
+        grp.close()
