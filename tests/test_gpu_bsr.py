@@ -2123,6 +2123,9 @@ def test_random_shapes_bits(oracle, device, seed):
         return C
 
     C = run()
+    if nnzb == 0:  # rocsparse_bsrmm.h:152-154's quick return: C untouched, beta or not
+        assert torch.equal(run().view(torch.int32), torch.from_numpy(C0).to(device).view(torch.int32))
+        return
     ref = oracle_bsrmm_f32(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0, alpha=alpha, beta=beta,
                            C=C0.reshape(-1)).reshape(mb * bs, n)
     ref64, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
@@ -2192,6 +2195,9 @@ def test_random_shapes_bs16_f16_bits(oracle, device, seed):
                            alpha=alpha, beta=beta)
     torch.cuda.synchronize()
     assert torch.equal(C1.view(torch.int32), C2.view(torch.int32)), what + ": analysed differs"
+    if nnzb == 0:  # rocsparse_bsrmm.h:152-154's quick return: C untouched
+        assert np.array_equal(C1.cpu().numpy().view(np.int32), C0.view(np.int32))
+        return
     ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v16.astype(np.float32),
                                  B16.astype(np.float32), n, 0)
     ref = alpha * ref + beta * C0.astype(np.float64)

@@ -153,3 +153,56 @@ def test_f64_status_codes(device):
                                    0) == 3
     with pytest.raises(TypeError):
         ops.csrmm(rp, rp[:0], torch.zeros(0, device=device), B, n=4, k=4, ldb=4, C=C, ldc=4)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_shapes_f64_bits(oracle, device, seed):
+    """fp64 CSR and BSR forms on random shapes (empty rows, K 1 to 300, bs 1 to 32,
+    both storage orders, random alpha / beta): bit for bit, signed zeros included,
+    the sequential fp64 oracles; the device csr2bsr of the same matrix equals the
+    host conversion bit for bit."""
+    from spmm_hip import prep
+    ops = _ops()
+    rng = np.random.default_rng(9500 + seed)
+    m, k = int(rng.integers(1, 3000)), int(rng.integers(1, 3000))
+    K = int(rng.choice([1, 3, 16, 64, 100, 128, 300]))
+    rp, ci, v = _csr(rng, m, k, min(int(rng.choice([0, 4, 40, 400])), k))
+    alpha, beta = float(rng.choice([1.0, -1.5])), float(rng.choice([0.0, 0.25]))
+    B = rng.standard_normal((k, K))
+    C0 = rng.standard_normal((m, K))
+    order = int(rng.integers(0, 2))
+    drp, dci, dv = _dev(rp, ci, v)
+    if order == 0:
+        dB, dC = _dev(B, C0.copy())
+        ops.csrmm(drp, dci, dv, dB, m=m, n=K, k=k, ldb=K, C=dC, ldc=K, alpha=alpha, beta=beta)
+        got = dC.cpu().numpy()
+    else:
+        dB, dC = _dev(np.ascontiguousarray(B.T), np.ascontiguousarray(C0.T))
+        ops.csrmm(drp, dci, dv, dB, m=m, n=K, k=k, ldb=k, order_b=ops.ORDER_COL, C=dC, ldc=m,
+                  order_c=ops.ORDER_COL, alpha=alpha, beta=beta)
+        got = dC.cpu().numpy().T
+    want = oracle_csrmm_d(oracle, m, K, rp, ci, v, B, K, 0, alpha=alpha, beta=beta,
+                          C=C0.copy().reshape(-1)).reshape(m, K)
+    what = f"f64 csr m={m} k={k} K={K} order={order} alpha={alpha} beta={beta}"
+    assert np.array_equal(np.ascontiguousarray(got).view(np.int64), want.view(np.int64)), what
+    # the same matrix in blocks: device csr2bsr against the host one, then the fp64 BSR form
+    bs = int(rng.choice([1, 2, 4, 8, 16, 32]))
+    hb = prep.csr2bsr(m, k, rp, ci, v.astype(np.float32), bs)
+    db = ops.csr2bsr(drp, dci, dv.float(), m=m, n=k, bs=bs)
+    for h, d, nm in zip(hb, db, ("rowptr", "colind", "values")):
+        assert np.array_equal(h.view(np.int32), d.cpu().numpy().view(np.int32)), f"csr2bsr {nm}"
+    brp, bci, bv32 = hb
+    mb, kb = (m + bs - 1) // bs, (k + bs - 1) // bs
+    bv = bv32.astype(np.float64)
+    Bp = np.zeros((kb * bs, K))
+    Bp[:k] = B
+    Cp = np.zeros((mb * bs, K))
+    Cp[:m] = C0
+    d1, d2, d3, dBp, dCp = _dev(brp, bci, bv, Bp, Cp.copy())
+    ops.bsrmm(d1, d2, d3, dBp, mb=mb, kb=kb, n=K, bs=bs, ldb=K, C=dCp, ldc=K, alpha=alpha, beta=beta)
+    wantb = oracle_bsrmm_d(oracle, 0, mb, K, bs, brp, bci, bv, Bp, K, 0, alpha=alpha, beta=beta,
+                           C=Cp.copy().reshape(-1)).reshape(mb * bs, K)
+    if bci.size == 0:  # rocsparse_bsrmm.h:152-154's quick return: C untouched, beta or not
+        wantb = Cp
+    assert np.array_equal(dCp.cpu().numpy().view(np.int64), wantb.view(np.int64)), \
+        f"f64 bsr bs={bs} {what}"
