@@ -34,6 +34,7 @@ def test_number_blocks_are_generated():
     assert text == g.headline_table(head, src)
     assert _block("README.md", "workloads") == g.workloads_table(lines, src)
     assert _block("INTEGRATION.md", "entries") == g.entries_table(head, lines, src)
+    assert _block("README.md", "sweep") == g.sweep_table(src)
 
 
 def test_bench_reads_the_same_pass():

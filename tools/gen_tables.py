@@ -7,7 +7,7 @@
 Reads the pass's `bench.log` (the default bench line: the headline with its BASELINE config
 3 / config 5 / products bs 32 side entries and the CPU baseline) and `workloads.jsonl` (one
 bench line per workload), and replaces everything between `<!-- numbers:NAME:begin -->` and
-`<!-- numbers:NAME:end -->` in README.md (NAME = headline, workloads) and INTEGRATION.md
+`<!-- numbers:NAME:end -->` in README.md (NAME = headline, workloads, sweep) and INTEGRATION.md
 (NAME = entries). No number in those blocks is typed by hand.
 """
 from __future__ import annotations
@@ -213,6 +213,23 @@ def entries_table(h: dict, lines: dict, src: str) -> str:
     return "\n".join(out)
 
 
+def sweep_table(src: str) -> str:
+    """The reference's own benchmark sweep (benchmark.py:3-31) of the pass, as
+    tools/ref_sweep.py --table prints it."""
+    import contextlib
+    import importlib.util
+    import io
+    spec = importlib.util.spec_from_file_location("ref_sweep", os.path.join(ROOT, "tools", "ref_sweep.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        mod.table(os.path.join(ROOT, src, "sweep.jsonl"))
+    return (f"From `{src}/sweep.jsonl` (`tools/ref_sweep.py`: the reference's own "
+            f"`benchmark.py` sweep on 131,072² random matrices, one MI355X):\n\n"
+            + buf.getvalue().rstrip("\n"))
+
+
 def replace_block(path: str, name: str, text: str) -> None:
     with open(path) as f:
         s = f.read()
@@ -228,10 +245,11 @@ def main() -> None:
     src = sys.argv[1] if len(sys.argv) > 1 else "profiles/r06_final"
     head, lines = load(os.path.join(ROOT, src))
     tables = {"headline": headline_table(head, src), "workloads": workloads_table(lines, src),
-              "entries": entries_table(head, lines, src)}
+              "entries": entries_table(head, lines, src), "sweep": sweep_table(src)}
     if "--write" in sys.argv:
         replace_block(os.path.join(ROOT, "README.md"), "headline", tables["headline"])
         replace_block(os.path.join(ROOT, "README.md"), "workloads", tables["workloads"])
+        replace_block(os.path.join(ROOT, "README.md"), "sweep", tables["sweep"])
         replace_block(os.path.join(ROOT, "INTEGRATION.md"), "entries", tables["entries"])
     else:
         for k, v in tables.items():
