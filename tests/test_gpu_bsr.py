@@ -194,6 +194,48 @@ def test_segments_with_staged_col_major_b(oracle, device):
     assert_normwise(C.cpu().numpy(), ref, absd, TOL_F32, "segments + staged col-major B")
 
 
+@pytest.mark.parametrize("layout", ["row", "col"])
+@pytest.mark.parametrize("n", [8, 100])
+def test_segments_long_rows_shallow_grid(oracle, device, layout, n):
+    """512 block rows of ~130 blocks (2^16 blocks or more): a shallow grid. Row-major
+    C splits the rows into segments summed by seg_fixup_kernel (each row past twice
+    the mean load per slot); column-major C (transB = 1 with column-major C is
+    test_bsrmm.cu:58's call) runs them longest first. Both layouts, the 64-column
+    tile (n = 8) and the 128-column one, alpha / beta on the column-major one;
+    against the f64 oracle, and the same bits on a second call. (Round 6 tried
+    splitting every row of such grids, column-major C included: slower on the
+    reference sweep at every fill, profiles/r06/ab_seg_shallow.log.)"""
+    ops = _ops()
+    rng = np.random.default_rng(5150 + n)
+    mb, kb, bs = 512, 400, 32
+    rp, ci, v = _rand_bsr(rng, mb, kb, bs, 0.33)
+    assert rp[-1] >= 1 << 16
+    m, k = mb * bs, kb * bs
+    B = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    alpha, beta = (1.0, 0.0) if layout == "row" else (0.5, -1.5)
+
+    def run():
+        if layout == "row":
+            drp, dci, dv, dB = _dev(rp, ci, v, B.reshape(-1))
+            dC = torch.full((m * n,), float("nan"), device=device)
+            ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=n)
+            torch.cuda.synchronize()
+            return dC.cpu().numpy().reshape(m, n)
+        drp, dci, dv, dB, dC = _dev(rp, ci, v, B.reshape(-1), np.ascontiguousarray(C0.T).reshape(-1))
+        ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=dC, ldc=m,
+                  order_c=ops.ORDER_COL, alpha=alpha, beta=beta)
+        torch.cuda.synchronize()
+        return dC.cpu().numpy().reshape(n, m).T
+
+    got = run()
+    ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
+    ref = alpha * ref + (beta * C0.astype(np.float64) if beta else 0.0)
+    absd = abs(alpha) * absd + (abs(beta) * np.abs(C0.astype(np.float64)) if beta else 0.0)
+    assert_normwise(got, ref, absd, TOL_F32, f"long rows, shallow grid, {layout} n={n}")
+    assert np.array_equal(got.view(np.uint32), run().view(np.uint32))
+
+
 @pytest.mark.parametrize("bs", [16, 32])
 @pytest.mark.parametrize("n", [1, 16, 33, 128, 512])
 @pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.5, 2.0)])
