@@ -591,8 +591,9 @@ def timed_loop(step, h, steps, warmup, world, dist, raw=False):
 
 
 def run_csr_weak(args, W, world, rank, dev, dist):
-    """N > 1, weak scaling (the default): every rank owns a products-size row
-    block of a world-times larger power-law graph (spmm_hip.dist.stacked_block:
+    """N > 1 with --scaling weak (config 4's strong form is the default): every
+    rank owns a products-size row block of a world-times larger power-law graph
+    (spmm_hip.dist.stacked_block:
     n rows, nnz nonzeros, the 1-GPU workload's per-GPU work), B replicated
     with world*n rows, C row-sharded in place. No collective in the step; the
     all-gather that would assemble C on every rank is timed after the timed
