@@ -211,6 +211,8 @@ def main() -> None:
     ap.add_argument("--skip-csr", action="store_true")
     ap.add_argument("--skip-bsr", action="store_true")
     ap.add_argument("--table", default=None, help="print the markdown tables of a sweep JSONL")
+    ap.add_argument("--bsr-options", type=int, default=0,
+                    help="spmm_set_bsr_options flags of the handle (1: dense-block product)")
     args = ap.parse_args()
     if args.table:
         table(args.table)
@@ -223,6 +225,8 @@ def main() -> None:
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234)
     h = ops.Handle()
+    if args.bsr_options:
+        h.set_bsr_options(args.bsr_options)
     d = c_void_p()
     assert L.spmm_create_mat_descr(byref(d)) == 0
     Ks = [int(x) for x in args.dims.split(",")]
