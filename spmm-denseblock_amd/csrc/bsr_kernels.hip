@@ -1032,6 +1032,15 @@ __global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int
 // instead of two; the second accumulator is not kept. The 128-column tile
 // computed 128 columns at n = 64, half of them clamped copies (the reference's
 // own sweep at dim 64, benchmark.py:5-8: bs 32 and 64 took the dim-128 time).
+// The panel probe's choice (panel_probe_kernel, bsr32_f32_panel_kernel below): the sampled
+// blocks hold at least kPanelMin of their 32 columns on average (from kPanelMinBlocks blocks).
+constexpr int kPanelSamples = 4096;
+constexpr unsigned kPanelMin = 24;
+constexpr int kPanelMinBlocks = 1 << 15;
+__device__ __forceinline__ bool panel_chosen(const unsigned long long* stat) {
+  return stat[1] > 0 && stat[0] >= (unsigned long long)kPanelMin * stat[1];
+}
+
 template <bool CROW, int XM, int P, int NA, bool O32 = false, bool PK = false, bool ANT = false,
           bool MSK = false, bool SUB = false, bool C64 = false>
 __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
@@ -1039,8 +1048,11 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
     float* __restrict__ C, int ldc, const int* __restrict__ order,
     const int4* __restrict__ segs = nullptr, float* __restrict__ part = nullptr,
-    const unsigned* __restrict__ masks = nullptr) {
+    const unsigned* __restrict__ masks = nullptr,
+    const unsigned long long* __restrict__ gate = nullptr) {
   static_assert(NA >= 2 && NA <= 4 && P >= 2 && P <= 16, "ring depths");
+  // the panel probe chose bsr32_f32_panel_kernel for this matrix (same bits): nothing to do
+  if (gate && panel_chosen(gate)) return;
   static_assert(!(SUB && MSK), "the analysed stream is bs 32 only");
   constexpr int DA = NA - 1;  // A blocks in flight ahead of the producer's block
   constexpr int LDA = SUB ? 64 : 32;  // row stride of a (sub-)block's values
@@ -1466,6 +1478,254 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
     __builtin_amdgcn_s_waitcnt(0);
     const size_t row = (size_t)br * 32 + j;
     for (int it = 0; it < (C64 ? 32 : 64); ++it) {
+      const int jl = 2 * it + h;
+      if (jt + jl < n) {
+        float* p = C + (size_t)(jt + jl) * ldc + row;
+        *p = epi(tile[jl * kTs + j], alpha, beta, p);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bs = 32 PANEL stream (round 6): the column stream's arithmetic for blocks that hold (nearly)
+// every column. On the reference sweep's matrices (test_bsrmm.cu: dense U(-1, 1) blocks) the
+// column stream spends 25 scalar instructions per nonzero column on its item bookkeeping and
+// keeps the MFMA pipe 32-49 % busy (profiles/r06/pmc_cell/). Here one wave per (block row, TW
+// output columns) copies each block's A (4 KB) and its whole B panel (32 rows x TW columns) into
+// LDS by LDS-DMA, D stages deep (every block issues the same number of copies, so the waits
+// are constants), and runs the block's columns in an unrolled loop: per nonzero column c, in
+// ascending order, the MFMAs the column stream issues for it (v_mfma_f32_32x32x1_2b_f32, lane
+// (j, h) A = row j's value of column c, B = columns 4j + 2h, + 1 of row c; C64: column 2j + h),
+// and nothing for an all-zero column. Each output is thus the same chain of fused
+// multiply-adds as in bsr32_f32_cs2_kernel, bit for bit, on every matrix; which of the two
+// runs is a question of speed only. panel_probe_kernel samples up to kPanelSamples blocks and
+// sums their nonzero-column counts (integers: the order of the atomic adds does not matter);
+// the panel stream runs when they hold at least kPanelMin of 32 columns on average, and both
+// kernels are launched, the unchosen one exiting at its first instruction.
+// kPanelProbeWgs workgroups of four waves stride over the samples, each wave keeping its sums
+// in a register; one pair of atomic adds per workgroup (a pair per sample, 8,192 adds on two
+// addresses, took 0.1 ms).
+constexpr int kPanelProbeWgs = 32;
+__global__ __launch_bounds__(256) void panel_probe_kernel(long long nnzb, int ns,
+                                                          const float* __restrict__ val,
+                                                          unsigned long long* __restrict__ stat) {
+  __shared__ unsigned part[4][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  unsigned cols = 0, cnt = 0;
+  for (int i = blockIdx.x * 4 + w; i < ns; i += gridDim.x * 4) {
+    const long long k = (long long)(((long double)i + 0.5L) * (long double)nnzb / ns);
+    const float* blk = val + (size_t)k * 1024 + j * 32 + 16 * h;
+    f32x4 x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = *reinterpret_cast<const f32x4*>(blk + 4 * q);
+    unsigned msk = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const unsigned long long bl =
+            __builtin_amdgcn_ballot_w64((__float_as_uint(x[q][e]) & 0x7fffffffu) != 0u);
+        msk |= ((unsigned)bl != 0u ? 1u : 0u) << (4 * q + e);
+        msk |= ((unsigned)(bl >> 32) != 0u ? 1u : 0u) << (16 + 4 * q + e);
+      }
+    cols += (unsigned)__builtin_popcount(msk);
+    ++cnt;
+  }
+  if (lane == 0) {
+    part[w][0] = cols;
+    part[w][1] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned c = part[0][0] + part[1][0] + part[2][0] + part[3][0];
+    const unsigned t = part[0][1] + part[1][1] + part[2][1] + part[3][1];
+    if (t) {
+      atomicAdd(&stat[0], (unsigned long long)c);
+      atomicAdd(&stat[1], (unsigned long long)t);
+    }
+  }
+}
+
+template <bool CROW, bool C64, int D>
+__global__ __launch_bounds__(64) void bsr32_f32_panel_kernel(
+    int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
+    const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
+    float* __restrict__ C, int ldc, const int* __restrict__ order,
+    const unsigned long long* __restrict__ stat) {
+  constexpr int TW = C64 ? 64 : 128;        // output columns of the wave
+  constexpr int kStage = 1024 + 32 * TW;    // floats: A block + B panel
+  constexpr int kOps = 4 + 32 * TW / 256;   // copies per block (16 B per lane each)
+  static_assert(D >= 2 && (D - 2) * kOps <= 63, "stages");
+  __shared__ __attribute__((aligned(16))) float smem[D * kStage];
+  if (!panel_chosen(stat)) return;
+  const int lane = threadIdx.x;
+  const int j = lane & 31, h = lane >> 5;
+  const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
+  const int jt = blockIdx.y * TW;
+  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  const unsigned lds0 = (unsigned)reinterpret_cast<uintptr_t>(smem);
+  // A copies: the column stream's swizzled layout (16-B chunk (l & 7) ^ ((r >> 1) & 7) of row r)
+  int a_src[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 8 * q + (lane >> 3);
+    a_src[q] = r * 32 + 4 * ((lane & 7) ^ ((r >> 1) & 7));
+  }
+  // B panel copies: instruction i covers rows (64 / (TW / 4)) i .. , lane l the 16 B at row
+  // RPI i + l / CPR, column chunk l % CPR (clamped inside the row: n >= 4, n % 4 == 0)
+  constexpr int CPR = TW / 4, RPI = 64 / CPR;
+  const int b_row = lane / CPR;
+  const int b_col = min(jt + 4 * (lane % CPR), n - 4);
+  auto issue = [&](int k, int st) {
+    const int kk = min(k, k1 - 1);
+    float* stage = smem + st * kStage;
+    const float* src = val + (size_t)kk * 1024;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(src + a_src[q & 1] + 16 * 32 * (q >> 1)),
+                                       (lds_void_t)(stage + 256 * q), 16, 0, 2);
+    const int bc = colind[kk];
+    const float* bsrc = B + ((size_t)bc * 32 + b_row) * ldb + b_col;
+#pragma unroll
+    for (int i = 0; i < 32 / RPI; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(bsrc + (size_t)(RPI * i) * ldb),
+                                       (lds_void_t)(stage + 1024 + TW * RPI * i), 16, 0, 0);
+  };
+  unsigned moff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    moff[i] = (unsigned)((2 * i + h) * 128 + 16 * ((j >> 2) ^ i) + 4 * (j & 3));
+  const unsigned a_row = (unsigned)(j * 128);
+  const int a_sw = (j >> 1) & 7;
+  const unsigned boff = C64 ? 4u * (unsigned)(2 * j + h) : 4u * (unsigned)(4 * j + 2 * h);
+
+  f32x32 u0, u1;
+#pragma unroll
+  for (int e = 0; e < 32; ++e) u0[e] = u1[e] = 0.f;
+  if (k0 < k1) {
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) issue(k0 + d, d);
+    int st = 0;
+    for (int k = k0; k < k1; ++k) {
+      // block k's copies landed (the D - 2 blocks issued after it may still be in flight);
+      // hand-placed: with D = 2 this is the double buffer's full wait, block k + 1's copies
+      // being issued right below, a block of MFMAs ahead of their use
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * kOps) : "memory");
+      // refill the stage block k - 1 used (its LDS reads all completed in the last round)
+      issue(k + D - 1, st == 0 ? D - 1 : st - 1);
+      const unsigned sb = lds0 + 4u * (unsigned)(st * kStage);
+      unsigned m;
+      {
+        f32x2 x[8];
+        asm volatile(
+            "ds_read2st64_b32 %0, %8 offset1:8\n\t"
+            "ds_read2st64_b32 %1, %9 offset1:8\n\t"
+            "ds_read2st64_b32 %2, %10 offset1:8\n\t"
+            "ds_read2st64_b32 %3, %11 offset1:8\n\t"
+            "ds_read2st64_b32 %4, %12 offset1:8\n\t"
+            "ds_read2st64_b32 %5, %13 offset1:8\n\t"
+            "ds_read2st64_b32 %6, %14 offset1:8\n\t"
+            "ds_read2st64_b32 %7, %15 offset1:8\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]),
+              "=&v"(x[6]), "=&v"(x[7])
+            : "v"(sb + moff[0]), "v"(sb + moff[1]), "v"(sb + moff[2]), "v"(sb + moff[3]),
+              "v"(sb + moff[4]), "v"(sb + moff[5]), "v"(sb + moff[6]), "v"(sb + moff[7])
+            : "memory");
+        unsigned t = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          t |= (__float_as_uint(x[i][0]) | __float_as_uint(x[i][1])) & 0x7fffffffu;
+        const unsigned long long bl = __builtin_amdgcn_ballot_w64(t != 0u);
+        m = (unsigned)bl | (unsigned)(bl >> 32);
+      }
+      // the block's columns, 8 at a time: their A values and B rows read, then the MFMAs of
+      // the nonzero ones in ascending order
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float a[8];
+        typedef typename std::conditional<C64, float, f32x2>::type brow_t;
+        brow_t b[8];
+#pragma unroll
+        for (int c8 = 0; c8 < 8; ++c8) {
+          const int c = 8 * g + c8;
+          const unsigned aaddr = sb + a_row + 16u * (unsigned)((c >> 2) ^ a_sw) + 4u * (unsigned)(c & 3);
+          const unsigned baddr = sb + 4096u + (unsigned)(c * TW * 4) + boff;
+          if constexpr (C64)
+            asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3"
+                         : "=&v"(a[c8]), "=&v"(b[c8]) : "v"(aaddr), "v"(baddr) : "memory");
+          else
+            asm volatile("ds_read_b32 %0, %2\n\tds_read_b64 %1, %3"
+                         : "=&v"(a[c8]), "=&v"(b[c8]) : "v"(aaddr), "v"(baddr) : "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int c8 = 0; c8 < 8; ++c8) {
+          if ((m >> (8 * g + c8)) & 1u) {
+            if constexpr (C64) {
+              u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(a[c8], b[c8], u0, 0, 0, 0);
+            } else {
+              u0 = __builtin_amdgcn_mfma_f32_32x32x1f32(a[c8], b[c8][0], u0, 0, 0, 0);
+              u1 = __builtin_amdgcn_mfma_f32_32x32x1f32(a[c8], b[c8][1], u1, 0, 0, 0);
+            }
+          }
+        }
+      }
+      st = st == D - 1 ? 0 : st + 1;
+    }
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // drain the clamped tail copies
+  }
+  if constexpr (CROW) {
+    const int col = jt + (C64 ? 2 : 4) * j;
+    if (col >= n) return;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const size_t row = (size_t)br * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if constexpr (C64) {
+        f32x2* p = reinterpret_cast<f32x2*>(C + row * ldc + col);
+        f32x2 v = {u0[e], u0[16 + e]};
+        if (beta == 0.f) {
+          v *= alpha;
+        } else {
+          const f32x2 c = *p;
+#pragma unroll
+          for (int i = 0; i < 2; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
+        }
+        __builtin_nontemporal_store(v, p);
+      } else {
+        f32x4* p = reinterpret_cast<f32x4*>(C + row * ldc + col);
+        f32x4 v = {u0[e], u1[e], u0[16 + e], u1[16 + e]};
+        if (beta == 0.f) {
+          v *= alpha;
+        } else {
+          const f32x4 c = *p;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = __builtin_fmaf(beta, c[i], alpha * v[i]);
+        }
+        __builtin_nontemporal_store(v, p);
+      }
+    }
+  } else {
+    constexpr int kTs = 36;
+    float* tile = smem;  // every copy has landed (waited above) and no wave reads the stages
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+      if constexpr (C64) {
+        tile[(2 * j) * kTs + row] = u0[e];
+        tile[(2 * j + 1) * kTs + row] = u0[16 + e];
+      } else {
+        tile[(4 * j) * kTs + row] = u0[e];
+        tile[(4 * j + 1) * kTs + row] = u1[e];
+        tile[(4 * j + 2) * kTs + row] = u0[16 + e];
+        tile[(4 * j + 3) * kTs + row] = u1[16 + e];
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const size_t row = (size_t)br * 32 + j;
+    for (int it = 0; it < TW / 2; ++it) {
       const int jl = 2 * it + h;
       if (jt + jl < n) {
         float* p = C + (size_t)(jt + jl) * ldc + row;
@@ -3883,18 +4143,35 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       // n <= 64: the 64-column tile (C64; grid.y is 1 either way, so the segments'
       // partial layout is the same)
       const bool c64 = n <= 64;
+      // the panel stream (same bits) when the probe finds the blocks dense: both kernels go
+      // out, the probe's sums choose on the device (no host round trip, graph-capturable)
+      unsigned long long* pstat = nullptr;
+      if (!msk && !sg && lv == kBsr32Cs && nnzb >= kPanelMinBlocks) {
+        if (spmm_status_t st2 = spmm::ensure_scratch(ctx, 2 * sizeof(unsigned long long))) {
+          timing_end(ctx, slot);
+          return st2;
+        }
+        pstat = static_cast<unsigned long long*>(ctx->scratch);
+        if (hipError_t e = hipMemsetAsync(pstat, 0, 2 * sizeof(*pstat), ctx->stream)) {
+          timing_end(ctx, slot);
+          return from_hip(e);
+        }
+        const int ns = std::min(nnzb, kPanelSamples);
+        hipLaunchKernelGGL(panel_probe_kernel, dim3(kPanelProbeWgs), dim3(256), 0, ctx->stream,
+                           (long long)nnzb, ns, val, pstat);
+      }
 #define CS2_ONE(C64_, O32_, PK_, ANT_)                                                           \
   do {                                                                                           \
     if (crow)                                                                                    \
       hipLaunchKernelGGL((bsr32_f32_cs2_kernel<true, 32, 6, 3, O32_, PK_, ANT_, false, false,    \
                                                C64_>),                                           \
                          g2, dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,       \
-                         alpha, beta, C, ldc, ord, sg, pt, masks);                               \
+                         alpha, beta, C, ldc, ord, sg, pt, masks, pstat);                        \
     else                                                                                         \
       hipLaunchKernelGGL((bsr32_f32_cs2_kernel<false, 32, 6, 3, O32_, PK_, ANT_, false, false,   \
                                                C64_>),                                           \
                          g2, dim3(64), 0, ctx->stream, mb, n, rowptr, colind, val, B, ldb,       \
-                         alpha, beta, C, ldc, ord, nullptr, nullptr, masks);                     \
+                         alpha, beta, C, ldc, ord, nullptr, nullptr, masks, pstat);              \
   } while (0)
 #define CS2_LAUNCH(O32_, PK_, ANT_)                                                              \
   do {                                                                                           \
@@ -3930,6 +4207,23 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       else CS2_LAUNCH(false, true, true);  // kBsr32CsWideLdb
 #undef CS2_LAUNCH
 #undef CS2_ONE
+      if (pstat) {
+        if (crow && c64)
+          hipLaunchKernelGGL((bsr32_f32_panel_kernel<true, true, 2>), g2, dim3(64), 0, ctx->stream,
+                             mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, ord, pstat);
+        else if (crow)
+          hipLaunchKernelGGL((bsr32_f32_panel_kernel<true, false, 2>), g2, dim3(64), 0,
+                             ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,
+                             ord, pstat);
+        else if (c64)
+          hipLaunchKernelGGL((bsr32_f32_panel_kernel<false, true, 2>), g2, dim3(64), 0,
+                             ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,
+                             ord, pstat);
+        else
+          hipLaunchKernelGGL((bsr32_f32_panel_kernel<false, false, 2>), g2, dim3(64), 0,
+                             ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,
+                             ord, pstat);
+      }
       if (spl)
         hipLaunchKernelGGL(seg_fixup_kernel, dim3(nspl, grid.y), dim3(256), 0, ctx->stream, n,
                            spl, pt, alpha, beta, C, ldc);

@@ -2252,3 +2252,61 @@ def test_random_shapes_bs16_f16_bits(oracle, device, seed):
         torch.cuda.synchronize()
         assert_normwise(C3.cpu().numpy(), ref, absd, TOL_F16_ACC, what + " grouped")
         grp.close()
+
+
+@pytest.mark.parametrize("layout,n", [("row", 64), ("row", 128), ("col", 64), ("col", 132)])
+@pytest.mark.parametrize("fill", ["dense", "mostly", "sparse"])
+def test_panel_stream_bits(oracle, device, layout, n, fill):
+    """The bs 32 panel stream (bsr32_f32_panel_kernel, round 6): from 2^15 blocks the drop-in
+    call probes the blocks' nonzero columns and, when they hold at least 24 of 32 on average,
+    runs the panel stream instead of the column stream. Both issue the same fused
+    multiply-adds per output in the same order and skip the same all-zero columns, so the
+    drop-in's bits equal the analysed entry's (the column stream on the analysis's masks) for
+    dense blocks (the reference sweep's), blocks with 4 zero columns each and zero blocks
+    (mostly), and column-sparse blocks (the column stream itself); both C layouts, the 64-
+    and 128-column tiles, alpha / beta on the column-major form; against the f64 oracle on
+    one case."""
+    ops = _ops()
+    rng = np.random.default_rng(7300 + n + {"dense": 0, "mostly": 1, "sparse": 2}[fill])
+    mb, kb, bs = 512, 256, 32
+    per_row = 66
+    ci = np.concatenate([np.sort(rng.choice(kb, per_row, replace=False)) for _ in range(mb)])
+    rp = np.arange(0, mb * per_row + 1, per_row, dtype=np.int32)
+    nnzb = ci.size
+    assert nnzb >= 1 << 15
+    vb = rng.uniform(-1, 1, (nnzb, bs, bs)).astype(np.float32)
+    if fill != "dense":
+        zc = 4 if fill == "mostly" else 20
+        cols = np.argsort(rng.random((nnzb, bs)), axis=1)[:, :zc]
+        vb[np.arange(nnzb)[:, None, None], np.arange(bs)[None, :, None], cols[:, None, :]] = 0.0
+        vb[rng.random(nnzb) < 0.01] = 0.0
+    v = vb.reshape(-1)
+    m, k = mb * bs, kb * bs
+    B = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    alpha, beta = (1.0, 0.0) if layout == "row" else (0.5, -1.5)
+    drp, dci, dv, dB = _dev(rp, ci.astype(np.int32), v, B.reshape(-1))
+    ld, oc = (n, ops.ORDER_ROW) if layout == "row" else (m, ops.ORDER_COL)
+
+    def fresh():
+        c = C0 if layout == "row" else np.ascontiguousarray(C0.T)
+        return torch.from_numpy(c.reshape(-1).copy()).cuda()
+
+    def host(t):
+        a = t.cpu().numpy()
+        return a.reshape(m, n) if layout == "row" else a.reshape(n, m).T
+
+    C1 = fresh()
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=C1, ldc=ld, order_c=oc,
+              alpha=alpha, beta=beta)
+    masks, vcol = ops.bsr32_analysis(dv, nnzb=nnzb)
+    C2 = fresh()
+    ops.bsrmm_analysed(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n, ldb=n, C=C2, ldc=ld,
+                       order_c=oc, alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    got, ref2 = host(C1), host(C2)
+    diff = got.view(np.uint32) != ref2.view(np.uint32)
+    assert not diff.any(), f"{fill} {layout} n={n}: {int(diff.sum())} elements differ in bits"
+    if fill == "mostly" and layout == "row" and n == 128:
+        ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
+        assert_normwise(got, ref, absd, TOL_F32, "panel stream")
