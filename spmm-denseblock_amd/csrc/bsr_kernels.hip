@@ -1037,6 +1037,12 @@ __global__ __launch_bounds__(1024) void block_row_order_kernel(int mb, const int
 constexpr int kPanelSamples = 4096;
 constexpr unsigned kPanelMin = 24;
 constexpr int kPanelMinBlocks = 1 << 15;
+#ifndef SPMM_PANEL_D64
+#define SPMM_PANEL_D64 2
+#endif
+#ifndef SPMM_PANEL_D128
+#define SPMM_PANEL_D128 2
+#endif
 __device__ __forceinline__ bool panel_chosen(const unsigned long long* stat) {
   return stat[1] > 0 && stat[0] >= (unsigned long long)kPanelMin * stat[1];
 }
@@ -1503,30 +1509,37 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
 // sums their nonzero-column counts (integers: the order of the atomic adds does not matter);
 // the panel stream runs when they hold at least kPanelMin of 32 columns on average, and both
 // kernels are launched, the unchosen one exiting at its first instruction.
-// kPanelProbeWgs workgroups of four waves stride over the samples, each wave keeping its sums
-// in a register; one pair of atomic adds per workgroup (a pair per sample, 8,192 adds on two
-// addresses, took 0.1 ms).
-constexpr int kPanelProbeWgs = 32;
+// Each wave takes kPanelPerWave samples, all of their loads issued together; one pair of
+// atomic adds per workgroup of four waves (a pair per sample, 8,192 adds on two addresses,
+// took 0.1 ms).
+constexpr int kPanelPerWave = 4;
 __global__ __launch_bounds__(256) void panel_probe_kernel(long long nnzb, int ns,
                                                           const float* __restrict__ val,
                                                           unsigned long long* __restrict__ stat) {
   __shared__ unsigned part[4][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 31, h = lane >> 5;
-  unsigned cols = 0, cnt = 0;
-  for (int i = blockIdx.x * 4 + w; i < ns; i += gridDim.x * 4) {
+  const int i0 = (blockIdx.x * 4 + w) * kPanelPerWave;
+  f32x4 x[kPanelPerWave][4];
+#pragma unroll
+  for (int t = 0; t < kPanelPerWave; ++t) {
+    const int i = min(i0 + t, ns - 1);
     const long long k = (long long)(((long double)i + 0.5L) * (long double)nnzb / ns);
     const float* blk = val + (size_t)k * 1024 + j * 32 + 16 * h;
-    f32x4 x[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = *reinterpret_cast<const f32x4*>(blk + 4 * q);
+    for (int q = 0; q < 4; ++q) x[t][q] = *reinterpret_cast<const f32x4*>(blk + 4 * q);
+  }
+  unsigned cols = 0, cnt = 0;
+#pragma unroll
+  for (int t = 0; t < kPanelPerWave; ++t) {
+    if (i0 + t >= ns) break;
     unsigned msk = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const unsigned long long bl =
-            __builtin_amdgcn_ballot_w64((__float_as_uint(x[q][e]) & 0x7fffffffu) != 0u);
+            __builtin_amdgcn_ballot_w64((__float_as_uint(x[t][q][e]) & 0x7fffffffu) != 0u);
         msk |= ((unsigned)bl != 0u ? 1u : 0u) << (4 * q + e);
         msk |= ((unsigned)(bl >> 32) != 0u ? 1u : 0u) << (16 + 4 * q + e);
       }
@@ -4157,8 +4170,8 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
           return from_hip(e);
         }
         const int ns = std::min(nnzb, kPanelSamples);
-        hipLaunchKernelGGL(panel_probe_kernel, dim3(kPanelProbeWgs), dim3(256), 0, ctx->stream,
-                           (long long)nnzb, ns, val, pstat);
+        hipLaunchKernelGGL(panel_probe_kernel, dim3((ns + 4 * kPanelPerWave - 1) / (4 * kPanelPerWave)),
+                           dim3(256), 0, ctx->stream, (long long)nnzb, ns, val, pstat);
       }
 #define CS2_ONE(C64_, O32_, PK_, ANT_)                                                           \
   do {                                                                                           \
@@ -4209,18 +4222,18 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
 #undef CS2_ONE
       if (pstat) {
         if (crow && c64)
-          hipLaunchKernelGGL((bsr32_f32_panel_kernel<true, true, 2>), g2, dim3(64), 0, ctx->stream,
+          hipLaunchKernelGGL((bsr32_f32_panel_kernel<true, true, SPMM_PANEL_D64>), g2, dim3(64), 0, ctx->stream,
                              mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, ord, pstat);
         else if (crow)
-          hipLaunchKernelGGL((bsr32_f32_panel_kernel<true, false, 2>), g2, dim3(64), 0,
+          hipLaunchKernelGGL((bsr32_f32_panel_kernel<true, false, SPMM_PANEL_D128>), g2, dim3(64), 0,
                              ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,
                              ord, pstat);
         else if (c64)
-          hipLaunchKernelGGL((bsr32_f32_panel_kernel<false, true, 2>), g2, dim3(64), 0,
+          hipLaunchKernelGGL((bsr32_f32_panel_kernel<false, true, SPMM_PANEL_D64>), g2, dim3(64), 0,
                              ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,
                              ord, pstat);
         else
-          hipLaunchKernelGGL((bsr32_f32_panel_kernel<false, false, 2>), g2, dim3(64), 0,
+          hipLaunchKernelGGL((bsr32_f32_panel_kernel<false, false, SPMM_PANEL_D128>), g2, dim3(64), 0,
                              ctx->stream, mb, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc,
                              ord, pstat);
       }
