@@ -1513,7 +1513,8 @@ __global__ __launch_bounds__(64) void bsr32_f32_cs2_kernel(
 // atomic adds per workgroup of four waves (a pair per sample, 8,192 adds on two addresses,
 // took 0.1 ms).
 constexpr int kPanelPerWave = 4;
-__global__ __launch_bounds__(256) void panel_probe_kernel(long long nnzb, int ns,
+// SUB (bs 64): the samples are 32 x 32 sub-blocks (nnzb counts them, four per block).
+__global__ __launch_bounds__(256) void panel_probe_kernel(long long nnzb, int ns, int sub,
                                                           const float* __restrict__ val,
                                                           unsigned long long* __restrict__ stat) {
   __shared__ unsigned part[4][2];
@@ -1525,7 +1526,8 @@ __global__ __launch_bounds__(256) void panel_probe_kernel(long long nnzb, int ns
   for (int t = 0; t < kPanelPerWave; ++t) {
     const int i = min(i0 + t, ns - 1);
     const long long k = (long long)(((long double)i + 0.5L) * (long double)nnzb / ns);
-    const float* blk = val + (size_t)k * 1024 + j * 32 + 16 * h;
+    const float* blk = sub ? val + (size_t)(k >> 2) * 4096 + (k & 2) * 1024 + (k & 1) * 32 + j * 64 + 16 * h
+                           : val + (size_t)k * 1024 + j * 32 + 16 * h;
 #pragma unroll
     for (int q = 0; q < 4; ++q) x[t][q] = *reinterpret_cast<const f32x4*>(blk + 4 * q);
   }
@@ -1561,7 +1563,9 @@ __global__ __launch_bounds__(256) void panel_probe_kernel(long long nnzb, int ns
   }
 }
 
-template <bool CROW, bool C64, int D>
+// SUB (bs 64): as the column stream's SUB form, one wave per 32-row half br of a block row,
+// walking the virtual 32 x 32 sub-blocks kk of its row (block kk / 2, column half kk % 2).
+template <bool CROW, bool C64, int D, bool SUB = false>
 __global__ __launch_bounds__(64) void bsr32_f32_panel_kernel(
     int mb, int n, const int* __restrict__ rowptr, const int* __restrict__ colind,
     const float* __restrict__ val, const float* __restrict__ B, int ldb, float alpha, float beta,
@@ -1577,14 +1581,16 @@ __global__ __launch_bounds__(64) void bsr32_f32_panel_kernel(
   const int j = lane & 31, h = lane >> 5;
   const int br = order ? order[blockIdx.x] : xcd_block_row(blockIdx.x, mb, 32);
   const int jt = blockIdx.y * TW;
-  const int k0 = rowptr[br], k1 = rowptr[br + 1];
+  const int k0 = SUB ? 2 * rowptr[br >> 1] : rowptr[br];
+  const int k1 = SUB ? 2 * rowptr[(br >> 1) + 1] : rowptr[br + 1];
   const unsigned lds0 = (unsigned)reinterpret_cast<uintptr_t>(smem);
   // A copies: the column stream's swizzled layout (16-B chunk (l & 7) ^ ((r >> 1) & 7) of row r)
+  constexpr int LDA = SUB ? 64 : 32;
   int a_src[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int r = 8 * q + (lane >> 3);
-    a_src[q] = r * 32 + 4 * ((lane & 7) ^ ((r >> 1) & 7));
+    a_src[q] = r * LDA + 4 * ((lane & 7) ^ ((r >> 1) & 7));
   }
   // B panel copies: instruction i covers rows (64 / (TW / 4)) i .. , lane l the 16 B at row
   // RPI i + l / CPR, column chunk l % CPR (clamped inside the row: n >= 4, n % 4 == 0)
@@ -1594,12 +1600,13 @@ __global__ __launch_bounds__(64) void bsr32_f32_panel_kernel(
   auto issue = [&](int k, int st) {
     const int kk = min(k, k1 - 1);
     float* stage = smem + st * kStage;
-    const float* src = val + (size_t)kk * 1024;
+    const float* src = SUB ? val + (size_t)(kk >> 1) * 4096 + (br & 1) * 2048 + (kk & 1) * 32
+                           : val + (size_t)kk * 1024;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((gbl_void_t)(src + a_src[q & 1] + 16 * 32 * (q >> 1)),
+      __builtin_amdgcn_global_load_lds((gbl_void_t)(src + a_src[q & 1] + 16 * LDA * (q >> 1)),
                                        (lds_void_t)(stage + 256 * q), 16, 0, 2);
-    const int bc = colind[kk];
+    const int bc = SUB ? 2 * colind[kk >> 1] + (kk & 1) : colind[kk];
     const float* bsrc = B + ((size_t)bc * 32 + b_row) * ldb + b_col;
 #pragma unroll
     for (int i = 0; i < 32 / RPI; ++i)
@@ -4171,7 +4178,7 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
         }
         const int ns = std::min(nnzb, kPanelSamples);
         hipLaunchKernelGGL(panel_probe_kernel, dim3((ns + 4 * kPanelPerWave - 1) / (4 * kPanelPerWave)),
-                           dim3(256), 0, ctx->stream, (long long)nnzb, ns, val, pstat);
+                           dim3(256), 0, ctx->stream, (long long)nnzb, ns, 0, val, pstat);
       }
 #define CS2_ONE(C64_, O32_, PK_, ANT_)                                                           \
   do {                                                                                           \
@@ -4253,10 +4260,27 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
       timing_end(ctx, slot);
       return st;
     }
+    // the panel stream over the sub-blocks when the probe finds them dense (same bits)
+    unsigned long long* pstat = nullptr;
+    if (narrow && 4LL * nnzb >= kPanelMinBlocks) {
+      if (spmm_status_t st2 = spmm::ensure_scratch(ctx, 2 * sizeof(unsigned long long))) {
+        timing_end(ctx, slot);
+        return st2;
+      }
+      pstat = static_cast<unsigned long long*>(ctx->scratch);
+      if (hipError_t e = hipMemsetAsync(pstat, 0, 2 * sizeof(*pstat), ctx->stream)) {
+        timing_end(ctx, slot);
+        return from_hip(e);
+      }
+      const long long nsub = 4LL * nnzb;
+      const int ns = (int)std::min<long long>(nsub, kPanelSamples);
+      hipLaunchKernelGGL(panel_probe_kernel, dim3((ns + 4 * kPanelPerWave - 1) / (4 * kPanelPerWave)),
+                         dim3(256), 0, ctx->stream, nsub, ns, 1, val, pstat);
+    }
 #define SUB_ONE(CR_, O32_, C64_)                                                                 \
   hipLaunchKernelGGL((bsr32_f32_cs2_kernel<CR_, 32, 6, 3, O32_, true, true, false, true, C64_>),  \
                      g2, dim3(64), 0, ctx->stream, mb2, n, rowptr, colind, val, B, ldb, alpha,   \
-                     beta, C, ldc, ord, nullptr, nullptr, nullptr)
+                     beta, C, ldc, ord, nullptr, nullptr, nullptr, pstat)
 #define SUB_LAUNCH(CR_, O32_)                                                                    \
   do {                                                                                           \
     if (n <= 64) SUB_ONE(CR_, O32_, true);  /* the 64-column tile */                             \
@@ -4269,6 +4293,16 @@ spmm_status_t launch_bsrmm_f32(spmm_context* ctx, spmm_direction_t dir, int mb, 
     }
 #undef SUB_LAUNCH
 #undef SUB_ONE
+    if (pstat) {
+#define PSUB(CR_, C64_, D_)                                                                       \
+  hipLaunchKernelGGL((bsr32_f32_panel_kernel<CR_, C64_, D_, true>), g2, dim3(64), 0, ctx->stream, \
+                     mb2, n, rowptr, colind, val, B, ldb, alpha, beta, C, ldc, ord, pstat)
+      if (crow && n <= 64) PSUB(true, true, SPMM_PANEL_D64);
+      else if (crow) PSUB(true, false, SPMM_PANEL_D128);
+      else if (n <= 64) PSUB(false, true, SPMM_PANEL_D64);
+      else PSUB(false, false, SPMM_PANEL_D128);
+#undef PSUB
+    }
   } else if (bs == 32 && vec_ok) {
     const int waves = n <= 32 ? 1 : (n <= 64 ? 2 : 4);
     dim3 grid(mb, (n + 32 * waves - 1) / (32 * waves));

@@ -2268,8 +2268,10 @@ def test_panel_stream_bits(oracle, device, layout, n, fill):
     one case."""
     ops = _ops()
     rng = np.random.default_rng(7300 + n + {"dense": 0, "mostly": 1, "sparse": 2}[fill])
-    mb, kb, bs = 512, 256, 32
-    per_row = 66
+    # rows of at most 64 blocks: a shallow grid cuts longer rows of a row-major C into segments
+    # (column stream, cs2_segments), which the panel stream leaves to the column stream
+    mb, kb, bs = 560, 256, 32
+    per_row = 60
     ci = np.concatenate([np.sort(rng.choice(kb, per_row, replace=False)) for _ in range(mb)])
     rp = np.arange(0, mb * per_row + 1, per_row, dtype=np.int32)
     nnzb = ci.size
@@ -2310,3 +2312,58 @@ def test_panel_stream_bits(oracle, device, layout, n, fill):
     if fill == "mostly" and layout == "row" and n == 128:
         ref, absd = oracle_bsrmm_f64(oracle, 0, mb, n, bs, rp, ci, v, B, n, 0)
         assert_normwise(got, ref, absd, TOL_F32, "panel stream")
+
+
+@pytest.mark.parametrize("layout,n", [("row", 64), ("row", 128), ("col", 128)])
+@pytest.mark.parametrize("fill", ["dense", "mostly"])
+def test_panel_stream_bs64_bits(device, layout, n, fill):
+    """bs 64 runs the bs 32 streams over its 32 x 32 sub-blocks; from 2^15 sub-blocks the
+    panel stream takes them when they are dense. Its bits equal the analysed bs 32 entry's
+    (the column stream) on the same matrix re-blocked to bs 32."""
+    ops = _ops()
+    rng = np.random.default_rng(7400 + n + (fill == "mostly"))
+    # 32 blocks per row: the bs 32 form's rows hold 64 sub-blocks, uncut (see above)
+    mb, kb, bs = 256, 128, 64
+    per_row = 32
+    ci = np.concatenate([np.sort(rng.choice(kb, per_row, replace=False)) for _ in range(mb)])
+    rp = np.arange(0, mb * per_row + 1, per_row, dtype=np.int32)
+    nnzb = ci.size
+    assert 4 * nnzb >= 1 << 15
+    vb = rng.uniform(-1, 1, (nnzb, bs, bs)).astype(np.float32)
+    if fill == "mostly":
+        cols = np.argsort(rng.random((nnzb, bs)), axis=1)[:, :8]
+        vb[np.arange(nnzb)[:, None, None], np.arange(bs)[None, :, None], cols[:, None, :]] = 0.0
+    # the same matrix as bs 32: block row 2R + h holds (2C, 2C + 1) for each block (R, C)
+    sub = vb.reshape(mb, per_row, 2, 32, 2, 32).transpose(0, 2, 1, 4, 3, 5)  # R, h, b, ch, 32, 32
+    v32 = np.ascontiguousarray(sub).reshape(-1)
+    ci32 = np.repeat(2 * ci.reshape(mb, 1, per_row), 2, axis=1)[..., None] + np.arange(2)
+    ci32 = ci32.reshape(-1).astype(np.int32)
+    rp32 = np.arange(0, 2 * mb * 2 * per_row + 1, 2 * per_row, dtype=np.int32)
+    m, k = mb * bs, kb * bs
+    B = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    alpha, beta = (1.0, 0.0) if layout == "row" else (0.5, -1.5)
+    ld, oc = (n, ops.ORDER_ROW) if layout == "row" else (m, ops.ORDER_COL)
+
+    def fresh():
+        c = C0 if layout == "row" else np.ascontiguousarray(C0.T)
+        return torch.from_numpy(c.reshape(-1).copy()).cuda()
+
+    def host(t):
+        a = t.cpu().numpy()
+        return a.reshape(m, n) if layout == "row" else a.reshape(n, m).T
+
+    drp, dci, dv, dB = _dev(rp, ci.astype(np.int32), vb.reshape(-1), B.reshape(-1))
+    C1 = fresh()
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=C1, ldc=ld, order_c=oc,
+              alpha=alpha, beta=beta)
+    del dv
+    drp2, dci2, dv2 = _dev(rp32, ci32, v32)
+    masks, vcol = ops.bsr32_analysis(dv2, nnzb=ci32.size)
+    C2 = fresh()
+    ops.bsrmm_analysed(drp2, dci2, vcol, masks, dB, mb=2 * mb, kb=2 * kb, n=n, ldb=n, C=C2,
+                       ldc=ld, order_c=oc, alpha=alpha, beta=beta)
+    torch.cuda.synchronize()
+    got, ref = host(C1), host(C2)
+    diff = got.view(np.uint32) != ref.view(np.uint32)
+    assert not diff.any(), f"bs 64 {fill} {layout} n={n}: {int(diff.sum())} elements differ"
