@@ -208,6 +208,33 @@ def main():
         bad += check(f"RCM reddit bsr{bs2}", run, reps)
         del brp, bci, bval, B2, C2
         torch.cuda.empty_cache()
+    # the bs 32 panel stream (dense blocks, the reference sweep's test_bsrmm matrices): reruns,
+    # both C layouts, and its bits against the analysed column stream's
+    g = torch.Generator(device=dev)
+    g.manual_seed(99)
+    mbp, per_row, K = 2048, 60, 128
+    bci = torch.sort(torch.rand((mbp, mbp), device=dev, generator=g).argsort(dim=1)[:, :per_row],
+                     dim=1)[0].to(torch.int32).reshape(-1).contiguous()
+    brp = torch.arange(0, mbp * per_row + 1, per_row, dtype=torch.int32, device=dev)
+    bval = torch.rand(bci.numel() * 1024, device=dev, generator=g) * 2 - 1
+    B = torch.rand((mbp * 32, K), device=dev, generator=g) * 2 - 1
+    masks, vcol = ops.bsr32_analysis(bval, nnzb=bci.numel())
+    for oc, tag in ((ops.ORDER_ROW, "row-major C"), (ops.ORDER_COL, "column-major C")):
+        C = torch.empty(mbp * 32 * K, device=dev)
+        ld = K if oc == ops.ORDER_ROW else mbp * 32
+
+        def run_p(C=C, oc=oc, ld=ld):
+            ops.bsrmm(brp, bci, bval, B, mb=mbp, kb=mbp, n=K, bs=32, ldb=K, C=C, ldc=ld, order_c=oc)
+            return C
+        bad += check(f"bsr32 fp32 K=128 dense blocks (panel stream, {tag})", run_p, reps)
+        C2 = torch.empty_like(C)
+        ops.bsrmm_analysed(brp, bci, vcol, masks, B, mb=mbp, kb=mbp, n=K, ldb=K, C=C2, ldc=ld,
+                           order_c=oc)
+        torch.cuda.synchronize()
+        d = int((run_p() != C2).sum())
+        print(f"bsr32 dense blocks ({tag}): panel stream vs the analysed column stream: {d} differing",
+              flush=True)
+        bad += d
     print(f"total differing elements: {bad}", flush=True)
     sys.exit(1 if bad else 0)
 
