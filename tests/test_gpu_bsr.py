@@ -2367,3 +2367,33 @@ def test_panel_stream_bs64_bits(device, layout, n, fill):
     got, ref = host(C1), host(C2)
     diff = got.view(np.uint32) != ref.view(np.uint32)
     assert not diff.any(), f"bs 64 {fill} {layout} n={n}: {int(diff.sum())} elements differ"
+
+
+def test_panel_stream_edges(device):
+    """The panel stream with row-major C and alpha / beta, a partial second column tile
+    (n = 132), empty block rows and all-zero blocks among dense ones: bits equal the
+    analysed column stream's."""
+    ops = _ops()
+    rng = np.random.default_rng(7500)
+    mb, kb, bs, n, per_row = 700, 256, 32, 132, 60
+    rows = [np.sort(rng.choice(kb, per_row, replace=False)) if r % 7 else np.zeros(0, int)
+            for r in range(mb)]
+    rp = np.concatenate([[0], np.cumsum([len(x) for x in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    nnzb = ci.size
+    assert nnzb >= 1 << 15
+    vb = rng.uniform(-1, 1, (nnzb, bs, bs)).astype(np.float32)
+    vb[rng.random(nnzb) < 0.02] = 0.0
+    m, k = mb * bs, kb * bs
+    B = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    drp, dci, dv, dB = _dev(rp, ci, vb.reshape(-1), B.reshape(-1))
+    C1 = torch.from_numpy(C0.reshape(-1).copy()).cuda()
+    ops.bsrmm(drp, dci, dv, dB, mb=mb, kb=kb, n=n, bs=bs, ldb=n, C=C1, ldc=n, alpha=-0.75,
+              beta=1.25)
+    masks, vcol = ops.bsr32_analysis(dv, nnzb=nnzb)
+    C2 = torch.from_numpy(C0.reshape(-1).copy()).cuda()
+    ops.bsrmm_analysed(drp, dci, vcol, masks, dB, mb=mb, kb=kb, n=n, ldb=n, C=C2, ldc=n,
+                       alpha=-0.75, beta=1.25)
+    torch.cuda.synchronize()
+    assert torch.equal(C1.view(torch.int32), C2.view(torch.int32))
